@@ -1,0 +1,142 @@
+/*
+ * nrk.h — C-ABI of libnrk.so, the MI355X (gfx950) kernels behind the
+ * NewsRecommend hot path.
+ *
+ * The reference (YuxuanZhao/NewsRecommend) has no native code: its hot path
+ * runs through PyTorch ATen (DIN.py) and faiss-cpu (Retrieval.py).  Each entry
+ * point below replaces one reference interface; the citation says which.  The
+ * Python side (newsrecommend_amd/_lib.py) binds these with ctypes, the way a
+ * maintainer of the reference would.
+ *
+ * Conventions (all entry points):
+ *   - every pointer is a DEVICE pointer owned by the caller (torch tensors),
+ *     except where a parameter says "host";
+ *   - the library never allocates, frees or synchronises; all work is enqueued
+ *     on `stream` (a hipStream_t passed as void*), so calls are graph-capturable;
+ *   - return 0 on success, a negative NRK_E* code on failure; the message is in
+ *     thread-local storage, read with nrk_last_error();
+ *   - no mutable global state: the library is re-entrant.
+ */
+#ifndef NRK_H
+#define NRK_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* error codes */
+#define NRK_OK 0
+#define NRK_EINVAL (-1)   /* bad argument (shape, k, metric, null pointer) */
+#define NRK_EWORKSPACE (-2) /* workspace too small */
+#define NRK_ELAUNCH (-3)  /* kernel launch failed */
+#define NRK_EUNSUPPORTED (-4)
+
+/* metrics: same numeric values as faiss::MetricType */
+#define NRK_METRIC_INNER_PRODUCT 0
+#define NRK_METRIC_L2 1
+
+/* element types of embedding tables */
+#define NRK_DTYPE_F32 0
+#define NRK_DTYPE_BF16 1
+
+const char* nrk_last_error(void);
+int nrk_version(void);
+
+/* ------------------------------------------------------------------------- *
+ * Flat (exhaustive) k-NN search — replaces faiss IndexFlatIP / IndexFlatL2
+ * `.add(x)` and `.search(x, k)` (reference call sites Retrieval.py:25-26,31-32
+ * and the assignment search Retrieval.py:21).  Semantics restated in
+ * oracle/knn_exact.c: exact scores, IP descending / squared L2 ascending,
+ * ties broken by lower id, k > ntotal padded with id -1.
+ * ------------------------------------------------------------------------- */
+
+/* Per-corpus state built once per add():
+ *   xb_bf16  [nb][dp] bf16 (uint16), dp = nrk_padded_dim(d), zero-padded
+ *   xb_meta  [nb][2] float: {||x||^2 (fp32, exact-rounded), ||x - bf16(x)|| rounded up}
+ *   stats    [4] float: {max ||bf16(x)||, max residual norm, max ||x||^2, 0},
+ *            accumulated with atomic max, so zero it before the first prepare
+ *            call of an index (prepare may be called on appended slices). */
+int nrk_padded_dim(int32_t d);
+int nrk_flat_prepare(const float* xb, int64_t nb, int32_t d, uint16_t* xb_bf16,
+                     float* xb_meta, float* stats, void* stream);
+
+/* Workspace bytes needed by nrk_knn_flat for this problem. */
+int nrk_knn_flat_workspace(int64_t nq, int64_t nb, int32_t d, int32_t k, size_t* ws_bytes);
+
+/* Exact top-k: bf16 MFMA screening with per-chunk candidate lists, fp64
+ * rescoring of the survivors, a certificate per query, and an exact fp64 scan
+ * for any query the certificate does not cover.
+ *   xq [nq][d] f32; xb [nb][d] f32 (used for the exact rescoring)
+ *   D  [nq][k] f32 (IP: inner product, L2: squared distance)
+ *   I  [nq][k] int64 (global id = local row + id_offset; -1 padding)
+ *   S  [nq][k] f64 exact scores (optional, may be NULL): the values D rounds;
+ *      used by the multi-shard merge so ties break exactly as on one device.
+ *   n_fallback (optional, device int32[1]): number of queries that needed the
+ *      exact scan (diagnostic). */
+int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const uint16_t* xb_bf16,
+                 const float* xb_meta, const float* stats, int64_t nb, int32_t d,
+                 int32_t k, int32_t metric, float* D, int64_t* I, double* S,
+                 int64_t id_offset, int32_t* n_fallback, void* ws, size_t ws_bytes,
+                 void* stream);
+
+/* Exact brute force (fp64, sequential-d order), no screening.  Used directly
+ * for small corpora (e.g. the 300-centroid coarse search, Retrieval.py:25-32)
+ * and as the certificate fallback. */
+int nrk_knn_exact(const float* xq, int64_t nq, const float* xb, int64_t nb, int32_t d,
+                  int32_t k, int32_t metric, float* D, int64_t* I, double* S,
+                  int64_t id_offset, void* stream);
+
+/* Merge per-shard top-k lists (multi-GPU corpus sharding; no reference
+ * counterpart — the reference is single-device).
+ *   S_parts [nparts][nq][k] f64 exact scores, I_parts [nparts][nq][k] int64
+ *   D [nq][k] f32, I [nq][k] int64, S [nq][k] f64 (optional)
+ * Order: IP descending / L2 ascending on the f64 score, then lower id. */
+int nrk_topk_merge(const double* S_parts, const int64_t* I_parts, int32_t nparts, int64_t nq,
+                   int32_t k, int32_t metric, float* D, int64_t* I, double* S, void* stream);
+
+/* ------------------------------------------------------------------------- *
+ * DIN local-activation unit + weighted-sum pool — replaces
+ * AttentionLayer.forward (DIN.py:103-111) and its autograd backward, fused
+ * with the history gather of TrainDataset.__getitem__ (DIN.py:84-86).
+ *
+ * Keys come from one of two sources:
+ *   dense:  keys [B][L][d] (dtype), hist_ids == NULL  (AttentionLayer(query, keys))
+ *   ids:    table [N][d] (dtype) + hist_ids [B][L] int32; id < 0 means an
+ *           all-zero padding row, as DIN.py:84-86 zero-fills the tail.
+ * The query enters through U = query @ W1[:, :d]^T + b1 ([B][A] f32), computed
+ * by the caller (a plain GEMM); W1k = W1[:, d:] is passed in `dtype`.
+ * Softmax runs over all L slots, padding included (DIN.py:108, no mask).
+ * ------------------------------------------------------------------------- */
+int nrk_din_attn_fwd(const void* keys, const int32_t* hist_ids, int64_t n_table, int32_t dtype,
+                     const float* U, const void* W1k, const float* w2, float b2,
+                     int32_t B, int32_t L, int32_t d, int32_t A,
+                     float* pooled, float* alpha, void* stream);
+
+/* Backward of the pool w.r.t. the attention parameters (the reference's
+ * embeddings are frozen inputs, so no key/query gradient is produced):
+ *   in : dpooled [B][d] f32, alpha [B][L] f32 (from fwd)
+ *   out: dU [B][A] f32 (= sum_j dz_j; caller forms dW1q = dU^T q, db1 = sum dU)
+ *        dW1k [A][d] f32, dw2 [A] f32, db2 [1] f32 — OVERWRITTEN (not accumulated).
+ *   ws  : f32 workspace of nrk_din_attn_bwd_workspace() bytes (per-workgroup slabs). */
+int nrk_din_attn_bwd_workspace(int32_t B, int32_t d, int32_t A, size_t* ws_bytes);
+int nrk_din_attn_bwd(const void* keys, const int32_t* hist_ids, int64_t n_table, int32_t dtype,
+                     const float* U, const void* W1k, const float* w2, float b2,
+                     int32_t B, int32_t L, int32_t d, int32_t A,
+                     const float* dpooled, const float* alpha,
+                     float* dU, float* dW1k, float* dw2, float* db2,
+                     void* ws, size_t ws_bytes, void* stream);
+
+/* Row gather (table [N][d] dtype -> out [n][d] f32), id < 0 -> zeros.
+ * Replaces the per-sample dict lookups of DIN.py:47-50,83 (target and
+ * candidate embeddings). */
+int nrk_gather_rows(const void* table, int64_t n_table, int32_t dtype, const int32_t* ids,
+                    int64_t n, int32_t d, float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NRK_H */

@@ -1,0 +1,99 @@
+"""ctypes binding of libnrk.so (the C-ABI in include/nrk.h).
+
+This is the binding a maintainer of the reference would add (the reference is
+Python calling native code through faiss's SWIG layer and torch's ATen): plain
+pointers, sizes and a hipStream_t.  There is no CPU fallback — a product call
+without the library, or with host tensors, raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libnrk.so")
+
+NRK_METRIC_INNER_PRODUCT = 0
+NRK_METRIC_L2 = 1
+NRK_DTYPE_F32 = 0
+NRK_DTYPE_BF16 = 1
+
+c_p = ctypes.c_void_p
+c_i32 = ctypes.c_int32
+c_i64 = ctypes.c_int64
+c_f32 = ctypes.c_float
+c_size = ctypes.c_size_t
+
+# name -> (restype, argtypes); mirrors include/nrk.h exactly (tests check both ways)
+SIGNATURES = {
+    "nrk_last_error": (ctypes.c_char_p, []),
+    "nrk_version": (ctypes.c_int, []),
+    "nrk_padded_dim": (ctypes.c_int, [c_i32]),
+    "nrk_flat_prepare": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_p, c_p, c_p]),
+    "nrk_knn_flat_workspace": (ctypes.c_int, [c_i64, c_i64, c_i32, c_i32, ctypes.POINTER(c_size)]),
+    "nrk_knn_flat": (ctypes.c_int, [c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_i32, c_i32, c_i32, c_p, c_p, c_p, c_i64,
+                                    c_p, c_p, c_size, c_p]),
+    "nrk_knn_exact": (ctypes.c_int, [c_p, c_i64, c_p, c_i64, c_i32, c_i32, c_i32, c_p, c_p, c_p, c_i64, c_p]),
+    "nrk_topk_merge": (ctypes.c_int, [c_p, c_p, c_i32, c_i64, c_i32, c_i32, c_p, c_p, c_p, c_p]),
+    "nrk_din_attn_fwd": (ctypes.c_int, [c_p, c_p, c_i64, c_i32, c_p, c_p, c_p, c_f32, c_i32, c_i32, c_i32, c_i32,
+                                        c_p, c_p, c_p]),
+    "nrk_din_attn_bwd_workspace": (ctypes.c_int, [c_i32, c_i32, c_i32, ctypes.POINTER(c_size)]),
+    "nrk_din_attn_bwd": (ctypes.c_int, [c_p, c_p, c_i64, c_i32, c_p, c_p, c_p, c_f32, c_i32, c_i32, c_i32, c_i32,
+                                        c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_size, c_p]),
+    "nrk_gather_rows": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_i64, c_i32, c_p, c_p]),
+}
+
+_lib = None
+
+
+class NrkError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH):
+    """Load libnrk.so.  torch is imported first so that its bundled HIP runtime
+    is the one the library's libamdhip64.so.7 dependency resolves to."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(path):
+            raise NrkError(f"{path} is missing: build it with `python -m newsrecommend_amd.build` "
+                           "(there is no CPU fallback for the HIP path)")
+        lib = ctypes.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = load().nrk_last_error().decode(errors="replace")
+        raise NrkError(f"{what or 'libnrk'} failed (code {rc}): {msg}")
+
+
+def ptr(t) -> int | None:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_device(*tensors, what: str = "libnrk") -> torch.device:
+    dev = None
+    for t in tensors:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise NrkError(f"{what}: tensors must live on the GPU (got {t.device}); the HIP path has no CPU fallback")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise NrkError(f"{what}: tensors on different devices ({dev} vs {t.device})")
+    return dev

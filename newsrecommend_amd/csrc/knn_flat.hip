@@ -1,0 +1,709 @@
+// knn_flat.hip — exact flat k-NN for gfx950 (replaces faiss IndexFlatIP /
+// IndexFlatL2 .search, Retrieval.py:21,25-32).
+//
+// Pipeline per search (all on the caller's stream, no host sync):
+//   1. query_prepare  : xq -> bf16 q^ (zero-padded to DP), per-query norms
+//   2. screen         : bf16 MFMA (32x32x16) query x corpus-chunk tiles; every
+//                       lane keeps its top-(M+1) screened scores in registers;
+//                       writes M candidates + the (M+1)-th score (theta) per
+//                       (query, chunk, lane-half)
+//   3. merge_rescore  : per query: bitonic-sort the union of candidates, take
+//                       the top KP, rescore them EXACTLY (fp64, sequential d —
+//                       bit-identical to oracle/knn_exact.c), sort, and certify
+//                       with a rigorous screening error bound that no item
+//                       outside the KP candidates can enter the exact top-k;
+//                       uncertified queries are appended to a fallback list
+//   4. exact_topk     : fp64 brute force for the fallback list (normally empty)
+// See DESIGN.md "K-GEMM-TOPK" for the bound and the roofline.
+#include <float.h>
+#include <math.h>
+
+#include "nrk_common.h"
+
+namespace nrk {
+
+// ================================================================ prepare ==
+__global__ void flat_prepare_kernel(const float* __restrict__ xb, int64_t nb, int d, int dp,
+                                    uint16_t* __restrict__ xbh, float* __restrict__ meta,
+                                    float* __restrict__ stats) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= nb) return;
+  double sx2 = 0.0, sh2 = 0.0, sr2 = 0.0;
+  for (int j = lane; j < dp; j += 64) {
+    float x = j < d ? xb[row * d + j] : 0.f;
+    uint16_t h = f32_to_bf16_rne(x);
+    float hf = bf16_to_f32(h);
+    double r = (double)x - (double)hf;
+    sx2 += (double)x * (double)x;
+    sh2 += (double)hf * (double)hf;
+    sr2 += r * r;
+    xbh[row * dp + j] = h;
+  }
+  sx2 = wave_sum(sx2);
+  sh2 = wave_sum(sh2);
+  sr2 = wave_sum(sr2);
+  if (lane == 0) {
+    meta[2 * row] = (float)sx2;
+    float rn = f64_to_f32_up(sqrt(sr2) * (1.0 + 1e-9));
+    meta[2 * row + 1] = rn;
+    atomic_max_nonneg(&stats[0], f64_to_f32_up(sqrt(sh2) * (1.0 + 1e-9)));
+    atomic_max_nonneg(&stats[1], rn);
+    atomic_max_nonneg(&stats[2], f64_to_f32_up(sx2 * (1.0 + 1e-9)));
+  }
+}
+
+// qmeta[4*q] = {||q^|| (up), ||q - q^|| (up), ||q||^2, 0}
+__global__ void query_prepare_kernel(const float* __restrict__ xq, int64_t nq, int64_t nq_pad, int d,
+                                     int dp, uint16_t* __restrict__ qh, double* __restrict__ qmeta) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= nq_pad) return;
+  double sq2 = 0.0, sh2 = 0.0, sr2 = 0.0;
+  for (int j = lane; j < dp; j += 64) {
+    float x = (row < nq && j < d) ? xq[row * d + j] : 0.f;
+    uint16_t h = f32_to_bf16_rne(x);
+    float hf = bf16_to_f32(h);
+    double r = (double)x - (double)hf;
+    sq2 += (double)x * (double)x;
+    sh2 += (double)hf * (double)hf;
+    sr2 += r * r;
+    qh[row * dp + j] = h;
+  }
+  sq2 = wave_sum(sq2);
+  sh2 = wave_sum(sh2);
+  sr2 = wave_sum(sr2);
+  if (lane == 0 && row < nq) {
+    qmeta[4 * row + 0] = sqrt(sh2) * (1.0 + 1e-9);
+    qmeta[4 * row + 1] = sqrt(sr2) * (1.0 + 1e-9);
+    qmeta[4 * row + 2] = sq2;
+    qmeta[4 * row + 3] = 0.0;
+  }
+}
+
+// ================================================================ screen ==
+// LDS swizzle so that the ds_read_b128 A-fragment reads (32 rows, one 16-B
+// chunk each, 16-lane groups) hit 16 distinct bank slots.
+template <int CPR>
+__device__ __forceinline__ int swz(int row) {
+  if constexpr (CPR >= 16) return row & 15;
+  else return (row / (16 / CPR)) & (CPR - 1);
+}
+
+// Sorted (descending) insertion into a register list of N entries.  Ties keep
+// the resident entry first (it has the lower id: a lane scans ids upward).
+template <int N>
+__device__ __forceinline__ void list_insert(float (&ls)[N], int (&li)[N], float v, int id) {
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    bool gt = v > ls[j];
+    float ts = gt ? v : ls[j];
+    int ti = gt ? id : li[j];
+    v = gt ? ls[j] : v;
+    id = gt ? li[j] : id;
+    ls[j] = ts;
+    li[j] = ti;
+  }
+}
+
+// One workgroup = WAVES waves; wave w owns QT tiles of 32 queries; the
+// workgroup streams one corpus chunk in 32-item tiles through a double-
+// buffered LDS image.  MFMA: A = items (rows), B = queries (cols) so each lane
+// holds ONE query (lane & 31) and 16 items of a tile.
+template <int DP, int QT, int M, int WAVES, bool L2>
+__global__ __launch_bounds__(WAVES * 64) void screen_kernel(
+    const uint16_t* __restrict__ qh, const uint16_t* __restrict__ xbh,
+    const float* __restrict__ xmeta, int64_t nq, int64_t nb, int64_t chunk, int nch, int nqt,
+    float* __restrict__ part_s, int* __restrict__ part_i, float* __restrict__ part_t) {
+  constexpr int CPR = DP / 8;            // 16-B chunks per row
+  constexpr int TILE_CHUNKS = 32 * CPR;  // chunks per 32-row tile
+  constexpr int NT = WAVES * 64;
+  constexpr int LPT = (TILE_CHUNKS + NT - 1) / NT;
+  constexpr int KS = DP / 16;
+  constexpr int WQ = WAVES * 32 * QT;  // queries per workgroup
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2][32 * DP];
+  __shared__ float lnorm[2][32];
+
+  // XCD-aware bijective remap: blocks with equal (blockIdx % 8) share an XCD;
+  // give each such group contiguous logical ids so the nqt query tiles of one
+  // chunk run together on one L2.
+  const int nblk = gridDim.x, b = blockIdx.x;
+  const int xg = b & 7, jj = b >> 3, q8 = nblk >> 3, r8 = nblk & 7;
+  const int logical = (xg < r8 ? xg * (q8 + 1) : r8 * (q8 + 1) + (xg - r8) * q8) + jj;
+  const int c = logical / nqt, qt = logical - c * nqt;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t ibeg = (int64_t)c * chunk;
+  const int64_t iend = ibeg + chunk < nb ? ibeg + chunk : nb;
+  const int ntiles = (int)cdiv(iend - ibeg, 32);
+
+  // query fragments (B operand): lane (r, h) holds q^[query][16s + 8h .. +8]
+  bf16x8 qf[QT][KS];
+#pragma unroll
+  for (int t = 0; t < QT; ++t) {
+    const int64_t qi = (int64_t)qt * WQ + (w * QT + t) * 32 + r;  // < nq_pad (zero rows)
+    const bf16x8* src = reinterpret_cast<const bf16x8*>(qh + qi * DP + 8 * h);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) qf[t][s] = src[2 * s];
+  }
+
+  float ls[QT][M + 1];
+  int li[QT][M + 1];
+#pragma unroll
+  for (int t = 0; t < QT; ++t)
+#pragma unroll
+    for (int j = 0; j <= M; ++j) {
+      ls[t][j] = -INFINITY;
+      li[t][j] = -1;
+    }
+
+  uint4 stage[LPT];
+  float nstage = 0.f;
+  auto load_tile = [&](int it) {
+    const int64_t i0 = ibeg + (int64_t)it * 32;
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+      const int f = tid + u * NT;
+      const int row = f / CPR, cc = f % CPR;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (f < TILE_CHUNKS && i0 + row < iend)
+        v = *reinterpret_cast<const uint4*>(xbh + (i0 + row) * DP + cc * 8);
+      stage[u] = v;
+    }
+    if constexpr (L2) {
+      if (tid < 32) nstage = (i0 + tid < iend) ? xmeta[2 * (i0 + tid)] : 0.f;
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < LPT; ++u) {
+      const int f = tid + u * NT;
+      if (f < TILE_CHUNKS) {
+        const int row = f / CPR, cc = f % CPR;
+        *reinterpret_cast<uint4*>(&lds[buf][row * DP + 8 * (cc ^ swz<CPR>(row))]) = stage[u];
+      }
+    }
+    if constexpr (L2) {
+      if (tid < 32) lnorm[buf][tid] = nstage;
+    }
+  };
+
+  if (ntiles > 0) {
+    load_tile(0);
+    store_tile(0);
+  }
+  __syncthreads();
+
+  for (int it = 0; it < ntiles; ++it) {
+    const int buf = it & 1;
+    if (it + 1 < ntiles) load_tile(it + 1);
+
+    f32x16 acc[QT];
+#pragma unroll
+    for (int t = 0; t < QT; ++t)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) acc[t][g] = 0.f;
+    const uint16_t* arow = &lds[buf][r * DP];
+    const int sw = swz<CPR>(r);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(arow + 8 * ((2 * s + h) ^ sw));
+#pragma unroll
+      for (int t = 0; t < QT; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[t][s], acc[t], 0, 0, 0);
+    }
+
+    // epilogue: screened scores -> per-lane candidate lists
+    const int64_t i0 = ibeg + (int64_t)it * 32;
+    const int nvalid = (int)((iend - i0) < 32 ? (iend - i0) : 32);
+#pragma unroll
+    for (int t = 0; t < QT; ++t) {
+      float sc[16];
+      float m = -INFINITY;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int ir = (g & 3) + 8 * (g >> 2) + 4 * h;
+        float v = acc[t][g];
+        if constexpr (L2) v = fmaf(2.f, v, -lnorm[buf][ir]);
+        v = ir < nvalid ? v : -INFINITY;
+        sc[g] = v;
+        m = fmaxf(m, v);
+      }
+      if (__any(m > ls[t][M])) {
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+          const int ir = (g & 3) + 8 * (g >> 2) + 4 * h;
+          if (__any(sc[g] > ls[t][M])) {
+            if (sc[g] > ls[t][M]) list_insert<M + 1>(ls[t], li[t], sc[g], (int)(i0 + ir));
+          }
+        }
+      }
+    }
+
+    if (it + 1 < ntiles) store_tile(buf ^ 1);
+    __syncthreads();
+  }
+
+  // candidates of this (query, chunk, half)
+#pragma unroll
+  for (int t = 0; t < QT; ++t) {
+    const int64_t qi = (int64_t)qt * WQ + (w * QT + t) * 32 + r;
+    if (qi < nq) {
+      const int64_t base = (qi * nch + c) * 2 + h;
+#pragma unroll
+      for (int j = 0; j < M; ++j) {
+        part_s[base * M + j] = ls[t][j];
+        part_i[base * M + j] = li[t][j];
+      }
+      part_t[base] = ls[t][M];
+    }
+  }
+}
+
+// ========================================================= merge/rescore ==
+__device__ __forceinline__ double exact_score(const float* __restrict__ qs, const float* __restrict__ x,
+                                              int d, bool l2) {
+  double acc = 0.0;
+  if (!l2) {
+    for (int j = 0; j < d; ++j) acc = fma((double)qs[j], (double)x[j], acc);
+  } else {
+    for (int j = 0; j < d; ++j) {
+      double t = (double)qs[j] - (double)x[j];
+      acc = fma(t, t, acc);
+    }
+  }
+  return acc;
+}
+
+__device__ __forceinline__ int pow2ceil(int n) {
+  int p = 1;
+  while (p < n) p <<= 1;
+  return p;
+}
+
+// One 256-thread workgroup per query.  Dynamic LDS: P doubles + P int64 (the
+// union), P2 doubles + P2 int64 (rescored), d floats (query), reductions.
+__global__ __launch_bounds__(256) void merge_rescore_kernel(
+    const float* __restrict__ part_s, const int* __restrict__ part_i, const float* __restrict__ part_t,
+    int nch, int M, int KP, int k, int dp, const float* __restrict__ xq, const float* __restrict__ xb,
+    int d, int l2, const double* __restrict__ qmeta, const float* __restrict__ stats,
+    float* __restrict__ D, int64_t* __restrict__ I, double* __restrict__ S, int64_t id_offset,
+    int* __restrict__ fb_list, int* __restrict__ fb_count) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int qi = blockIdx.x, tid = threadIdx.x;
+  const int U = nch * 2 * M, P = pow2ceil(U);
+  double* g = reinterpret_cast<double*>(smem);
+  int64_t* id = reinterpret_cast<int64_t*>(g + P);
+  const int P2 = pow2ceil(KP);
+  double* g2 = reinterpret_cast<double*>(id + P);
+  int64_t* id2 = reinterpret_cast<int64_t*>(g2 + P2);
+  float* qs = reinterpret_cast<float*>(id2 + P2);
+  __shared__ float red[256];
+  __shared__ int s_valid;
+
+  const float* ps = part_s + (int64_t)qi * U;
+  const int* pi = part_i + (int64_t)qi * U;
+  for (int i = tid; i < P; i += 256) {
+    float v = i < U ? ps[i] : -INFINITY;
+    g[i] = (double)v;
+    id[i] = (i < U && v != -INFINITY) ? (int64_t)pi[i] : INT64_MAX;
+  }
+  float th = -INFINITY;
+  for (int i = tid; i < nch * 2; i += 256) th = fmaxf(th, part_t[(int64_t)qi * nch * 2 + i]);
+  red[tid] = th;
+  for (int i = tid; i < d; i += 256) qs[i] = xq[(int64_t)qi * d + i];
+  if (tid == 0) s_valid = 0;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) red[tid] = fmaxf(red[tid], red[tid + o]);
+    __syncthreads();
+  }
+  const float theta_lanes = red[0];
+  block_bitonic_sort(g, id, P);
+  for (int i = tid; i < P; i += 256)
+    if (id[i] != INT64_MAX) atomicAdd(&s_valid, 1);
+  __syncthreads();
+  const int V = s_valid;
+  const int kp = KP < V ? KP : V;
+  const double theta = fmax((double)theta_lanes, kp < V ? g[kp] : -INFINITY);
+
+  // exact rescoring of the top kp screened candidates
+  for (int i = tid; i < P2; i += 256) {
+    if (i < kp) {
+      const int64_t item = id[i];
+      const double s = exact_score(qs, xb + item * d, d, l2 != 0);
+      g2[i] = l2 ? -s : s;
+      id2[i] = item;
+    } else {
+      g2[i] = -INFINITY;
+      id2[i] = INT64_MAX;
+    }
+  }
+  __syncthreads();
+  block_bitonic_sort(g2, id2, P2);
+
+  if (tid == 0) {
+    bool ok = kp >= k;
+    if (ok && theta != -INFINITY) {
+      const double nqh = qmeta[4 * qi + 0], nrq = qmeta[4 * qi + 1], qn2 = qmeta[4 * qi + 2];
+      const double Xh = stats[0], R = stats[1], NX = stats[2];
+      const double gam = (double)dp * 0x1p-22;
+      const double bip = gam * nqh * Xh + nqh * R + nrq * Xh + nrq * R;
+      const double kth = g2[k - 1];
+      if (!l2) {
+        const double lim = theta + bip;
+        ok = kth - lim > 1e-12 * (fabs(lim) + fabs(kth));
+      } else {
+        const double B = 2.0 * bip + 0x1p-21 * (NX + nqh * Xh);
+        const double lo = qn2 - theta - B;  // lower bound on any outsider's distance
+        ok = lo - (-kth) > 1e-12 * (fabs(lo) + fabs(kth) + qn2);
+      }
+    }
+    if (!ok) fb_list[atomicAdd(fb_count, 1)] = qi;
+  }
+  for (int j = tid; j < k; j += 256) {
+    const int64_t o = (int64_t)qi * k + j;
+    const bool valid = j < kp;
+    const double s = valid ? (l2 ? -g2[j] : g2[j]) : (l2 ? DBL_MAX : -DBL_MAX);
+    D[o] = valid ? (float)s : (l2 ? FLT_MAX : -FLT_MAX);
+    I[o] = valid ? id2[j] + id_offset : -1;
+    if (S) S[o] = s;
+  }
+}
+
+// ============================================================ exact top-k ==
+// Workgroups loop over a query list (fallback) or over all queries (direct
+// exact mode).  Block top-k kept in LDS: list [0,k), staged candidates
+// [k, k+256), bitonic-merged whenever something was staged.
+__global__ __launch_bounds__(256) void exact_topk_kernel(
+    const float* __restrict__ xq, int64_t nq, const float* __restrict__ xb, int64_t nb, int d, int k,
+    int l2, const int* __restrict__ qlist, const int* __restrict__ qcount, float* __restrict__ D,
+    int64_t* __restrict__ I, double* __restrict__ S, int64_t id_offset) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int P = pow2ceil(k + 256);
+  double* g = reinterpret_cast<double*>(smem);
+  int64_t* id = reinterpret_cast<int64_t*>(g + P);
+  float* qs = reinterpret_cast<float*>(id + P);
+  __shared__ int s_nst, s_cnt;
+  const int tid = threadIdx.x;
+  const int64_t nwork = qcount ? (int64_t)*qcount : nq;
+  for (int64_t wi = blockIdx.x; wi < nwork; wi += gridDim.x) {
+    const int64_t qi = qlist ? (int64_t)qlist[wi] : wi;
+    for (int i = tid; i < P; i += 256) {
+      g[i] = -INFINITY;
+      id[i] = INT64_MAX;
+    }
+    for (int i = tid; i < d; i += 256) qs[i] = xq[qi * d + i];
+    if (tid == 0) {
+      s_nst = 0;
+      s_cnt = 0;
+    }
+    __syncthreads();
+    for (int64_t base = 0; base < nb; base += 256) {
+      const int64_t i = base + tid;
+      const int cnt = s_cnt;
+      const double tg = g[k - 1];
+      const int64_t tidx = id[k - 1];
+      if (i < nb) {
+        const double s = exact_score(qs, xb + i * d, d, l2 != 0);
+        const double gv = l2 ? -s : s;
+        if (cnt < k || better(gv, i, tg, tidx)) {
+          const int pos = atomicAdd(&s_nst, 1);
+          g[k + pos] = gv;
+          id[k + pos] = i;
+        }
+      }
+      __syncthreads();
+      const int nst = s_nst;
+      if (nst > 0) {
+        block_bitonic_sort(g, id, P);
+        for (int j = k + tid; j < P; j += 256) {
+          g[j] = -INFINITY;
+          id[j] = INT64_MAX;
+        }
+        __syncthreads();
+        if (tid == 0) {
+          s_cnt = cnt + nst < k ? cnt + nst : k;
+          s_nst = 0;
+        }
+      }
+      __syncthreads();
+    }
+    for (int j = tid; j < k; j += 256) {
+      const int64_t o = qi * k + j;
+      const bool valid = id[j] != INT64_MAX;
+      const double s = valid ? (l2 ? -g[j] : g[j]) : (l2 ? DBL_MAX : -DBL_MAX);
+      D[o] = valid ? (float)s : (l2 ? FLT_MAX : -FLT_MAX);
+      I[o] = valid ? id[j] + id_offset : -1;
+      if (S) S[o] = s;
+    }
+    __syncthreads();
+  }
+}
+
+// ============================================================ shard merge ==
+__global__ void topk_merge_kernel(const double* __restrict__ Sp, const int64_t* __restrict__ Ip, int nparts,
+                                  int64_t nq, int k, int l2, float* __restrict__ D, int64_t* __restrict__ I,
+                                  double* __restrict__ S) {
+  const int64_t qi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (qi >= nq) return;
+  int pos[16];
+  for (int p = 0; p < nparts; ++p) pos[p] = 0;
+  for (int j = 0; j < k; ++j) {
+    int best = -1;
+    double bg = 0.0;
+    int64_t bi = 0;
+    for (int p = 0; p < nparts; ++p) {
+      if (pos[p] >= k) continue;
+      const int64_t o = ((int64_t)p * nq + qi) * k + pos[p];
+      const int64_t ii = Ip[o];
+      if (ii < 0) continue;
+      const double gv = l2 ? -Sp[o] : Sp[o];
+      if (best < 0 || better(gv, ii, bg, bi)) {
+        best = p;
+        bg = gv;
+        bi = ii;
+      }
+    }
+    const int64_t oo = qi * k + j;
+    if (best < 0) {
+      D[oo] = l2 ? FLT_MAX : -FLT_MAX;
+      I[oo] = -1;
+      if (S) S[oo] = l2 ? DBL_MAX : -DBL_MAX;
+    } else {
+      const double s = l2 ? -bg : bg;
+      D[oo] = (float)s;
+      I[oo] = bi;
+      if (S) S[oo] = s;
+      pos[best]++;
+    }
+  }
+}
+
+// ================================================================== plan ==
+struct FlatPlan {
+  bool exact_only;
+  int dp, qt, M, waves, wq, nqt, nch, U, KP;
+  int64_t nq_pad, chunk;
+  size_t off_qh, off_qmeta, off_ps, off_pi, off_pt, off_fbl, off_fbc, total;
+};
+
+static int padded_dim(int d) {
+  if (d <= 32) return 32;
+  if (d <= 64) return 64;
+  if (d <= 128) return 128;
+  if (d <= 256) return 256;
+  return (int)align_up((size_t)d, 32);
+}
+
+static int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : dflt;
+}
+
+static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
+  FlatPlan p;
+  memset(&p, 0, sizeof(p));
+  p.dp = padded_dim(d);
+  p.exact_only = nb < env_int("NRK_EXACT_BELOW", 16384) || d > 256 || k > 256 || nb >= (1ll << 31) || nq == 0;
+  if (p.exact_only) {
+    p.off_fbc = 0;
+    p.total = 256;
+    return p;
+  }
+  p.waves = 4;
+  if (k <= 16) { p.M = 4; p.qt = 2; }
+  else if (k <= 64) { p.M = 8; p.qt = 2; }
+  else { p.M = 16; p.qt = 1; }
+  if (p.dp == 256) p.qt = 1;
+  p.wq = p.waves * 32 * p.qt;
+  p.nqt = (int)cdiv(nq, p.wq);
+  p.nq_pad = (int64_t)p.nqt * p.wq;
+  int target = env_int("NRK_SCREEN_WGS", 1536);
+  int64_t nch = target / (p.nqt > 0 ? p.nqt : 1);
+  if (nch < 1) nch = 1;
+  int64_t max_by_u = 2048 / (2 * p.M);
+  if (nch > max_by_u) nch = max_by_u;
+  int64_t max_by_len = cdiv(nb, 1024);
+  if (nch > max_by_len) nch = max_by_len;
+  if (nch < 1) nch = 1;
+  p.chunk = (int64_t)align_up((size_t)cdiv(nb, nch), 32);
+  p.nch = (int)cdiv(nb, p.chunk);
+  p.U = p.nch * 2 * p.M;
+  int kp = 2 * k > 32 ? 2 * k : 32;
+  if (kp < k + 16) kp = k + 16;
+  if (kp > p.U) kp = p.U;
+  if (kp > 1024) kp = 1024;
+  p.KP = kp;
+  if (p.KP < k) {
+    p.exact_only = true;
+    p.off_fbc = 0;
+    p.total = 256;
+    return p;
+  }
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    size_t o = off;
+    off = align_up(off + bytes, 256);
+    return o;
+  };
+  p.off_fbc = take(16);
+  p.off_qh = take((size_t)p.nq_pad * p.dp * 2);
+  p.off_qmeta = take((size_t)nq * 4 * 8);
+  p.off_ps = take((size_t)nq * p.U * 4);
+  p.off_pi = take((size_t)nq * p.U * 4);
+  p.off_pt = take((size_t)nq * p.nch * 2 * 4);
+  p.off_fbl = take((size_t)nq * 4);
+  p.total = off;
+  return p;
+}
+
+typedef void (*screen_fn)(const uint16_t*, const uint16_t*, const float*, int64_t, int64_t, int64_t, int,
+                          int, float*, int*, float*);
+
+template <int DP, int QT, int M, bool L2>
+static screen_fn pick2() {
+  return screen_kernel<DP, QT, M, 4, L2>;
+}
+
+template <int DP, bool L2>
+static screen_fn pick1(int qt, int M) {
+  if (M == 4) return qt == 2 ? pick2<DP, 2, 4, L2>() : pick2<DP, 1, 4, L2>();
+  if (M == 8) return qt == 2 ? pick2<DP, 2, 8, L2>() : pick2<DP, 1, 8, L2>();
+  return pick2<DP, 1, 16, L2>();
+}
+
+static screen_fn pick_screen(int dp, int qt, int M, bool l2) {
+  switch (dp) {
+    case 32: return l2 ? pick1<32, true>(qt, M) : pick1<32, false>(qt, M);
+    case 64: return l2 ? pick1<64, true>(qt, M) : pick1<64, false>(qt, M);
+    case 128: return l2 ? pick1<128, true>(qt, M) : pick1<128, false>(qt, M);
+    case 256: return l2 ? pick1<256, true>(qt, M) : pick1<256, false>(qt, M);
+  }
+  return nullptr;
+}
+
+}  // namespace nrk
+
+using namespace nrk;
+
+static int host_pow2ceil(int n) {
+  int p = 1;
+  while (p < n) p <<= 1;
+  return p;
+}
+
+static int exact_launch(const float* xq, int64_t nq, const float* xb, int64_t nb, int d, int k, int l2,
+                        const int* qlist, const int* qcount, int64_t max_work, float* D, int64_t* I,
+                        double* S, int64_t id_offset, hipStream_t st) {
+  const int P = host_pow2ceil(k + 256);
+  const size_t smem = (size_t)P * 16 + (size_t)d * 4;
+  if (smem > 160 * 1024) return fail(NRK_EUNSUPPORTED, "exact search: k=%d d=%d needs %zu B of LDS", k, d, smem);
+  int grid = (int)(max_work < 2048 ? max_work : 2048);
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(exact_topk_kernel, dim3(grid), dim3(256), smem, st, xq, nq, xb, nb, d, k, l2, qlist, qcount,
+                     D, I, S, id_offset);
+  NRK_CHECK_LAUNCH("exact_topk_kernel");
+  return NRK_OK;
+}
+
+extern "C" int nrk_padded_dim(int32_t d) { return padded_dim(d); }
+
+extern "C" int nrk_flat_prepare(const float* xb, int64_t nb, int32_t d, uint16_t* xb_bf16, float* xb_meta,
+                                float* stats, void* stream) {
+  NRK_CHECK_ARG(d > 0 && nb >= 0, "flat_prepare: bad shape nb=%lld d=%d", (long long)nb, d);
+  if (nb == 0) return NRK_OK;
+  NRK_CHECK_ARG(xb && xb_bf16 && xb_meta && stats, "flat_prepare: null pointer");
+  const int dp = padded_dim(d);
+  const int rows_per_block = 4;
+  hipLaunchKernelGGL(flat_prepare_kernel, dim3((unsigned)cdiv(nb, rows_per_block)), dim3(64 * rows_per_block), 0,
+                     (hipStream_t)stream, xb, nb, d, dp, xb_bf16, xb_meta, stats);
+  NRK_CHECK_LAUNCH("flat_prepare_kernel");
+  return NRK_OK;
+}
+
+extern "C" int nrk_knn_flat_workspace(int64_t nq, int64_t nb, int32_t d, int32_t k, size_t* ws_bytes) {
+  NRK_CHECK_ARG(ws_bytes && nq >= 0 && nb >= 0 && d > 0 && k > 0, "knn_flat_workspace: bad arguments");
+  *ws_bytes = make_plan(nq, nb, d, k).total;
+  return NRK_OK;
+}
+
+extern "C" int nrk_knn_exact(const float* xq, int64_t nq, const float* xb, int64_t nb, int32_t d, int32_t k,
+                             int32_t metric, float* D, int64_t* I, double* S, int64_t id_offset, void* stream) {
+  NRK_CHECK_ARG(d > 0 && k > 0 && k <= 1024 && nq >= 0 && nb >= 0, "knn_exact: bad shape nq=%lld nb=%lld d=%d k=%d",
+                (long long)nq, (long long)nb, d, k);
+  NRK_CHECK_ARG(metric == NRK_METRIC_INNER_PRODUCT || metric == NRK_METRIC_L2, "knn_exact: bad metric %d", metric);
+  if (nq == 0) return NRK_OK;
+  NRK_CHECK_ARG(xq && D && I && (xb || nb == 0), "knn_exact: null pointer");
+  return exact_launch(xq, nq, xb, nb, d, k, metric == NRK_METRIC_L2, nullptr, nullptr, nq, D, I, S, id_offset,
+                      (hipStream_t)stream);
+}
+
+extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const uint16_t* xb_bf16,
+                            const float* xb_meta, const float* stats, int64_t nb, int32_t d, int32_t k,
+                            int32_t metric, float* D, int64_t* I, double* S, int64_t id_offset,
+                            int32_t* n_fallback, void* ws, size_t ws_bytes, void* stream) {
+  NRK_CHECK_ARG(d > 0 && k > 0 && k <= 1024 && nq >= 0 && nb >= 0, "knn_flat: bad shape nq=%lld nb=%lld d=%d k=%d",
+                (long long)nq, (long long)nb, d, k);
+  NRK_CHECK_ARG(metric == NRK_METRIC_INNER_PRODUCT || metric == NRK_METRIC_L2, "knn_flat: bad metric %d", metric);
+  hipStream_t st = (hipStream_t)stream;
+  const FlatPlan p = make_plan(nq, nb, d, k);
+  if (ws_bytes < p.total) return fail(NRK_EWORKSPACE, "knn_flat: workspace %zu < %zu bytes", ws_bytes, p.total);
+  NRK_CHECK_ARG(ws != nullptr, "knn_flat: null workspace");
+  char* w = static_cast<char*>(ws);
+  int* fbc = reinterpret_cast<int*>(w + p.off_fbc);
+  if (hipMemsetAsync(fbc, 0, 16, st) != hipSuccess) return fail(NRK_ELAUNCH, "knn_flat: memset failed");
+  if (n_fallback && hipMemsetAsync(n_fallback, 0, 4, st) != hipSuccess)
+    return fail(NRK_ELAUNCH, "knn_flat: memset failed");
+  if (nq == 0) return NRK_OK;
+  NRK_CHECK_ARG(xq && D && I && (xb || nb == 0), "knn_flat: null pointer");
+  const int l2 = metric == NRK_METRIC_L2;
+  if (p.exact_only) {
+    return exact_launch(xq, nq, xb, nb, d, k, l2, nullptr, nullptr, nq, D, I, S, id_offset, st);
+  }
+  NRK_CHECK_ARG(xb_bf16 && xb_meta && stats, "knn_flat: index not prepared (null bf16/meta/stats)");
+  uint16_t* qh = reinterpret_cast<uint16_t*>(w + p.off_qh);
+  double* qmeta = reinterpret_cast<double*>(w + p.off_qmeta);
+  float* ps = reinterpret_cast<float*>(w + p.off_ps);
+  int* pi = reinterpret_cast<int*>(w + p.off_pi);
+  float* pt = reinterpret_cast<float*>(w + p.off_pt);
+  int* fbl = reinterpret_cast<int*>(w + p.off_fbl);
+
+  hipLaunchKernelGGL(query_prepare_kernel, dim3((unsigned)cdiv(p.nq_pad, 4)), dim3(256), 0, st, xq, nq, p.nq_pad, d,
+                     p.dp, qh, qmeta);
+  NRK_CHECK_LAUNCH("query_prepare_kernel");
+
+  screen_fn fn = pick_screen(p.dp, p.qt, p.M, l2 != 0);
+  if (!fn) return fail(NRK_EUNSUPPORTED, "knn_flat: no screen kernel for dp=%d", p.dp);
+  const int nblk = p.nqt * p.nch;
+  hipLaunchKernelGGL(fn, dim3(nblk), dim3(p.waves * 64), 0, st, qh, xb_bf16, xb_meta, nq, nb, p.chunk, p.nch, p.nqt,
+                     ps, pi, pt);
+  NRK_CHECK_LAUNCH("screen_kernel");
+
+  const int P = host_pow2ceil(p.U), P2 = host_pow2ceil(p.KP);
+  const size_t smem = (size_t)P * 16 + (size_t)P2 * 16 + (size_t)d * 4;
+  if (smem > 150 * 1024) return fail(NRK_EUNSUPPORTED, "knn_flat: merge needs %zu B LDS", smem);
+  hipLaunchKernelGGL(merge_rescore_kernel, dim3((unsigned)nq), dim3(256), smem, st, ps, pi, pt, p.nch, p.M, p.KP, k,
+                     p.dp, xq, xb, d, l2, qmeta, stats, D, I, S, id_offset, fbl, fbc);
+  NRK_CHECK_LAUNCH("merge_rescore_kernel");
+
+  int rc = exact_launch(xq, nq, xb, nb, d, k, l2, fbl, fbc, 256, D, I, S, id_offset, st);
+  if (rc != NRK_OK) return rc;
+  if (n_fallback && hipMemcpyAsync(n_fallback, fbc, 4, hipMemcpyDeviceToDevice, st) != hipSuccess)
+    return fail(NRK_ELAUNCH, "knn_flat: copy of fallback count failed");
+  return NRK_OK;
+}
+
+extern "C" int nrk_topk_merge(const double* S_parts, const int64_t* I_parts, int32_t nparts, int64_t nq, int32_t k,
+                              int32_t metric, float* D, int64_t* I, double* S, void* stream) {
+  NRK_CHECK_ARG(nparts >= 1 && nparts <= 16 && k > 0 && nq >= 0, "topk_merge: bad arguments nparts=%d k=%d", nparts,
+                k);
+  NRK_CHECK_ARG(metric == NRK_METRIC_INNER_PRODUCT || metric == NRK_METRIC_L2, "topk_merge: bad metric %d", metric);
+  if (nq == 0) return NRK_OK;
+  NRK_CHECK_ARG(S_parts && I_parts && D && I, "topk_merge: null pointer");
+  hipLaunchKernelGGL(topk_merge_kernel, dim3((unsigned)cdiv(nq, 256)), dim3(256), 0, (hipStream_t)stream, S_parts,
+                     I_parts, nparts, nq, k, metric == NRK_METRIC_L2, D, I, S);
+  NRK_CHECK_LAUNCH("topk_merge_kernel");
+  return NRK_OK;
+}

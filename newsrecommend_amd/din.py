@@ -1,0 +1,257 @@
+"""DIN ranker on MI355X — drop-in for the reference's DIN.py call surface.
+
+Same names, constructor arguments, forward signatures and state_dict keys as
+the reference (DIN.py:94-137), so `news/DIN_model.pth` checkpoints load both
+ways.  The attention layer's arithmetic (DIN.py:103-111) runs in libnrk's HIP
+kernels (K-LAU-POOL fwd/bwd, with the history gather fused in); the small
+BN/MLP head (DIN.py:117-122, ~1% of the flops) stays in torch.
+
+Two ways in:
+  * `DIN.forward(query, history)` — the reference's dense form: query (b, d),
+    history (b, L, d) (fp32 gives the fp32 parity path; bf16 the bf16 path).
+  * `DIN.forward_ids(table, target_ids, hist_ids)` — the id form: a device-
+    resident embedding table (N, d) (fp32 or bf16) plus int32 ids, padding
+    id -1 meaning an all-zero row (as DIN.py:84-86 zero-fills).  This removes
+    the CPU gather and host->device copy of TrainDataset.__getitem__.
+
+There is no CPU path: CPU tensors raise (use oracle/din_oracle.py, a test-only
+restatement, for CPU checks).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F  # noqa: F401  (parity with the reference's imports)
+
+from . import _lib
+
+
+def _dtype_code(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return _lib.NRK_DTYPE_F32
+    if t.dtype == torch.bfloat16:
+        return _lib.NRK_DTYPE_BF16
+    raise TypeError(f"DIN attention supports float32 / bfloat16 embeddings, got {t.dtype}")
+
+
+_KERNEL_DIMS = (32, 64, 128, 256)
+
+
+def _kernel_dim(d: int) -> int:
+    """Embedding widths with a compiled kernel; other widths are zero-padded
+    (zero columns change neither z, alpha nor the pooled sum)."""
+    for k in _KERNEL_DIMS:
+        if d <= k:
+            return k
+    raise ValueError(f"DIN attention: emb_dim {d} > 256 is not supported")
+
+
+def _pad_last(t: torch.Tensor, width: int) -> torch.Tensor:
+    return t if t.shape[-1] == width else torch.nn.functional.pad(t, (0, width - t.shape[-1]))
+
+
+class _LauPool(torch.autograd.Function):
+    """AttentionLayer forward/backward through nrk_din_attn_fwd/bwd.
+
+    keys_src is either dense keys (B, L, d) (hist_ids None) or a table (N, d)
+    addressed by hist_ids (B, L) int32.  Gradients flow to W1, b1, W2, b2 and
+    the query; the keys/table are frozen inputs as in the reference."""
+
+    @staticmethod
+    def forward(ctx, query, W1, b1, W2, b2, keys_src, hist_ids, L):
+        dev = _lib.require_device(query, W1, keys_src, hist_ids, what="DIN attention")
+        B, d = query.shape
+        A = W1.shape[0]
+        dtype = _dtype_code(keys_src)
+        Dk = _kernel_dim(d)
+        keys_src = _pad_last(keys_src, Dk).contiguous()
+        U = torch.addmm(b1, query, W1[:, :d].t()).contiguous()  # (B, A) f32: the query half of W1 [q; k] + b1
+        W1k = _pad_last(W1[:, d:], Dk).contiguous()
+        W1k_k = W1k if dtype == _lib.NRK_DTYPE_F32 else W1k.to(torch.bfloat16)
+        w2 = W2.reshape(-1).contiguous()
+        pooled = torch.empty((B, Dk), dtype=torch.float32, device=dev)
+        alpha = torch.empty((B, L), dtype=torch.float32, device=dev)
+        n_table = keys_src.shape[0] if hist_ids is not None else 0
+        # softmax is shift-invariant (DIN.py:108): b2 never changes alpha or the
+        # pooled output, so it is not sent (reading it would need a host sync).
+        _lib.check(_lib.load().nrk_din_attn_fwd(
+            _lib.ptr(keys_src), _lib.ptr(hist_ids), n_table, dtype, _lib.ptr(U), _lib.ptr(W1k_k), _lib.ptr(w2), 0.0,
+            B, L, Dk, A, _lib.ptr(pooled), _lib.ptr(alpha), _lib.stream(dev)), "din_attn_fwd")
+        ctx.save_for_backward(query, W1, U, W1k_k, w2, alpha, keys_src, hist_ids)
+        ctx.meta = (B, L, d, Dk, A, dtype, n_table)
+        return pooled if Dk == d else pooled[:, :d]
+
+    @staticmethod
+    def backward(ctx, dpooled):
+        query, W1, U, W1k_k, w2, alpha, keys_src, hist_ids = ctx.saved_tensors
+        B, L, d, Dk, A, dtype, n_table = ctx.meta
+        dev = query.device
+        dpooled = _pad_last(dpooled.float(), Dk).contiguous()
+        dU = torch.empty((B, A), dtype=torch.float32, device=dev)
+        dW1k = torch.empty((A, Dk), dtype=torch.float32, device=dev)
+        dw2 = torch.empty((A,), dtype=torch.float32, device=dev)
+        db2 = torch.empty((1,), dtype=torch.float32, device=dev)
+        L_ = _lib.load()
+        sz = _lib.c_size(0)
+        _lib.check(L_.nrk_din_attn_bwd_workspace(B, Dk, A, sz), "din_attn_bwd_workspace")
+        ws = torch.empty(max(sz.value // 4, 1), dtype=torch.float32, device=dev)
+        _lib.check(L_.nrk_din_attn_bwd(
+            _lib.ptr(keys_src), _lib.ptr(hist_ids), n_table, dtype, _lib.ptr(U), _lib.ptr(W1k_k), _lib.ptr(w2), 0.0,
+            B, L, Dk, A, _lib.ptr(dpooled), _lib.ptr(alpha), _lib.ptr(dU), _lib.ptr(dW1k), _lib.ptr(dw2), _lib.ptr(db2),
+            _lib.ptr(ws), ws.numel() * 4, _lib.stream(dev)), "din_attn_bwd")
+        dW1 = torch.cat([dU.t() @ query, dW1k[:, :d]], dim=1)
+        db1 = dU.sum(dim=0)
+        dquery = dU @ W1[:, :d] if ctx.needs_input_grad[0] else None
+        return dquery, dW1, db1, dw2.view(1, A), db2, None, None, None
+
+
+class AttentionLayer(nn.Module):
+    """DIN.py:94-111.  attn = Sequential(Linear(2d, A), ReLU, Linear(A, 1))."""
+
+    def __init__(self, emb_dim, attn_units):
+        super().__init__()
+        self.attn = nn.Sequential(
+            nn.Linear(emb_dim * 2, attn_units),
+            nn.ReLU(),
+            nn.Linear(attn_units, 1),
+        )
+
+    def _params(self):
+        return self.attn[0].weight, self.attn[0].bias, self.attn[2].weight, self.attn[2].bias
+
+    def forward(self, query, keys):  # (b, d), (b, L, d) -> (b, d)
+        b, L, d = keys.shape
+        W1, b1, W2, b2 = self._params()
+        return _LauPool.apply(query.float(), W1, b1, W2, b2, keys, None, L)
+
+    def forward_ids(self, query, table, hist_ids):
+        """query (b, d) f32; table (N, d) f32/bf16 on device; hist_ids (b, L) int32 (-1 = zero row)."""
+        if hist_ids.dtype != torch.int32:
+            hist_ids = hist_ids.to(torch.int32)
+        W1, b1, W2, b2 = self._params()
+        return _LauPool.apply(query.float(), W1, b1, W2, b2, table, hist_ids.contiguous(), hist_ids.shape[1])
+
+
+def gather_rows(table: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
+    """table[ids] as f32 (ids < 0 -> zero rows) through nrk_gather_rows."""
+    dev = _lib.require_device(table, ids, what="gather_rows")
+    ids = ids.to(torch.int32).contiguous()
+    n = ids.numel()
+    d = table.shape[1]
+    out = torch.empty((n, d), dtype=torch.float32, device=dev)
+    _lib.check(_lib.load().nrk_gather_rows(_lib.ptr(table.contiguous()), table.shape[0], _dtype_code(table),
+                                           _lib.ptr(ids), n, d, _lib.ptr(out), _lib.stream(dev)), "gather_rows")
+    return out.view(*ids.shape, d)
+
+
+class DIN(nn.Module):
+    """DIN.py:113-137 — same submodules, init and state_dict keys."""
+
+    def __init__(self, emb_dim, attn_units, fc_units, dropout_rate):
+        super().__init__()
+        self.attn = AttentionLayer(emb_dim, attn_units)
+        self.fc = nn.Sequential(
+            nn.BatchNorm1d(emb_dim * 2),
+            nn.Linear(emb_dim * 2, fc_units), nn.ReLU(), nn.Dropout(dropout_rate), nn.BatchNorm1d(fc_units),
+            nn.Linear(fc_units, fc_units // 2), nn.ReLU(), nn.Dropout(dropout_rate), nn.BatchNorm1d(fc_units // 2),
+            nn.Linear(fc_units // 2, 1),
+        )
+        self.sigmoid = nn.Sigmoid()
+        for m in self.modules():  # same init order as DIN.py:124-128 -> same params under one seed
+            if isinstance(m, nn.Linear):
+                nn.init.xavier_normal_(m.weight)
+                if m.bias is not None:
+                    nn.init.constant_(m.bias, 0)
+
+    def forward(self, query, history):
+        weighted = self.attn(query, history)
+        return self.fc(torch.cat([query.float(), weighted], dim=1))
+
+    def predict(self, target, history):
+        return self.sigmoid(self(target, history))
+
+    def forward_ids(self, table, target_ids, hist_ids):
+        query = gather_rows(table, target_ids)
+        weighted = self.attn.forward_ids(query, table, hist_ids)
+        return self.fc(torch.cat([query, weighted], dim=1))
+
+
+# ----------------------------------------------------------------- loops --
+def _batch_logits(model, batch, device):
+    if "history_ids" in batch:  # id form: batch carries ids, the model's table lives on the device
+        table = batch["table"]
+        return model.forward_ids(table, batch["target_ids"].to(device, non_blocking=True),
+                                 batch["history_ids"].to(device, non_blocking=True))
+    return model(batch["target_emb"].to(device, non_blocking=True), batch["history_emb"].to(device, non_blocking=True))
+
+
+def train(model, loader, optimizer, criterion, device, clip=1.0):
+    """DIN.py:139-153: one epoch of BCE + clip_grad_norm_(clip) + optimizer
+    step; returns the mean of the per-batch losses.  The losses are summed on
+    the device and read back once (the reference syncs every step, DIN.py:152)."""
+    model.train()
+    total = torch.zeros((), dtype=torch.float64, device=device)
+    n = 0
+    for batch in loader:
+        label = batch["label"].to(device, non_blocking=True)
+        optimizer.zero_grad()
+        loss = criterion(_batch_logits(model, batch, device), label)
+        loss.backward()
+        nn.utils.clip_grad_norm_(model.parameters(), clip)
+        optimizer.step()
+        total += loss.detach()
+        n += 1
+    return (total / max(n, 1)).item()
+
+
+def ndcg_from_logits(logits: torch.Tensor, labels: torch.Tensor, seg: torch.Tensor, nseg: int, k: int):
+    """Per-segment NDCG@k with one relevant item (DIN.py:181-189), on device.
+    Rank of the positive = 1 + #{p_j > p_pos} + #{j before pos with p_j == p_pos}
+    (a stable descending order; the reference's np.argsort is unstable on exact
+    ties, which this cannot reproduce)."""
+    probs = torch.sigmoid(logits)
+    dev = logits.device
+    pos_mask = labels > 0.5
+    idx = torch.arange(logits.numel(), device=dev)
+    # position of the first positive per segment (reference labels one-hot at the first match)
+    big = torch.full((nseg,), logits.numel(), dtype=torch.long, device=dev)
+    first_pos = big.scatter_reduce(0, seg[pos_mask], idx[pos_mask], reduce="amin", include_self=True)
+    has_pos = first_pos < logits.numel()
+    fp = first_pos.clamp(max=logits.numel() - 1)
+    p_pos = probs[fp][seg]
+    before = (probs > p_pos) | ((probs == p_pos) & (idx < fp[seg]))
+    rank = torch.zeros(nseg, dtype=torch.long, device=dev).index_add_(0, seg, before.long()) + 1
+    nd = torch.where(has_pos & (rank <= k), 1.0 / torch.log2(rank.double() + 1.0), torch.zeros_like(rank,
+                                                                                                   dtype=torch.double))
+    return nd
+
+
+def evaluate(model, loader, criterion, device, k):
+    """DIN.py:155-193: per-user BCE and NDCG@k over ragged candidate lists.
+    All users of a batch are scored in ONE forward (BN in eval mode is row-
+    independent, so this equals the reference's per-user loop); per-user
+    loss/NDCG are segment reductions on the device, read back once."""
+    model.eval()
+    loss_sum = torch.zeros((), dtype=torch.float64, device=device)
+    ndcg_sum = torch.zeros((), dtype=torch.float64, device=device)
+    users = 0
+    with torch.no_grad():
+        for batch in loader:
+            hist = batch["history_emb"].to(device, non_blocking=True).float()
+            cands = batch["cand_embs"]
+            labs = batch["labels"]
+            nu, L, d = hist.shape
+            counts = torch.tensor([c.shape[0] for c in cands], device=device)
+            seg = torch.repeat_interleave(torch.arange(nu, device=device), counts)
+            cand = torch.cat([c.to(device, non_blocking=True).float() for c in cands], 0)
+            lab = torch.cat([x.to(device, non_blocking=True).float() for x in labs], 0)
+            # candidate row i attends over its user's history: address the
+            # (nu*L, d) history as a table with per-row ids seg*L + j
+            hid = (seg[:, None] * L + torch.arange(L, device=device)[None, :]).to(torch.int32)
+            logits = model.fc(torch.cat([cand, model.attn.forward_ids(cand, hist.reshape(nu * L, d), hid)], 1)).view(-1)
+            per = nn.functional.binary_cross_entropy_with_logits(logits, lab, reduction="none")
+            seg_loss = torch.zeros(nu, dtype=torch.float64, device=device).index_add_(0, seg, per.double())
+            loss_sum += (seg_loss / counts.double()).sum()
+            ndcg_sum += ndcg_from_logits(logits, lab, seg, nu, k).sum()
+            users += nu
+    return (loss_sum / users).item(), (ndcg_sum / users).item()

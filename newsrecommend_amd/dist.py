@@ -1,0 +1,74 @@
+"""Corpus sharding across the GPUs of one node.
+
+The reference is single-device; faiss-cpu searches one in-process index.  Here
+each rank (one process per GPU, torch.distributed over RCCL/xGMI) holds a
+contiguous row block of the corpus and answers every query against it; the
+per-shard top-k lists — exact fp64 scores + global ids — are exchanged with ONE
+all_gather (packed into a single int64 buffer: 16 B per (query, rank, slot)) and
+merged on every rank by nrk_topk_merge with the same (score, lower id) rule, so
+the result is identical to a single search over the whole corpus.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from . import faiss as nf
+
+
+def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous, balanced row block of rank `rank`."""
+    base, rem = divmod(n, world)
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+def pack_results(S: torch.Tensor, I: torch.Tensor) -> torch.Tensor:
+    """(nq, k) f64 + (nq, k) int64 -> (nq, 2k) int64 (bit copy of S)."""
+    return torch.cat([S.contiguous().view(torch.int64), I.contiguous()], dim=1)
+
+
+def unpack_results(buf: torch.Tensor, k: int):
+    """(world, nq, 2k) int64 -> S (world, nq, k) f64, I (world, nq, k) int64."""
+    return buf[..., :k].contiguous().view(torch.float64), buf[..., k:].contiguous()
+
+
+def all_gather_results(S: torch.Tensor, I: torch.Tensor, group=None):
+    """One collective for all shards' lists.  Works on nccl (RCCL) and gloo."""
+    world = dist.get_world_size(group)
+    local = pack_results(S, I)
+    out = torch.empty((world, *local.shape), dtype=local.dtype, device=local.device)
+    if dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(out, local, group=group)
+    else:
+        dist.all_gather(list(out.unbind(0)), local, group=group)
+    return unpack_results(out, S.shape[1])
+
+
+class ShardedIndexFlat:
+    """IndexFlatIP / IndexFlatL2 whose rows are split over the ranks of `group`."""
+
+    def __init__(self, d: int, metric: int, group=None, device=None):
+        self.group = group
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.metric = metric
+        self.local = nf.IndexFlat(d, metric, device=device)
+        self.offset = 0
+        self.ntotal = 0
+
+    def add_full(self, xb):
+        """Every rank passes the full corpus (or a generator-identical copy);
+        each keeps only its own block."""
+        n = xb.shape[0]
+        lo, hi = shard_range(n, self.rank, self.world)
+        self.offset, self.ntotal = lo, n
+        self.local.add(xb[lo:hi])
+
+    def search_device(self, xq: torch.Tensor, k: int):
+        D, I, S = self.local.search_device(xq, k, exact_scores=True, id_offset=self.offset)
+        if self.world == 1:
+            return D, I
+        S_all, I_all = all_gather_results(S, I, self.group)
+        Dm, Im, _ = nf.topk_merge(S_all, I_all, k, self.metric)
+        return Dm, Im

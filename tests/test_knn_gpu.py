@@ -1,0 +1,154 @@
+"""GPU parity: libnrk flat search (through the faiss-compatible wrapper and the
+C-ABI) against the oracle — indices bit-exact, D bit-exact (the fp32 rounding
+of the same fp64 scores)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import knn_oracle as ko
+
+pytestmark = pytest.mark.gpu
+
+
+def _mixture(nb, nq, d, seed, centers=64, sigma=0.35):
+    rng = np.random.default_rng(seed)
+    c = rng.standard_normal((centers, d)).astype(np.float32)
+    xb = (c[rng.integers(0, centers, nb)] + sigma * rng.standard_normal((nb, d))).astype(np.float32)
+    xq = (c[rng.integers(0, centers, nq)] + sigma * rng.standard_normal((nq, d))).astype(np.float32)
+    return xq, xb
+
+
+def _check(xq, xb, k, metric, gpu, exact_below=None, monkeypatch=None):
+    from newsrecommend_amd import faiss as nf
+
+    idx = nf.IndexFlat(xb.shape[1], metric)
+    idx.add(xb)
+    D, I = idx.search(xq, k)
+    Do, Io, So = ko.exact_search(xq, xb, k, metric)
+    np.testing.assert_array_equal(I, Io)
+    np.testing.assert_array_equal(D, Do)
+    return idx
+
+
+@pytest.mark.parametrize("metric", [ko.METRIC_IP, ko.METRIC_L2])
+def test_c1_shape(gpu, metric):
+    """configs[0]: 10k x 64, 1k queries, k=5 (screening path: NRK_EXACT_BELOW default 16384 -> exact path;
+    both paths are covered by the larger tests)."""
+    xq, xb = _mixture(10_000, 1000, 64, seed=1)
+    _check(xq, xb, 5, metric, gpu)
+
+
+@pytest.mark.parametrize("metric", [ko.METRIC_IP, ko.METRIC_L2])
+@pytest.mark.parametrize("d,k", [(128, 5), (64, 10), (100, 32), (256, 5), (32, 1), (128, 100)])
+def test_screened_path(gpu, metric, d, k):
+    xq, xb = _mixture(60_001, 300, d, seed=d + k)
+    idx = _check(xq, xb, k, metric, gpu)
+    assert idx.last_fallback is not None
+
+
+def test_gaussian_unstructured(gpu):
+    rng = np.random.default_rng(7)
+    xb = rng.standard_normal((50_000, 128)).astype(np.float32)
+    xq = rng.standard_normal((257, 128)).astype(np.float32)
+    for metric in (ko.METRIC_IP, ko.METRIC_L2):
+        _check(xq, xb, 10, metric, gpu)
+
+
+def test_duplicates_and_ties_take_lower_id(gpu):
+    """Exact duplicates straddling chunks and lanes: the certificate cannot
+    separate them, so these queries go through the fp64 fallback, which must
+    return the lower ids first."""
+    xq, xb = _mixture(40_000, 64, 64, seed=3)
+    for j in (5, 17_000, 39_999, 20_001):
+        xb[j] = xb[3]
+    xq[0] = xb[3]
+    xq[1] = xb[3] * 2
+    for metric in (ko.METRIC_IP, ko.METRIC_L2):
+        idx = _check(xq, xb, 4, metric, gpu)
+    _, I = idx.search(xq[:1], 4)
+    assert I[0].tolist() == [3, 5, 17000, 20001]
+
+
+def test_k_exceeds_ntotal_and_empty(gpu):
+    from newsrecommend_amd import faiss as nf
+
+    xq, xb = _mixture(5, 3, 16, seed=4)
+    for metric in (ko.METRIC_IP, ko.METRIC_L2):
+        idx = nf.IndexFlat(16, metric)
+        idx.add(xb)
+        D, I = idx.search(xq, 8)
+        Do, Io, _ = ko.exact_search(xq, xb, 8, metric)
+        np.testing.assert_array_equal(I, Io)
+        np.testing.assert_array_equal(D, Do)
+        empty = nf.IndexFlat(16, metric)
+        D, I = empty.search(xq, 2)
+        assert (I == -1).all()
+
+
+def test_incremental_add_and_torch_io(gpu):
+    from newsrecommend_amd import faiss as nf
+
+    xq, xb = _mixture(30_000, 100, 128, seed=8)
+    idx = nf.IndexFlatIP(128)
+    for lo in range(0, 30_000, 7_000):
+        idx.add(xb[lo:lo + 7_000])
+    assert idx.ntotal == 30_000
+    D, I = idx.search(torch.from_numpy(xq).cuda(), 5)
+    assert D.is_cuda and I.dtype == torch.int64
+    _, Io, _ = ko.exact_search(xq, xb, 5, ko.METRIC_IP)
+    np.testing.assert_array_equal(I.cpu().numpy(), Io)
+
+
+def test_retrieval_centroid_search(gpu):
+    """Retrieval.py:25-34 shape: IndexFlatL2 over 300 centroids, nq=1 searches."""
+    from newsrecommend_amd import faiss as nf
+
+    xq, xb = _mixture(300, 50, 256, seed=9)
+    idx = nf.IndexFlatL2(256)
+    idx.add(xb)
+    _, Io, _ = ko.exact_search(xq, xb, 1, ko.METRIC_L2)
+    for i in range(0, 50, 7):
+        _, I = idx.search(xq[i].reshape(1, 256), 1)
+        assert I[0, 0] == Io[i, 0]
+
+
+def test_shard_merge_kernel(gpu):
+    from newsrecommend_amd import faiss as nf
+
+    xq, xb = _mixture(20_000, 64, 64, seed=10)
+    xb[15_000] = xb[2]
+    xq[0] = xb[2]
+    for metric in (ko.METRIC_IP, ko.METRIC_L2):
+        parts_S, parts_I = [], []
+        for lo, hi in ((0, 6_000), (6_000, 6_001), (6_001, 20_000)):
+            D, I, S = nf.knn_exact(torch.from_numpy(xq).cuda(), torch.from_numpy(xb[lo:hi]).cuda(), 7, metric,
+                                   id_offset=lo)
+            parts_S.append(S)
+            parts_I.append(I)
+        Dm, Im, Sm = nf.topk_merge(torch.stack(parts_S), torch.stack(parts_I), 7, metric)
+        Do, Io, So = ko.exact_search(xq, xb, 7, metric)
+        np.testing.assert_array_equal(Im.cpu().numpy(), Io)
+        np.testing.assert_array_equal(Sm.cpu().numpy(), So)
+
+
+def test_full_size_properties(gpu):
+    """configs[1] size (1M x 128, nq=4096, k=5): size-independent properties —
+    every returned score equals an fp64 recomputation, lists are sorted with
+    ids ascending on ties, and a sample of queries equals the oracle."""
+    from newsrecommend_amd import faiss as nf
+    from newsrecommend_amd.data import clustered_corpus
+
+    xb = clustered_corpus(1_000_000, 128, seed=1234, device="cuda")
+    xq = clustered_corpus(4096, 128, seed=4321, device="cuda")
+    idx = nf.IndexFlatIP(128)
+    idx.add(xb)
+    D, I, S = idx.search_device(xq, 5, exact_scores=True)
+    assert (I >= 0).all()
+    rows = xb[I.view(-1)].double().view(4096, 5, 128)
+    s64 = (rows * xq.double()[:, None, :]).sum(-1)
+    assert torch.allclose(s64, S, rtol=0, atol=1e-9)
+    assert (S[:, :-1] >= S[:, 1:]).all()
+    sample = torch.arange(0, 4096, 97)
+    _, Io, So = ko.exact_search(xq[sample].cpu().numpy(), xb.cpu().numpy(), 5, ko.METRIC_IP)
+    np.testing.assert_array_equal(I[sample].cpu().numpy(), Io)
+    assert int(idx.last_fallback.item()) <= 41  # certificate covers (nearly) every query
