@@ -1,0 +1,336 @@
+#!/usr/bin/env python3
+"""bench.py — the driver's benchmark contract for the NewsRecommend hot path.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Headline (BASELINE.json `metric`, configs[1]): exact flat retrieval, 1M x 128
+items, batches of nq = 4096 queries, k = 5, inner product.  One STEP = one
+search of one 4096-query batch (inputs resident in HBM).  At N > 1 the corpus
+is row-sharded over the ranks (fixed 1M corpus: strong scaling); each rank
+searches its shard and the per-shard exact top-k lists are merged after ONE
+RCCL all_gather (newsrecommend_amd.dist).  value = queries answered / max-
+over-ranks wall time of the K timed steps.
+
+Secondary record `din` (configs[2]): DIN training, bf16 table of 2M items,
+5M synthetic click rows, L = 50, d = 128, A = 128, F = 32; one step = fwd +
+bwd + clip + Adam on a batch of --din-batch rows; data-parallel replicas with
+a gradient all_reduce at N > 1.
+
+Rank 0 prints ONE JSON line.  `roofline` is the screening kernel (MFMA-bound)
+timed live with HIP events on its launch stream; `cpu_baseline` times the
+oracle's restatement of faiss-cpu's flat search on this host's cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+BF16_DENSE_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 MFMA
+HBM_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s HBM3E spec
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return rank, world, torch.device("cuda", local)
+
+
+def barrier(world):
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def max_over_ranks(x: float, world: int, dev) -> float:
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def cpu_cores() -> int:
+    n = os.environ.get("OMP_NUM_THREADS")
+    return int(n) if n else len(os.sched_getaffinity(0))
+
+
+# ------------------------------------------------------------ retrieval --
+def bench_flat(args, rank, world, dev):
+    from newsrecommend_amd import _lib
+    from newsrecommend_amd.data import clustered_corpus
+    from newsrecommend_amd.dist import ShardedIndexFlat
+
+    metric = 0 if args.metric == "ip" else 1
+    xb = clustered_corpus(args.nb, args.d, seed=1234, device=dev)
+    xq = clustered_corpus(args.nq, args.d, seed=4321, device=dev)
+    index = ShardedIndexFlat(args.d, metric, device=dev)
+    index.add_full(xb)
+    keep_full = rank == 0
+    xb_host = xb.cpu().numpy() if keep_full else None
+    del xb
+    torch.cuda.empty_cache()
+    nb_local = index.local.ntotal
+
+    for _ in range(args.warmup):
+        D, I = index.search_device(xq, args.k)
+    barrier(world)
+    evs = [_lib.StageEvents() for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        D, I = index.search_device(xq, args.k) if world > 1 else index.local.search_device(
+            xq, args.k, stage_events=evs[s])[:2]
+        if world > 1:  # stage timing of the local search only
+            pass
+    barrier(world)
+    el = max_over_ranks(time.perf_counter() - t0, world, dev)
+    qps = args.nq * args.steps / el
+
+    # per-stage device times (rank-local), averaged over the timed steps
+    if world > 1:  # one extra instrumented local search per step-count for the stage split
+        for s in range(args.steps):
+            index.local.search_device(xq, args.k, exact_scores=True, id_offset=index.offset, stage_events=evs[s])
+        torch.cuda.synchronize()
+    st = np.array([e.elapsed_ms() for e in evs])
+    stage_ms = st.mean(0)
+    screen_ms = float(stage_ms[1])
+    flops = 2.0 * args.nq * nb_local * args.d
+    achieved = flops / (screen_ms * 1e-3) / 1e12
+    fallback = int(index.local.last_fallback.item())
+
+    out = {
+        "value": qps, "unit": "queries/s", "ms_per_step": el / args.steps * 1e3,
+        "stages_ms": {"query_prepare": float(stage_ms[0]), "screen": screen_ms,
+                      "merge_rescore": float(stage_ms[2]), "exact_fallback": float(stage_ms[3])},
+        "fallback_queries": fallback,
+        "roofline": {"bound": "mfma", "kernel": "screen_kernel (bf16 v_mfma_f32_32x32x16)",
+                     "achieved": achieved, "peak": BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / BF16_DENSE_TFLOPS, "traffic": _pmc_traffic(args, world),
+                     "algorithmic": f"2*nq*nb_local*d = {flops:.4g} flop per launch"},
+    }
+    if rank == 0:
+        out["recall_at_5"], out["exact_match"] = _recall(args, xq, xb_host, D, I, metric)
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = _cpu_flat(args, xq, xb_host, metric)
+    return out
+
+
+def _recall(args, xq, xb_host, D, I, metric):
+    from oracle import knn_oracle as ko
+
+    sample = np.arange(0, args.nq, max(1, args.nq // 64))
+    q = xq.cpu().numpy()[sample]
+    _, Io, _ = ko.exact_search(q, xb_host, args.k, metric)
+    Ig = I.cpu().numpy()[sample]
+    rec = float(np.mean([len(set(a[:5]) & set(b[:5])) / min(5, args.k) for a, b in zip(Ig, Io)]))
+    return rec, bool(np.array_equal(Ig, Io))
+
+
+def _cpu_flat(args, xq, xb_host, metric):
+    """oracle.knn_oracle.faiss_port (faiss-cpu's blocked-BLAS flat search,
+    restated) on a bounded query sample against the FULL corpus."""
+    from oracle import knn_oracle as ko
+
+    q = xq.cpu().numpy()
+    n = 64
+    t = time.perf_counter()
+    ko.faiss_port(q[:n], xb_host, args.k, metric)
+    dt = time.perf_counter() - t
+    budget = args.cpu_seconds
+    n2 = int(min(args.nq, max(n, n * budget / max(dt, 1e-3))))
+    n2 = max(n, (n2 // 64) * 64)
+    t = time.perf_counter()
+    ko.faiss_port(q[:n2], xb_host, args.k, metric)
+    dt = time.perf_counter() - t
+    return {"value": n2 / dt, "unit": "queries/s", "cores": cpu_cores(), "kind": "port",
+            "sample": f"{n2} of the {args.nq} queries x full {args.nb}x{args.d} corpus, k={args.k}, "
+                      f"oracle.knn_oracle.faiss_port (numpy fp32 BLAS blocks + top-k), {dt:.1f} s"}
+
+
+def _pmc_traffic(args, world):
+    """HBM bytes per screen launch from a committed rocprofv3 --pmc summary for
+    this exact workload (profiles/pmc_screen.json), else null."""
+    p = os.path.join(ROOT, "profiles", "pmc_screen.json")
+    try:
+        j = json.load(open(p))
+        key = f"nb={args.nb},d={args.d},nq={args.nq},k={args.k},metric={args.metric},gpus={world}"
+        return j.get(key, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+# ------------------------------------------------------------------ DIN --
+def bench_din(args, rank, world, dev):
+    from newsrecommend_amd.data import synthetic_click_rows
+    from newsrecommend_amd.din import DIN, KernelTimer
+
+    torch.manual_seed(42)
+    n_items, L, d, A, F = args.din_items, 50, 128, 128, 32
+    g = torch.Generator(device=dev).manual_seed(1)
+    table = (torch.randn((n_items, d), generator=g, device=dev) * 0.5).to(torch.bfloat16)
+    rows = args.din_rows
+    hist, tgt, lab = synthetic_click_rows(rows, n_items, L, seed=7 + rank, device=dev)
+    model = DIN(d, A, F, 0.36).to(dev)
+    opt = torch.optim.Adam(model.parameters(), lr=1.62e-3, weight_decay=8.96e-5)
+    crit = torch.nn.BCEWithLogitsLoss()
+    B = args.din_batch
+    perm = torch.randperm(rows, device=dev)
+    nbatch = rows // B
+
+    def step(s):
+        idx = perm[(s % nbatch) * B:(s % nbatch + 1) * B]
+        logits = model.forward_ids(table, tgt[idx], hist[idx])
+        loss = crit(logits, lab[idx])
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        if world > 1:
+            flat = torch.cat([p.grad.reshape(-1) for p in model.parameters()])
+            dist.all_reduce(flat)
+            flat /= world
+            o = 0
+            for p in model.parameters():
+                n = p.numel()
+                p.grad.copy_(flat[o:o + n].view_as(p))
+                o += n
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        opt.step()
+        return loss
+
+    model.train()
+    for s in range(args.warmup):
+        step(s)
+    barrier(world)
+    with KernelTimer() as kt:
+        t0 = time.perf_counter()
+        for s in range(args.steps):
+            loss = step(args.warmup + s)
+        barrier(world)
+        el = max_over_ranks(time.perf_counter() - t0, world, dev)
+    sps = B * args.steps * world / el
+    fwd_ms, bwd_ms = kt.mean_ms("fwd"), kt.mean_ms("bwd")
+    fwd_bytes = B * (L * d * 2 + 4 * L + 4 * A + 4 * d + 4 * L)
+    bwd_bytes = B * (L * d * 2 + 4 * L + 4 * A + 4 * d + 4 * L + 4 * A)
+    fwd_gbs = fwd_bytes / (fwd_ms * 1e-3) / 1e9
+    bwd_gbs = bwd_bytes / (bwd_ms * 1e-3) / 1e9
+    out = {
+        "metric": "DIN train samples/s", "value": sps, "unit": "samples/s", "ms_per_step": el / args.steps * 1e3,
+        "config": {"workload": "configs[2]: DIN train bf16, 5M synthetic click rows, seq_len=50, emb_dim=128",
+                   "rows": rows, "items": n_items, "batch": B, "attn_units": A, "fc_units": F,
+                   "parallelism": f"dp{world}"},
+        "final_loss": float(loss.item()),
+        "kernels_ms": {"attn_fwd": fwd_ms, "attn_bwd+reduce": bwd_ms},
+        "roofline_fwd": {"bound": "hbm", "achieved": fwd_gbs, "peak": HBM_GBS, "unit": "GB/s",
+                         "frac": fwd_gbs / HBM_GBS, "traffic": None,
+                         "algorithmic": f"{fwd_bytes // B} B/sample x {B} samples"},
+        "roofline_bwd": {"bound": "hbm", "achieved": bwd_gbs, "peak": HBM_GBS, "unit": "GB/s",
+                         "frac": bwd_gbs / HBM_GBS, "traffic": None,
+                         "algorithmic": f"{bwd_bytes // B} B/sample x {B} samples"},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = _cpu_din(args, n_items, L, d, A, F)
+    return out
+
+
+def _cpu_din(args, n_items, L, d, A, F):
+    """oracle.din_oracle (numpy float64 restatement of DIN.py's train step:
+    forward, backward, clip, Adam) on a bounded sample of rows."""
+    from oracle import din_oracle as o
+    from newsrecommend_amd.din import DIN
+
+    rng = np.random.default_rng(0)
+    Bc = 1024
+    table = (rng.standard_normal((20000, d)) * 0.5).astype(np.float32)
+    m = DIN(d, A, F, 0.0)
+    p = {k: v.numpy().astype(np.float64) for k, v in m.state_dict().items() if "num_batches" not in k}
+    params = {k: v for k, v in p.items() if "running" not in k}
+    state = {}
+    t = time.perf_counter()
+    n = 0
+    while time.perf_counter() - t < args.cpu_seconds / 2 or n < 2:
+        ln = rng.integers(1, L + 1, Bc)
+        idx = np.where(np.arange(L)[None] < ln[:, None], rng.integers(0, 20000, (Bc, L)), -1)
+        keys = np.where(idx[..., None] >= 0, table[np.maximum(idx, 0)], 0.0)
+        q = table[rng.integers(0, 20000, Bc)]
+        y = (rng.random((Bc, 1)) < 0.5).astype(np.float64)
+        full = dict(p)
+        full.update(params)
+        lg, _, _, c = o.din_forward(full, q, keys, train=True)
+        g = o.din_backward(full, c, lg, y)
+        g, _ = o.clip_grad_norm(g, 1.0)
+        params = o.adam_step(params, g, state, 1.62e-3, 8.96e-5)
+        n += 1
+    dt = time.perf_counter() - t
+    return {"value": n * Bc / dt, "unit": "samples/s", "cores": cpu_cores(), "kind": "port",
+            "sample": f"{n} train steps x {Bc} rows (L={L}, d={d}), oracle.din_oracle numpy fp64, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", choices=["flat", "din", "all"], default="all")
+    ap.add_argument("--nb", type=int, default=1_000_000)
+    ap.add_argument("--d", type=int, default=128)
+    ap.add_argument("--nq", type=int, default=4096)
+    ap.add_argument("--k", type=int, default=5)
+    ap.add_argument("--metric", choices=["ip", "l2"], default="ip")
+    ap.add_argument("--din-rows", type=int, default=5_000_000)
+    ap.add_argument("--din-items", type=int, default=2_000_000)
+    ap.add_argument("--din-batch", type=int, default=4096)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank, world, dev = setup(args)
+    rec = {"metric": METRIC, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "bf16",
+           "data": "synthetic"}
+    if args.workload in ("flat", "all"):
+        r = bench_flat(args, rank, world, dev)
+        rec.update({k: r[k] for k in ("value", "unit", "ms_per_step")})
+        rec["config"] = {"workload": f"configs[1]: flat kNN {args.nb}x{args.d}, batch={args.nq} queries, k={args.k}, "
+                                     f"{args.metric.upper()}", "nb": args.nb, "d": args.d, "nq": args.nq, "k": args.k,
+                         "metric": args.metric, "screen": "bf16 MFMA, fp32 accumulate", "rescore": "f64 exact",
+                         "parallelism": f"corpus-shard{world} + RCCL all_gather merge" if world > 1 else "single GPU"}
+        for k in ("roofline", "stages_ms", "fallback_queries", "recall_at_5", "exact_match", "cpu_baseline"):
+            if k in r:
+                rec[k] = r[k]
+    if args.workload in ("din", "all"):
+        r = bench_din(args, rank, world, dev)
+        if args.workload == "din":
+            rec.update({"metric": r["metric"], "value": r["value"], "unit": r["unit"], "ms_per_step": r["ms_per_step"],
+                        "config": r["config"], "scaling": "weak", "roofline": r["roofline_fwd"]})
+            if "cpu_baseline" in r:
+                rec["cpu_baseline"] = r["cpu_baseline"]
+        rec["din"] = r
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -75,12 +75,16 @@ int nrk_knn_flat_workspace(int64_t nq, int64_t nb, int32_t d, int32_t k, size_t*
  *   S  [nq][k] f64 exact scores (optional, may be NULL): the values D rounds;
  *      used by the multi-shard merge so ties break exactly as on one device.
  *   n_fallback (optional, device int32[1]): number of queries that needed the
- *      exact scan (diagnostic). */
+ *      exact scan (diagnostic).
+ *   stage_events (optional, host array of NRK_KNN_STAGES+1 hipEvent_t created by
+ *      the caller): recorded on `stream` before each stage and after the last,
+ *      so a benchmark can time the screening kernel alone.  NULL in production. */
+#define NRK_KNN_STAGES 4 /* query_prepare, screen, merge_rescore, exact fallback */
 int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const uint16_t* xb_bf16,
                  const float* xb_meta, const float* stats, int64_t nb, int32_t d,
                  int32_t k, int32_t metric, float* D, int64_t* I, double* S,
                  int64_t id_offset, int32_t* n_fallback, void* ws, size_t ws_bytes,
-                 void* stream);
+                 void* const* stage_events, void* stream);
 
 /* Exact brute force (fp64, sequential-d order), no screening.  Used directly
  * for small corpora (e.g. the 300-centroid coarse search, Retrieval.py:25-32)

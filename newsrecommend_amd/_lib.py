@@ -34,7 +34,7 @@ SIGNATURES = {
     "nrk_flat_prepare": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_p, c_p, c_p]),
     "nrk_knn_flat_workspace": (ctypes.c_int, [c_i64, c_i64, c_i32, c_i32, ctypes.POINTER(c_size)]),
     "nrk_knn_flat": (ctypes.c_int, [c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_i32, c_i32, c_i32, c_p, c_p, c_p, c_i64,
-                                    c_p, c_p, c_size, c_p]),
+                                    c_p, c_p, c_size, c_p, c_p]),
     "nrk_knn_exact": (ctypes.c_int, [c_p, c_i64, c_p, c_i64, c_i32, c_i32, c_i32, c_p, c_p, c_p, c_i64, c_p]),
     "nrk_topk_merge": (ctypes.c_int, [c_p, c_p, c_i32, c_i64, c_i32, c_i32, c_p, c_p, c_p, c_p]),
     "nrk_din_attn_fwd": (ctypes.c_int, [c_p, c_p, c_i64, c_i32, c_p, c_p, c_p, c_f32, c_i32, c_i32, c_i32, c_i32,
@@ -97,3 +97,54 @@ def require_device(*tensors, what: str = "libnrk") -> torch.device:
         elif t.device != dev:
             raise NrkError(f"{what}: tensors on different devices ({dev} vs {t.device})")
     return dev
+
+
+# ------------------------------------------------ HIP events (bench timing) --
+_hip = None
+
+
+def _hiprt():
+    """The HIP runtime torch loaded (same process-wide libamdhip64.so.7)."""
+    global _hip
+    if _hip is None:
+        import torch  # noqa: F401
+        h = ctypes.CDLL("libamdhip64.so.7", mode=ctypes.RTLD_GLOBAL)
+        h.hipEventCreate.argtypes = [ctypes.POINTER(c_p)]
+        h.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), c_p, c_p]
+        h.hipEventSynchronize.argtypes = [c_p]
+        h.hipEventDestroy.argtypes = [c_p]
+        _hip = h
+    return _hip
+
+
+class StageEvents:
+    """NRK_KNN_STAGES+1 hipEvent_t for nrk_knn_flat's stage_events."""
+
+    N = 5
+
+    def __init__(self):
+        h = _hiprt()
+        self.ev = (c_p * self.N)()
+        for i in range(self.N):
+            e = c_p()
+            if h.hipEventCreate(ctypes.byref(e)) != 0:
+                raise NrkError("hipEventCreate failed")
+            self.ev[i] = e
+
+    def elapsed_ms(self):
+        h = _hiprt()
+        h.hipEventSynchronize(self.ev[self.N - 1])
+        out = []
+        for i in range(self.N - 1):
+            t = ctypes.c_float(0)
+            h.hipEventElapsedTime(ctypes.byref(t), self.ev[i], self.ev[i + 1])
+            out.append(t.value)
+        return out
+
+    def __del__(self):
+        try:
+            h = _hiprt()
+            for i in range(self.N):
+                h.hipEventDestroy(self.ev[i])
+        except Exception:
+            pass

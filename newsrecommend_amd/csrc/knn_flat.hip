@@ -643,7 +643,8 @@ extern "C" int nrk_knn_exact(const float* xq, int64_t nq, const float* xb, int64
 extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const uint16_t* xb_bf16,
                             const float* xb_meta, const float* stats, int64_t nb, int32_t d, int32_t k,
                             int32_t metric, float* D, int64_t* I, double* S, int64_t id_offset,
-                            int32_t* n_fallback, void* ws, size_t ws_bytes, void* stream) {
+                            int32_t* n_fallback, void* ws, size_t ws_bytes, void* const* stage_events,
+                            void* stream) {
   NRK_CHECK_ARG(d > 0 && k > 0 && k <= 1024 && nq >= 0 && nb >= 0, "knn_flat: bad shape nq=%lld nb=%lld d=%d k=%d",
                 (long long)nq, (long long)nb, d, k);
   NRK_CHECK_ARG(metric == NRK_METRIC_INNER_PRODUCT || metric == NRK_METRIC_L2, "knn_flat: bad metric %d", metric);
@@ -663,6 +664,9 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
     return exact_launch(xq, nq, xb, nb, d, k, l2, nullptr, nullptr, nq, D, I, S, id_offset, st);
   }
   NRK_CHECK_ARG(xb_bf16 && xb_meta && stats, "knn_flat: index not prepared (null bf16/meta/stats)");
+  auto mark = [&](int i) {
+    if (stage_events) hipEventRecord((hipEvent_t)stage_events[i], st);
+  };
   uint16_t* qh = reinterpret_cast<uint16_t*>(w + p.off_qh);
   double* qmeta = reinterpret_cast<double*>(w + p.off_qmeta);
   float* ps = reinterpret_cast<float*>(w + p.off_ps);
@@ -670,6 +674,7 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
   float* pt = reinterpret_cast<float*>(w + p.off_pt);
   int* fbl = reinterpret_cast<int*>(w + p.off_fbl);
 
+  mark(0);
   hipLaunchKernelGGL(query_prepare_kernel, dim3((unsigned)cdiv(p.nq_pad, 4)), dim3(256), 0, st, xq, nq, p.nq_pad, d,
                      p.dp, qh, qmeta);
   NRK_CHECK_LAUNCH("query_prepare_kernel");
@@ -677,6 +682,7 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
   screen_fn fn = pick_screen(p.dp, p.qt, p.M, l2 != 0);
   if (!fn) return fail(NRK_EUNSUPPORTED, "knn_flat: no screen kernel for dp=%d", p.dp);
   const int nblk = p.nqt * p.nch;
+  mark(1);
   hipLaunchKernelGGL(fn, dim3(nblk), dim3(p.waves * 64), 0, st, qh, xb_bf16, xb_meta, nq, nb, p.chunk, p.nch, p.nqt,
                      ps, pi, pt);
   NRK_CHECK_LAUNCH("screen_kernel");
@@ -684,12 +690,15 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
   const int P = host_pow2ceil(p.U), P2 = host_pow2ceil(p.KP);
   const size_t smem = (size_t)P * 16 + (size_t)P2 * 16 + (size_t)d * 4;
   if (smem > 150 * 1024) return fail(NRK_EUNSUPPORTED, "knn_flat: merge needs %zu B LDS", smem);
+  mark(2);
   hipLaunchKernelGGL(merge_rescore_kernel, dim3((unsigned)nq), dim3(256), smem, st, ps, pi, pt, p.nch, p.M, p.KP, k,
                      p.dp, xq, xb, d, l2, qmeta, stats, D, I, S, id_offset, fbl, fbc);
   NRK_CHECK_LAUNCH("merge_rescore_kernel");
 
+  mark(3);
   int rc = exact_launch(xq, nq, xb, nb, d, k, l2, fbl, fbc, 256, D, I, S, id_offset, st);
   if (rc != NRK_OK) return rc;
+  mark(4);
   if (n_fallback && hipMemcpyAsync(n_fallback, fbc, 4, hipMemcpyDeviceToDevice, st) != hipSuccess)
     return fail(NRK_ELAUNCH, "knn_flat: copy of fallback count failed");
   return NRK_OK;

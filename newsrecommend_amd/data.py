@@ -155,11 +155,13 @@ def custom_collate_fn(batch):
 
 # ------------------------------------------------------------- synthetic --
 def clustered_corpus(n: int, d: int, n_centers: int = 1024, sigma: float = 0.35, seed: int = 1234,
-                     device=None) -> torch.Tensor:
-    """item = centre[z] + sigma * N(0, I), centres ~ N(0, I),
+                     device=None, center_seed: int = 1234) -> torch.Tensor:
+    """item = centre[z] + sigma * N(0, I), centres ~ N(0, I)
+    (drawn from `center_seed`, so corpus and queries share one mixture),
     z uniform; float32 (n, d).  Generated on `device` (GPU for large n)."""
-    g = torch.Generator(device=device or "cpu").manual_seed(seed)
-    centers = torch.randn((n_centers, d), generator=g, device=device)
+    gc = torch.Generator(device=device or "cpu").manual_seed(center_seed)
+    centers = torch.randn((n_centers, d), generator=gc, device=device)
+    g = torch.Generator(device=device or "cpu").manual_seed(seed + 7919)
     out = torch.empty((n, d), dtype=torch.float32, device=device)
     step = 1 << 20
     for lo in range(0, n, step):

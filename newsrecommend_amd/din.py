@@ -50,6 +50,45 @@ def _pad_last(t: torch.Tensor, width: int) -> torch.Tensor:
     return t if t.shape[-1] == width else torch.nn.functional.pad(t, (0, width - t.shape[-1]))
 
 
+class KernelTimer:
+    """Bench hook: while active, brackets each attention kernel launch with
+    torch.cuda.Event pairs on the launch stream (the current stream)."""
+
+    active = None
+
+    def __init__(self):
+        self.fwd, self.bwd = [], []
+
+    def __enter__(self):
+        KernelTimer.active = self
+        return self
+
+    def __exit__(self, *exc):
+        KernelTimer.active = None
+
+    @staticmethod
+    def mark(kind):
+        t = KernelTimer.active
+        if t is None:
+            return None
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    @staticmethod
+    def push(kind, start):
+        t = KernelTimer.active
+        if t is None or start is None:
+            return
+        end = torch.cuda.Event(enable_timing=True)
+        end.record()
+        (t.fwd if kind == "fwd" else t.bwd).append((start, end))
+
+    def mean_ms(self, kind, skip=0):
+        ev = (self.fwd if kind == "fwd" else self.bwd)[skip:]
+        return sum(a.elapsed_time(b) for a, b in ev) / max(len(ev), 1)
+
+
 class _LauPool(torch.autograd.Function):
     """AttentionLayer forward/backward through nrk_din_attn_fwd/bwd.
 
@@ -74,9 +113,11 @@ class _LauPool(torch.autograd.Function):
         n_table = keys_src.shape[0] if hist_ids is not None else 0
         # softmax is shift-invariant (DIN.py:108): b2 never changes alpha or the
         # pooled output, so it is not sent (reading it would need a host sync).
+        t0 = KernelTimer.mark("fwd")
         _lib.check(_lib.load().nrk_din_attn_fwd(
             _lib.ptr(keys_src), _lib.ptr(hist_ids), n_table, dtype, _lib.ptr(U), _lib.ptr(W1k_k), _lib.ptr(w2), 0.0,
             B, L, Dk, A, _lib.ptr(pooled), _lib.ptr(alpha), _lib.stream(dev)), "din_attn_fwd")
+        KernelTimer.push("fwd", t0)
         ctx.save_for_backward(query, W1, U, W1k_k, w2, alpha, keys_src, hist_ids)
         ctx.meta = (B, L, d, Dk, A, dtype, n_table)
         return pooled if Dk == d else pooled[:, :d]
@@ -95,10 +136,12 @@ class _LauPool(torch.autograd.Function):
         sz = _lib.c_size(0)
         _lib.check(L_.nrk_din_attn_bwd_workspace(B, Dk, A, sz), "din_attn_bwd_workspace")
         ws = torch.empty(max(sz.value // 4, 1), dtype=torch.float32, device=dev)
+        t0 = KernelTimer.mark("bwd")
         _lib.check(L_.nrk_din_attn_bwd(
             _lib.ptr(keys_src), _lib.ptr(hist_ids), n_table, dtype, _lib.ptr(U), _lib.ptr(W1k_k), _lib.ptr(w2), 0.0,
             B, L, Dk, A, _lib.ptr(dpooled), _lib.ptr(alpha), _lib.ptr(dU), _lib.ptr(dW1k), _lib.ptr(dw2), _lib.ptr(db2),
             _lib.ptr(ws), ws.numel() * 4, _lib.stream(dev)), "din_attn_bwd")
+        KernelTimer.push("bwd", t0)
         dW1 = torch.cat([dU.t() @ query, dW1k[:, :d]], dim=1)
         db1 = dU.sum(dim=0)
         dquery = dU @ W1[:, :d] if ctx.needs_input_grad[0] else None

@@ -118,7 +118,8 @@ class IndexFlat:
             self._ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=self.device)
         return self._ws
 
-    def search_device(self, xq: torch.Tensor, k: int, exact_scores: bool = False, id_offset: int = 0):
+    def search_device(self, xq: torch.Tensor, k: int, exact_scores: bool = False, id_offset: int = 0,
+                      stage_events=None):
         """Device-in, device-out search: returns (D f32, I int64[, S f64]) on the GPU."""
         k = int(k)
         if k <= 0:
@@ -139,7 +140,8 @@ class IndexFlat:
                 _lib.ptr(xq), nq, _lib.ptr(self._xb[:n]) if n else None, _lib.ptr(self._xbh[:n]) if n else None,
                 _lib.ptr(self._meta[:n]) if n else None, _lib.ptr(self._stats), n, self.d, k, self.metric_type,
                 _lib.ptr(D), _lib.ptr(I), _lib.ptr(S), int(id_offset), _lib.ptr(self.last_fallback), _lib.ptr(ws),
-                ws.numel(), _lib.stream(self.device)), "knn_flat")
+                ws.numel(), stage_events.ev if stage_events is not None else None, _lib.stream(self.device)),
+                "knn_flat")
         return (D, I, S) if exact_scores else (D, I)
 
     def search(self, x, k):
