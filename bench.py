@@ -121,7 +121,7 @@ def bench_flat(args, rank, world, dev):
 
     out = {
         "value": qps, "unit": "queries/s", "ms_per_step": el / args.steps * 1e3,
-        "stages_ms": {"query_prepare": float(stage_ms[0]), "screen": screen_ms,
+        "stages_ms": {"query_prepare+tau_prepass": float(stage_ms[0]), "screen": screen_ms,
                       "merge_rescore": float(stage_ms[2]), "exact_fallback": float(stage_ms[3])},
         "fallback_queries": fallback,
         "roofline": {"bound": "mfma", "kernel": "screen_kernel (bf16 v_mfma_f32_32x32x16)",

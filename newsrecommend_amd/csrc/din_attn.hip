@@ -397,16 +397,27 @@ __global__ __launch_bounds__(256) void din_bwd_kernel(
   }
 }
 
-__global__ void din_bwd_reduce_kernel(const float* __restrict__ slabs, int nslab, int A, int D,
-                                      float* __restrict__ dW1k, float* __restrict__ dw2, float* __restrict__ db2) {
+// Sum the per-workgroup slabs in a fixed order (deterministic): a block owns
+// 64 consecutive outputs; its 4 waves each sum every 4th slab, then combine.
+__global__ __launch_bounds__(256) void din_bwd_reduce_kernel(const float* __restrict__ slabs, int nslab, int A, int D,
+                                                             float* __restrict__ dW1k, float* __restrict__ dw2,
+                                                             float* __restrict__ db2) {
+  __shared__ float part[4][64];
   const size_t n = slab_floats(A, D);
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (size_t)A * D + A + 1) return;
+  const size_t nout = (size_t)A * D + A + 1;
+  const int o = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const size_t i = (size_t)blockIdx.x * 64 + o;
   float s = 0.f;
-  for (int j = 0; j < nslab; ++j) s += slabs[(size_t)j * n + i];
-  if (i < (size_t)A * D) dW1k[i] = s;
-  else if (i < (size_t)A * D + A) dw2[i - (size_t)A * D] = s;
-  else db2[0] = s;
+  if (i < nout)
+    for (int j = g; j < nslab; j += 4) s += slabs[(size_t)j * n + i];
+  part[g][o] = s;
+  __syncthreads();
+  if (g == 0 && i < nout) {
+    const float t = (part[0][o] + part[1][o]) + (part[2][o] + part[3][o]);
+    if (i < (size_t)A * D) dW1k[i] = t;
+    else if (i < (size_t)A * D + A) dw2[i - (size_t)A * D] = t;
+    else db2[0] = t;
+  }
 }
 
 // ================================================================ gather ==
@@ -434,9 +445,12 @@ using namespace nrk;
 
 namespace {
 
-int din_grid(int B) {
-  const char* e = getenv("NRK_DIN_WGS");
-  int cap = e && *e ? atoi(e) : 1024;
+int din_grid(int B, bool bwd) {
+  // forward: many small workgroups; backward: one workgroup per CU (its
+  // registers allow one wave per SIMD) so the per-workgroup gradient slabs
+  // stay few
+  const char* e = getenv(bwd ? "NRK_DIN_BWD_WGS" : "NRK_DIN_WGS");
+  int cap = e && *e ? atoi(e) : (bwd ? 256 : 1024);
   return B < cap ? B : cap;
 }
 
@@ -492,7 +506,7 @@ extern "C" int nrk_din_attn_fwd(const void* keys, const int32_t* hist_ids, int64
   const size_t smem = fwd_smem(bf, d, L);
   NRK_CHECK_ARG(smem <= 160 * 1024, "din_fwd: L=%d d=%d needs %zu B LDS", L, d, smem);
   NRK_DIN_DISPATCH(bf, d, {
-    hipLaunchKernelGGL((din_fwd_kernel<kBF, kD>), dim3(din_grid(B)), dim3(256), smem, (hipStream_t)stream, keys,
+    hipLaunchKernelGGL((din_fwd_kernel<kBF, kD>), dim3(din_grid(B, false)), dim3(256), smem, (hipStream_t)stream, keys,
                        hist_ids, n_table, U, W1k, w2, b2, B, L, A, pooled, alpha);
   });
   NRK_CHECK_LAUNCH("din_fwd_kernel");
@@ -501,7 +515,7 @@ extern "C" int nrk_din_attn_fwd(const void* keys, const int32_t* hist_ids, int64
 
 extern "C" int nrk_din_attn_bwd_workspace(int32_t B, int32_t d, int32_t A, size_t* ws_bytes) {
   NRK_CHECK_ARG(ws_bytes != nullptr, "din_bwd_workspace: null");
-  *ws_bytes = (size_t)(B > 0 ? din_grid(B) : 1) * slab_floats(A, d) * 4;
+  *ws_bytes = (size_t)(B > 0 ? din_grid(B, true) : 1) * slab_floats(A, d) * 4;
   return NRK_OK;
 }
 
@@ -521,7 +535,7 @@ extern "C" int nrk_din_attn_bwd(const void* keys, const int32_t* hist_ids, int64
     return NRK_OK;
   }
   NRK_CHECK_ARG(U && W1k && w2 && dpooled && alpha && dU && ws, "din_bwd: null pointer");
-  const int grid = din_grid(B);
+  const int grid = din_grid(B, true);
   const size_t need = (size_t)grid * slab_floats(A, d) * 4;
   if (ws_bytes < need) return fail(NRK_EWORKSPACE, "din_bwd: workspace %zu < %zu", ws_bytes, need);
   const bool bf = dtype == NRK_DTYPE_BF16;
@@ -534,7 +548,7 @@ extern "C" int nrk_din_attn_bwd(const void* keys, const int32_t* hist_ids, int64
   });
   NRK_CHECK_LAUNCH("din_bwd_kernel");
   const size_t nout = (size_t)A * d + A + 1;
-  hipLaunchKernelGGL(din_bwd_reduce_kernel, dim3((unsigned)cdiv((int64_t)nout, 256)), dim3(256), 0, st, slabs, grid, A,
+  hipLaunchKernelGGL(din_bwd_reduce_kernel, dim3((unsigned)cdiv((int64_t)nout, 64)), dim3(256), 0, st, slabs, grid, A,
                      d, dW1k, dw2, db2);
   NRK_CHECK_LAUNCH("din_bwd_reduce_kernel");
   return NRK_OK;

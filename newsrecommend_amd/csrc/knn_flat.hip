@@ -107,26 +107,36 @@ __device__ __forceinline__ void list_insert(float (&ls)[N], int (&li)[N], float 
 }
 
 // One workgroup = WAVES waves; wave w owns QT tiles of 32 queries; the
-// workgroup streams one corpus chunk in 32-item tiles through a double-
-// buffered LDS image.  MFMA: A = items (rows), B = queries (cols) so each lane
-// holds ONE query (lane & 31) and 16 items of a tile.
-template <int DP, int QT, int M, int WAVES, bool L2>
-__global__ __launch_bounds__(WAVES * 64) void screen_kernel(
-    const uint16_t* __restrict__ qh, const uint16_t* __restrict__ xbh,
-    const float* __restrict__ xmeta, int64_t nq, int64_t nb, int64_t chunk, int nch, int nqt,
-    float* __restrict__ part_s, int* __restrict__ part_i, float* __restrict__ part_t) {
-  constexpr int CPR = DP / 8;            // 16-B chunks per row
-  constexpr int TILE_CHUNKS = 32 * CPR;  // chunks per 32-row tile
+// workgroup streams one corpus chunk in 64-item tiles, staged HBM -> LDS with
+// global_load_lds (double buffered; the XOR swizzle is applied to the SOURCE
+// address since the DMA writes LDS lane-linearly).  MFMA 32x32x16 bf16 with
+// A = items (rows), B = queries (cols): each lane holds ONE query (lane & 31)
+// and 16 items of each 32-item sub-tile.
+//
+// MODE 1 (threshold pre-pass): visits every TSTRIDE-th tile of its chunk and
+//   writes each lane's maximum screened score: many short, disjoint lane
+//   streams, so the R-th largest of a query's lane maxima (tau_select_kernel)
+//   is a proven lower bound on that query's global R-th best screened score.
+// MODE 0 (main pass): every lane keeps its top-(M+1) screened scores in
+//   registers, admitting only scores above max(its (M+1)-th, tau[q]); the
+//   pre-pass bound removes the warm-up insertions that otherwise dominate.
+//   The merge's certificate includes tau[q] in theta.
+template <int DP, int QT, int M, int WAVES, bool L2, int MODE, int EPI = 0>
+__global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
+    const uint16_t* __restrict__ qh, const uint16_t* __restrict__ xbh, const float* __restrict__ xmeta,
+    int64_t nq, int64_t nb, int64_t chunk, int nch, int nqt, int tstride, float* __restrict__ part_s,
+    int* __restrict__ part_i, float* __restrict__ part_t, const float* __restrict__ tau_q) {
+  constexpr int CPR = DP / 8;        // 16-B chunks per row
+  constexpr int TI = 64;  // items per tile (TI/32 sub-tiles of 32) between barriers
+  constexpr int TCH = TI * CPR;      // 16-B chunks per tile
   constexpr int NT = WAVES * 64;
-  constexpr int LPT = (TILE_CHUNKS + NT - 1) / NT;
+  constexpr int GPT = TCH / NT;      // glds instructions per thread per tile
+  static_assert(TCH % NT == 0, "tile must split evenly over the workgroup");
   constexpr int KS = DP / 16;
-  constexpr int WQ = WAVES * 32 * QT;  // queries per workgroup
-  __shared__ __attribute__((aligned(16))) uint16_t lds[2][32 * DP];
-  __shared__ float lnorm[2][32];
+  constexpr int WQ = WAVES * 32 * QT;
+  constexpr int BUF = TI * DP + 2 * TI;  // uint16 per buffer: rows + TI float norms
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BUF];
 
-  // XCD-aware bijective remap: blocks with equal (blockIdx % 8) share an XCD;
-  // give each such group contiguous logical ids so the nqt query tiles of one
-  // chunk run together on one L2.
   const int nblk = gridDim.x, b = blockIdx.x;
   const int xg = b & 7, jj = b >> 3, q8 = nblk >> 3, r8 = nblk & 7;
   const int logical = (xg < r8 ? xg * (q8 + 1) : r8 * (q8 + 1) + (xg - r8) * q8) + jj;
@@ -136,129 +146,181 @@ __global__ __launch_bounds__(WAVES * 64) void screen_kernel(
   const int r = lane & 31, h = lane >> 5;
   const int64_t ibeg = (int64_t)c * chunk;
   const int64_t iend = ibeg + chunk < nb ? ibeg + chunk : nb;
-  const int ntiles = (int)cdiv(iend - ibeg, 32);
+  const int ntiles = (int)cdiv(cdiv(iend - ibeg, TI), tstride);  // visited tiles
 
-  // query fragments (B operand): lane (r, h) holds q^[query][16s + 8h .. +8]
   bf16x8 qf[QT][KS];
+  int64_t qidx[QT];
 #pragma unroll
   for (int t = 0; t < QT; ++t) {
-    const int64_t qi = (int64_t)qt * WQ + (w * QT + t) * 32 + r;  // < nq_pad (zero rows)
-    const bf16x8* src = reinterpret_cast<const bf16x8*>(qh + qi * DP + 8 * h);
+    qidx[t] = (int64_t)qt * WQ + (w * QT + t) * 32 + r;  // < nq_pad (zero rows)
+    const bf16x8* src = reinterpret_cast<const bf16x8*>(qh + qidx[t] * DP + 8 * h);
 #pragma unroll
     for (int s = 0; s < KS; ++s) qf[t][s] = src[2 * s];
   }
-
   float ls[QT][M + 1];
   int li[QT][M + 1];
+  float tau[QT];
 #pragma unroll
-  for (int t = 0; t < QT; ++t)
+  for (int t = 0; t < QT; ++t) {
+    tau[t] = (MODE == 0 && tau_q && qidx[t] < nq) ? tau_q[qidx[t]] : -INFINITY;
 #pragma unroll
     for (int j = 0; j <= M; ++j) {
       ls[t][j] = -INFINITY;
       li[t][j] = -1;
     }
+  }
 
-  uint4 stage[LPT];
-  float nstage = 0.f;
-  auto load_tile = [&](int it) {
-    const int64_t i0 = ibeg + (int64_t)it * 32;
+  // HBM -> LDS (lane-linear destination, inverse-swizzled source)
+  auto issue_tile = [&](int it, int buf) {
+    const int64_t i0 = ibeg + (int64_t)it * tstride * TI;
+    typedef __attribute__((address_space(3))) void* lds_ptr;
 #pragma unroll
-    for (int u = 0; u < LPT; ++u) {
-      const int f = tid + u * NT;
-      const int row = f / CPR, cc = f % CPR;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (f < TILE_CHUNKS && i0 + row < iend)
-        v = *reinterpret_cast<const uint4*>(xbh + (i0 + row) * DP + cc * 8);
-      stage[u] = v;
+    for (int u = 0; u < GPT; ++u) {
+      const int p = u * NT + tid;
+      const int row = p / CPR, pc = p % CPR;
+      const int cc = pc ^ swz<CPR>(row);
+      int64_t gi = i0 + row;
+      gi = gi < nb ? gi : nb - 1;  // rows past the chunk are masked in the epilogue
+      __builtin_amdgcn_global_load_lds(xbh + gi * DP + cc * 8, (lds_ptr)(lds + buf * BUF + (u * NT + w * 64) * 8), 16,
+                                       0, 0);
     }
     if constexpr (L2) {
-      if (tid < 32) nstage = (i0 + tid < iend) ? xmeta[2 * (i0 + tid)] : 0.f;
-    }
-  };
-  auto store_tile = [&](int buf) {
-#pragma unroll
-    for (int u = 0; u < LPT; ++u) {
-      const int f = tid + u * NT;
-      if (f < TILE_CHUNKS) {
-        const int row = f / CPR, cc = f % CPR;
-        *reinterpret_cast<uint4*>(&lds[buf][row * DP + 8 * (cc ^ swz<CPR>(row))]) = stage[u];
+      if (w == 0) {
+        int64_t gi = i0 + lane;
+        gi = gi < nb ? gi : nb - 1;
+        __builtin_amdgcn_global_load_lds(xmeta + 2 * gi, (lds_ptr)(lds + buf * BUF + TI * DP), 4, 0, 0);
       }
     }
-    if constexpr (L2) {
-      if (tid < 32) lnorm[buf][tid] = nstage;
-    }
   };
 
-  if (ntiles > 0) {
-    load_tile(0);
-    store_tile(0);
-  }
-  __syncthreads();
-
+  if (ntiles > 0) issue_tile(0, 0);
   for (int it = 0; it < ntiles; ++it) {
     const int buf = it & 1;
-    if (it + 1 < ntiles) load_tile(it + 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // tile `it` landed; everyone is done with buffer buf^1
+    if (it + 1 < ntiles) issue_tile(it + 1, buf ^ 1);
 
-    f32x16 acc[QT];
+    const uint16_t* tile = lds + buf * BUF;
+    const float* lnorm = reinterpret_cast<const float*>(tile + TI * DP);
+    const int64_t i0 = ibeg + (int64_t)it * tstride * TI;
+    const int nvalid = (int)((iend - i0) < TI ? (iend - i0) : TI);
 #pragma unroll
-    for (int t = 0; t < QT; ++t)
-#pragma unroll
-      for (int g = 0; g < 16; ++g) acc[t][g] = 0.f;
-    const uint16_t* arow = &lds[buf][r * DP];
-    const int sw = swz<CPR>(r);
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const bf16x8 a = *reinterpret_cast<const bf16x8*>(arow + 8 * ((2 * s + h) ^ sw));
+    for (int st = 0; st < TI / 32; ++st) {
+      f32x16 acc[QT];
 #pragma unroll
       for (int t = 0; t < QT; ++t)
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[t][s], acc[t], 0, 0, 0);
-    }
-
-    // epilogue: screened scores -> per-lane candidate lists
-    const int64_t i0 = ibeg + (int64_t)it * 32;
-    const int nvalid = (int)((iend - i0) < 32 ? (iend - i0) : 32);
 #pragma unroll
-    for (int t = 0; t < QT; ++t) {
-      float sc[16];
-      float m = -INFINITY;
+        for (int g = 0; g < 16; ++g) acc[t][g] = 0.f;
+      const int row = 32 * st + r;
+      const uint16_t* arow = tile + row * DP;
+      const int sw = swz<CPR>(row);
 #pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        const int ir = (g & 3) + 8 * (g >> 2) + 4 * h;
-        float v = acc[t][g];
-        if constexpr (L2) v = fmaf(2.f, v, -lnorm[buf][ir]);
-        v = ir < nvalid ? v : -INFINITY;
-        sc[g] = v;
-        m = fmaxf(m, v);
+      for (int s = 0; s < KS; ++s) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(arow + 8 * ((2 * s + h) ^ sw));
+#pragma unroll
+        for (int t = 0; t < QT; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[t][s], acc[t], 0, 0, 0);
       }
-      if (__any(m > ls[t][M])) {
+      if constexpr (EPI == 2) {  // ablation: MFMA only
+#pragma unroll
+        for (int t = 0; t < QT; ++t) asm volatile("" ::"v"(acc[t][0]), "v"(acc[t][5]), "v"(acc[t][15]));
+        continue;
+      }
+      const bool full = nvalid >= 32 * (st + 1);
+#pragma unroll
+      for (int t = 0; t < QT; ++t) {
+        float sc[16];
+        float m4[4];
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
-          const int ir = (g & 3) + 8 * (g >> 2) + 4 * h;
-          if (__any(sc[g] > ls[t][M])) {
-            if (sc[g] > ls[t][M]) list_insert<M + 1>(ls[t], li[t], sc[g], (int)(i0 + ir));
+          const int ir = 32 * st + (g & 3) + 8 * (g >> 2) + 4 * h;
+          float v = acc[t][g];
+          if constexpr (L2) v = fmaf(2.f, v, -lnorm[ir]);
+          if (!full) v = ir < nvalid ? v : -INFINITY;
+          sc[g] = v;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) m4[j] = fmaxf(fmaxf(sc[4 * j], sc[4 * j + 1]), fmaxf(sc[4 * j + 2], sc[4 * j + 3]));
+        const float m = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
+        if constexpr (MODE == 1 || EPI == 1) {  // pre-pass (or ablation): lane maximum only
+          ls[t][0] = fmaxf(ls[t][0], m);
+          continue;
+        }
+        // rare path: descend only into 4-row groups that beat the threshold
+        if (__any(m > fmaxf(ls[t][M], tau[t]))) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (__any(m4[j] > fmaxf(ls[t][M], tau[t]))) {
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const int g = 4 * j + i;
+                const int ir = 32 * st + i + 8 * j + 4 * h;
+                const float thr = fmaxf(ls[t][M], tau[t]);
+                if (sc[g] > thr) list_insert<M + 1>(ls[t], li[t], sc[g], (int)(i0 + ir));
+              }
+            }
           }
         }
       }
     }
-
-    if (it + 1 < ntiles) store_tile(buf ^ 1);
-    __syncthreads();
   }
 
-  // candidates of this (query, chunk, half)
 #pragma unroll
   for (int t = 0; t < QT; ++t) {
-    const int64_t qi = (int64_t)qt * WQ + (w * QT + t) * 32 + r;
+    const int64_t qi = qidx[t];
     if (qi < nq) {
       const int64_t base = (qi * nch + c) * 2 + h;
+      if constexpr (MODE == 1) {
+        part_t[base] = ls[t][0];
+      } else {
 #pragma unroll
-      for (int j = 0; j < M; ++j) {
-        part_s[base * M + j] = ls[t][j];
-        part_i[base * M + j] = li[t][j];
+        for (int j = 0; j < M; ++j) {
+          part_s[base * M + j] = ls[t][j];
+          part_i[base * M + j] = li[t][j];
+        }
+        part_t[base] = ls[t][M];
       }
-      part_t[base] = ls[t][M];
     }
   }
+}
+
+// tau[q] = the R-th largest finite lane maximum of the pre-pass (or -inf if
+// there are fewer than R): R distinct items score at least this much, so it
+// never exceeds the query's global R-th best screened score.  One wave per
+// query; values in registers; R rounds of wave-argmax extraction.
+__global__ __launch_bounds__(256) void tau_select_kernel(const float* __restrict__ premax, int nvals, int R,
+                                                         int64_t nq, float* __restrict__ tau) {
+  const int lane = threadIdx.x & 63;
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= nq) return;
+  constexpr int VPL = 16;  // nvals <= 64 * VPL
+  float v[VPL];
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const int i = j * 64 + lane;
+    v[j] = i < nvals ? premax[q * nvals + i] : -INFINITY;
+  }
+  float last = -INFINITY;
+  for (int round = 0; round < R; ++round) {
+    float m = -INFINITY;
+    int mj = 0;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j)
+      if (v[j] > m) { m = v[j]; mj = j; }
+    float wm = m;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) wm = fmaxf(wm, __shfl_xor(wm, o, 64));
+    last = wm;
+    if (wm == -INFINITY) break;
+    // remove ONE occurrence: the lowest lane holding the maximum
+    const unsigned long long hit = __ballot(m == wm);
+    if (lane == __ffsll((long long)hit) - 1) {
+#pragma unroll
+      for (int j = 0; j < VPL; ++j)
+        if (j == mj) v[j] = -INFINITY;
+    }
+  }
+  if (lane == 0) tau[q] = last;
 }
 
 // ========================================================= merge/rescore ==
@@ -287,9 +349,9 @@ __device__ __forceinline__ int pow2ceil(int n) {
 __global__ __launch_bounds__(256) void merge_rescore_kernel(
     const float* __restrict__ part_s, const int* __restrict__ part_i, const float* __restrict__ part_t,
     int nch, int M, int KP, int k, int dp, const float* __restrict__ xq, const float* __restrict__ xb,
-    int d, int l2, const double* __restrict__ qmeta, const float* __restrict__ stats,
-    float* __restrict__ D, int64_t* __restrict__ I, double* __restrict__ S, int64_t id_offset,
-    int* __restrict__ fb_list, int* __restrict__ fb_count) {
+    int64_t nb, int d, int l2, const double* __restrict__ qmeta, const float* __restrict__ stats,
+    const float* __restrict__ tau_q, float* __restrict__ D, int64_t* __restrict__ I, double* __restrict__ S,
+    int64_t id_offset, int* __restrict__ fb_list, int* __restrict__ fb_count) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int qi = blockIdx.x, tid = threadIdx.x;
   const int U = nch * 2 * M, P = pow2ceil(U);
@@ -306,8 +368,10 @@ __global__ __launch_bounds__(256) void merge_rescore_kernel(
   const int* pi = part_i + (int64_t)qi * U;
   for (int i = tid; i < P; i += 256) {
     float v = i < U ? ps[i] : -INFINITY;
-    g[i] = (double)v;
-    id[i] = (i < U && v != -INFINITY) ? (int64_t)pi[i] : INT64_MAX;
+    const int64_t item = i < U ? (int64_t)pi[i] : -1;
+    const bool ok = v != -INFINITY && item >= 0 && item < nb;  // never dereference an unset slot
+    g[i] = ok ? (double)v : -INFINITY;
+    id[i] = ok ? item : INT64_MAX;
   }
   float th = -INFINITY;
   for (int i = tid; i < nch * 2; i += 256) th = fmaxf(th, part_t[(int64_t)qi * nch * 2 + i]);
@@ -326,7 +390,8 @@ __global__ __launch_bounds__(256) void merge_rescore_kernel(
   __syncthreads();
   const int V = s_valid;
   const int kp = KP < V ? KP : V;
-  const double theta = fmax((double)theta_lanes, kp < V ? g[kp] : -INFINITY);
+  double theta = fmax((double)theta_lanes, kp < V ? g[kp] : -INFINITY);
+  if (tau_q) theta = fmax(theta, (double)tau_q[qi]);  // items below the bound were never kept
 
   // exact rescoring of the top kp screened candidates
   for (int i = tid; i < P2; i += 256) {
@@ -483,10 +548,11 @@ __global__ void topk_merge_kernel(const double* __restrict__ Sp, const int64_t* 
 
 // ================================================================== plan ==
 struct FlatPlan {
-  bool exact_only;
+  bool exact_only, tau;
   int dp, qt, M, waves, wq, nqt, nch, U, KP;
-  int64_t nq_pad, chunk;
-  size_t off_qh, off_qmeta, off_ps, off_pi, off_pt, off_fbl, off_fbc, total;
+  int R, nch_pre, tstride;  // threshold pre-pass: bound rank, chunks, tile stride
+  int64_t nq_pad, chunk, chunk_pre;
+  size_t off_qh, off_qmeta, off_ps, off_pi, off_pt, off_fbl, off_fbc, off_tau, off_pre, total;
 };
 
 static int padded_dim(int d) {
@@ -513,14 +579,18 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
     return p;
   }
   p.waves = 4;
-  if (k <= 16) { p.M = 4; p.qt = 2; }
-  else if (k <= 64) { p.M = 8; p.qt = 2; }
+  // M: per-lane list length.  tau: sampled pre-pass bound on the R-th best
+  // screened score (R > k with margin), used while R stays small.
+  if (k <= 8) { p.M = 4; p.qt = 2; }
+  else if (k <= 24) { p.M = 8; p.qt = 1; }
   else { p.M = 16; p.qt = 1; }
+  p.R = k <= 8 ? 16 : 2 * k;
+  p.tau = k <= 24 && env_int("NRK_SCREEN_TAU", 1) != 0;
   if (p.dp == 256) p.qt = 1;
   p.wq = p.waves * 32 * p.qt;
   p.nqt = (int)cdiv(nq, p.wq);
   p.nq_pad = (int64_t)p.nqt * p.wq;
-  int target = env_int("NRK_SCREEN_WGS", 1536);
+  int target = env_int("NRK_SCREEN_WGS", 1024);
   int64_t nch = target / (p.nqt > 0 ? p.nqt : 1);
   if (nch < 1) nch = 1;
   int64_t max_by_u = 2048 / (2 * p.M);
@@ -528,7 +598,7 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
   int64_t max_by_len = cdiv(nb, 1024);
   if (nch > max_by_len) nch = max_by_len;
   if (nch < 1) nch = 1;
-  p.chunk = (int64_t)align_up((size_t)cdiv(nb, nch), 32);
+  p.chunk = (int64_t)align_up((size_t)cdiv(nb, nch), 64);
   p.nch = (int)cdiv(nb, p.chunk);
   p.U = p.nch * 2 * p.M;
   int kp = 2 * k > 32 ? 2 * k : 32;
@@ -542,6 +612,21 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
     p.total = 256;
     return p;
   }
+  // pre-pass: every tstride-th 64-item tile, chunks small enough that each
+  // query gets >= 8R short lane streams (their maxima are distinct items)
+  p.tstride = env_int("NRK_PRE_STRIDE", 8);
+  {
+    const int TI = 64;  // must equal screen_kernel TI
+    int64_t tiles = cdiv(nb, TI);
+    int64_t want = 4 * p.R;  // 2 lanes per chunk -> 8R streams
+    if (want > 512) want = 512;
+    int64_t maxc = cdiv(tiles, p.tstride);
+    if (want > maxc) want = maxc;
+    if (want < 1) want = 1;
+    p.chunk_pre = cdiv(cdiv(tiles, want), p.tstride) * p.tstride * TI;
+    p.nch_pre = (int)cdiv(nb, p.chunk_pre);
+    if (2 * p.nch_pre < p.R) p.tau = false;
+  }
   size_t off = 0;
   auto take = [&](size_t bytes) {
     size_t o = off;
@@ -549,6 +634,8 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
     return o;
   };
   p.off_fbc = take(16);
+  p.off_tau = take((size_t)nq * 4);
+  p.off_pre = take((size_t)nq * p.nch_pre * 2 * 4);
   p.off_qh = take((size_t)p.nq_pad * p.dp * 2);
   p.off_qmeta = take((size_t)nq * 4 * 8);
   p.off_ps = take((size_t)nq * p.U * 4);
@@ -559,27 +646,34 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
   return p;
 }
 
-typedef void (*screen_fn)(const uint16_t*, const uint16_t*, const float*, int64_t, int64_t, int64_t, int,
-                          int, float*, int*, float*);
+typedef void (*screen_fn)(const uint16_t*, const uint16_t*, const float*, int64_t, int64_t, int64_t, int, int, int,
+                          float*, int*, float*, const float*);
 
-template <int DP, int QT, int M, bool L2>
-static screen_fn pick2() {
-  return screen_kernel<DP, QT, M, 4, L2>;
+template <int DP, int QT, int M, bool L2, int MODE>
+static screen_fn pick3() {
+  if constexpr (DP == 128 && QT == 2 && M == 4 && !L2 && MODE == 0) {
+    const int epi = env_int("NRK_SCREEN_EPI", 0);
+    if (epi == 1) return screen_kernel<DP, QT, M, 4, L2, MODE, 1>;
+    if (epi == 2) return screen_kernel<DP, QT, M, 4, L2, MODE, 2>;
+  }
+  return screen_kernel<DP, QT, M, 4, L2, MODE>;
 }
 
 template <int DP, bool L2>
-static screen_fn pick1(int qt, int M) {
-  if (M == 4) return qt == 2 ? pick2<DP, 2, 4, L2>() : pick2<DP, 1, 4, L2>();
-  if (M == 8) return qt == 2 ? pick2<DP, 2, 8, L2>() : pick2<DP, 1, 8, L2>();
-  return pick2<DP, 1, 16, L2>();
+static screen_fn pick1(int qt, int M, bool pre) {
+  constexpr int Q2 = DP == 256 ? 1 : 2;  // DP=256 always runs one query tile per wave
+  if (pre) return qt == 2 ? pick3<DP, Q2, 1, L2, 1>() : pick3<DP, 1, 1, L2, 1>();
+  if (M == 4) return qt == 2 ? pick3<DP, Q2, 4, L2, 0>() : pick3<DP, 1, 4, L2, 0>();
+  if (M == 8) return pick3<DP, 1, 8, L2, 0>();
+  return pick3<DP, 1, 16, L2, 0>();
 }
 
-static screen_fn pick_screen(int dp, int qt, int M, bool l2) {
+static screen_fn pick_screen(int dp, int qt, int M, bool l2, bool pre) {
   switch (dp) {
-    case 32: return l2 ? pick1<32, true>(qt, M) : pick1<32, false>(qt, M);
-    case 64: return l2 ? pick1<64, true>(qt, M) : pick1<64, false>(qt, M);
-    case 128: return l2 ? pick1<128, true>(qt, M) : pick1<128, false>(qt, M);
-    case 256: return l2 ? pick1<256, true>(qt, M) : pick1<256, false>(qt, M);
+    case 32: return l2 ? pick1<32, true>(qt, M, pre) : pick1<32, false>(qt, M, pre);
+    case 64: return l2 ? pick1<64, true>(qt, M, pre) : pick1<64, false>(qt, M, pre);
+    case 128: return l2 ? pick1<128, true>(qt, M, pre) : pick1<128, false>(qt, M, pre);
+    case 256: return l2 ? pick1<256, true>(qt, M, pre) : pick1<256, false>(qt, M, pre);
   }
   return nullptr;
 }
@@ -673,18 +767,30 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
   int* pi = reinterpret_cast<int*>(w + p.off_pi);
   float* pt = reinterpret_cast<float*>(w + p.off_pt);
   int* fbl = reinterpret_cast<int*>(w + p.off_fbl);
+  float* tau = reinterpret_cast<float*>(w + p.off_tau);
+  float* pre = reinterpret_cast<float*>(w + p.off_pre);
 
   mark(0);
   hipLaunchKernelGGL(query_prepare_kernel, dim3((unsigned)cdiv(p.nq_pad, 4)), dim3(256), 0, st, xq, nq, p.nq_pad, d,
                      p.dp, qh, qmeta);
   NRK_CHECK_LAUNCH("query_prepare_kernel");
+  if (p.tau) {
+    screen_fn pf = pick_screen(p.dp, p.qt, p.M, l2 != 0, true);
+    if (!pf) return fail(NRK_EUNSUPPORTED, "knn_flat: no pre-pass kernel for dp=%d", p.dp);
+    hipLaunchKernelGGL(pf, dim3(p.nqt * p.nch_pre), dim3(p.waves * 64), 0, st, qh, xb_bf16, xb_meta, nq, nb,
+                       p.chunk_pre, p.nch_pre, p.nqt, p.tstride, nullptr, nullptr, pre, nullptr);
+    NRK_CHECK_LAUNCH("screen_kernel (pre-pass)");
+    hipLaunchKernelGGL(tau_select_kernel, dim3((unsigned)cdiv(nq, 4)), dim3(256), 0, st, pre, 2 * p.nch_pre, p.R, nq,
+                       tau);
+    NRK_CHECK_LAUNCH("tau_select_kernel");
+  }
 
-  screen_fn fn = pick_screen(p.dp, p.qt, p.M, l2 != 0);
+  screen_fn fn = pick_screen(p.dp, p.qt, p.M, l2 != 0, false);
   if (!fn) return fail(NRK_EUNSUPPORTED, "knn_flat: no screen kernel for dp=%d", p.dp);
   const int nblk = p.nqt * p.nch;
   mark(1);
-  hipLaunchKernelGGL(fn, dim3(nblk), dim3(p.waves * 64), 0, st, qh, xb_bf16, xb_meta, nq, nb, p.chunk, p.nch, p.nqt,
-                     ps, pi, pt);
+  hipLaunchKernelGGL(fn, dim3(nblk), dim3(p.waves * 64), 0, st, qh, xb_bf16, xb_meta, nq, nb, p.chunk, p.nch, p.nqt, 1,
+                     ps, pi, pt, p.tau ? tau : nullptr);
   NRK_CHECK_LAUNCH("screen_kernel");
 
   const int P = host_pow2ceil(p.U), P2 = host_pow2ceil(p.KP);
@@ -692,7 +798,7 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
   if (smem > 150 * 1024) return fail(NRK_EUNSUPPORTED, "knn_flat: merge needs %zu B LDS", smem);
   mark(2);
   hipLaunchKernelGGL(merge_rescore_kernel, dim3((unsigned)nq), dim3(256), smem, st, ps, pi, pt, p.nch, p.M, p.KP, k,
-                     p.dp, xq, xb, d, l2, qmeta, stats, D, I, S, id_offset, fbl, fbc);
+                     p.dp, xq, xb, nb, d, l2, qmeta, stats, p.tau ? tau : nullptr, D, I, S, id_offset, fbl, fbc);
   NRK_CHECK_LAUNCH("merge_rescore_kernel");
 
   mark(3);
