@@ -18,6 +18,8 @@
 #include <float.h>
 #include <math.h>
 
+#include <type_traits>
+
 #include "nrk_common.h"
 
 namespace nrk {
@@ -89,6 +91,8 @@ __device__ __forceinline__ int swz(int row) {
   if constexpr (CPR >= 16) return row & 15;
   else return (row / (16 / CPR)) & (CPR - 1);
 }
+
+__device__ __forceinline__ float fmax_ieee(float a, float b) { return __builtin_elementwise_maximum(a, b); }
 
 // Sorted (descending) insertion into a register list of N entries.  Ties keep
 // the resident entry first (it has the lower id: a lane scans ids upward).
@@ -226,42 +230,50 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
         for (int t = 0; t < QT; ++t) asm volatile("" ::"v"(acc[t][0]), "v"(acc[t][5]), "v"(acc[t][15]));
         continue;
       }
-      const bool full = nvalid >= 32 * (st + 1);
+      // Epilogue.  MASKED only for the (rare) partial last tile of a chunk: a
+      // wave-uniform branch, so full tiles carry no per-score selects.
+      auto epilogue = [&](auto masked_tag) {
+        constexpr bool MASKED = decltype(masked_tag)::value;
 #pragma unroll
-      for (int t = 0; t < QT; ++t) {
-        float sc[16];
-        float m4[4];
+        for (int t = 0; t < QT; ++t) {
+          float sc[16];
 #pragma unroll
-        for (int g = 0; g < 16; ++g) {
-          const int ir = 32 * st + (g & 3) + 8 * (g >> 2) + 4 * h;
-          float v = acc[t][g];
-          if constexpr (L2) v = fmaf(2.f, v, -lnorm[ir]);
-          if (!full) v = ir < nvalid ? v : -INFINITY;
-          sc[g] = v;
-        }
+          for (int g = 0; g < 16; ++g) {
+            const int ir = 32 * st + (g & 3) + 8 * (g >> 2) + 4 * h;
+            float v = acc[t][g];
+            if constexpr (L2) v = fmaf(2.f, v, -lnorm[ir]);
+            if constexpr (MASKED) v = ir < nvalid ? v : -INFINITY;
+            sc[g] = v;
+          }
+          // IEEE maximum (v_maximum3_f32): no canonicalising moves on MFMA outputs
+          float m4[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) m4[j] = fmaxf(fmaxf(sc[4 * j], sc[4 * j + 1]), fmaxf(sc[4 * j + 2], sc[4 * j + 3]));
-        const float m = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
-        if constexpr (MODE == 1 || EPI == 1) {  // pre-pass (or ablation): lane maximum only
-          ls[t][0] = fmaxf(ls[t][0], m);
-          continue;
-        }
-        // rare path: descend only into 4-row groups that beat the threshold
-        if (__any(m > fmaxf(ls[t][M], tau[t]))) {
+          for (int j = 0; j < 4; ++j)
+            m4[j] = fmax_ieee(fmax_ieee(sc[4 * j], sc[4 * j + 1]), fmax_ieee(sc[4 * j + 2], sc[4 * j + 3]));
+          const float m = fmax_ieee(fmax_ieee(m4[0], m4[1]), fmax_ieee(m4[2], m4[3]));
+          if constexpr (MODE == 1 || EPI == 1) {  // pre-pass (or ablation): lane maximum only
+            ls[t][0] = fmax_ieee(ls[t][0], m);
+            continue;
+          }
+          // rare path: descend only into 4-row groups that beat the threshold
+          if (__any(m > fmaxf(ls[t][M], tau[t]))) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            if (__any(m4[j] > fmaxf(ls[t][M], tau[t]))) {
+            for (int j = 0; j < 4; ++j) {
+              if (__any(m4[j] > fmaxf(ls[t][M], tau[t]))) {
 #pragma unroll
-              for (int i = 0; i < 4; ++i) {
-                const int g = 4 * j + i;
-                const int ir = 32 * st + i + 8 * j + 4 * h;
-                const float thr = fmaxf(ls[t][M], tau[t]);
-                if (sc[g] > thr) list_insert<M + 1>(ls[t], li[t], sc[g], (int)(i0 + ir));
+                for (int i = 0; i < 4; ++i) {
+                  const int g = 4 * j + i;
+                  const int ir = 32 * st + i + 8 * j + 4 * h;
+                  const float thr = fmaxf(ls[t][M], tau[t]);
+                  if (sc[g] > thr) list_insert<M + 1>(ls[t], li[t], sc[g], (int)(i0 + ir));
+                }
               }
             }
           }
         }
-      }
+      };
+      if (nvalid >= 32 * (st + 1)) epilogue(std::false_type{});
+      else epilogue(std::true_type{});
     }
   }
 
@@ -434,6 +446,149 @@ __global__ __launch_bounds__(256) void merge_rescore_kernel(
     D[o] = valid ? (float)s : (l2 ? FLT_MAX : -FLT_MAX);
     I[o] = valid ? id2[j] + id_offset : -1;
     if (S) S[o] = s;
+  }
+}
+
+// Wave-per-query variant (used when the pre-pass bound is active, so only a
+// few dozen union entries are valid): compact the valid entries with
+// ballot/mbcnt into this wave's LDS slice, select the top KP by rank
+// counting, rescore them exactly, rank again, certify.  No block barriers.
+// Queries whose union holds more than WCAP valid entries defer to the
+// fallback list (exact scan), which keeps the result exact.
+template <int WCAP>
+__global__ __launch_bounds__(256) void merge_rescore_wave_kernel(
+    const float* __restrict__ part_s, const int* __restrict__ part_i, const float* __restrict__ part_t, int nch,
+    int M, int KP, int k, int dp, const float* __restrict__ xq, const float* __restrict__ xb, int64_t nb, int d, int l2,
+    const double* __restrict__ qmeta, const float* __restrict__ stats, const float* __restrict__ tau_q,
+    float* __restrict__ D, int64_t* __restrict__ I, double* __restrict__ S, int64_t id_offset,
+    int* __restrict__ fb_list, int* __restrict__ fb_count, int nq) {
+  __shared__ float cs[4][WCAP];   // screened score of compacted candidates
+  __shared__ int ci[4][WCAP];     // their ids
+  __shared__ double es[4][64];    // exact goodness of the rescored top-KP
+  __shared__ int64_t ei[4][64];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int qi = blockIdx.x * 4 + wv;
+  if (qi >= nq) return;
+  const int U = nch * 2 * M;
+  const float* ps = part_s + (int64_t)qi * U;
+  const int* pi = part_i + (int64_t)qi * U;
+
+  // 1. compact valid entries
+  int V = 0;
+  bool overflow = false;
+  for (int base = 0; base < U; base += 64) {
+    const int i = base + lane;
+    const float v = i < U ? ps[i] : -INFINITY;
+    const int item = i < U ? pi[i] : -1;
+    const bool ok = v != -INFINITY && item >= 0 && item < nb;
+    const unsigned long long bal = __ballot(ok);
+    const int pos = V + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+    if (ok && pos < WCAP) {
+      cs[wv][pos] = v;
+      ci[wv][pos] = item;
+    }
+    V += __popcll(bal);
+  }
+  if (V > WCAP) overflow = true;
+  float th = -INFINITY;
+  for (int i = lane; i < nch * 2; i += 64) th = fmaxf(th, part_t[(int64_t)qi * nch * 2 + i]);
+  th = wave_max(th);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int Vc = V < WCAP ? V : WCAP;
+
+  // 2. rank each candidate (screened score desc, lower id first); keep top kp
+  const int kp = KP < Vc ? KP : Vc;
+  double theta = fmax((double)th, tau_q ? (double)tau_q[qi] : -INFINITY);
+  int my_rank[WCAP / 64];
+#pragma unroll
+  for (int u = 0; u < WCAP / 64; ++u) {
+    const int e = u * 64 + lane;
+    int rk = 1 << 30;
+    if (e < Vc) {
+      const float ve = cs[wv][e];
+      const int ie = ci[wv][e];
+      rk = 0;
+      for (int j = 0; j < Vc; ++j) {
+        const float vj = cs[wv][j];
+        rk += (vj > ve) || (vj == ve && ci[wv][j] < ie);
+      }
+    }
+    my_rank[u] = rk;
+  }
+  // theta gets the (kp+1)-th screened score when candidates were cut
+  float cut = -INFINITY;
+#pragma unroll
+  for (int u = 0; u < WCAP / 64; ++u)
+    if (my_rank[u] == kp) cut = cs[wv][u * 64 + lane];
+  theta = fmax(theta, (double)wave_max(cut));
+
+  // 3. exact rescoring of the kp survivors -> es/ei[rank]
+  const float* q = xq + (int64_t)qi * d;
+#pragma unroll
+  for (int u = 0; u < WCAP / 64; ++u) {
+    const int rk = my_rank[u];
+    if (rk < kp) {
+      const int64_t item = ci[wv][u * 64 + lane];
+      const double sc = exact_score(q, xb + item * d, d, l2 != 0);
+      es[wv][rk] = l2 ? -sc : sc;
+      ei[wv][rk] = item;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+  // 4. exact ranks (kp <= 64: one entry per lane)
+  int er = 1 << 30;
+  double eg = -INFINITY;
+  int64_t eid = INT64_MAX;
+  if (lane < kp) {
+    eg = es[wv][lane];
+    eid = ei[wv][lane];
+    er = 0;
+    for (int j = 0; j < kp; ++j) {
+      const double gj = es[wv][j];
+      er += better(gj, ei[wv][j], eg, eid);
+    }
+  }
+  // k-th exact goodness for the certificate
+  double kth = -INFINITY;
+  {
+    double cand = (er == k - 1) ? eg : -INFINITY;
+    for (int o = 32; o > 0; o >>= 1) cand = fmax(cand, __shfl_xor(cand, o, 64));
+    kth = cand;
+  }
+  bool ok = !overflow && kp >= k;
+  if (ok && theta != -INFINITY) {
+    const double nqh = qmeta[4 * qi + 0], nrq = qmeta[4 * qi + 1], qn2 = qmeta[4 * qi + 2];
+    const double Xh = stats[0], R = stats[1], NX = stats[2];
+    const double gam = (double)dp * 0x1p-22;
+    const double bip = gam * nqh * Xh + nqh * R + nrq * Xh + nrq * R;
+    if (!l2) {
+      const double lim = theta + bip;
+      ok = kth - lim > 1e-12 * (fabs(lim) + fabs(kth));
+    } else {
+      const double B = 2.0 * bip + 0x1p-21 * (NX + nqh * Xh);
+      const double lo = qn2 - theta - B;
+      ok = lo - (-kth) > 1e-12 * (fabs(lo) + fabs(kth) + qn2);
+    }
+  }
+  if (lane == 0 && !ok) fb_list[atomicAdd(fb_count, 1)] = qi;
+  // 5. outputs: lane with exact rank j writes slot j
+  if (er < k) {
+    const int64_t o = (int64_t)qi * k + er;
+    const double sc = l2 ? -eg : eg;
+    D[o] = (float)sc;
+    I[o] = eid + id_offset;
+    if (S) S[o] = sc;
+  }
+  for (int j = kp + lane; j < k; j += 64) {  // fewer than k candidates: pad (the fallback rewrites)
+    const int64_t o = (int64_t)qi * k + j;
+    D[o] = l2 ? FLT_MAX : -FLT_MAX;
+    I[o] = -1;
+    if (S) S[o] = l2 ? DBL_MAX : -DBL_MAX;
   }
 }
 
@@ -793,13 +948,20 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
                      ps, pi, pt, p.tau ? tau : nullptr);
   NRK_CHECK_LAUNCH("screen_kernel");
 
-  const int P = host_pow2ceil(p.U), P2 = host_pow2ceil(p.KP);
-  const size_t smem = (size_t)P * 16 + (size_t)P2 * 16 + (size_t)d * 4;
-  if (smem > 150 * 1024) return fail(NRK_EUNSUPPORTED, "knn_flat: merge needs %zu B LDS", smem);
   mark(2);
-  hipLaunchKernelGGL(merge_rescore_kernel, dim3((unsigned)nq), dim3(256), smem, st, ps, pi, pt, p.nch, p.M, p.KP, k,
-                     p.dp, xq, xb, nb, d, l2, qmeta, stats, p.tau ? tau : nullptr, D, I, S, id_offset, fbl, fbc);
-  NRK_CHECK_LAUNCH("merge_rescore_kernel");
+  if (p.tau && p.KP <= 64 && env_int("NRK_MERGE_WAVE", 0)) {
+    hipLaunchKernelGGL(merge_rescore_wave_kernel<256>, dim3((unsigned)cdiv(nq, 4)), dim3(256), 0, st, ps, pi, pt,
+                       p.nch, p.M, p.KP, k, p.dp, xq, xb, nb, d, l2, qmeta, stats, tau, D, I, S, id_offset, fbl, fbc,
+                       (int)nq);
+    NRK_CHECK_LAUNCH("merge_rescore_wave_kernel");
+  } else {
+    const int P = host_pow2ceil(p.U), P2 = host_pow2ceil(p.KP);
+    const size_t smem = (size_t)P * 16 + (size_t)P2 * 16 + (size_t)d * 4;
+    if (smem > 150 * 1024) return fail(NRK_EUNSUPPORTED, "knn_flat: merge needs %zu B LDS", smem);
+    hipLaunchKernelGGL(merge_rescore_kernel, dim3((unsigned)nq), dim3(256), smem, st, ps, pi, pt, p.nch, p.M, p.KP, k,
+                       p.dp, xq, xb, nb, d, l2, qmeta, stats, p.tau ? tau : nullptr, D, I, S, id_offset, fbl, fbc);
+    NRK_CHECK_LAUNCH("merge_rescore_kernel");
+  }
 
   mark(3);
   int rc = exact_launch(xq, nq, xb, nb, d, k, l2, fbl, fbc, 256, D, I, S, id_offset, st);
