@@ -192,14 +192,21 @@ def bench_din(args, rank, world, dev):
     rows = args.din_rows
     hist, tgt, lab = synthetic_click_rows(rows, n_items, L, seed=7 + rank, device=dev)
     model = DIN(d, A, F, 0.36).to(dev)
-    opt = torch.optim.Adam(model.parameters(), lr=1.62e-3, weight_decay=8.96e-5)
     crit = torch.nn.BCEWithLogitsLoss()
     B = args.din_batch
     perm = torch.randperm(rows, device=dev)
     nbatch = rows // B
+    graphed = world == 1 and not args.din_eager
+    opt = torch.optim.Adam(model.parameters(), lr=1.62e-3, weight_decay=8.96e-5, capturable=graphed)
+    if graphed:
+        from newsrecommend_amd.din import GraphedTrainStep
+
+        trainer = GraphedTrainStep(model, opt, crit, table, hist, tgt, lab, B)
 
     def step(s):
         idx = perm[(s % nbatch) * B:(s % nbatch + 1) * B]
+        if graphed:
+            return trainer.step(idx)
         logits = model.forward_ids(table, tgt[idx], hist[idx])
         loss = crit(logits, lab[idx])
         opt.zero_grad(set_to_none=True)
@@ -221,12 +228,18 @@ def bench_din(args, rank, world, dev):
     for s in range(args.warmup):
         step(s)
     barrier(world)
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        loss = step(args.warmup + s)
+    barrier(world)
+    el = max_over_ranks(time.perf_counter() - t0, world, dev)
+    # attention kernel times: a few extra eager steps with event brackets
     with KernelTimer() as kt:
-        t0 = time.perf_counter()
-        for s in range(args.steps):
-            loss = step(args.warmup + s)
-        barrier(world)
-        el = max_over_ranks(time.perf_counter() - t0, world, dev)
+        for s in range(3):
+            lg = model.forward_ids(table, tgt[perm[:B]], hist[perm[:B]])
+            crit(lg, lab[perm[:B]]).backward()
+        torch.cuda.synchronize()
+    model.zero_grad(set_to_none=True)
     sps = B * args.steps * world / el
     fwd_ms, bwd_ms = kt.mean_ms("fwd"), kt.mean_ms("bwd")
     fwd_bytes = B * (L * d * 2 + 4 * L + 4 * A + 4 * d + 4 * L)
@@ -237,7 +250,7 @@ def bench_din(args, rank, world, dev):
         "metric": "DIN train samples/s", "value": sps, "unit": "samples/s", "ms_per_step": el / args.steps * 1e3,
         "config": {"workload": "configs[2]: DIN train bf16, 5M synthetic click rows, seq_len=50, emb_dim=128",
                    "rows": rows, "items": n_items, "batch": B, "attn_units": A, "fc_units": F,
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}", "step": "hip graph" if graphed else "eager"},
         "final_loss": float(loss.item()),
         "kernels_ms": {"attn_fwd": fwd_ms, "attn_bwd+reduce": bwd_ms},
         "roofline_fwd": {"bound": "hbm", "achieved": fwd_gbs, "peak": HBM_GBS, "unit": "GB/s",
@@ -300,6 +313,7 @@ def main():
     ap.add_argument("--din-items", type=int, default=2_000_000)
     ap.add_argument("--din-batch", type=int, default=4096)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--din-eager", action="store_true", help="no HIP-graph capture of the DIN train step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 

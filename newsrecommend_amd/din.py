@@ -298,3 +298,62 @@ def evaluate(model, loader, criterion, device, k):
             ndcg_sum += ndcg_from_logits(logits, lab, seg, nu, k).sum()
             users += nu
     return (loss_sum / users).item(), (ndcg_sum / users).item()
+
+
+class GraphedTrainStep:
+    """One DIN training step (DIN.py:143-151: forward, BCE, backward,
+    clip_grad_norm_, optimizer step) captured once into a HIP graph and
+    replayed per batch.  Id form only: the embedding table stays resident on
+    the device and each replay gathers its batch rows by index inside the
+    graph, so a step costs one small index copy plus one graph launch.
+
+    optimizer must be created with capturable=True (Adam/AdamW)."""
+
+    def __init__(self, model, optimizer, criterion, table, hist_ids, target_ids, labels, batch_size, clip=1.0,
+                 warmup=3):
+        self.model, self.opt, self.crit = model, optimizer, criterion
+        self.table, self.hist_all, self.tgt_all, self.lab_all = table, hist_ids, target_ids, labels
+        self.B, self.clip = batch_size, clip
+        dev = table.device
+        self.idx = torch.zeros(batch_size, dtype=torch.long, device=dev)
+        model.train()
+        # warm-up and capture execute real steps: snapshot the model so that
+        # they leave no trace (parameters, BN statistics, optimizer moments)
+        snap = {k: v.detach().clone() for k, v in model.state_dict().items()}
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):  # warm-up on a side stream (allocator, lazy optimizer state)
+            for _ in range(max(warmup, 1)):
+                self._body()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        self.opt.zero_grad(set_to_none=True)
+        with torch.cuda.graph(self.graph):
+            self.loss = self._body()
+        with torch.no_grad():
+            for k, v in model.state_dict().items():
+                v.copy_(snap[k])
+            for st in self.opt.state.values():  # Adam(capturable): moments and step restart at 0
+                for v in st.values():
+                    if torch.is_tensor(v):
+                        v.zero_()
+            for p in model.parameters():
+                if p.grad is not None:
+                    p.grad.zero_()
+
+    def _body(self):
+        h = self.hist_all.index_select(0, self.idx)
+        t = self.tgt_all.index_select(0, self.idx)
+        y = self.lab_all.index_select(0, self.idx)
+        loss = self.crit(self.model.forward_ids(self.table, t, h), y)
+        loss.backward()
+        nn.utils.clip_grad_norm_(self.model.parameters(), self.clip)
+        self.opt.step()
+        self.opt.zero_grad(set_to_none=False)
+        return loss
+
+    def step(self, batch_index: torch.Tensor):
+        """Run one step on rows `batch_index` (device int64, length batch_size); returns the device loss."""
+        self.idx.copy_(batch_index, non_blocking=True)
+        self.graph.replay()
+        return self.loss
