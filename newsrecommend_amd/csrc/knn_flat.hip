@@ -94,6 +94,38 @@ __device__ __forceinline__ int swz(int row) {
 
 __device__ __forceinline__ float fmax_ieee(float a, float b) { return __builtin_elementwise_maximum(a, b); }
 
+// Buffer-descriptor LDS-DMA.  The AMDGPU buffer-resource builtins exist only in
+// the device compilation pass; the host pass (which only needs the kernel
+// stubs) silently drops every kernel whose body names them.
+struct BufRsrc {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __amdgpu_buffer_rsrc_t r;
+#endif
+};
+__device__ __forceinline__ BufRsrc make_rsrc(const void* base, int bytes) {
+  BufRsrc b;
+#if defined(__HIP_DEVICE_COMPILE__)
+  b.r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
+#else
+  (void)base;
+  (void)bytes;
+#endif
+  return b;
+}
+#if defined(__HIP_DEVICE_COMPILE__)
+#define NRK_BUFFER_LOAD_LDS(SIZE)                                                                         \
+  __device__ __forceinline__ void buffer_load_lds##SIZE(const BufRsrc& b, void* lds_dst, int vo, int so) { \
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(b.r, (__attribute__((address_space(3))) void*)lds_dst, SIZE, vo, \
+                                             so, 0, 0);                                                  \
+  }
+#else
+#define NRK_BUFFER_LOAD_LDS(SIZE) \
+  __device__ __forceinline__ void buffer_load_lds##SIZE(const BufRsrc&, void*, int, int) {}
+#endif
+NRK_BUFFER_LOAD_LDS(16)
+NRK_BUFFER_LOAD_LDS(4)
+#undef NRK_BUFFER_LOAD_LDS
+
 // Sorted (descending) insertion into a register list of N entries.  Ties keep
 // the resident entry first (it has the lower id: a lane scans ids upward).
 template <int N>
@@ -174,38 +206,42 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
     }
   }
 
-  // HBM -> LDS (lane-linear destination, inverse-swizzled source)
-  auto issue_tile = [&](int it, int buf) {
-    const int64_t i0 = ibeg + (int64_t)it * tstride * TI;
-    typedef __attribute__((address_space(3))) void* lds_ptr;
+  // HBM -> LDS through chunk-relative buffer descriptors: rows past the chunk
+  // fall outside num_records and read as 0 (masked in the epilogue); each
+  // lane's inverse-swizzled 32-bit offset is fixed, only the scalar tile
+  // offset changes, so staging costs no per-tile vector address math.
+  typedef __attribute__((address_space(3))) void* lds_ptr;
+  const int64_t cnt = iend - ibeg > 0 ? iend - ibeg : 0;
+  const BufRsrc xrs = make_rsrc(xbh + ibeg * DP, (int)(cnt * DP * 2));
+  const BufRsrc nrs = make_rsrc(xmeta + 2 * ibeg, (int)(cnt * 8));
+  int voff[GPT];
 #pragma unroll
-    for (int u = 0; u < GPT; ++u) {
-      const int p = u * NT + tid;
-      const int row = p / CPR, pc = p % CPR;
-      const int cc = pc ^ swz<CPR>(row);
-      int64_t gi = i0 + row;
-      gi = gi < nb ? gi : nb - 1;  // rows past the chunk are masked in the epilogue
-      __builtin_amdgcn_global_load_lds(xbh + gi * DP + cc * 8, (lds_ptr)(lds + buf * BUF + (u * NT + w * 64) * 8), 16,
-                                       0, 0);
-    }
+  for (int u = 0; u < GPT; ++u) {
+    const int p = u * NT + tid;
+    const int row = p / CPR, pc = p % CPR;
+    voff[u] = row * DP * 2 + 16 * (pc ^ swz<CPR>(row));
+  }
+  auto issue_tile = [&](int it, auto buf_c) {
+    constexpr int buf = decltype(buf_c)::value;
+    const int soff = it * tstride * TI * DP * 2;
+#pragma unroll
+    for (int u = 0; u < GPT; ++u)
+      buffer_load_lds16(xrs, lds + buf * BUF + (u * NT + w * 64) * 8, voff[u], soff);
     if constexpr (L2) {
-      if (w == 0) {
-        int64_t gi = i0 + lane;
-        gi = gi < nb ? gi : nb - 1;
-        __builtin_amdgcn_global_load_lds(xmeta + 2 * gi, (lds_ptr)(lds + buf * BUF + TI * DP), 4, 0, 0);
-      }
+      if (w == 0)
+        buffer_load_lds4(nrs, lds + buf * BUF + TI * DP, lane * 8, it * tstride * TI * 8);
     }
   };
 
-  if (ntiles > 0) issue_tile(0, 0);
-  for (int it = 0; it < ntiles; ++it) {
-    const int buf = it & 1;
+  // one 64-item tile (buffer index is a compile-time constant: immediate LDS offsets)
+  auto tile = [&](int it, auto buf_c) {
+    constexpr int buf = decltype(buf_c)::value;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // tile `it` landed; everyone is done with buffer buf^1
-    if (it + 1 < ntiles) issue_tile(it + 1, buf ^ 1);
+    __syncthreads();  // tile `it` landed; everyone is done with the other buffer
+    if (it + 1 < ntiles) issue_tile(it + 1, std::integral_constant<int, buf ^ 1>{});
 
-    const uint16_t* tile = lds + buf * BUF;
-    const float* lnorm = reinterpret_cast<const float*>(tile + TI * DP);
+    const uint16_t* tl = lds + buf * BUF;
+    const float* lnorm = reinterpret_cast<const float*>(tl + TI * DP);
     const int64_t i0 = ibeg + (int64_t)it * tstride * TI;
     const int nvalid = (int)((iend - i0) < TI ? (iend - i0) : TI);
 #pragma unroll
@@ -216,7 +252,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
 #pragma unroll
         for (int g = 0; g < 16; ++g) acc[t][g] = 0.f;
       const int row = 32 * st + r;
-      const uint16_t* arow = tile + row * DP;
+      const uint16_t* arow = tl + row * DP;
       const int sw = swz<CPR>(row);
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
@@ -275,6 +311,12 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
       if (nvalid >= 32 * (st + 1)) epilogue(std::false_type{});
       else epilogue(std::true_type{});
     }
+  };
+
+  if (ntiles > 0) issue_tile(0, std::integral_constant<int, 0>{});
+  for (int it = 0; it < ntiles; it += 2) {
+    tile(it, std::integral_constant<int, 0>{});
+    if (it + 1 < ntiles) tile(it + 1, std::integral_constant<int, 1>{});
   }
 
 #pragma unroll
@@ -753,6 +795,9 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
   int64_t max_by_len = cdiv(nb, 1024);
   if (nch > max_by_len) nch = max_by_len;
   if (nch < 1) nch = 1;
+  // buffer descriptors address a chunk with 32-bit offsets: keep chunks < 1 GiB
+  const int64_t min_nch = cdiv(nb * (int64_t)p.dp * 2, (int64_t)1 << 30);
+  if (nch < min_nch) nch = min_nch;
   p.chunk = (int64_t)align_up((size_t)cdiv(nb, nch), 64);
   p.nch = (int)cdiv(nb, p.chunk);
   p.U = p.nch * 2 * p.M;
@@ -774,6 +819,8 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
     const int TI = 64;  // must equal screen_kernel TI
     int64_t tiles = cdiv(nb, TI);
     int64_t want = 4 * p.R;  // 2 lanes per chunk -> 8R streams
+    const int64_t min_pre = cdiv(nb * (int64_t)p.dp * 2, (int64_t)1 << 30);
+    if (want < min_pre) want = min_pre;
     if (want > 512) want = 512;
     int64_t maxc = cdiv(tiles, p.tstride);
     if (want > maxc) want = maxc;
@@ -914,7 +961,7 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
   }
   NRK_CHECK_ARG(xb_bf16 && xb_meta && stats, "knn_flat: index not prepared (null bf16/meta/stats)");
   auto mark = [&](int i) {
-    if (stage_events) hipEventRecord((hipEvent_t)stage_events[i], st);
+    if (stage_events) (void)hipEventRecord((hipEvent_t)stage_events[i], st);
   };
   uint16_t* qh = reinterpret_cast<uint16_t*>(w + p.off_qh);
   double* qmeta = reinterpret_cast<double*>(w + p.off_qmeta);
