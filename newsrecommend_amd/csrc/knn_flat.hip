@@ -398,6 +398,29 @@ __device__ __forceinline__ int pow2ceil(int n) {
   return p;
 }
 
+// Fallback bookkeeping shared by the merge kernels and the tiled fallback.
+// An uncertified query gets a slot s (list[s] = query) and, for s < slots, the
+// merge's exact k-th (goodness, id): every item of the true top-k is at least
+// that good, so the fallback only has to collect those.
+struct FbState {
+  int* list;        // [nq] queries, in slot order
+  int* count;       // [0] = slots used, [1] = overflow count
+  int slots;        // slots with candidate storage
+  double* thr_g;    // [slots]
+  int64_t* thr_i;   // [slots]
+  int* n;           // [slots] candidates seen (may exceed cap)
+  int force;        // testing: certify nothing
+  __device__ void push(int qi, double g, int64_t i) const {
+    const int s = atomicAdd(count, 1);
+    list[s] = qi;
+    if (s < slots) {
+      thr_g[s] = g;
+      thr_i[s] = i;
+      n[s] = 0;
+    }
+  }
+};
+
 // One 256-thread workgroup per query.  Dynamic LDS: P doubles + P int64 (the
 // union), P2 doubles + P2 int64 (rescored), d floats (query), reductions.
 __global__ __launch_bounds__(256) void merge_rescore_kernel(
@@ -405,7 +428,7 @@ __global__ __launch_bounds__(256) void merge_rescore_kernel(
     int nch, int M, int KP, int k, int dp, const float* __restrict__ xq, const float* __restrict__ xb,
     int64_t nb, int d, int l2, const double* __restrict__ qmeta, const float* __restrict__ stats,
     const float* __restrict__ tau_q, float* __restrict__ D, int64_t* __restrict__ I, double* __restrict__ S,
-    int64_t id_offset, int* __restrict__ fb_list, int* __restrict__ fb_count) {
+    int64_t id_offset, FbState fb) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int qi = blockIdx.x, tid = threadIdx.x;
   const int U = nch * 2 * M, P = pow2ceil(U);
@@ -479,7 +502,8 @@ __global__ __launch_bounds__(256) void merge_rescore_kernel(
         ok = lo - (-kth) > 1e-12 * (fabs(lo) + fabs(kth) + qn2);
       }
     }
-    if (!ok) fb_list[atomicAdd(fb_count, 1)] = qi;
+    if (fb.force) ok = false;
+    if (!ok) fb.push(qi, kp >= k ? g2[k - 1] : -INFINITY, kp >= k ? id2[k - 1] : (int64_t)-1);
   }
   for (int j = tid; j < k; j += 256) {
     const int64_t o = (int64_t)qi * k + j;
@@ -502,8 +526,8 @@ __global__ __launch_bounds__(256) void merge_rescore_wave_kernel(
     const float* __restrict__ part_s, const int* __restrict__ part_i, const float* __restrict__ part_t, int nch,
     int M, int KP, int k, int dp, const float* __restrict__ xq, const float* __restrict__ xb, int64_t nb, int d, int l2,
     const double* __restrict__ qmeta, const float* __restrict__ stats, const float* __restrict__ tau_q,
-    float* __restrict__ D, int64_t* __restrict__ I, double* __restrict__ S, int64_t id_offset,
-    int* __restrict__ fb_list, int* __restrict__ fb_count, int nq) {
+    float* __restrict__ D, int64_t* __restrict__ I, double* __restrict__ S, int64_t id_offset, FbState fb,
+    int nq) {
   __shared__ float cs[4][WCAP];   // screened score of compacted candidates
   __shared__ int ci[4][WCAP];     // their ids
   __shared__ double es[4][64];    // exact goodness of the rescored top-KP
@@ -617,7 +641,10 @@ __global__ __launch_bounds__(256) void merge_rescore_wave_kernel(
       ok = lo - (-kth) > 1e-12 * (fabs(lo) + fabs(kth) + qn2);
     }
   }
-  if (lane == 0 && !ok) fb_list[atomicAdd(fb_count, 1)] = qi;
+  if (fb.force) ok = false;
+  const unsigned long long kb = __ballot(er == k - 1);
+  const int64_t kid = kb ? __shfl(eid, __ffsll((long long)kb) - 1, 64) : (int64_t)-1;
+  if (lane == 0 && !ok) fb.push(qi, kb ? kth : -INFINITY, kid);
   // 5. outputs: lane with exact rank j writes slot j
   if (er < k) {
     const int64_t o = (int64_t)qi * k + er;
@@ -704,6 +731,91 @@ __global__ __launch_bounds__(256) void exact_topk_kernel(
   }
 }
 
+// ========================================================= tiled fallback ==
+// Chip-wide fp64 scan for the fallback slots: 64-row fp32 tiles staged in LDS
+// (row stride d+1, so lane = row reads are bank-conflict free), each wave
+// scores its tile against slots w, w+4, ... (the query pointer is wave-uniform)
+// with exact_score, and keeps the items at least as good as the slot's
+// threshold.  Cost = slots x nb x d fp64 FMA, spread over every CU.
+constexpr int FB_TR = 64;
+
+__global__ __launch_bounds__(256) void fallback_scan_kernel(const float* __restrict__ xq,
+                                                            const float* __restrict__ xb, int64_t nb, int d,
+                                                            int l2, FbState fb, double* __restrict__ cand_g,
+                                                            int64_t* __restrict__ cand_i, int cap) {
+  extern __shared__ float tile[];
+  const int c0 = *fb.count;
+  const int cnt = c0 < fb.slots ? c0 : fb.slots;
+  if (cnt == 0) return;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int ds = d + 1;
+  const int64_t ntiles = cdiv(nb, (int64_t)FB_TR);
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int64_t r0 = t * FB_TR;
+    const int rows = nb - r0 < FB_TR ? (int)(nb - r0) : FB_TR;
+    __syncthreads();
+    for (int e = threadIdx.x; e < rows * d; e += 256) {
+      const int r = e / d;
+      tile[r * ds + (e - r * d)] = xb[r0 * d + e];
+    }
+    __syncthreads();
+    if (lane >= rows) continue;
+    const float* row = tile + lane * ds;
+    const int64_t item = r0 + lane;
+    for (int s = wv; s < cnt; s += 4) {
+      const int qi = fb.list[s];
+      const double acc = exact_score(xq + (int64_t)qi * d, row, d, l2 != 0);
+      const double gv = l2 ? -acc : acc;
+      const int64_t ti = fb.thr_i[s];
+      if (item == ti || better(gv, item, fb.thr_g[s], ti)) {
+        const int pos = atomicAdd(&fb.n[s], 1);
+        if (pos < cap) {
+          cand_g[(int64_t)s * cap + pos] = gv;
+          cand_i[(int64_t)s * cap + pos] = item;
+        }
+      }
+    }
+  }
+}
+
+// Per slot: sort the collected candidates and write the top k.  Slots whose
+// list overflowed (or that have no storage) go to the overflow list, which the
+// block-per-query exact kernel finishes.
+__global__ __launch_bounds__(256) void fallback_select_kernel(FbState fb, const double* __restrict__ cand_g,
+                                                              const int64_t* __restrict__ cand_i, int cap, int k,
+                                                              int l2, float* __restrict__ D, int64_t* __restrict__ I,
+                                                              double* __restrict__ S, int64_t id_offset,
+                                                              int* __restrict__ ov_list) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* g = reinterpret_cast<double*>(smem);
+  int64_t* id = reinterpret_cast<int64_t*>(g + pow2ceil(cap));  // the sort pads n up to a power of two
+  const int cnt = *fb.count;
+  const int tid = threadIdx.x;
+  for (int s = blockIdx.x; s < cnt; s += gridDim.x) {
+    const int qi = fb.list[s];
+    const int n = s < fb.slots ? fb.n[s] : cap + 1;
+    if (n > cap || n < k) {
+      if (tid == 0) ov_list[atomicAdd(&fb.count[1], 1)] = qi;
+      continue;
+    }
+    const int P = pow2ceil(n);
+    for (int i = tid; i < P; i += 256) {
+      g[i] = i < n ? cand_g[(int64_t)s * cap + i] : -INFINITY;
+      id[i] = i < n ? cand_i[(int64_t)s * cap + i] : INT64_MAX;
+    }
+    __syncthreads();
+    block_bitonic_sort(g, id, P);
+    for (int j = tid; j < k; j += 256) {
+      const int64_t o = (int64_t)qi * k + j;
+      const double sc = l2 ? -g[j] : g[j];
+      D[o] = (float)sc;
+      I[o] = id[j] + id_offset;
+      if (S) S[o] = sc;
+    }
+    __syncthreads();
+  }
+}
+
 // ============================================================ shard merge ==
 __global__ void topk_merge_kernel(const double* __restrict__ Sp, const int64_t* __restrict__ Ip, int nparts,
                                   int64_t nq, int k, int l2, float* __restrict__ D, int64_t* __restrict__ I,
@@ -748,8 +860,10 @@ struct FlatPlan {
   bool exact_only, tau;
   int dp, qt, M, waves, wq, nqt, nch, U, KP;
   int R, nch_pre, tstride;  // threshold pre-pass: bound rank, chunks, tile stride
+  int fb_slots, fb_cap;     // tiled fallback: slots with candidate storage, candidates per slot
   int64_t nq_pad, chunk, chunk_pre;
   size_t off_qh, off_qmeta, off_ps, off_pi, off_pt, off_fbl, off_fbc, off_tau, off_pre, total;
+  size_t off_fbt, off_fbi, off_fbn, off_fcg, off_fci, off_ovl;
 };
 
 static int padded_dim(int d) {
@@ -758,6 +872,12 @@ static int padded_dim(int d) {
   if (d <= 128) return 128;
   if (d <= 256) return 256;
   return (int)align_up((size_t)d, 32);
+}
+
+static int host_pow2ceil(int n) {
+  int p = 1;
+  while (p < n) p <<= 1;
+  return p;
 }
 
 static int env_int(const char* name, int dflt) {
@@ -844,6 +964,20 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
   p.off_pi = take((size_t)nq * p.U * 4);
   p.off_pt = take((size_t)nq * p.nch * 2 * 4);
   p.off_fbl = take((size_t)nq * 4);
+  // fallback storage: candidates at least as good as the merge's k-th; the cap
+  // leaves room for 2k + 64 (ties and near-ties), overflow goes to exact_topk
+  p.fb_slots = (int)(nq < 4096 ? nq : 4096);
+  p.fb_cap = host_pow2ceil(2 * k + 64);
+  if (p.fb_cap < 512) p.fb_cap = 512;
+  p.fb_cap = env_int("NRK_FB_CAP", p.fb_cap);
+  if (p.fb_cap < 1) p.fb_cap = 1;
+  if (p.fb_cap > 8192) p.fb_cap = 8192;  // select kernel sorts cap x 16 B in LDS
+  p.off_fbt = take((size_t)p.fb_slots * 8);
+  p.off_fbi = take((size_t)p.fb_slots * 8);
+  p.off_fbn = take((size_t)p.fb_slots * 4);
+  p.off_fcg = take((size_t)p.fb_slots * p.fb_cap * 8);
+  p.off_fci = take((size_t)p.fb_slots * p.fb_cap * 8);
+  p.off_ovl = take((size_t)nq * 4);
   p.total = off;
   return p;
 }
@@ -884,11 +1018,6 @@ static screen_fn pick_screen(int dp, int qt, int M, bool l2, bool pre) {
 
 using namespace nrk;
 
-static int host_pow2ceil(int n) {
-  int p = 1;
-  while (p < n) p <<= 1;
-  return p;
-}
 
 static int exact_launch(const float* xq, int64_t nq, const float* xb, int64_t nb, int d, int k, int l2,
                         const int* qlist, const int* qcount, int64_t max_work, float* D, int64_t* I,
@@ -969,6 +1098,17 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
   int* pi = reinterpret_cast<int*>(w + p.off_pi);
   float* pt = reinterpret_cast<float*>(w + p.off_pt);
   int* fbl = reinterpret_cast<int*>(w + p.off_fbl);
+  FbState fb;
+  fb.list = fbl;
+  fb.count = fbc;
+  fb.slots = p.fb_slots;
+  fb.thr_g = reinterpret_cast<double*>(w + p.off_fbt);
+  fb.thr_i = reinterpret_cast<int64_t*>(w + p.off_fbi);
+  fb.n = reinterpret_cast<int*>(w + p.off_fbn);
+  fb.force = env_int("NRK_FORCE_FALLBACK", 0);
+  double* fcg = reinterpret_cast<double*>(w + p.off_fcg);
+  int64_t* fci = reinterpret_cast<int64_t*>(w + p.off_fci);
+  int* ovl = reinterpret_cast<int*>(w + p.off_ovl);
   float* tau = reinterpret_cast<float*>(w + p.off_tau);
   float* pre = reinterpret_cast<float*>(w + p.off_pre);
 
@@ -998,20 +1138,29 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
   mark(2);
   if (p.tau && p.KP <= 64 && env_int("NRK_MERGE_WAVE", 0)) {
     hipLaunchKernelGGL(merge_rescore_wave_kernel<256>, dim3((unsigned)cdiv(nq, 4)), dim3(256), 0, st, ps, pi, pt,
-                       p.nch, p.M, p.KP, k, p.dp, xq, xb, nb, d, l2, qmeta, stats, tau, D, I, S, id_offset, fbl, fbc,
-                       (int)nq);
+                       p.nch, p.M, p.KP, k, p.dp, xq, xb, nb, d, l2, qmeta, stats, tau, D, I, S, id_offset, fb, (int)nq);
     NRK_CHECK_LAUNCH("merge_rescore_wave_kernel");
   } else {
     const int P = host_pow2ceil(p.U), P2 = host_pow2ceil(p.KP);
     const size_t smem = (size_t)P * 16 + (size_t)P2 * 16 + (size_t)d * 4;
     if (smem > 150 * 1024) return fail(NRK_EUNSUPPORTED, "knn_flat: merge needs %zu B LDS", smem);
     hipLaunchKernelGGL(merge_rescore_kernel, dim3((unsigned)nq), dim3(256), smem, st, ps, pi, pt, p.nch, p.M, p.KP, k,
-                       p.dp, xq, xb, nb, d, l2, qmeta, stats, p.tau ? tau : nullptr, D, I, S, id_offset, fbl, fbc);
+                       p.dp, xq, xb, nb, d, l2, qmeta, stats, p.tau ? tau : nullptr, D, I, S, id_offset, fb);
     NRK_CHECK_LAUNCH("merge_rescore_kernel");
   }
 
   mark(3);
-  int rc = exact_launch(xq, nq, xb, nb, d, k, l2, fbl, fbc, 256, D, I, S, id_offset, st);
+  {
+    const int64_t ntiles = cdiv(nb, (int64_t)FB_TR);
+    const int grid = (int)(ntiles < 2048 ? ntiles : 2048);
+    hipLaunchKernelGGL(fallback_scan_kernel, dim3(grid), dim3(256), (size_t)FB_TR * (d + 1) * 4, st, xq, xb, nb, d,
+                       l2, fb, fcg, fci, p.fb_cap);
+    NRK_CHECK_LAUNCH("fallback_scan_kernel");
+    hipLaunchKernelGGL(fallback_select_kernel, dim3(256), dim3(256), (size_t)host_pow2ceil(p.fb_cap) * 16, st, fb, fcg, fci,
+                       p.fb_cap, k, l2, D, I, S, id_offset, ovl);
+    NRK_CHECK_LAUNCH("fallback_select_kernel");
+  }
+  int rc = exact_launch(xq, nq, xb, nb, d, k, l2, ovl, fbc + 1, 256, D, I, S, id_offset, st);
   if (rc != NRK_OK) return rc;
   mark(4);
   if (n_fallback && hipMemcpyAsync(n_fallback, fbc, 4, hipMemcpyDeviceToDevice, st) != hipSuccess)

@@ -152,3 +152,20 @@ def test_full_size_properties(gpu):
     _, Io, So = ko.exact_search(xq[sample].cpu().numpy(), xb.cpu().numpy(), 5, ko.METRIC_IP)
     np.testing.assert_array_equal(I[sample].cpu().numpy(), Io)
     assert int(idx.last_fallback.item()) <= 41  # certificate covers (nearly) every query
+
+
+@pytest.mark.parametrize("cap", [None, "6"])
+def test_forced_fallback_paths(gpu, monkeypatch, cap):
+    """Every query uncertified (NRK_FORCE_FALLBACK): the tiled fp64 fallback
+    (scan + select) must reproduce the oracle; with a tiny candidate cap the
+    overflow path (block-per-query exact kernel) must too."""
+    monkeypatch.setenv("NRK_FORCE_FALLBACK", "1")
+    if cap:
+        monkeypatch.setenv("NRK_FB_CAP", cap)
+    xq, xb = _mixture(50_000, 200, 96, seed=11)
+    xb[40_000] = xb[7]
+    xq[3] = xb[7]
+    for metric in (ko.METRIC_IP, ko.METRIC_L2):
+        for k in (1, 5, 40):
+            idx = _check(xq, xb, k, metric, gpu)
+            assert int(idx.last_fallback.item()) == 200
