@@ -133,6 +133,50 @@ int nrk_din_attn_bwd(const void* keys, const int32_t* hist_ids, int64_t n_table,
                      float* dU, float* dW1k, float* dw2, float* db2,
                      void* ws, size_t ws_bytes, void* stream);
 
+/* ------------------------------------------------------ inverted lists --
+ * faiss Clustering / IndexIVFFlat building blocks (Retrieval.py:11-23).
+ *
+ * Stable grouping of ids by list (counting sort; ids ascending inside each
+ * list, i.e. faiss's insertion order):
+ *   assign [n] int64 list of each id (must be in [0, nlist); *n_bad counts violations)
+ *   list_off [nlist+1] int64 (out), pos2id [n] int64 (out), pos2list [n] int32 (out)
+ * Replaces `cluster_to_articles[i] = ids[assign == i]` (Retrieval.py:22-23)
+ * and the list append of IndexIVFFlat.add. */
+int nrk_group_by_list_workspace(int64_t n, int32_t nlist, size_t* ws_bytes);
+int nrk_group_by_list(const int64_t* assign, int64_t n, int32_t nlist, int64_t* list_off,
+                      int64_t* pos2id, int32_t* pos2list, int32_t* n_bad, void* ws,
+                      size_t ws_bytes, void* stream);
+
+/* List-major copy of the screening rows of nrk_flat_prepare:
+ * xbh_ivf[pos] = xb_bf16[pos2id[pos]] (padded dim), meta_ivf likewise. */
+int nrk_ivf_pack(const int64_t* pos2id, int64_t n, int32_t d, const uint16_t* xb_bf16,
+                 const float* xb_meta, uint16_t* xbh_ivf, float* meta_ivf, void* stream);
+
+/* k-means update step (faiss Clustering.train, Retrieval.py:14-18):
+ * centroids[c] = (sum over the members of c, fp64, in id order) / |c| for
+ * every non-empty list of (list_off, pos2id); empty clusters are left as they
+ * are (the caller splits them, as faiss does). */
+int nrk_kmeans_update(const float* x, int32_t d, const int64_t* list_off, const int64_t* pos2id,
+                      int32_t k, float* centroids, void* stream);
+
+/* IVF-Flat search (faiss IndexIVFFlat.search; BASELINE configs[3]).
+ *   probe [nq][nprobe] int64: the coarse quantizer's lists per query (-1: none)
+ *   xb [n][d] f32 in id order (exact rescoring); xbh_ivf / meta_ivf list-major
+ *   (nrk_ivf_pack); stats from nrk_flat_prepare over the same rows;
+ *   list_off / pos2id / pos2list from nrk_group_by_list; max_list = largest list.
+ * Result: the exact top-k (same order and ties as nrk_knn_flat) among the
+ * items of the probed lists.  Outputs and stage_events as nrk_knn_flat
+ * (stage 0 = query prepare + grouping by list). */
+int nrk_ivf_search_workspace(int64_t nq, int32_t nprobe, int32_t nlist, int64_t max_list,
+                             int32_t d, int32_t k, size_t* ws_bytes);
+int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe, int32_t nprobe,
+                   const float* xb, const uint16_t* xbh_ivf, const float* meta_ivf,
+                   const float* stats, const int64_t* list_off, const int64_t* pos2id,
+                   const int32_t* pos2list, int32_t nlist, int64_t n, int64_t max_list,
+                   int32_t d, int32_t k, int32_t metric, float* D, int64_t* I, double* S,
+                   int64_t id_offset, int32_t* n_fallback, void* ws, size_t ws_bytes,
+                   void* const* stage_events, void* stream);
+
 /* Row gather (table [N][d] dtype -> out [n][d] f32), id < 0 -> zeros.
  * Replaces the per-sample dict lookups of DIN.py:47-50,83 (target and
  * candidate embeddings). */

@@ -37,6 +37,13 @@ SIGNATURES = {
                                     c_p, c_p, c_size, c_p, c_p]),
     "nrk_knn_exact": (ctypes.c_int, [c_p, c_i64, c_p, c_i64, c_i32, c_i32, c_i32, c_p, c_p, c_p, c_i64, c_p]),
     "nrk_topk_merge": (ctypes.c_int, [c_p, c_p, c_i32, c_i64, c_i32, c_i32, c_p, c_p, c_p, c_p]),
+    "nrk_group_by_list_workspace": (ctypes.c_int, [c_i64, c_i32, ctypes.POINTER(c_size)]),
+    "nrk_group_by_list": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_p, c_p, c_p, c_p, c_size, c_p]),
+    "nrk_ivf_pack": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_p, c_p, c_p, c_p]),
+    "nrk_kmeans_update": (ctypes.c_int, [c_p, c_i32, c_p, c_p, c_i32, c_p, c_p]),
+    "nrk_ivf_search_workspace": (ctypes.c_int, [c_i64, c_i32, c_i32, c_i64, c_i32, c_i32, ctypes.POINTER(c_size)]),
+    "nrk_ivf_search": (ctypes.c_int, [c_p, c_i64, c_p, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i32, c_i64, c_i64,
+                                      c_i32, c_i32, c_i32, c_p, c_p, c_p, c_i64, c_p, c_p, c_size, c_p, c_p]),
     "nrk_din_attn_fwd": (ctypes.c_int, [c_p, c_p, c_i64, c_i32, c_p, c_p, c_p, c_f32, c_i32, c_i32, c_i32, c_i32,
                                         c_p, c_p, c_p]),
     "nrk_din_attn_bwd_workspace": (ctypes.c_int, [c_i32, c_i32, c_i32, ctypes.POINTER(c_size)]),

@@ -157,11 +157,25 @@ __device__ __forceinline__ void list_insert(float (&ls)[N], int (&li)[N], float 
 //   registers, admitting only scores above max(its (M+1)-th, tau[q]); the
 //   pre-pass bound removes the warm-up insertions that otherwise dominate.
 //   The merge's certificate includes tau[q] in theta.
+//
+// MODE 2 (IVF list scan): the block's work item comes from a device table —
+//   (list l, tile of the queries probing l, chunk of l).  qh holds the probing
+//   queries gathered list-major (segments padded to WQ rows); slot_pair maps a
+//   gathered row back to its (query, probe) pair, whose candidates land at
+//   [(pair * cmax + chunk) * 2 + half].
+struct IvfScreen {
+  const int* work_off;     // [nlist + 1] prefix of work items per list
+  const int64_t* list_off; // [nlist + 1] list ranges in the list-major corpus
+  const int* seg_off;      // [nlist] first gathered query row of each list
+  const int* slot_pair;    // [slots] q * nprobe + p, or -1 for padding
+  int nlist, ch, cmax;
+};
+
 template <int DP, int QT, int M, int WAVES, bool L2, int MODE, int EPI = 0>
 __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
     const uint16_t* __restrict__ qh, const uint16_t* __restrict__ xbh, const float* __restrict__ xmeta,
     int64_t nq, int64_t nb, int64_t chunk, int nch, int nqt, int tstride, float* __restrict__ part_s,
-    int* __restrict__ part_i, float* __restrict__ part_t, const float* __restrict__ tau_q) {
+    int* __restrict__ part_i, float* __restrict__ part_t, const float* __restrict__ tau_q, IvfScreen iv) {
   constexpr int CPR = DP / 8;        // 16-B chunks per row
   constexpr int TI = 64;  // items per tile (TI/32 sub-tiles of 32) between barriers
   constexpr int TCH = TI * CPR;      // 16-B chunks per tile
@@ -176,12 +190,34 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
   const int nblk = gridDim.x, b = blockIdx.x;
   const int xg = b & 7, jj = b >> 3, q8 = nblk >> 3, r8 = nblk & 7;
   const int logical = (xg < r8 ? xg * (q8 + 1) : r8 * (q8 + 1) + (xg - r8) * q8) + jj;
-  const int c = logical / nqt, qt = logical - c * nqt;
+  int c, qt;
+  int64_t ibeg, iend, seg0 = 0;
+  if constexpr (MODE == 2) {
+    if (logical >= iv.work_off[iv.nlist]) return;
+    int lo = 0, hi = iv.nlist;  // largest l with work_off[l] <= logical (empty lists own no items)
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (iv.work_off[mid] <= logical) lo = mid;
+      else hi = mid;
+    }
+    const int64_t lb = iv.list_off[lo], le = iv.list_off[lo + 1];
+    const int nchl = (int)cdiv(le - lb, (int64_t)iv.ch);
+    const int local = logical - iv.work_off[lo];
+    qt = local / nchl;
+    c = local - qt * nchl;
+    ibeg = lb + (int64_t)c * iv.ch;
+    iend = ibeg + iv.ch < le ? ibeg + iv.ch : le;
+    seg0 = iv.seg_off[lo];
+    qh += seg0 * DP;  // this list's query segment
+  } else {
+    c = logical / nqt;
+    qt = logical - c * nqt;
+    ibeg = (int64_t)c * chunk;
+    iend = ibeg + chunk < nb ? ibeg + chunk : nb;
+  }
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
-  const int64_t ibeg = (int64_t)c * chunk;
-  const int64_t iend = ibeg + chunk < nb ? ibeg + chunk : nb;
   const int ntiles = (int)cdiv(cdiv(iend - ibeg, TI), tstride);  // visited tiles
 
   bf16x8 qf[QT][KS];
@@ -322,8 +358,14 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
 #pragma unroll
   for (int t = 0; t < QT; ++t) {
     const int64_t qi = qidx[t];
-    if (qi < nq) {
-      const int64_t base = (qi * nch + c) * 2 + h;
+    int64_t base = -1;
+    if constexpr (MODE == 2) {
+      const int pair = iv.slot_pair[seg0 + qi];
+      if (pair >= 0) base = ((int64_t)pair * iv.cmax + c) * 2 + h;
+    } else if (qi < nq) {
+      base = (qi * nch + c) * 2 + h;
+    }
+    if (base >= 0) {
       if constexpr (MODE == 1) {
         part_t[base] = ls[t][0];
       } else {
@@ -421,6 +463,16 @@ struct FbState {
   }
 };
 
+// IVF restriction for the exact paths: only items of the query's probed lists
+// are eligible (faiss IndexIVF semantics); rows are addressed by id.
+struct IvfFb {
+  const int64_t* pos2id;    // [n] list-major position -> id (nullptr: flat index)
+  const int* pos2list;      // [n]
+  const int64_t* list_off;  // [nlist + 1]
+  const int64_t* probe;     // [nq][nprobe] probed lists (-1: none)
+  int nprobe;
+};
+
 // One 256-thread workgroup per query.  Dynamic LDS: P doubles + P int64 (the
 // union), P2 doubles + P2 int64 (rescored), d floats (query), reductions.
 __global__ __launch_bounds__(256) void merge_rescore_kernel(
@@ -428,7 +480,7 @@ __global__ __launch_bounds__(256) void merge_rescore_kernel(
     int nch, int M, int KP, int k, int dp, const float* __restrict__ xq, const float* __restrict__ xb,
     int64_t nb, int d, int l2, const double* __restrict__ qmeta, const float* __restrict__ stats,
     const float* __restrict__ tau_q, float* __restrict__ D, int64_t* __restrict__ I, double* __restrict__ S,
-    int64_t id_offset, FbState fb) {
+    int64_t id_offset, FbState fb, const int64_t* __restrict__ pos2id) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int qi = blockIdx.x, tid = threadIdx.x;
   const int U = nch * 2 * M, P = pow2ceil(U);
@@ -448,7 +500,7 @@ __global__ __launch_bounds__(256) void merge_rescore_kernel(
     const int64_t item = i < U ? (int64_t)pi[i] : -1;
     const bool ok = v != -INFINITY && item >= 0 && item < nb;  // never dereference an unset slot
     g[i] = ok ? (double)v : -INFINITY;
-    id[i] = ok ? item : INT64_MAX;
+    id[i] = ok ? (pos2id ? pos2id[item] : item) : INT64_MAX;  // IVF: list position -> id
   }
   float th = -INFINITY;
   for (int i = tid; i < nch * 2; i += 256) th = fmaxf(th, part_t[(int64_t)qi * nch * 2 + i]);
@@ -668,7 +720,7 @@ __global__ __launch_bounds__(256) void merge_rescore_wave_kernel(
 __global__ __launch_bounds__(256) void exact_topk_kernel(
     const float* __restrict__ xq, int64_t nq, const float* __restrict__ xb, int64_t nb, int d, int k,
     int l2, const int* __restrict__ qlist, const int* __restrict__ qcount, float* __restrict__ D,
-    int64_t* __restrict__ I, double* __restrict__ S, int64_t id_offset) {
+    int64_t* __restrict__ I, double* __restrict__ S, int64_t id_offset, IvfFb iv) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int P = pow2ceil(k + 256);
   double* g = reinterpret_cast<double*>(smem);
@@ -689,12 +741,21 @@ __global__ __launch_bounds__(256) void exact_topk_kernel(
       s_cnt = 0;
     }
     __syncthreads();
-    for (int64_t base = 0; base < nb; base += 256) {
-      const int64_t i = base + tid;
+    const int nrange = iv.pos2id ? iv.nprobe : 1;
+    for (int pr = 0; pr < nrange; ++pr) {
+    int64_t lo = 0, hi = nb;
+    if (iv.pos2id) {
+      const int64_t l = iv.probe[qi * iv.nprobe + pr];
+      lo = l >= 0 ? iv.list_off[l] : 0;
+      hi = l >= 0 ? iv.list_off[l + 1] : 0;
+    }
+    for (int64_t base = lo; base < hi; base += 256) {
+      const int64_t pp = base + tid;  // position (== id for a flat index)
+      const int64_t i = pp < hi ? (iv.pos2id ? iv.pos2id[pp] : pp) : nb;
       const int cnt = s_cnt;
       const double tg = g[k - 1];
       const int64_t tidx = id[k - 1];
-      if (i < nb) {
+      if (pp < hi) {
         const double s = exact_score(qs, xb + i * d, d, l2 != 0);
         const double gv = l2 ? -s : s;
         if (cnt < k || better(gv, i, tg, tidx)) {
@@ -719,6 +780,7 @@ __global__ __launch_bounds__(256) void exact_topk_kernel(
       }
       __syncthreads();
     }
+    }
     for (int j = tid; j < k; j += 256) {
       const int64_t o = qi * k + j;
       const bool valid = id[j] != INT64_MAX;
@@ -742,7 +804,7 @@ constexpr int FB_TR = 64;
 __global__ __launch_bounds__(256) void fallback_scan_kernel(const float* __restrict__ xq,
                                                             const float* __restrict__ xb, int64_t nb, int d,
                                                             int l2, FbState fb, double* __restrict__ cand_g,
-                                                            int64_t* __restrict__ cand_i, int cap) {
+                                                            int64_t* __restrict__ cand_i, int cap, IvfFb iv) {
   extern __shared__ float tile[];
   const int c0 = *fb.count;
   const int cnt = c0 < fb.slots ? c0 : fb.slots;
@@ -754,16 +816,29 @@ __global__ __launch_bounds__(256) void fallback_scan_kernel(const float* __restr
     const int64_t r0 = t * FB_TR;
     const int rows = nb - r0 < FB_TR ? (int)(nb - r0) : FB_TR;
     __syncthreads();
-    for (int e = threadIdx.x; e < rows * d; e += 256) {
-      const int r = e / d;
-      tile[r * ds + (e - r * d)] = xb[r0 * d + e];
+    if (iv.pos2id) {  // IVF: gather rows by id
+      for (int e = threadIdx.x; e < rows * d; e += 256) {
+        const int r = e / d;
+        tile[r * ds + (e - r * d)] = xb[iv.pos2id[r0 + r] * d + (e - r * d)];
+      }
+    } else {
+      for (int e = threadIdx.x; e < rows * d; e += 256) {
+        const int r = e / d;
+        tile[r * ds + (e - r * d)] = xb[r0 * d + e];
+      }
     }
     __syncthreads();
     if (lane >= rows) continue;
     const float* row = tile + lane * ds;
-    const int64_t item = r0 + lane;
+    const int64_t item = iv.pos2id ? iv.pos2id[r0 + lane] : r0 + lane;
+    const int mylist = iv.pos2id ? iv.pos2list[r0 + lane] : 0;
     for (int s = wv; s < cnt; s += 4) {
       const int qi = fb.list[s];
+      if (iv.pos2id) {
+        bool member = false;
+        for (int pr = 0; pr < iv.nprobe; ++pr) member |= iv.probe[(int64_t)qi * iv.nprobe + pr] == mylist;
+        if (!member) continue;
+      }
       const double acc = exact_score(xq + (int64_t)qi * d, row, d, l2 != 0);
       const double gv = l2 ? -acc : acc;
       const int64_t ti = fb.thr_i[s];
@@ -983,7 +1058,7 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
 }
 
 typedef void (*screen_fn)(const uint16_t*, const uint16_t*, const float*, int64_t, int64_t, int64_t, int, int, int,
-                          float*, int*, float*, const float*);
+                          float*, int*, float*, const float*, IvfScreen);
 
 template <int DP, int QT, int M, bool L2, int MODE>
 static screen_fn pick3() {
@@ -995,21 +1070,29 @@ static screen_fn pick3() {
   return screen_kernel<DP, QT, M, 4, L2, MODE>;
 }
 
-template <int DP, bool L2>
-static screen_fn pick1(int qt, int M, bool pre) {
+template <int DP, bool L2, int MODE>
+static screen_fn pick2(int qt, int M) {
   constexpr int Q2 = DP == 256 ? 1 : 2;  // DP=256 always runs one query tile per wave
-  if (pre) return qt == 2 ? pick3<DP, Q2, 1, L2, 1>() : pick3<DP, 1, 1, L2, 1>();
-  if (M == 4) return qt == 2 ? pick3<DP, Q2, 4, L2, 0>() : pick3<DP, 1, 4, L2, 0>();
-  if (M == 8) return pick3<DP, 1, 8, L2, 0>();
-  return pick3<DP, 1, 16, L2, 0>();
+  if (M == 4) return qt == 2 ? pick3<DP, Q2, 4, L2, MODE>() : pick3<DP, 1, 4, L2, MODE>();
+  if (M == 8) return pick3<DP, 1, 8, L2, MODE>();
+  return pick3<DP, 1, 16, L2, MODE>();
 }
 
-static screen_fn pick_screen(int dp, int qt, int M, bool l2, bool pre) {
+// mode: 0 main pass, 1 threshold pre-pass, 2 IVF list scan
+template <int DP, bool L2>
+static screen_fn pick1(int qt, int M, int mode) {
+  constexpr int Q2 = DP == 256 ? 1 : 2;
+  if (mode == 1) return qt == 2 ? pick3<DP, Q2, 1, L2, 1>() : pick3<DP, 1, 1, L2, 1>();
+  if (mode == 2) return pick2<DP, L2, 2>(qt, M);
+  return pick2<DP, L2, 0>(qt, M);
+}
+
+static screen_fn pick_screen(int dp, int qt, int M, bool l2, int mode) {
   switch (dp) {
-    case 32: return l2 ? pick1<32, true>(qt, M, pre) : pick1<32, false>(qt, M, pre);
-    case 64: return l2 ? pick1<64, true>(qt, M, pre) : pick1<64, false>(qt, M, pre);
-    case 128: return l2 ? pick1<128, true>(qt, M, pre) : pick1<128, false>(qt, M, pre);
-    case 256: return l2 ? pick1<256, true>(qt, M, pre) : pick1<256, false>(qt, M, pre);
+    case 32: return l2 ? pick1<32, true>(qt, M, mode) : pick1<32, false>(qt, M, mode);
+    case 64: return l2 ? pick1<64, true>(qt, M, mode) : pick1<64, false>(qt, M, mode);
+    case 128: return l2 ? pick1<128, true>(qt, M, mode) : pick1<128, false>(qt, M, mode);
+    case 256: return l2 ? pick1<256, true>(qt, M, mode) : pick1<256, false>(qt, M, mode);
   }
   return nullptr;
 }
@@ -1021,14 +1104,14 @@ using namespace nrk;
 
 static int exact_launch(const float* xq, int64_t nq, const float* xb, int64_t nb, int d, int k, int l2,
                         const int* qlist, const int* qcount, int64_t max_work, float* D, int64_t* I,
-                        double* S, int64_t id_offset, hipStream_t st) {
+                        double* S, int64_t id_offset, hipStream_t st, IvfFb iv = IvfFb{}) {
   const int P = host_pow2ceil(k + 256);
   const size_t smem = (size_t)P * 16 + (size_t)d * 4;
   if (smem > 160 * 1024) return fail(NRK_EUNSUPPORTED, "exact search: k=%d d=%d needs %zu B of LDS", k, d, smem);
   int grid = (int)(max_work < 2048 ? max_work : 2048);
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(exact_topk_kernel, dim3(grid), dim3(256), smem, st, xq, nq, xb, nb, d, k, l2, qlist, qcount,
-                     D, I, S, id_offset);
+                     D, I, S, id_offset, iv);
   NRK_CHECK_LAUNCH("exact_topk_kernel");
   return NRK_OK;
 }
@@ -1117,22 +1200,22 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
                      p.dp, qh, qmeta);
   NRK_CHECK_LAUNCH("query_prepare_kernel");
   if (p.tau) {
-    screen_fn pf = pick_screen(p.dp, p.qt, p.M, l2 != 0, true);
+    screen_fn pf = pick_screen(p.dp, p.qt, p.M, l2 != 0, 1);
     if (!pf) return fail(NRK_EUNSUPPORTED, "knn_flat: no pre-pass kernel for dp=%d", p.dp);
     hipLaunchKernelGGL(pf, dim3(p.nqt * p.nch_pre), dim3(p.waves * 64), 0, st, qh, xb_bf16, xb_meta, nq, nb,
-                       p.chunk_pre, p.nch_pre, p.nqt, p.tstride, nullptr, nullptr, pre, nullptr);
+                       p.chunk_pre, p.nch_pre, p.nqt, p.tstride, nullptr, nullptr, pre, nullptr, IvfScreen{});
     NRK_CHECK_LAUNCH("screen_kernel (pre-pass)");
     hipLaunchKernelGGL(tau_select_kernel, dim3((unsigned)cdiv(nq, 4)), dim3(256), 0, st, pre, 2 * p.nch_pre, p.R, nq,
                        tau);
     NRK_CHECK_LAUNCH("tau_select_kernel");
   }
 
-  screen_fn fn = pick_screen(p.dp, p.qt, p.M, l2 != 0, false);
+  screen_fn fn = pick_screen(p.dp, p.qt, p.M, l2 != 0, 0);
   if (!fn) return fail(NRK_EUNSUPPORTED, "knn_flat: no screen kernel for dp=%d", p.dp);
   const int nblk = p.nqt * p.nch;
   mark(1);
   hipLaunchKernelGGL(fn, dim3(nblk), dim3(p.waves * 64), 0, st, qh, xb_bf16, xb_meta, nq, nb, p.chunk, p.nch, p.nqt, 1,
-                     ps, pi, pt, p.tau ? tau : nullptr);
+                     ps, pi, pt, p.tau ? tau : nullptr, IvfScreen{});
   NRK_CHECK_LAUNCH("screen_kernel");
 
   mark(2);
@@ -1145,7 +1228,7 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
     const size_t smem = (size_t)P * 16 + (size_t)P2 * 16 + (size_t)d * 4;
     if (smem > 150 * 1024) return fail(NRK_EUNSUPPORTED, "knn_flat: merge needs %zu B LDS", smem);
     hipLaunchKernelGGL(merge_rescore_kernel, dim3((unsigned)nq), dim3(256), smem, st, ps, pi, pt, p.nch, p.M, p.KP, k,
-                       p.dp, xq, xb, nb, d, l2, qmeta, stats, p.tau ? tau : nullptr, D, I, S, id_offset, fb);
+                       p.dp, xq, xb, nb, d, l2, qmeta, stats, p.tau ? tau : nullptr, D, I, S, id_offset, fb, nullptr);
     NRK_CHECK_LAUNCH("merge_rescore_kernel");
   }
 
@@ -1154,7 +1237,7 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
     const int64_t ntiles = cdiv(nb, (int64_t)FB_TR);
     const int grid = (int)(ntiles < 2048 ? ntiles : 2048);
     hipLaunchKernelGGL(fallback_scan_kernel, dim3(grid), dim3(256), (size_t)FB_TR * (d + 1) * 4, st, xq, xb, nb, d,
-                       l2, fb, fcg, fci, p.fb_cap);
+                       l2, fb, fcg, fci, p.fb_cap, IvfFb{});
     NRK_CHECK_LAUNCH("fallback_scan_kernel");
     hipLaunchKernelGGL(fallback_select_kernel, dim3(256), dim3(256), (size_t)host_pow2ceil(p.fb_cap) * 16, st, fb, fcg, fci,
                        p.fb_cap, k, l2, D, I, S, id_offset, ovl);
@@ -1178,5 +1261,294 @@ extern "C" int nrk_topk_merge(const double* S_parts, const int64_t* I_parts, int
   hipLaunchKernelGGL(topk_merge_kernel, dim3((unsigned)cdiv(nq, 256)), dim3(256), 0, (hipStream_t)stream, S_parts,
                      I_parts, nparts, nq, k, metric == NRK_METRIC_L2, D, I, S);
   NRK_CHECK_LAUNCH("topk_merge_kernel");
+  return NRK_OK;
+}
+
+// ============================================================== IVF-Flat ==
+// faiss IndexIVFFlat.search (BASELINE configs[3]; the inverted lists of
+// Retrieval.py:21-23).  The caller supplies the probed lists (the coarse
+// quantizer's top-nprobe, a flat search over the centroids).  List-major
+// batching: every (query, probe) pair is grouped under its list, each list's
+// probing queries are gathered into a padded bf16 segment, and the screen
+// kernel (MODE 2) runs (list, query tile, list chunk) work items, so each list
+// chunk is streamed once per 32*QT*WAVES queries.  Merge, certificate and the
+// exact fallback are the flat path's, restricted to the probed lists.
+namespace nrk {
+
+__global__ void ivf_count_kernel(const int64_t* __restrict__ probe, int64_t npairs, int nlist, int* __restrict__ cnt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npairs) return;
+  const int64_t l = probe[i];
+  if (l >= 0 && l < nlist) atomicAdd(&cnt[l], 1);
+}
+
+// One block: per-list query segments (padded to wq rows) and work-item prefix.
+__global__ __launch_bounds__(1024) void ivf_plan_kernel(const int* __restrict__ cnt,
+                                                        const int64_t* __restrict__ list_off, int nlist, int wq,
+                                                        int ch, int* __restrict__ seg_off, int* __restrict__ work_off,
+                                                        int* __restrict__ fill) {
+  __shared__ int s_seg[1024], s_work[1024];
+  const int t = threadIdx.x;
+  const int per = (nlist + 1023) / 1024;
+  const int lo = t * per < nlist ? t * per : nlist, hi = lo + per < nlist ? lo + per : nlist;
+  int ss = 0, sw = 0;
+  for (int l = lo; l < hi; ++l) {
+    const int rows = (cnt[l] + wq - 1) / wq * wq;
+    const int nchl = (int)cdiv(list_off[l + 1] - list_off[l], (int64_t)ch);
+    ss += rows;
+    sw += rows / wq * nchl;
+  }
+  s_seg[t] = ss;
+  s_work[t] = sw;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const int a = t >= o ? s_seg[t - o] : 0, b = t >= o ? s_work[t - o] : 0;
+    __syncthreads();
+    s_seg[t] += a;
+    s_work[t] += b;
+    __syncthreads();
+  }
+  int es = s_seg[t] - ss, ew = s_work[t] - sw;
+  for (int l = lo; l < hi; ++l) {
+    const int rows = (cnt[l] + wq - 1) / wq * wq;
+    const int nchl = (int)cdiv(list_off[l + 1] - list_off[l], (int64_t)ch);
+    seg_off[l] = es;
+    work_off[l] = ew;
+    fill[l] = 0;
+    es += rows;
+    ew += rows / wq * nchl;
+  }
+  if (t == 1023) {
+    seg_off[nlist] = s_seg[1023];
+    work_off[nlist] = s_work[1023];
+  }
+}
+
+__global__ void ivf_scatter_kernel(const int64_t* __restrict__ probe, int64_t npairs, int nlist,
+                                   const int* __restrict__ seg_off, int* __restrict__ fill,
+                                   int* __restrict__ slot_pair) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npairs) return;
+  const int64_t l = probe[i];
+  if (l < 0 || l >= nlist) return;
+  slot_pair[seg_off[l] + atomicAdd(&fill[l], 1)] = (int)i;
+}
+
+// gathered query rows: one wave per slot row (padding rows are zeroed)
+__global__ void ivf_gather_kernel(const uint16_t* __restrict__ qh, int dp, int nprobe,
+                                  const int* __restrict__ slot_pair, const int* __restrict__ seg_off, int nlist,
+                                  int64_t max_rows, uint16_t* __restrict__ qh_ivf) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= max_rows || row >= seg_off[nlist]) return;
+  const int pair = slot_pair[row];
+  const int64_t q = pair >= 0 ? pair / nprobe : 0;
+  for (int j = lane * 4; j < dp; j += 256) {
+    uint2 v = make_uint2(0u, 0u);
+    if (pair >= 0) v = *reinterpret_cast<const uint2*>(qh + q * dp + j);
+    *reinterpret_cast<uint2*>(qh_ivf + row * dp + j) = v;
+  }
+}
+
+struct IvfPlan {
+  int dp, qt, M, waves, wq, ch, cmax, U, KP, nqt;
+  int fb_slots, fb_cap;
+  int64_t nq_pad, max_rows, ub;
+  size_t off_fbc, off_cnt, off_fill, off_seg, off_work, off_sp, off_qh, off_qmeta, off_qi, off_ps, off_pi, off_pt,
+      off_fbl, off_fbt, off_fbi, off_fbn, off_fcg, off_fci, off_ovl, total;
+};
+
+static IvfPlan make_ivf_plan(int64_t nq, int nprobe, int nlist, int64_t max_list, int d, int k) {
+  IvfPlan p;
+  memset(&p, 0, sizeof(p));
+  p.dp = padded_dim(d);
+  p.waves = 4;
+  if (k <= 8) { p.M = 4; p.qt = 2; }
+  else if (k <= 24) { p.M = 8; p.qt = 1; }
+  else { p.M = 16; p.qt = 1; }
+  if (p.dp == 256) p.qt = 1;
+  p.wq = p.waves * 32 * p.qt;
+  p.nqt = (int)cdiv(nq, p.wq);
+  p.nq_pad = (int64_t)p.nqt * p.wq;
+  int kp = 2 * k > 32 ? 2 * k : 32;
+  if (kp < k + 16) kp = k + 16;
+  // chunking of a list: the union per query (nprobe * cmax * 2M) stays <= 4096
+  // entries, but holds at least kp; chunks are >= 2048 items where lists allow
+  const int per = nprobe * 2 * p.M;
+  int cmax_lim = 4096 / per;
+  if (cmax_lim < 1) cmax_lim = 1;
+  const int cmax_min = (int)cdiv(kp, per);
+  if (cmax_lim < cmax_min) cmax_lim = cmax_min;
+  const int64_t ml = max_list > 0 ? max_list : 1;
+  int64_t ch = (int64_t)align_up((size_t)cdiv(ml, cmax_lim), 64);
+  int64_t ch_floor = (int64_t)align_up((size_t)cdiv(ml, cmax_min), 64);
+  if (ch_floor > 2048) ch_floor = 2048;
+  if (ch < ch_floor) ch = ch_floor;
+  const int64_t ch_gib = ((int64_t)1 << 30) / (p.dp * 2) / 64 * 64;  // buffer descriptor range
+  if (ch > ch_gib) ch = ch_gib;
+  p.ch = (int)env_int("NRK_IVF_CHUNK", (int)ch);
+  p.cmax = (int)cdiv(ml, (int64_t)p.ch);
+  p.U = nprobe * p.cmax * 2 * p.M;
+  p.KP = kp < p.U ? kp : p.U;
+  if (p.KP > 1024) p.KP = 1024;
+  const int64_t npairs = nq * nprobe;
+  p.max_rows = npairs + (int64_t)nlist * (p.wq - 1);
+  p.max_rows = (p.max_rows + p.wq - 1) / p.wq * p.wq;
+  p.ub = (cdiv(npairs, (int64_t)p.wq) + nlist) * p.cmax;
+  p.fb_slots = (int)(nq < 4096 ? nq : 4096);
+  p.fb_cap = host_pow2ceil(2 * k + 64);
+  if (p.fb_cap < 512) p.fb_cap = 512;
+  p.fb_cap = env_int("NRK_FB_CAP", p.fb_cap);
+  if (p.fb_cap < 1) p.fb_cap = 1;
+  if (p.fb_cap > 8192) p.fb_cap = 8192;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    size_t o = off;
+    off = align_up(off + bytes, 256);
+    return o;
+  };
+  p.off_fbc = take(16);
+  p.off_cnt = take((size_t)nlist * 4);
+  p.off_fill = take((size_t)nlist * 4);
+  p.off_seg = take((size_t)(nlist + 1) * 4);
+  p.off_work = take((size_t)(nlist + 1) * 4);
+  p.off_sp = take((size_t)p.max_rows * 4);
+  p.off_qh = take((size_t)p.nq_pad * p.dp * 2);
+  p.off_qmeta = take((size_t)nq * 4 * 8);
+  p.off_qi = take((size_t)p.max_rows * p.dp * 2);
+  p.off_ps = take((size_t)nq * p.U * 4);
+  p.off_pi = take((size_t)nq * p.U * 4);
+  p.off_pt = take((size_t)nq * nprobe * p.cmax * 2 * 4);
+  p.off_fbl = take((size_t)nq * 4);
+  p.off_fbt = take((size_t)p.fb_slots * 8);
+  p.off_fbi = take((size_t)p.fb_slots * 8);
+  p.off_fbn = take((size_t)p.fb_slots * 4);
+  p.off_fcg = take((size_t)p.fb_slots * p.fb_cap * 8);
+  p.off_fci = take((size_t)p.fb_slots * p.fb_cap * 8);
+  p.off_ovl = take((size_t)nq * 4);
+  p.total = off;
+  return p;
+}
+
+}  // namespace nrk
+
+extern "C" int nrk_ivf_search_workspace(int64_t nq, int32_t nprobe, int32_t nlist, int64_t max_list, int32_t d,
+                                        int32_t k, size_t* ws_bytes) {
+  NRK_CHECK_ARG(ws_bytes && nq >= 0 && nprobe > 0 && nlist > 0 && max_list >= 0 && d > 0 && d <= 256 && k > 0 &&
+                    k <= 256,
+                "ivf_search_workspace: bad arguments");
+  *ws_bytes = make_ivf_plan(nq, nprobe, nlist, max_list, d, k).total;
+  return NRK_OK;
+}
+
+extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe, int32_t nprobe, const float* xb,
+                              const uint16_t* xbh_ivf, const float* meta_ivf, const float* stats,
+                              const int64_t* list_off, const int64_t* pos2id, const int32_t* pos2list, int32_t nlist,
+                              int64_t n, int64_t max_list, int32_t d, int32_t k, int32_t metric, float* D, int64_t* I,
+                              double* S, int64_t id_offset, int32_t* n_fallback, void* ws, size_t ws_bytes,
+                              void* const* stage_events, void* stream) {
+  NRK_CHECK_ARG(nq >= 0 && nprobe > 0 && nlist > 0 && n >= 0 && max_list >= 0 && d > 0 && d <= 256 && k > 0 &&
+                    k <= 256,
+                "ivf_search: bad shape nq=%lld nprobe=%d nlist=%d d=%d k=%d", (long long)nq, nprobe, nlist, d, k);
+  NRK_CHECK_ARG(metric == NRK_METRIC_INNER_PRODUCT || metric == NRK_METRIC_L2, "ivf_search: bad metric %d", metric);
+  NRK_CHECK_ARG(n < ((int64_t)1 << 31), "ivf_search: %lld rows exceed int32 positions", (long long)n);
+  hipStream_t st = (hipStream_t)stream;
+  const IvfPlan p = make_ivf_plan(nq, nprobe, nlist, max_list, d, k);
+  if (ws_bytes < p.total) return fail(NRK_EWORKSPACE, "ivf_search: workspace %zu < %zu bytes", ws_bytes, p.total);
+  NRK_CHECK_ARG(ws != nullptr, "ivf_search: null workspace");
+  char* w = static_cast<char*>(ws);
+  int* fbc = reinterpret_cast<int*>(w + p.off_fbc);
+  if (hipMemsetAsync(fbc, 0, 16, st) != hipSuccess) return fail(NRK_ELAUNCH, "ivf_search: memset failed");
+  if (n_fallback && hipMemsetAsync(n_fallback, 0, 4, st) != hipSuccess)
+    return fail(NRK_ELAUNCH, "ivf_search: memset failed");
+  if (nq == 0) return NRK_OK;
+  NRK_CHECK_ARG(xq && probe && D && I && list_off, "ivf_search: null pointer");
+  NRK_CHECK_ARG(n == 0 || (xb && xbh_ivf && meta_ivf && stats && pos2id && pos2list), "ivf_search: null index data");
+  const int l2 = metric == NRK_METRIC_L2;
+  auto mark = [&](int i) {
+    if (stage_events) (void)hipEventRecord((hipEvent_t)stage_events[i], st);
+  };
+  int* cnt = reinterpret_cast<int*>(w + p.off_cnt);
+  int* fill = reinterpret_cast<int*>(w + p.off_fill);
+  int* seg = reinterpret_cast<int*>(w + p.off_seg);
+  int* work = reinterpret_cast<int*>(w + p.off_work);
+  int* sp = reinterpret_cast<int*>(w + p.off_sp);
+  uint16_t* qh = reinterpret_cast<uint16_t*>(w + p.off_qh);
+  double* qmeta = reinterpret_cast<double*>(w + p.off_qmeta);
+  uint16_t* qi = reinterpret_cast<uint16_t*>(w + p.off_qi);
+  float* ps = reinterpret_cast<float*>(w + p.off_ps);
+  int* pi = reinterpret_cast<int*>(w + p.off_pi);
+  float* pt = reinterpret_cast<float*>(w + p.off_pt);
+  FbState fb;
+  fb.list = reinterpret_cast<int*>(w + p.off_fbl);
+  fb.count = fbc;
+  fb.slots = p.fb_slots;
+  fb.thr_g = reinterpret_cast<double*>(w + p.off_fbt);
+  fb.thr_i = reinterpret_cast<int64_t*>(w + p.off_fbi);
+  fb.n = reinterpret_cast<int*>(w + p.off_fbn);
+  fb.force = env_int("NRK_FORCE_FALLBACK", 0);
+  double* fcg = reinterpret_cast<double*>(w + p.off_fcg);
+  int64_t* fci = reinterpret_cast<int64_t*>(w + p.off_fci);
+  int* ovl = reinterpret_cast<int*>(w + p.off_ovl);
+  IvfFb ivf{pos2id, pos2list, list_off, probe, nprobe};
+  const int64_t npairs = nq * nprobe;
+
+  mark(0);
+  // group (query, probe) pairs by list
+  if (hipMemsetAsync(cnt, 0, (size_t)nlist * 4, st) != hipSuccess ||
+      hipMemsetAsync(sp, 0xff, (size_t)p.max_rows * 4, st) != hipSuccess ||
+      hipMemsetAsync(pi, 0xff, (size_t)nq * p.U * 4, st) != hipSuccess ||
+      hipMemsetAsync(pt, 0xff, (size_t)nq * nprobe * p.cmax * 2 * 4, st) != hipSuccess)
+    return fail(NRK_ELAUNCH, "ivf_search: memset failed");
+  hipLaunchKernelGGL(query_prepare_kernel, dim3((unsigned)cdiv(p.nq_pad, 4)), dim3(256), 0, st, xq, nq, p.nq_pad, d,
+                     p.dp, qh, qmeta);
+  NRK_CHECK_LAUNCH("query_prepare_kernel");
+  hipLaunchKernelGGL(ivf_count_kernel, dim3((unsigned)cdiv(npairs, 256)), dim3(256), 0, st, probe, npairs, nlist, cnt);
+  NRK_CHECK_LAUNCH("ivf_count_kernel");
+  hipLaunchKernelGGL(ivf_plan_kernel, dim3(1), dim3(1024), 0, st, cnt, list_off, nlist, p.wq, p.ch, seg, work, fill);
+  NRK_CHECK_LAUNCH("ivf_plan_kernel");
+  hipLaunchKernelGGL(ivf_scatter_kernel, dim3((unsigned)cdiv(npairs, 256)), dim3(256), 0, st, probe, npairs, nlist,
+                     seg, fill, sp);
+  NRK_CHECK_LAUNCH("ivf_scatter_kernel");
+  hipLaunchKernelGGL(ivf_gather_kernel, dim3((unsigned)cdiv(p.max_rows, 4)), dim3(256), 0, st, qh, p.dp, nprobe, sp,
+                     seg, nlist, p.max_rows, qi);
+  NRK_CHECK_LAUNCH("ivf_gather_kernel");
+
+  mark(1);
+  if (n > 0) {
+    screen_fn fn = pick_screen(p.dp, p.qt, p.M, l2 != 0, 2);
+    if (!fn) return fail(NRK_EUNSUPPORTED, "ivf_search: no screen kernel for dp=%d", p.dp);
+    IvfScreen is{work, list_off, seg, sp, nlist, p.ch, p.cmax};
+    hipLaunchKernelGGL(fn, dim3((unsigned)p.ub), dim3(p.waves * 64), 0, st, qi, xbh_ivf, meta_ivf, nq, n, 0, 0, 0, 1,
+                       ps, pi, pt, nullptr, is);
+    NRK_CHECK_LAUNCH("screen_kernel (ivf)");
+  }
+
+  mark(2);
+  {
+    const int P = host_pow2ceil(p.U), P2 = host_pow2ceil(p.KP);
+    const size_t smem = (size_t)P * 16 + (size_t)P2 * 16 + (size_t)d * 4;
+    if (smem > 150 * 1024) return fail(NRK_EUNSUPPORTED, "ivf_search: merge needs %zu B LDS", smem);
+    hipLaunchKernelGGL(merge_rescore_kernel, dim3((unsigned)nq), dim3(256), smem, st, ps, pi, pt, nprobe * p.cmax,
+                       p.M, p.KP, k, p.dp, xq, xb, n, d, l2, qmeta, stats, nullptr, D, I, S, id_offset, fb, pos2id);
+    NRK_CHECK_LAUNCH("merge_rescore_kernel (ivf)");
+  }
+
+  mark(3);
+  if (n > 0) {
+    const int64_t ntiles = cdiv(n, (int64_t)FB_TR);
+    const int grid = (int)(ntiles < 2048 ? ntiles : 2048);
+    hipLaunchKernelGGL(fallback_scan_kernel, dim3(grid), dim3(256), (size_t)FB_TR * (d + 1) * 4, st, xq, xb, n, d, l2,
+                       fb, fcg, fci, p.fb_cap, ivf);
+    NRK_CHECK_LAUNCH("fallback_scan_kernel (ivf)");
+  }
+  hipLaunchKernelGGL(fallback_select_kernel, dim3(256), dim3(256), (size_t)host_pow2ceil(p.fb_cap) * 16, st, fb, fcg,
+                     fci, p.fb_cap, k, l2, D, I, S, id_offset, ovl);
+  NRK_CHECK_LAUNCH("fallback_select_kernel (ivf)");
+  int rc = exact_launch(xq, nq, xb, n, d, k, l2, ovl, fbc + 1, 256, D, I, S, id_offset, st, ivf);
+  if (rc != NRK_OK) return rc;
+  mark(4);
+  if (n_fallback && hipMemcpyAsync(n_fallback, fbc, 4, hipMemcpyDeviceToDevice, st) != hipSuccess)
+    return fail(NRK_ELAUNCH, "ivf_search: copy of fallback count failed");
   return NRK_OK;
 }

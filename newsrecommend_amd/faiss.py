@@ -2,6 +2,8 @@
 Python API the reference's retrieval path uses).
 
 Reference call sites (Retrieval.py):
+  :12-18 clustering = faiss.Clustering(256, 300); .niter; .train(x, IndexHNSWFlat(256, 32))
+  :21-23 _, assign = index.search(xb, 1); cluster_to_articles (IndexIVFFlat.list_ids)
   :25  centroid_index = faiss.IndexFlatL2(embeddings_size)
   :26  centroid_index.add(centroids)
   :31-32 _, I = centroid_index.search(profile, 1)
@@ -161,6 +163,291 @@ class IndexFlatIP(IndexFlat):
 class IndexFlatL2(IndexFlat):
     def __init__(self, d: int, device=None):
         super().__init__(d, METRIC_L2, device)
+
+
+class IndexHNSWFlat(IndexFlat):
+    """faiss.IndexHNSWFlat(d, M) (Retrieval.py:16), the assignment index of the
+    reference's k-means and of `index.search(xb, 1)` (Retrieval.py:21).
+
+    faiss's HNSW is an approximate graph walk over the centroids; on the GPU a
+    brute-force pass over a few hundred centroids is cheaper than a graph walk,
+    so this index answers EXACTLY (recall 1.0, a superset of HNSW's quality;
+    DESIGN.md).  `M` and `hnsw.efSearch` are accepted and recorded only."""
+
+    class _Params:
+        def __init__(self, M):
+            self.M = M
+            self.efSearch = 16
+            self.efConstruction = 40
+
+    def __init__(self, d: int, M: int = 32, metric: int = METRIC_L2, device=None):
+        super().__init__(d, metric, device)
+        self.hnsw = self._Params(int(M))
+
+
+# ------------------------------------------------------------- k-means --
+class Clustering:
+    """faiss.Clustering(d, k) (Retrieval.py:12-18): `.niter`, `.verbose`,
+    `.seed`, `.max_points_per_centroid`, `.spherical`, `.train(x, index)`,
+    `.centroids`, `.obj`.
+
+    Algorithm (faiss's, with the deterministic choices restated in
+    oracle/ivf_oracle.py): subsample to k * max_points_per_centroid rows,
+    init from random distinct rows, then `niter` x {assign with `index`
+    (reset + add(centroids) + search(x, 1), as faiss does), centroid = mean of
+    members (nrk_group_by_list + nrk_kmeans_update: fp64 sums in id order),
+    split empty clusters}.  All arithmetic on the GPU; only the split step
+    reads the k cluster sizes back."""
+
+    def __init__(self, d: int, k: int, device=None):
+        self.d = int(d)
+        self.k = int(k)
+        self.niter = 25
+        self.nredo = 1
+        self.verbose = False
+        self.spherical = False
+        self.seed = 1234
+        self.max_points_per_centroid = 256
+        self.min_points_per_centroid = 39
+        self.device = torch.device(device) if device is not None else None
+        self.centroids = torch.empty(0, dtype=torch.float32)
+        self.obj: list[float] = []
+        self.iteration_stats: list[dict] = []
+
+    def _subsample(self, x: torch.Tensor) -> torch.Tensor:
+        n = x.shape[0]
+        cap = self.k * self.max_points_per_centroid
+        if n > cap:
+            perm = np.sort(np.random.default_rng(self.seed).permutation(n)[:cap])
+            return x[torch.from_numpy(perm).to(x.device)].contiguous()
+        return x
+
+    def _split(self, cent: torch.Tensor, counts: np.ndarray, n: int) -> int:
+        """faiss split_clusters: refill empty clusters from a size-weighted
+        random cluster with a +-1/1024 symmetric perturbation."""
+        if (counts > 0).all():
+            return 0
+        c = cent.cpu().numpy()
+        k, d = c.shape
+        rng = np.random.default_rng(1234)
+        hassign = counts.astype(np.float64).copy()
+        up, dn = np.float32(1 + 1.0 / 1024), np.float32(1 - 1.0 / 1024)
+        even = (np.arange(d) % 2) == 0
+        nsplit = 0
+        for ci in range(k):
+            if hassign[ci] != 0:
+                continue
+            cj = 0
+            while True:
+                if rng.random() < (hassign[cj] - 1.0) / float(n - k):
+                    break
+                cj = (cj + 1) % k
+            c[ci] = c[cj]
+            c[ci] = np.where(even, c[ci] * up, c[ci] * dn)
+            c[cj] = np.where(even, c[cj] * dn, c[cj] * up)
+            hassign[ci] = np.floor(hassign[cj] / 2)
+            hassign[cj] -= hassign[ci]
+            nsplit += 1
+        cent.copy_(torch.from_numpy(c))
+        return nsplit
+
+    def train(self, x, index=None):
+        L = _lib.load()
+        if index is None:
+            index = IndexFlatL2(self.d, device=self.device)
+        dev = index.device
+        xt = x.detach().to(dev, torch.float32).contiguous() if isinstance(x, torch.Tensor) else \
+            torch.from_numpy(np.ascontiguousarray(x, np.float32)).to(dev)
+        if xt.dim() != 2 or xt.shape[1] != self.d:
+            raise AssertionError(f"expected (n, {self.d}) training data")
+        n0 = xt.shape[0]
+        if n0 < self.k:
+            raise RuntimeError(f"Number of training points ({n0}) should be at least as large as number of "
+                               f"clusters ({self.k})")
+        xs = self._subsample(xt)
+        n = xs.shape[0]
+        init = np.random.default_rng(self.seed + 1).permutation(n)[: self.k]
+        cent = xs[torch.from_numpy(init).to(dev)].contiguous()
+        list_off = torch.empty(self.k + 1, dtype=torch.int64, device=dev)
+        pos2id = torch.empty(n, dtype=torch.int64, device=dev)
+        pos2list = torch.empty(n, dtype=torch.int32, device=dev)
+        bad = torch.zeros(1, dtype=torch.int32, device=dev)
+        sz = _lib.c_size(0)
+        _lib.check(L.nrk_group_by_list_workspace(n, self.k, sz), "group_by_list_workspace")
+        ws = torch.empty(max(sz.value, 1), dtype=torch.uint8, device=dev)
+        self.obj = []
+        self.iteration_stats = []
+        with torch.cuda.device(dev):
+            for it in range(self.niter):
+                index.reset()
+                index.add(cent)
+                _, I, S = index.search_device(xs, 1, exact_scores=True)
+                labels = I[:, 0].contiguous()
+                obj = float(S[:, 0].sum().item())
+                _lib.check(L.nrk_group_by_list(_lib.ptr(labels), n, self.k, _lib.ptr(list_off), _lib.ptr(pos2id),
+                                               _lib.ptr(pos2list), _lib.ptr(bad), _lib.ptr(ws), ws.numel(),
+                                               _lib.stream(dev)), "group_by_list")
+                _lib.check(L.nrk_kmeans_update(_lib.ptr(xs), self.d, _lib.ptr(list_off), _lib.ptr(pos2id), self.k,
+                                               _lib.ptr(cent), _lib.stream(dev)), "kmeans_update")
+                counts = torch.diff(list_off).cpu().numpy()
+                nsplit = self._split(cent, counts, n)
+                if self.spherical:
+                    cent.div_(cent.double().norm(dim=1, keepdim=True).clamp_min(1e-20).float())
+                self.obj.append(obj)
+                self.iteration_stats.append({"obj": obj, "nsplit": nsplit})
+                if self.verbose:
+                    print(f"  Iteration {it} objective={obj:g} nsplit={nsplit}")
+        index.reset()
+        index.add(cent)
+        self.centroids = cent
+        return self
+
+
+def kmeans_assign(index: "IndexFlat", x: torch.Tensor):
+    """labels of x under `index` (nearest centroid), device in/out."""
+    _, I = index.search_device(x, 1)
+    return I[:, 0].contiguous()
+
+
+# --------------------------------------------------------------- IVF --
+class IndexIVFFlat:
+    """faiss.IndexIVFFlat(quantizer, d, nlist, metric) (BASELINE configs[3]).
+
+    train(x): faiss Clustering(d, nlist) with the quantizer as the assignment
+    index (the quantizer ends up holding the centroids).  add(x): ids continue
+    from ntotal; rows are assigned by the quantizer and the inverted lists
+    (ids ascending inside a list) are rebuilt on the device.  search(x, k):
+    the quantizer's top-`nprobe` lists, then nrk_ivf_search: the exact top-k
+    among the probed lists' items (D/I as IndexFlat).  HBM per row: f32 row
+    (exact rescoring) + bf16 list-major screening row + norms + 12 B of list
+    bookkeeping."""
+
+    def __init__(self, quantizer: IndexFlat, d: int, nlist: int, metric: int = METRIC_L2, device=None):
+        if metric not in (METRIC_INNER_PRODUCT, METRIC_L2):
+            raise ValueError(f"unsupported metric {metric}")
+        self.quantizer = quantizer
+        self.d = int(d)
+        self.nlist = int(nlist)
+        self.metric_type = int(metric)
+        self.nprobe = 1
+        self.cp = Clustering(d, nlist)
+        self.device = quantizer.device if device is None else torch.device(device)
+        self.is_trained = quantizer.ntotal == self.nlist
+        self.flat = IndexFlat(d, metric, device=self.device)  # id-order rows, bf16 copy, norms, stats
+        self._assign = torch.empty(0, dtype=torch.int64, device=self.device)
+        self._ws = None
+        self.last_fallback = None
+        self._lists_valid = True
+        self._n_lists = 0
+        self.list_off = torch.zeros(self.nlist + 1, dtype=torch.int64, device=self.device)
+        self.pos2id = torch.empty(0, dtype=torch.int64, device=self.device)
+        self.pos2list = torch.empty(0, dtype=torch.int32, device=self.device)
+        self.xbh_ivf = torch.empty((0, self.flat.dp), dtype=torch.int16, device=self.device)
+        self.meta_ivf = torch.empty((0, 2), dtype=torch.float32, device=self.device)
+        self.max_list = 0
+
+    @property
+    def ntotal(self) -> int:
+        return self.flat.ntotal
+
+    def train(self, x):
+        if self.quantizer.ntotal == self.nlist and self.is_trained:
+            return
+        self.cp.train(x, self.quantizer)
+        self.is_trained = True
+
+    def _rebuild_lists(self):
+        L = _lib.load()
+        n = self.ntotal
+        dev = self.device
+        with torch.cuda.device(dev):
+            self.pos2id = torch.empty(n, dtype=torch.int64, device=dev)
+            self.pos2list = torch.empty(n, dtype=torch.int32, device=dev)
+            bad = torch.zeros(1, dtype=torch.int32, device=dev)
+            sz = _lib.c_size(0)
+            _lib.check(L.nrk_group_by_list_workspace(n, self.nlist, sz), "group_by_list_workspace")
+            ws = torch.empty(max(sz.value, 1), dtype=torch.uint8, device=dev)
+            _lib.check(L.nrk_group_by_list(_lib.ptr(self._assign), n, self.nlist, _lib.ptr(self.list_off),
+                                           _lib.ptr(self.pos2id), _lib.ptr(self.pos2list), _lib.ptr(bad),
+                                           _lib.ptr(ws), ws.numel(), _lib.stream(dev)), "group_by_list")
+            self.xbh_ivf = torch.empty((n, self.flat.dp), dtype=torch.int16, device=dev)
+            self.meta_ivf = torch.empty((n, 2), dtype=torch.float32, device=dev)
+            _lib.check(L.nrk_ivf_pack(_lib.ptr(self.pos2id), n, self.d, _lib.ptr(self.flat._xbh[:n]),
+                                      _lib.ptr(self.flat._meta[:n]), _lib.ptr(self.xbh_ivf), _lib.ptr(self.meta_ivf),
+                                      _lib.stream(dev)), "ivf_pack")
+            if int(bad.item()):
+                raise _lib.NrkError("IndexIVFFlat.add: assignment outside [0, nlist)")
+            sizes = torch.diff(self.list_off)
+            self.max_list = int(sizes.max().item()) if n else 0
+
+    def add(self, x):
+        if not self.is_trained:
+            raise RuntimeError("IndexIVFFlat: train() before add()")
+        xt, _ = self.flat._as_input(x)
+        if xt.shape[0] == 0:
+            return
+        labels = kmeans_assign(self.quantizer, xt)
+        self.flat.add(xt)
+        self._assign = torch.cat([self._assign, labels])
+        self._rebuild_lists()
+
+    def reset(self):
+        self.flat.reset()
+        self._assign = torch.empty(0, dtype=torch.int64, device=self.device)
+        self.list_off.zero_()
+        self.max_list = 0
+
+    def get_list_size(self, l: int) -> int:
+        return int((self.list_off[l + 1] - self.list_off[l]).item())
+
+    def list_ids(self, l: int) -> np.ndarray:
+        """ids of inverted list l, ascending (cluster_to_articles, Retrieval.py:22-23)."""
+        lo, hi = int(self.list_off[l].item()), int(self.list_off[l + 1].item())
+        return self.pos2id[lo:hi].cpu().numpy()
+
+    def _workspace(self, nbytes: int):
+        if self._ws is None or self._ws.numel() < nbytes:
+            self._ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    def search_device(self, xq: torch.Tensor, k: int, exact_scores: bool = False, id_offset: int = 0,
+                      stage_events=None, probe: torch.Tensor | None = None):
+        k = int(k)
+        if k <= 0:
+            raise ValueError("k must be positive")
+        L = _lib.load()
+        nq = xq.shape[0]
+        nprobe = max(1, min(int(self.nprobe), self.nlist))
+        if probe is None:
+            _, probe = self.quantizer.search_device(xq, nprobe)
+        dev = self.device
+        D = torch.empty((nq, k), dtype=torch.float32, device=dev)
+        I = torch.empty((nq, k), dtype=torch.int64, device=dev)
+        S = torch.empty((nq, k), dtype=torch.float64, device=dev) if exact_scores else None
+        if self.last_fallback is None:
+            self.last_fallback = torch.zeros(1, dtype=torch.int32, device=dev)
+        n = self.ntotal
+        f = self.flat
+        with torch.cuda.device(dev):
+            sz = _lib.c_size(0)
+            _lib.check(L.nrk_ivf_search_workspace(nq, nprobe, self.nlist, self.max_list, self.d, k, sz),
+                       "ivf_search_workspace")
+            ws = self._workspace(sz.value)
+            _lib.check(L.nrk_ivf_search(
+                _lib.ptr(xq), nq, _lib.ptr(probe.contiguous()), nprobe, _lib.ptr(f._xb[:n]) if n else None,
+                _lib.ptr(self.xbh_ivf) if n else None, _lib.ptr(self.meta_ivf) if n else None, _lib.ptr(f._stats),
+                _lib.ptr(self.list_off), _lib.ptr(self.pos2id) if n else None,
+                _lib.ptr(self.pos2list) if n else None, self.nlist, n, self.max_list, self.d, k, self.metric_type,
+                _lib.ptr(D), _lib.ptr(I), _lib.ptr(S), int(id_offset), _lib.ptr(self.last_fallback), _lib.ptr(ws),
+                ws.numel(), stage_events.ev if stage_events is not None else None, _lib.stream(dev)), "ivf_search")
+        return (D, I, S) if exact_scores else (D, I)
+
+    def search(self, x, k):
+        xt, was_numpy = self.flat._as_input(x)
+        D, I = self.search_device(xt, k)
+        if was_numpy:
+            return D.cpu().numpy(), I.cpu().numpy()
+        return D, I
 
 
 def knn_exact(xq: torch.Tensor, xb: torch.Tensor, k: int, metric: int = METRIC_L2, id_offset: int = 0):

@@ -1,0 +1,171 @@
+"""GPU parity for the index-building half of retrieval (Retrieval.py:11-23)
+and IVF-Flat search (BASELINE configs[3]) against oracle/ivf_oracle.py:
+grouping by list and k-means centroids bit-exact, IVF indices bit-exact and D
+equal to the fp32 rounding of the same fp64 scores."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ivf_oracle as io
+from oracle import knn_oracle as ko
+
+pytestmark = pytest.mark.gpu
+
+
+def _mixture(nb, nq, d, seed, centers=64, sigma=0.35):
+    rng = np.random.default_rng(seed)
+    c = rng.standard_normal((centers, d)).astype(np.float32)
+    xb = (c[rng.integers(0, centers, nb)] + sigma * rng.standard_normal((nb, d))).astype(np.float32)
+    xq = (c[rng.integers(0, centers, nq)] + sigma * rng.standard_normal((nq, d))).astype(np.float32)
+    return xq, xb
+
+
+@pytest.mark.parametrize("n,nlist", [(1, 3), (4095, 5), (4096 * 3 + 17, 300), (50_000, 5000)])
+def test_group_by_list(gpu, n, nlist):
+    from newsrecommend_amd import _lib
+
+    rng = np.random.default_rng(n)
+    assign = rng.integers(0, nlist, n).astype(np.int64)
+    if nlist > 4:
+        assign[assign == 2] = 1  # an empty list
+    L = _lib.load()
+    a = torch.from_numpy(assign).cuda()
+    off = torch.empty(nlist + 1, dtype=torch.int64, device="cuda")
+    p2i = torch.empty(n, dtype=torch.int64, device="cuda")
+    p2l = torch.empty(n, dtype=torch.int32, device="cuda")
+    bad = torch.zeros(1, dtype=torch.int32, device="cuda")
+    sz = _lib.c_size(0)
+    _lib.check(L.nrk_group_by_list_workspace(n, nlist, sz))
+    ws = torch.empty(sz.value, dtype=torch.uint8, device="cuda")
+    _lib.check(L.nrk_group_by_list(_lib.ptr(a), n, nlist, _lib.ptr(off), _lib.ptr(p2i), _lib.ptr(p2l), _lib.ptr(bad),
+                                   _lib.ptr(ws), ws.numel(), _lib.stream()))
+    o_off, o_p2i = io.group_by_list(assign, nlist)
+    np.testing.assert_array_equal(off.cpu().numpy(), o_off)
+    np.testing.assert_array_equal(p2i.cpu().numpy(), o_p2i)
+    np.testing.assert_array_equal(p2l.cpu().numpy(), assign[o_p2i])
+    assert bad.item() == 0
+
+
+@pytest.mark.parametrize("metric", [ko.METRIC_L2, ko.METRIC_IP])
+def test_clustering_matches_oracle(gpu, metric):
+    """faiss.Clustering semantics incl. subsampling (n > k * max_points) and
+    the empty-cluster split (duplicated rows make the init pick twins)."""
+    from newsrecommend_amd import faiss as nf
+
+    _, x = _mixture(9000, 1, 32, seed=21, centers=20)
+    x[1::7] = x[0]  # many exact duplicates -> twin centroids -> empty clusters
+    k = 40
+    cl = nf.Clustering(32, k)
+    cl.niter = 6
+    cl.max_points_per_centroid = 200  # 9000 > 40 * 200: subsample path
+    idx = nf.IndexFlat(32, metric)
+    cl.train(x, idx)
+    cent, obj = io.kmeans(x, k, niter=6, seed=1234, max_points_per_centroid=200, metric=metric)
+    np.testing.assert_array_equal(cl.centroids.cpu().numpy(), cent)
+    np.testing.assert_allclose(cl.obj, obj, rtol=1e-9)
+    assert sum(s["nsplit"] for s in cl.iteration_stats) > 0
+    assert idx.ntotal == k  # the assignment index ends holding the centroids (faiss)
+
+
+def _ivf(xb, nlist, metric, seed=0):
+    from newsrecommend_amd import faiss as nf
+
+    q = nf.IndexFlatL2(xb.shape[1])
+    ivf = nf.IndexIVFFlat(q, xb.shape[1], nlist, metric)
+    ivf.cp.niter = 4
+    ivf.train(xb)
+    ivf.add(xb)
+    return ivf
+
+
+@pytest.mark.parametrize("metric", [ko.METRIC_IP, ko.METRIC_L2])
+@pytest.mark.parametrize("d,k,nprobe", [(64, 5, 8), (128, 10, 4), (96, 40, 16), (256, 5, 3), (128, 1, 1)])
+def test_ivf_search_matches_oracle(gpu, metric, d, k, nprobe):
+    xq, xb = _mixture(40_000, 300, d, seed=d + k)
+    ivf = _ivf(xb, 50, metric)
+    ivf.nprobe = nprobe
+    D, I = ivf.search(xq, k)
+    cent = ivf.quantizer._xb[:50].cpu().numpy()
+    assign = ivf._assign.cpu().numpy()
+    Do, Io, So, probe = io.ivf_search(xq, xb, cent, assign, nprobe, k, metric)
+    np.testing.assert_array_equal(I, Io)
+    np.testing.assert_array_equal(D, Do)
+    assert ivf.max_list == int(np.bincount(assign, minlength=50).max())
+
+
+def test_ivf_all_lists_equals_flat_and_list_ids(gpu):
+    from newsrecommend_amd import faiss as nf
+
+    xq, xb = _mixture(30_000, 100, 64, seed=5)
+    xb[20_000] = xb[11]
+    xq[0] = xb[11]
+    ivf = _ivf(xb, 20, ko.METRIC_L2)
+    ivf.nprobe = 20
+    D, I = ivf.search(xq, 7)
+    Df, If, _ = ko.exact_search(xq, xb, 7, ko.METRIC_L2)
+    np.testing.assert_array_equal(I, If)
+    np.testing.assert_array_equal(D, Df)
+    assign = ivf._assign.cpu().numpy()
+    for l in (0, 7, 19):
+        np.testing.assert_array_equal(ivf.list_ids(l), np.nonzero(assign == l)[0])
+    flat = nf.IndexFlatL2(64)
+    flat.add(xb)
+    Dg, Ig = flat.search(xq, 7)
+    np.testing.assert_array_equal(Ig, I)
+
+
+@pytest.mark.parametrize("cap", [None, "3"])
+def test_ivf_forced_fallback(gpu, monkeypatch, cap):
+    monkeypatch.setenv("NRK_FORCE_FALLBACK", "1")
+    if cap:
+        monkeypatch.setenv("NRK_FB_CAP", cap)
+    xq, xb = _mixture(20_000, 64, 64, seed=6)
+    for metric in (ko.METRIC_IP, ko.METRIC_L2):
+        ivf = _ivf(xb, 30, metric)
+        ivf.nprobe = 5
+        D, I = ivf.search(xq, 6)
+        Do, Io, _, _ = io.ivf_search(xq, xb, ivf.quantizer._xb[:30].cpu().numpy(), ivf._assign.cpu().numpy(), 5, 6,
+                                     metric)
+        np.testing.assert_array_equal(I, Io)
+        np.testing.assert_array_equal(D, Do)
+        assert int(ivf.last_fallback.item()) == 64
+
+
+def test_ivf_k_exceeds_probed_items_pads(gpu):
+    from newsrecommend_amd import faiss as nf
+
+    xq, xb = _mixture(200, 5, 32, seed=7, centers=4)
+    ivf = _ivf(xb, 40, ko.METRIC_L2)
+    ivf.nprobe = 1
+    D, I = ivf.search(xq, 64)
+    Do, Io, _, _ = io.ivf_search(xq, xb, ivf.quantizer._xb[:40].cpu().numpy(), ivf._assign.cpu().numpy(), 1, 64,
+                                 ko.METRIC_L2)
+    np.testing.assert_array_equal(I, Io)
+    assert (I == -1).any()
+
+
+def test_retrieval_py_flow(gpu):
+    """Retrieval.py:11-34 end to end: Clustering with an IndexHNSWFlat
+    assignment index, index.search(xb, 1), cluster_to_articles, then the
+    centroid IndexFlatL2 search per user profile."""
+    from newsrecommend_amd import faiss as nf
+
+    _, xb = _mixture(12_000, 1, 256, seed=8, centers=40)
+    ids = np.arange(10**6, 10**6 + 12_000)
+    clustering = nf.Clustering(256, 30)
+    clustering.niter = 5
+    index = nf.IndexHNSWFlat(256, 32)
+    clustering.train(xb, index)
+    centroids = nf.vector_float_to_array(clustering.centroids).reshape(30, 256)
+    _, assign = index.search(xb, 1)
+    cluster_to_articles = {i: ids[assign.ravel() == i] for i in range(30)}
+    cent_o, _ = io.kmeans(xb, 30, niter=5, seed=1234, max_points_per_centroid=256)
+    np.testing.assert_array_equal(centroids, cent_o)
+    lab_o, _ = io.assign_nearest(xb, cent_o)
+    np.testing.assert_array_equal(assign.ravel(), lab_o)
+    centroid_index = nf.IndexFlatL2(256)
+    centroid_index.add(centroids)
+    profile = xb[:5].mean(0, keepdims=True)
+    _, I = centroid_index.search(profile, 1)
+    assert I[0, 0] == io.assign_nearest(profile, cent_o)[0][0]
+    assert sum(len(v) for v in cluster_to_articles.values()) == 12_000
