@@ -25,33 +25,44 @@
 namespace nrk {
 
 // ================================================================ prepare ==
+// One wave per row, grid-stride; the three corpus maxima are reduced per wave
+// and published with one atomic each (per-row atomics on three addresses
+// serialise at the L2).
 __global__ void flat_prepare_kernel(const float* __restrict__ xb, int64_t nb, int d, int dp,
                                     uint16_t* __restrict__ xbh, float* __restrict__ meta,
                                     float* __restrict__ stats) {
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (row >= nb) return;
-  double sx2 = 0.0, sh2 = 0.0, sr2 = 0.0;
-  for (int j = lane; j < dp; j += 64) {
-    float x = j < d ? xb[row * d + j] : 0.f;
-    uint16_t h = f32_to_bf16_rne(x);
-    float hf = bf16_to_f32(h);
-    double r = (double)x - (double)hf;
-    sx2 += (double)x * (double)x;
-    sh2 += (double)hf * (double)hf;
-    sr2 += r * r;
-    xbh[row * dp + j] = h;
+  const int64_t wave0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  float m0 = 0.f, m1 = 0.f, m2 = 0.f;
+  for (int64_t row = wave0; row < nb; row += nwaves) {
+    double sx2 = 0.0, sh2 = 0.0, sr2 = 0.0;
+    for (int j = lane; j < dp; j += 64) {
+      float x = j < d ? xb[row * d + j] : 0.f;
+      uint16_t h = f32_to_bf16_rne(x);
+      float hf = bf16_to_f32(h);
+      double r = (double)x - (double)hf;
+      sx2 += (double)x * (double)x;
+      sh2 += (double)hf * (double)hf;
+      sr2 += r * r;
+      xbh[row * dp + j] = h;
+    }
+    sx2 = wave_sum(sx2);
+    sh2 = wave_sum(sh2);
+    sr2 = wave_sum(sr2);
+    const float rn = f64_to_f32_up(sqrt(sr2) * (1.0 + 1e-9));
+    if (lane == 0) {
+      meta[2 * row] = (float)sx2;
+      meta[2 * row + 1] = rn;
+    }
+    m0 = fmaxf(m0, f64_to_f32_up(sqrt(sh2) * (1.0 + 1e-9)));
+    m1 = fmaxf(m1, rn);
+    m2 = fmaxf(m2, f64_to_f32_up(sx2 * (1.0 + 1e-9)));
   }
-  sx2 = wave_sum(sx2);
-  sh2 = wave_sum(sh2);
-  sr2 = wave_sum(sr2);
-  if (lane == 0) {
-    meta[2 * row] = (float)sx2;
-    float rn = f64_to_f32_up(sqrt(sr2) * (1.0 + 1e-9));
-    meta[2 * row + 1] = rn;
-    atomic_max_nonneg(&stats[0], f64_to_f32_up(sqrt(sh2) * (1.0 + 1e-9)));
-    atomic_max_nonneg(&stats[1], rn);
-    atomic_max_nonneg(&stats[2], f64_to_f32_up(sx2 * (1.0 + 1e-9)));
+  if (lane == 0 && wave0 < nb) {
+    atomic_max_nonneg(&stats[0], m0);
+    atomic_max_nonneg(&stats[1], m1);
+    atomic_max_nonneg(&stats[2], m2);
   }
 }
 
@@ -163,13 +174,37 @@ __device__ __forceinline__ void list_insert(float (&ls)[N], int (&li)[N], float 
 //   queries gathered list-major (segments padded to WQ rows); slot_pair maps a
 //   gathered row back to its (query, probe) pair, whose candidates land at
 //   [(pair * cmax + chunk) * 2 + half].
+// MODE 3 (IVF collect): MODE 2's work items, no lane lists: every item whose
+//   screened score reaches the query's threshold is appended to the query's
+//   candidate buffer (rare: the threshold sits just below the k-th best).
+// MODE 4 (IVF lane maxima): MODE 2's work items, MODE 1's epilogue (each lane
+//   writes the maximum screened score of its stream).
 struct IvfScreen {
   const int* work_off;     // [nlist + 1] prefix of work items per list
   const int64_t* list_off; // [nlist + 1] list ranges in the list-major corpus
   const int* seg_off;      // [nlist] first gathered query row of each list
   const int* slot_pair;    // [slots] q * nprobe + p, or -1 for padding
   int nlist, ch, cmax;
+  // MODE 3 (collect): append every item whose screened score >= thr_q[query]
+  const float* thr_q;
+  int* cand_cnt;           // [nq]
+  int* cand_pos;           // [nq][cap] list-major positions
+  int cap, nprobe;
 };
+
+// MODE 3 block-local candidate staging: hits are appended with LDS atomics and
+// flushed at the end of the work item with ONE global atomic per query row
+// (returning global atomics in the epilogue would stall the wave for ~1 us).
+template <int WQ>
+struct CollectLds {
+  static constexpr int CAP = 1024;
+  int n;
+  int qcnt[WQ];
+  int qid[WQ];
+  int base[WQ];
+  int2 ent[CAP];  // {row | rank << 8, position}
+};
+struct NoLds {};
 
 template <int DP, int QT, int M, int WAVES, bool L2, int MODE, int EPI = 0>
 __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
@@ -186,197 +221,270 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
   constexpr int WQ = WAVES * 32 * QT;
   constexpr int BUF = TI * DP + 2 * TI;  // uint16 per buffer: rows + TI float norms
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BUF];
+  __shared__ std::conditional_t<MODE == 3, CollectLds<WQ>, NoLds> cl;
 
   const int nblk = gridDim.x, b = blockIdx.x;
   const int xg = b & 7, jj = b >> 3, q8 = nblk >> 3, r8 = nblk & 7;
-  const int logical = (xg < r8 ? xg * (q8 + 1) : r8 * (q8 + 1) + (xg - r8) * q8) + jj;
-  int c, qt;
-  int64_t ibeg, iend, seg0 = 0;
-  if constexpr (MODE == 2) {
-    if (logical >= iv.work_off[iv.nlist]) return;
-    int lo = 0, hi = iv.nlist;  // largest l with work_off[l] <= logical (empty lists own no items)
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (iv.work_off[mid] <= logical) lo = mid;
-      else hi = mid;
+  const int logical0 = (xg < r8 ? xg * (q8 + 1) : r8 * (q8 + 1) + (xg - r8) * q8) + jj;
+  // IVF modes loop persistently over the device work table; flat modes run
+  // exactly one item per block
+  const int total = MODE >= 2 ? iv.work_off[iv.nlist] : nblk;
+  for (int logical = logical0; logical < total; logical += nblk) {
+    if (logical != logical0) __syncthreads();  // the previous item is done with the LDS buffers
+    int c, qt;
+    int64_t ibeg, iend, seg0 = 0;
+    if constexpr (MODE >= 2) {
+      int lo = 0, hi = iv.nlist;  // largest l with work_off[l] <= logical (empty lists own no items)
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (iv.work_off[mid] <= logical) lo = mid;
+        else hi = mid;
+      }
+      const int64_t lb = iv.list_off[lo], le = iv.list_off[lo + 1];
+      const int nchl = (int)cdiv(le - lb, (int64_t)iv.ch);
+      const int local = logical - iv.work_off[lo];
+      qt = local / nchl;
+      c = local - qt * nchl;
+      ibeg = lb + (int64_t)c * iv.ch;
+      iend = ibeg + iv.ch < le ? ibeg + iv.ch : le;
+      seg0 = iv.seg_off[lo];
+    } else {
+      c = logical / nqt;
+      qt = logical - c * nqt;
+      ibeg = (int64_t)c * chunk;
+      iend = ibeg + chunk < nb ? ibeg + chunk : nb;
     }
-    const int64_t lb = iv.list_off[lo], le = iv.list_off[lo + 1];
-    const int nchl = (int)cdiv(le - lb, (int64_t)iv.ch);
-    const int local = logical - iv.work_off[lo];
-    qt = local / nchl;
-    c = local - qt * nchl;
-    ibeg = lb + (int64_t)c * iv.ch;
-    iend = ibeg + iv.ch < le ? ibeg + iv.ch : le;
-    seg0 = iv.seg_off[lo];
-    qh += seg0 * DP;  // this list's query segment
-  } else {
-    c = logical / nqt;
-    qt = logical - c * nqt;
-    ibeg = (int64_t)c * chunk;
-    iend = ibeg + chunk < nb ? ibeg + chunk : nb;
-  }
 
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int r = lane & 31, h = lane >> 5;
-  const int ntiles = (int)cdiv(cdiv(iend - ibeg, TI), tstride);  // visited tiles
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int ntiles = (int)cdiv(cdiv(iend - ibeg, TI), tstride);  // visited tiles
 
-  bf16x8 qf[QT][KS];
-  int64_t qidx[QT];
-#pragma unroll
-  for (int t = 0; t < QT; ++t) {
-    qidx[t] = (int64_t)qt * WQ + (w * QT + t) * 32 + r;  // < nq_pad (zero rows)
-    const bf16x8* src = reinterpret_cast<const bf16x8*>(qh + qidx[t] * DP + 8 * h);
-#pragma unroll
-    for (int s = 0; s < KS; ++s) qf[t][s] = src[2 * s];
-  }
-  float ls[QT][M + 1];
-  int li[QT][M + 1];
-  float tau[QT];
-#pragma unroll
-  for (int t = 0; t < QT; ++t) {
-    tau[t] = (MODE == 0 && tau_q && qidx[t] < nq) ? tau_q[qidx[t]] : -INFINITY;
-#pragma unroll
-    for (int j = 0; j <= M; ++j) {
-      ls[t][j] = -INFINITY;
-      li[t][j] = -1;
+    bf16x8 qf[QT][KS];
+    int64_t qidx[QT];
+  #pragma unroll
+    for (int t = 0; t < QT; ++t) {
+      qidx[t] = (int64_t)qt * WQ + (w * QT + t) * 32 + r;  // < nq_pad (zero rows)
+      const bf16x8* src = reinterpret_cast<const bf16x8*>(qh + (seg0 + qidx[t]) * DP + 8 * h);
+  #pragma unroll
+      for (int s = 0; s < KS; ++s) qf[t][s] = src[2 * s];
     }
-  }
-
-  // HBM -> LDS through chunk-relative buffer descriptors: rows past the chunk
-  // fall outside num_records and read as 0 (masked in the epilogue); each
-  // lane's inverse-swizzled 32-bit offset is fixed, only the scalar tile
-  // offset changes, so staging costs no per-tile vector address math.
-  typedef __attribute__((address_space(3))) void* lds_ptr;
-  const int64_t cnt = iend - ibeg > 0 ? iend - ibeg : 0;
-  const BufRsrc xrs = make_rsrc(xbh + ibeg * DP, (int)(cnt * DP * 2));
-  const BufRsrc nrs = make_rsrc(xmeta + 2 * ibeg, (int)(cnt * 8));
-  int voff[GPT];
-#pragma unroll
-  for (int u = 0; u < GPT; ++u) {
-    const int p = u * NT + tid;
-    const int row = p / CPR, pc = p % CPR;
-    voff[u] = row * DP * 2 + 16 * (pc ^ swz<CPR>(row));
-  }
-  auto issue_tile = [&](int it, auto buf_c) {
-    constexpr int buf = decltype(buf_c)::value;
-    const int soff = it * tstride * TI * DP * 2;
-#pragma unroll
-    for (int u = 0; u < GPT; ++u)
-      buffer_load_lds16(xrs, lds + buf * BUF + (u * NT + w * 64) * 8, voff[u], soff);
-    if constexpr (L2) {
-      if (w == 0)
-        buffer_load_lds4(nrs, lds + buf * BUF + TI * DP, lane * 8, it * tstride * TI * 8);
+    float ls[QT][M + 1];
+    int li[QT][M + 1];
+    float tau[QT];
+    float cthr[QT];  // MODE 3: collect threshold of the lane's query
+    int cq[QT];      // MODE 3: the lane's query (-1: padding row)
+  #pragma unroll
+    for (int t = 0; t < QT; ++t) {
+      tau[t] = (MODE == 0 && tau_q && qidx[t] < nq) ? tau_q[qidx[t]] : -INFINITY;
+      if constexpr (MODE == 3) {
+        const int pair = iv.slot_pair[seg0 + qidx[t]];
+        cq[t] = pair >= 0 ? pair / iv.nprobe : -1;
+        cthr[t] = pair >= 0 ? iv.thr_q[cq[t]] : INFINITY;
+        const int row = (w * QT + t) * 32 + r;
+        if (h == 0) {
+          cl.qid[row] = cq[t];
+          cl.qcnt[row] = 0;
+        }
+      }
+  #pragma unroll
+      for (int j = 0; j <= M; ++j) {
+        ls[t][j] = -INFINITY;
+        li[t][j] = -1;
+      }
     }
-  };
 
-  // one 64-item tile (buffer index is a compile-time constant: immediate LDS offsets)
-  auto tile = [&](int it, auto buf_c) {
-    constexpr int buf = decltype(buf_c)::value;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // tile `it` landed; everyone is done with the other buffer
-    if (it + 1 < ntiles) issue_tile(it + 1, std::integral_constant<int, buf ^ 1>{});
+    // HBM -> LDS through chunk-relative buffer descriptors: rows past the chunk
+    // fall outside num_records and read as 0 (masked in the epilogue); each
+    // lane's inverse-swizzled 32-bit offset is fixed, only the scalar tile
+    // offset changes, so staging costs no per-tile vector address math.
+    typedef __attribute__((address_space(3))) void* lds_ptr;
+    const int64_t cnt = iend - ibeg > 0 ? iend - ibeg : 0;
+    const BufRsrc xrs = make_rsrc(xbh + ibeg * DP, (int)(cnt * DP * 2));
+    const BufRsrc nrs = make_rsrc(xmeta + 2 * ibeg, (int)(cnt * 8));
+    int voff[GPT];
+  #pragma unroll
+    for (int u = 0; u < GPT; ++u) {
+      const int p = u * NT + tid;
+      const int row = p / CPR, pc = p % CPR;
+      voff[u] = row * DP * 2 + 16 * (pc ^ swz<CPR>(row));
+    }
+    auto issue_tile = [&](int it, auto buf_c) {
+      constexpr int buf = decltype(buf_c)::value;
+      const int soff = it * tstride * TI * DP * 2;
+  #pragma unroll
+      for (int u = 0; u < GPT; ++u)
+        buffer_load_lds16(xrs, lds + buf * BUF + (u * NT + w * 64) * 8, voff[u], soff);
+      if constexpr (L2) {
+        if (w == 0)
+          buffer_load_lds4(nrs, lds + buf * BUF + TI * DP, lane * 8, it * tstride * TI * 8);
+      }
+    };
 
-    const uint16_t* tl = lds + buf * BUF;
-    const float* lnorm = reinterpret_cast<const float*>(tl + TI * DP);
-    const int64_t i0 = ibeg + (int64_t)it * tstride * TI;
-    const int nvalid = (int)((iend - i0) < TI ? (iend - i0) : TI);
-#pragma unroll
-    for (int st = 0; st < TI / 32; ++st) {
-      f32x16 acc[QT];
-#pragma unroll
-      for (int t = 0; t < QT; ++t)
-#pragma unroll
-        for (int g = 0; g < 16; ++g) acc[t][g] = 0.f;
-      const int row = 32 * st + r;
-      const uint16_t* arow = tl + row * DP;
-      const int sw = swz<CPR>(row);
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(arow + 8 * ((2 * s + h) ^ sw));
-#pragma unroll
+    // one 64-item tile (buffer index is a compile-time constant: immediate LDS offsets)
+    auto tile = [&](int it, auto buf_c) {
+      constexpr int buf = decltype(buf_c)::value;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // tile `it` landed; everyone is done with the other buffer
+      if (it + 1 < ntiles) issue_tile(it + 1, std::integral_constant<int, buf ^ 1>{});
+
+      const uint16_t* tl = lds + buf * BUF;
+      const float* lnorm = reinterpret_cast<const float*>(tl + TI * DP);
+      const int64_t i0 = ibeg + (int64_t)it * tstride * TI;
+      const int nvalid = (int)((iend - i0) < TI ? (iend - i0) : TI);
+  #pragma unroll
+      for (int st = 0; st < TI / 32; ++st) {
+        f32x16 acc[QT];
+  #pragma unroll
         for (int t = 0; t < QT; ++t)
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[t][s], acc[t], 0, 0, 0);
-      }
-      if constexpr (EPI == 2) {  // ablation: MFMA only
-#pragma unroll
-        for (int t = 0; t < QT; ++t) asm volatile("" ::"v"(acc[t][0]), "v"(acc[t][5]), "v"(acc[t][15]));
-        continue;
-      }
-      // Epilogue.  MASKED only for the (rare) partial last tile of a chunk: a
-      // wave-uniform branch, so full tiles carry no per-score selects.
-      auto epilogue = [&](auto masked_tag) {
-        constexpr bool MASKED = decltype(masked_tag)::value;
-#pragma unroll
-        for (int t = 0; t < QT; ++t) {
-          float sc[16];
-#pragma unroll
-          for (int g = 0; g < 16; ++g) {
-            const int ir = 32 * st + (g & 3) + 8 * (g >> 2) + 4 * h;
-            float v = acc[t][g];
-            if constexpr (L2) v = fmaf(2.f, v, -lnorm[ir]);
-            if constexpr (MASKED) v = ir < nvalid ? v : -INFINITY;
-            sc[g] = v;
-          }
-          // IEEE maximum (v_maximum3_f32): no canonicalising moves on MFMA outputs
-          float m4[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            m4[j] = fmax_ieee(fmax_ieee(sc[4 * j], sc[4 * j + 1]), fmax_ieee(sc[4 * j + 2], sc[4 * j + 3]));
-          const float m = fmax_ieee(fmax_ieee(m4[0], m4[1]), fmax_ieee(m4[2], m4[3]));
-          if constexpr (MODE == 1 || EPI == 1) {  // pre-pass (or ablation): lane maximum only
-            ls[t][0] = fmax_ieee(ls[t][0], m);
-            continue;
-          }
-          // rare path: descend only into 4-row groups that beat the threshold
-          if (__any(m > fmaxf(ls[t][M], tau[t]))) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              if (__any(m4[j] > fmaxf(ls[t][M], tau[t]))) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                  const int g = 4 * j + i;
-                  const int ir = 32 * st + i + 8 * j + 4 * h;
-                  const float thr = fmaxf(ls[t][M], tau[t]);
-                  if (sc[g] > thr) list_insert<M + 1>(ls[t], li[t], sc[g], (int)(i0 + ir));
+  #pragma unroll
+          for (int g = 0; g < 16; ++g) acc[t][g] = 0.f;
+        const int row = 32 * st + r;
+        const uint16_t* arow = tl + row * DP;
+        const int sw = swz<CPR>(row);
+  #pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(arow + 8 * ((2 * s + h) ^ sw));
+  #pragma unroll
+          for (int t = 0; t < QT; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[t][s], acc[t], 0, 0, 0);
+        }
+        if constexpr (EPI == 2) {  // ablation: MFMA only
+  #pragma unroll
+          for (int t = 0; t < QT; ++t) asm volatile("" ::"v"(acc[t][0]), "v"(acc[t][5]), "v"(acc[t][15]));
+          continue;
+        }
+        // Epilogue.  MASKED only for the (rare) partial last tile of a chunk: a
+        // wave-uniform branch, so full tiles carry no per-score selects.
+        auto epilogue = [&](auto masked_tag) {
+          constexpr bool MASKED = decltype(masked_tag)::value;
+  #pragma unroll
+          for (int t = 0; t < QT; ++t) {
+            float sc[16];
+  #pragma unroll
+            for (int g = 0; g < 16; ++g) {
+              const int ir = 32 * st + (g & 3) + 8 * (g >> 2) + 4 * h;
+              float v = acc[t][g];
+              if constexpr (L2) v = fmaf(2.f, v, -lnorm[ir]);
+              if constexpr (MASKED) v = ir < nvalid ? v : -INFINITY;
+              sc[g] = v;
+            }
+            // IEEE maximum (v_maximum3_f32): no canonicalising moves on MFMA outputs
+            float m4[4];
+  #pragma unroll
+            for (int j = 0; j < 4; ++j)
+              m4[j] = fmax_ieee(fmax_ieee(sc[4 * j], sc[4 * j + 1]), fmax_ieee(sc[4 * j + 2], sc[4 * j + 3]));
+            const float m = fmax_ieee(fmax_ieee(m4[0], m4[1]), fmax_ieee(m4[2], m4[3]));
+            if constexpr (MODE == 3) {  // collect: append every score at or above the threshold
+              if (__any(m >= cthr[t])) {
+  #pragma unroll
+                for (int g = 0; g < 16; ++g) {
+                  if (sc[g] >= cthr[t]) {
+                    const int ir = 32 * st + (g & 3) + 8 * (g >> 2) + 4 * h;
+                    const int e = atomicAdd(&cl.n, 1);
+                    if (e < CollectLds<WQ>::CAP) {
+                      const int row = (w * QT + t) * 32 + r;
+                      const int rank = atomicAdd(&cl.qcnt[row], 1);
+                      cl.ent[e] = make_int2(row | (rank << 8), (int)(i0 + ir));
+                    } else if (__builtin_nontemporal_load(&iv.cand_cnt[cq[t]]) <= iv.cap) {
+                      // staging full: append directly (stop once the query overflowed)
+                      const int pos = atomicAdd(&iv.cand_cnt[cq[t]], 1);
+                      if (pos < iv.cap) iv.cand_pos[(int64_t)cq[t] * iv.cap + pos] = (int)(i0 + ir);
+                    }
+                  }
+                }
+              }
+              continue;
+            }
+            if constexpr (MODE == 4) {  // lane maximum and its position (new maxima are rare)
+              if (__any(m > ls[t][0])) {
+  #pragma unroll
+                for (int g = 0; g < 16; ++g) {
+                  if (sc[g] > ls[t][0]) {
+                    ls[t][0] = sc[g];
+                    li[t][0] = (int)(i0 + 32 * st + (g & 3) + 8 * (g >> 2) + 4 * h);
+                  }
+                }
+              }
+              continue;
+            }
+            if constexpr (MODE == 1 || EPI == 1) {  // pre-pass (or ablation): lane maximum only
+              ls[t][0] = fmax_ieee(ls[t][0], m);
+              continue;
+            }
+            // rare path: descend only into 4-row groups that beat the threshold
+            if (__any(m > fmaxf(ls[t][M], tau[t]))) {
+  #pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                if (__any(m4[j] > fmaxf(ls[t][M], tau[t]))) {
+  #pragma unroll
+                  for (int i = 0; i < 4; ++i) {
+                    const int g = 4 * j + i;
+                    const int ir = 32 * st + i + 8 * j + 4 * h;
+                    const float thr = fmaxf(ls[t][M], tau[t]);
+                    if (sc[g] > thr) list_insert<M + 1>(ls[t], li[t], sc[g], (int)(i0 + ir));
+                  }
                 }
               }
             }
           }
-        }
-      };
-      if (nvalid >= 32 * (st + 1)) epilogue(std::false_type{});
-      else epilogue(std::true_type{});
-    }
-  };
+        };
+        if (nvalid >= 32 * (st + 1)) epilogue(std::false_type{});
+        else epilogue(std::true_type{});
+      }
+    };
 
-  if (ntiles > 0) issue_tile(0, std::integral_constant<int, 0>{});
-  for (int it = 0; it < ntiles; it += 2) {
-    tile(it, std::integral_constant<int, 0>{});
-    if (it + 1 < ntiles) tile(it + 1, std::integral_constant<int, 1>{});
-  }
-
-#pragma unroll
-  for (int t = 0; t < QT; ++t) {
-    const int64_t qi = qidx[t];
-    int64_t base = -1;
-    if constexpr (MODE == 2) {
-      const int pair = iv.slot_pair[seg0 + qi];
-      if (pair >= 0) base = ((int64_t)pair * iv.cmax + c) * 2 + h;
-    } else if (qi < nq) {
-      base = (qi * nch + c) * 2 + h;
+    if constexpr (MODE == 3) {
+      if (tid == 0) cl.n = 0;  // ordered before any append by the first tile's barrier
     }
-    if (base >= 0) {
-      if constexpr (MODE == 1) {
-        part_t[base] = ls[t][0];
-      } else {
-#pragma unroll
-        for (int j = 0; j < M; ++j) {
-          part_s[base * M + j] = ls[t][j];
-          part_i[base * M + j] = li[t][j];
+    if (ntiles > 0) issue_tile(0, std::integral_constant<int, 0>{});
+    for (int it = 0; it < ntiles; it += 2) {
+      tile(it, std::integral_constant<int, 0>{});
+      if (it + 1 < ntiles) tile(it + 1, std::integral_constant<int, 1>{});
+    }
+
+    if constexpr (MODE == 3) {  // flush the staged candidates
+      __syncthreads();
+      for (int row = tid; row < WQ; row += NT) {
+        const int n_r = cl.qcnt[row];
+        cl.base[row] = n_r > 0 ? atomicAdd(&iv.cand_cnt[cl.qid[row]], n_r) : 0;
+      }
+      __syncthreads();
+      const int ne = cl.n < CollectLds<WQ>::CAP ? cl.n : CollectLds<WQ>::CAP;
+      for (int e = tid; e < ne; e += NT) {
+        const int2 en = cl.ent[e];
+        const int row = en.x & 255, dst = cl.base[row] + (en.x >> 8);
+        if (dst < iv.cap) iv.cand_pos[(int64_t)cl.qid[row] * iv.cap + dst] = en.y;
+      }
+      continue;
+    }
+
+  #pragma unroll
+    for (int t = 0; t < QT; ++t) {
+      const int64_t qi = qidx[t];
+      int64_t base = -1;
+      if constexpr (MODE == 3) {
+        continue;  // collect mode writes its candidates as it goes
+      } else if constexpr (MODE == 2 || MODE == 4) {
+        const int pair = iv.slot_pair[seg0 + qi];
+        if (pair >= 0) base = ((int64_t)pair * iv.cmax + c) * 2 + h;
+      } else if (qi < nq) {
+        base = (qi * nch + c) * 2 + h;
+      }
+      if (base >= 0) {
+        if constexpr (MODE == 1 || MODE == 4) {
+          part_t[base] = ls[t][0];
+          if constexpr (MODE == 4) part_i[base] = li[t][0];
+        } else {
+  #pragma unroll
+          for (int j = 0; j < M; ++j) {
+            part_s[base * M + j] = ls[t][j];
+            part_i[base * M + j] = li[t][j];
+          }
+          part_t[base] = ls[t][M];
         }
-        part_t[base] = ls[t][M];
       }
     }
+
   }
 }
 
@@ -384,11 +492,18 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
 // there are fewer than R): R distinct items score at least this much, so it
 // never exceeds the query's global R-th best screened score.  One wave per
 // query; values in registers; R rounds of wave-argmax extraction.
+//
+// With ids_in (IVF phase A: the position of each lane maximum), ids_out[q][i]
+// receives the position of the i-th extracted maximum (-1 past the end).
 __global__ __launch_bounds__(256) void tau_select_kernel(const float* __restrict__ premax, int nvals, int R,
-                                                         int64_t nq, float* __restrict__ tau) {
+                                                         int64_t nq, float* __restrict__ tau,
+                                                         const int* __restrict__ ids_in = nullptr,
+                                                         int* __restrict__ ids_out = nullptr) {
   const int lane = threadIdx.x & 63;
   const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (q >= nq) return;
+  if (ids_out)
+    for (int i = lane; i < R; i += 64) ids_out[q * R + i] = -1;
   constexpr int VPL = 16;  // nvals <= 64 * VPL
   float v[VPL];
 #pragma unroll
@@ -414,6 +529,7 @@ __global__ __launch_bounds__(256) void tau_select_kernel(const float* __restrict
 #pragma unroll
       for (int j = 0; j < VPL; ++j)
         if (j == mj) v[j] = -INFINITY;
+      if (ids_out) ids_out[q * R + round] = ids_in[q * nvals + mj * 64 + lane];
     }
   }
   if (lane == 0) tau[q] = last;
@@ -1078,12 +1194,14 @@ static screen_fn pick2(int qt, int M) {
   return pick3<DP, 1, 16, L2, MODE>();
 }
 
-// mode: 0 main pass, 1 threshold pre-pass, 2 IVF list scan
+// mode: 0 main pass, 1 threshold pre-pass, 2 IVF list scan, 3 IVF collect, 4 IVF lane maxima
 template <int DP, bool L2>
 static screen_fn pick1(int qt, int M, int mode) {
   constexpr int Q2 = DP == 256 ? 1 : 2;
   if (mode == 1) return qt == 2 ? pick3<DP, Q2, 1, L2, 1>() : pick3<DP, 1, 1, L2, 1>();
   if (mode == 2) return pick2<DP, L2, 2>(qt, M);
+  if (mode == 3) return qt == 2 ? pick3<DP, Q2, 1, L2, 3>() : pick3<DP, 1, 1, L2, 3>();
+  if (mode == 4) return qt == 2 ? pick3<DP, Q2, 1, L2, 4>() : pick3<DP, 1, 1, L2, 4>();
   return pick2<DP, L2, 0>(qt, M);
 }
 
@@ -1125,7 +1243,8 @@ extern "C" int nrk_flat_prepare(const float* xb, int64_t nb, int32_t d, uint16_t
   NRK_CHECK_ARG(xb && xb_bf16 && xb_meta && stats, "flat_prepare: null pointer");
   const int dp = padded_dim(d);
   const int rows_per_block = 4;
-  hipLaunchKernelGGL(flat_prepare_kernel, dim3((unsigned)cdiv(nb, rows_per_block)), dim3(64 * rows_per_block), 0,
+  const int64_t blocks = cdiv(nb, rows_per_block) < 8192 ? cdiv(nb, rows_per_block) : 8192;
+  hipLaunchKernelGGL(flat_prepare_kernel, dim3((unsigned)blocks), dim3(64 * rows_per_block), 0,
                      (hipStream_t)stream, xb, nb, d, dp, xb_bf16, xb_meta, stats);
   NRK_CHECK_LAUNCH("flat_prepare_kernel");
   return NRK_OK;
@@ -1350,12 +1469,120 @@ __global__ void ivf_gather_kernel(const uint16_t* __restrict__ qh, int dp, int n
   }
 }
 
+// IVF phase A seed: exact rescoring of the R best lane maxima of the nearest
+// list (distinct real items) -> e_k = their k-th best exact (goodness, id),
+// a lower bound on the true k-th best s_k.  Every true top-k item x then has
+// screened(x) >= exact(x) - B >= e_k - B =: T (screened units, rounded down;
+// same error bound B_q as the flat certificate), and (e_k, id) is the
+// fallback threshold.  Fewer than k seeds: the query goes to the fallback.
+__global__ __launch_bounds__(256) void ivf_seed_kernel(const int* __restrict__ seed_pos, int R, int k,
+                                                       const int64_t* __restrict__ pos2id,
+                                                       const float* __restrict__ xq, const float* __restrict__ xb,
+                                                       int d, int l2, const double* __restrict__ qmeta,
+                                                       const float* __restrict__ stats, int dp,
+                                                       float* __restrict__ thr, double* __restrict__ lb_g,
+                                                       int64_t* __restrict__ lb_i, int* __restrict__ cand_cnt,
+                                                       int cap) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int q = blockIdx.x, tid = threadIdx.x;
+  const int P = pow2ceil(R);
+  double* g = reinterpret_cast<double*>(smem);
+  int64_t* id = reinterpret_cast<int64_t*>(g + P);
+  float* qs = reinterpret_cast<float*>(id + P);
+  __shared__ int s_valid;
+  if (tid == 0) s_valid = 0;
+  for (int i = tid; i < d; i += 256) qs[i] = xq[(int64_t)q * d + i];
+  __syncthreads();
+  for (int i = tid; i < P; i += 256) {
+    const int pos = i < R ? seed_pos[(int64_t)q * R + i] : -1;
+    if (pos >= 0) {
+      const int64_t item = pos2id[pos];
+      const double sc = exact_score(qs, xb + item * d, d, l2 != 0);
+      g[i] = l2 ? -sc : sc;
+      id[i] = item;
+      atomicAdd(&s_valid, 1);
+    } else {
+      g[i] = -INFINITY;
+      id[i] = INT64_MAX;
+    }
+  }
+  __syncthreads();
+  block_bitonic_sort(g, id, P);
+  if (tid != 0) return;
+  if (s_valid < k) {  // too few seeds for a bound: no collection, straight to the fallback
+    thr[q] = INFINITY;
+    lb_g[q] = -INFINITY;
+    lb_i[q] = -1;
+    cand_cnt[q] = cap + 1;
+    return;
+  }
+  const double ek = g[k - 1];
+  const double nqh = qmeta[4 * q + 0], nrq = qmeta[4 * q + 1], qn2 = qmeta[4 * q + 2];
+  const double Xh = stats[0], Rr = stats[1], NX = stats[2];
+  const double gam = (double)dp * 0x1p-22;
+  const double bip = gam * nqh * Xh + nqh * Rr + nrq * Xh + nrq * Rr;
+  const double B = l2 ? 2.0 * bip + 0x1p-21 * (NX + nqh * Xh) : bip;
+  double t = (l2 ? qn2 + ek : ek) - B;
+  t -= 1e-9 * (fabs(t) + fabs(ek) + qn2 + B);  // slack for the fp64 evaluation of the bound itself
+  float f = (float)t;
+  if ((double)f > t) f = nextafterf(f, -INFINITY);
+  thr[q] = f < -FLT_MAX ? -FLT_MAX : f;
+  lb_g[q] = ek;
+  lb_i[q] = id[k - 1];
+}
+
+// IVF phase B: exact rescoring of every collected candidate, top-k.  Queries
+// whose buffer overflowed go to the fallback with threshold (e_k, id).
+__global__ __launch_bounds__(256) void collect_rescore_kernel(
+    const int* __restrict__ cand_cnt, const int* __restrict__ cand_pos, int cap, const int64_t* __restrict__ pos2id,
+    const float* __restrict__ xq, const float* __restrict__ xb, int d, int k, int l2,
+    const double* __restrict__ lb_g, const int64_t* __restrict__ lb_i, float* __restrict__ D,
+    int64_t* __restrict__ I, double* __restrict__ S, int64_t id_offset, FbState fb) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int qi = blockIdx.x, tid = threadIdx.x;
+  const int c = cand_cnt[qi];
+  if (c > cap) {
+    if (tid == 0) fb.push(qi, lb_g[qi], lb_i[qi]);
+    return;
+  }
+  const int P = pow2ceil(c > 0 ? c : 1);
+  double* g = reinterpret_cast<double*>(smem);
+  int64_t* id = reinterpret_cast<int64_t*>(g + P);
+  float* qs = reinterpret_cast<float*>(id + P);
+  for (int i = tid; i < d; i += 256) qs[i] = xq[(int64_t)qi * d + i];
+  __syncthreads();
+  for (int i = tid; i < P; i += 256) {
+    if (i < c) {
+      const int64_t item = pos2id[cand_pos[(int64_t)qi * cap + i]];
+      const double sc = exact_score(qs, xb + item * d, d, l2 != 0);
+      g[i] = l2 ? -sc : sc;
+      id[i] = item;
+    } else {
+      g[i] = -INFINITY;
+      id[i] = INT64_MAX;
+    }
+  }
+  __syncthreads();
+  block_bitonic_sort(g, id, P);
+  for (int j = tid; j < k; j += 256) {
+    const int64_t o = (int64_t)qi * k + j;
+    const bool valid = j < c;
+    const double sc = valid ? (l2 ? -g[j] : g[j]) : (l2 ? DBL_MAX : -DBL_MAX);
+    D[o] = valid ? (float)sc : (l2 ? FLT_MAX : -FLT_MAX);
+    I[o] = valid ? id[j] + id_offset : -1;
+    if (S) S[o] = sc;
+  }
+}
+
 struct IvfPlan {
-  int dp, qt, M, waves, wq, ch, cmax, U, KP, nqt;
+  int dp, qt, M, waves, wq, nqt;
+  int nA, chA, cmaxA, R;    // phase A: lane maxima (+positions) over the nA nearest lists, R seeds
+  int chB, cmaxB, cap;      // phase B: all probed lists, collect above e_k - B
   int fb_slots, fb_cap;
-  int64_t nq_pad, max_rows, ub;
-  size_t off_fbc, off_cnt, off_fill, off_seg, off_work, off_sp, off_qh, off_qmeta, off_qi, off_ps, off_pi, off_pt,
-      off_fbl, off_fbt, off_fbi, off_fbn, off_fcg, off_fci, off_ovl, total;
+  int64_t nq_pad, max_rows, ubA, ubB;
+  size_t off_fbc, off_cnt, off_fill, off_seg, off_work, off_sp, off_qh, off_qmeta, off_qi, off_p0, off_ps, off_pi,
+      off_pt, off_pa, off_tau, off_seed, off_lbg, off_lbi, off_thr, off_ccnt, off_cpos, off_fbl, off_fbt, off_fbi, off_fbn, off_fcg, off_fci,
+      off_ovl, total;
 };
 
 static IvfPlan make_ivf_plan(int64_t nq, int nprobe, int nlist, int64_t max_list, int d, int k) {
@@ -1370,31 +1597,42 @@ static IvfPlan make_ivf_plan(int64_t nq, int nprobe, int nlist, int64_t max_list
   p.wq = p.waves * 32 * p.qt;
   p.nqt = (int)cdiv(nq, p.wq);
   p.nq_pad = (int64_t)p.nqt * p.wq;
-  int kp = 2 * k > 32 ? 2 * k : 32;
-  if (kp < k + 16) kp = k + 16;
-  // chunking of a list: the union per query (nprobe * cmax * 2M) stays <= 4096
-  // entries, but holds at least kp; chunks are >= 2048 items where lists allow
-  const int per = nprobe * 2 * p.M;
-  int cmax_lim = 4096 / per;
-  if (cmax_lim < 1) cmax_lim = 1;
-  const int cmax_min = (int)cdiv(kp, per);
-  if (cmax_lim < cmax_min) cmax_lim = cmax_min;
   const int64_t ml = max_list > 0 ? max_list : 1;
-  int64_t ch = (int64_t)align_up((size_t)cdiv(ml, cmax_lim), 64);
-  int64_t ch_floor = (int64_t)align_up((size_t)cdiv(ml, cmax_min), 64);
-  if (ch_floor > 2048) ch_floor = 2048;
-  if (ch < ch_floor) ch = ch_floor;
   const int64_t ch_gib = ((int64_t)1 << 30) / (p.dp * 2) / 64 * 64;  // buffer descriptor range
-  if (ch > ch_gib) ch = ch_gib;
-  p.ch = (int)env_int("NRK_IVF_CHUNK", (int)ch);
-  p.cmax = (int)cdiv(ml, (int64_t)p.ch);
-  p.U = nprobe * p.cmax * 2 * p.M;
-  p.KP = kp < p.U ? kp : p.U;
-  if (p.KP > 1024) p.KP = 1024;
+  // phase A: the nA nearest lists per query in chunks of ~1024 items (2 lane
+  // streams per chunk and query; more streams -> tighter seeds); tau_select
+  // takes <= 1024 values per query
+  p.nA = nprobe < 2 ? nprobe : 2;
+  int64_t chA = env_int("NRK_IVF_CHUNK_A", 1024);
+  if (chA < 64) chA = 64;
+  chA = (int64_t)align_up((size_t)chA, 64);
+  const int64_t cmax_a = 512 / p.nA;
+  if (cdiv(ml, chA) > cmax_a) chA = (int64_t)align_up((size_t)cdiv(ml, cmax_a), 64);
+  if (chA > ch_gib) chA = ch_gib;
+  p.chA = (int)chA;
+  p.cmaxA = (int)cdiv(ml, chA);
+  p.R = 2 * k > 32 ? 2 * k : 32;  // seeds rescored exactly
+  if (p.R > 2 * p.nA * p.cmaxA) p.R = 2 * p.nA * p.cmaxA;
+  if (p.R < 1) p.R = 1;
+  // phase B: chunk size only sets the work-item granularity
+  int64_t chB = env_int("NRK_IVF_CHUNK", 4096);
+  if (chB < 64) chB = 64;
+  chB = (int64_t)align_up((size_t)chB, 64);
+  if (chB > ch_gib) chB = ch_gib;
+  p.chB = (int)chB;
+  p.cmaxB = (int)cdiv(ml, chB);
+  p.cap = env_int("NRK_IVF_CAP", 2048);
+  if (p.cap < k) p.cap = k;
+  if (p.cap > 8192) p.cap = 8192;
   const int64_t npairs = nq * nprobe;
   p.max_rows = npairs + (int64_t)nlist * (p.wq - 1);
   p.max_rows = (p.max_rows + p.wq - 1) / p.wq * p.wq;
-  p.ub = (cdiv(npairs, (int64_t)p.wq) + nlist) * p.cmax;
+  // persistent grids over the device work tables (upper bound on the items)
+  const int64_t gcap = env_int("NRK_IVF_GRID", 2048);
+  p.ubA = (cdiv(nq * p.nA, (int64_t)p.wq) + nlist) * p.cmaxA;
+  p.ubB = (cdiv(npairs, (int64_t)p.wq) + nlist) * p.cmaxB;
+  if (p.ubA > gcap) p.ubA = gcap;
+  if (p.ubB > gcap) p.ubB = gcap;
   p.fb_slots = (int)(nq < 4096 ? nq : 4096);
   p.fb_cap = host_pow2ceil(2 * k + 64);
   if (p.fb_cap < 512) p.fb_cap = 512;
@@ -1416,9 +1654,16 @@ static IvfPlan make_ivf_plan(int64_t nq, int nprobe, int nlist, int64_t max_list
   p.off_qh = take((size_t)p.nq_pad * p.dp * 2);
   p.off_qmeta = take((size_t)nq * 4 * 8);
   p.off_qi = take((size_t)p.max_rows * p.dp * 2);
-  p.off_ps = take((size_t)nq * p.U * 4);
-  p.off_pi = take((size_t)nq * p.U * 4);
-  p.off_pt = take((size_t)nq * nprobe * p.cmax * 2 * 4);
+  p.off_p0 = take((size_t)nq * p.nA * 8);
+  p.off_pt = take((size_t)nq * p.nA * p.cmaxA * 2 * 4);
+  p.off_pa = take((size_t)nq * p.nA * p.cmaxA * 2 * 4);
+  p.off_tau = take((size_t)nq * 4);
+  p.off_seed = take((size_t)nq * p.R * 4);
+  p.off_lbg = take((size_t)nq * 8);
+  p.off_lbi = take((size_t)nq * 8);
+  p.off_thr = take((size_t)nq * 4);
+  p.off_ccnt = take((size_t)nq * 4);
+  p.off_cpos = take((size_t)nq * p.cap * 4);
   p.off_fbl = take((size_t)nq * 4);
   p.off_fbt = take((size_t)p.fb_slots * 8);
   p.off_fbi = take((size_t)p.fb_slots * 8);
@@ -1428,6 +1673,27 @@ static IvfPlan make_ivf_plan(int64_t nq, int nprobe, int nlist, int64_t max_list
   p.off_ovl = take((size_t)nq * 4);
   p.total = off;
   return p;
+}
+
+// group (query, probe) pairs by list and gather the probing queries list-major
+static int ivf_group(const int64_t* probe, int64_t nq, int nprobe, int nlist, const int64_t* list_off, int wq, int ch,
+                     int dp, int64_t max_rows, const uint16_t* qh, int* cnt, int* fill, int* seg, int* work, int* sp,
+                     uint16_t* qi, hipStream_t st) {
+  const int64_t npairs = nq * nprobe;
+  if (hipMemsetAsync(cnt, 0, (size_t)nlist * 4, st) != hipSuccess ||
+      hipMemsetAsync(sp, 0xff, (size_t)max_rows * 4, st) != hipSuccess)
+    return fail(NRK_ELAUNCH, "ivf_search: memset failed");
+  hipLaunchKernelGGL(ivf_count_kernel, dim3((unsigned)cdiv(npairs, 256)), dim3(256), 0, st, probe, npairs, nlist, cnt);
+  NRK_CHECK_LAUNCH("ivf_count_kernel");
+  hipLaunchKernelGGL(ivf_plan_kernel, dim3(1), dim3(1024), 0, st, cnt, list_off, nlist, wq, ch, seg, work, fill);
+  NRK_CHECK_LAUNCH("ivf_plan_kernel");
+  hipLaunchKernelGGL(ivf_scatter_kernel, dim3((unsigned)cdiv(npairs, 256)), dim3(256), 0, st, probe, npairs, nlist,
+                     seg, fill, sp);
+  NRK_CHECK_LAUNCH("ivf_scatter_kernel");
+  hipLaunchKernelGGL(ivf_gather_kernel, dim3((unsigned)cdiv(max_rows, 4)), dim3(256), 0, st, qh, dp, nprobe, sp, seg,
+                     nlist, max_rows, qi);
+  NRK_CHECK_LAUNCH("ivf_gather_kernel");
+  return NRK_OK;
 }
 
 }  // namespace nrk
@@ -1476,9 +1742,16 @@ extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe,
   uint16_t* qh = reinterpret_cast<uint16_t*>(w + p.off_qh);
   double* qmeta = reinterpret_cast<double*>(w + p.off_qmeta);
   uint16_t* qi = reinterpret_cast<uint16_t*>(w + p.off_qi);
-  float* ps = reinterpret_cast<float*>(w + p.off_ps);
-  int* pi = reinterpret_cast<int*>(w + p.off_pi);
+  int64_t* p0 = reinterpret_cast<int64_t*>(w + p.off_p0);
   float* pt = reinterpret_cast<float*>(w + p.off_pt);
+  int* pa = reinterpret_cast<int*>(w + p.off_pa);
+  float* tau = reinterpret_cast<float*>(w + p.off_tau);
+  int* seed = reinterpret_cast<int*>(w + p.off_seed);
+  double* lbg = reinterpret_cast<double*>(w + p.off_lbg);
+  int64_t* lbi = reinterpret_cast<int64_t*>(w + p.off_lbi);
+  float* thr = reinterpret_cast<float*>(w + p.off_thr);
+  int* ccnt = reinterpret_cast<int*>(w + p.off_ccnt);
+  int* cpos = reinterpret_cast<int*>(w + p.off_cpos);
   FbState fb;
   fb.list = reinterpret_cast<int*>(w + p.off_fbl);
   fb.count = fbc;
@@ -1486,52 +1759,67 @@ extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe,
   fb.thr_g = reinterpret_cast<double*>(w + p.off_fbt);
   fb.thr_i = reinterpret_cast<int64_t*>(w + p.off_fbi);
   fb.n = reinterpret_cast<int*>(w + p.off_fbn);
-  fb.force = env_int("NRK_FORCE_FALLBACK", 0);
+  fb.force = 0;
   double* fcg = reinterpret_cast<double*>(w + p.off_fcg);
   int64_t* fci = reinterpret_cast<int64_t*>(w + p.off_fci);
   int* ovl = reinterpret_cast<int*>(w + p.off_ovl);
   IvfFb ivf{pos2id, pos2list, list_off, probe, nprobe};
-  const int64_t npairs = nq * nprobe;
+  const bool force_fb = env_int("NRK_FORCE_FALLBACK", 0) != 0;
 
   mark(0);
-  // group (query, probe) pairs by list
-  if (hipMemsetAsync(cnt, 0, (size_t)nlist * 4, st) != hipSuccess ||
-      hipMemsetAsync(sp, 0xff, (size_t)p.max_rows * 4, st) != hipSuccess ||
-      hipMemsetAsync(pi, 0xff, (size_t)nq * p.U * 4, st) != hipSuccess ||
-      hipMemsetAsync(pt, 0xff, (size_t)nq * nprobe * p.cmax * 2 * 4, st) != hipSuccess)
-    return fail(NRK_ELAUNCH, "ivf_search: memset failed");
   hipLaunchKernelGGL(query_prepare_kernel, dim3((unsigned)cdiv(p.nq_pad, 4)), dim3(256), 0, st, xq, nq, p.nq_pad, d,
                      p.dp, qh, qmeta);
   NRK_CHECK_LAUNCH("query_prepare_kernel");
-  hipLaunchKernelGGL(ivf_count_kernel, dim3((unsigned)cdiv(npairs, 256)), dim3(256), 0, st, probe, npairs, nlist, cnt);
-  NRK_CHECK_LAUNCH("ivf_count_kernel");
-  hipLaunchKernelGGL(ivf_plan_kernel, dim3(1), dim3(1024), 0, st, cnt, list_off, nlist, p.wq, p.ch, seg, work, fill);
-  NRK_CHECK_LAUNCH("ivf_plan_kernel");
-  hipLaunchKernelGGL(ivf_scatter_kernel, dim3((unsigned)cdiv(npairs, 256)), dim3(256), 0, st, probe, npairs, nlist,
-                     seg, fill, sp);
-  NRK_CHECK_LAUNCH("ivf_scatter_kernel");
-  hipLaunchKernelGGL(ivf_gather_kernel, dim3((unsigned)cdiv(p.max_rows, 4)), dim3(256), 0, st, qh, p.dp, nprobe, sp,
-                     seg, nlist, p.max_rows, qi);
-  NRK_CHECK_LAUNCH("ivf_gather_kernel");
+  if (n > 0) {
+    // ---- phase A: lane maxima over the nearest list of every query -> tau
+    if (hipMemcpy2DAsync(p0, (size_t)p.nA * 8, probe, (size_t)nprobe * 8, (size_t)p.nA * 8, (size_t)nq,
+                         hipMemcpyDeviceToDevice, st) != hipSuccess ||
+        hipMemsetAsync(pt, 0xff, (size_t)nq * p.nA * p.cmaxA * 2 * 4, st) != hipSuccess ||  // NaN: never selected
+        hipMemsetAsync(ccnt, 0, (size_t)nq * 4, st) != hipSuccess)
+      return fail(NRK_ELAUNCH, "ivf_search: copy/memset failed");
+    int rc =
+        ivf_group(p0, nq, p.nA, nlist, list_off, p.wq, p.chA, p.dp, p.max_rows, qh, cnt, fill, seg, work, sp, qi, st);
+    if (rc != NRK_OK) return rc;
+    screen_fn fa = pick_screen(p.dp, p.qt, p.M, l2 != 0, 4);
+    if (!fa) return fail(NRK_EUNSUPPORTED, "ivf_search: no screen kernel for dp=%d", p.dp);
+    IvfScreen isa{work, list_off, seg, sp, nlist, p.chA, p.cmaxA, nullptr, nullptr, nullptr, 0, p.nA};
+    hipLaunchKernelGGL(fa, dim3((unsigned)p.ubA), dim3(p.waves * 64), 0, st, qi, xbh_ivf, meta_ivf, nq, n, 0, 0, 0, 1,
+                       nullptr, pa, pt, nullptr, isa);
+    NRK_CHECK_LAUNCH("screen_kernel (ivf phase A)");
+    hipLaunchKernelGGL(tau_select_kernel, dim3((unsigned)cdiv(nq, 4)), dim3(256), 0, st, pt, 2 * p.nA * p.cmaxA, p.R,
+                       nq, tau, pa, seed);
+    NRK_CHECK_LAUNCH("tau_select_kernel (ivf)");
+    hipLaunchKernelGGL(ivf_seed_kernel, dim3((unsigned)nq), dim3(256), (size_t)host_pow2ceil(p.R) * 16 + (size_t)d * 4,
+                       st, seed, p.R, k, pos2id, xq, xb, d, l2, qmeta, stats, p.dp, thr, lbg, lbi, ccnt, p.cap);
+    NRK_CHECK_LAUNCH("ivf_seed_kernel");
+    NRK_CHECK_LAUNCH("ivf_thr_kernel");
+    // ---- phase B grouping: every probed list
+    rc = ivf_group(probe, nq, nprobe, nlist, list_off, p.wq, p.chB, p.dp, p.max_rows, qh, cnt, fill, seg, work, sp, qi,
+                   st);
+    if (rc != NRK_OK) return rc;
+  } else if (hipMemsetAsync(ccnt, 0, (size_t)nq * 4, st) != hipSuccess) {  // empty index: all -1
+    return fail(NRK_ELAUNCH, "ivf_search: memset");
+  }
 
   mark(1);
   if (n > 0) {
-    screen_fn fn = pick_screen(p.dp, p.qt, p.M, l2 != 0, 2);
-    if (!fn) return fail(NRK_EUNSUPPORTED, "ivf_search: no screen kernel for dp=%d", p.dp);
-    IvfScreen is{work, list_off, seg, sp, nlist, p.ch, p.cmax};
-    hipLaunchKernelGGL(fn, dim3((unsigned)p.ub), dim3(p.waves * 64), 0, st, qi, xbh_ivf, meta_ivf, nq, n, 0, 0, 0, 1,
-                       ps, pi, pt, nullptr, is);
-    NRK_CHECK_LAUNCH("screen_kernel (ivf)");
+    // ---- phase B: collect every probed item at or above e_k - B_q
+    screen_fn fbk = pick_screen(p.dp, p.qt, p.M, l2 != 0, 3);
+    if (!fbk) return fail(NRK_EUNSUPPORTED, "ivf_search: no collect kernel for dp=%d", p.dp);
+    IvfScreen isb{work, list_off, seg, sp, nlist, p.chB, p.cmaxB, thr, ccnt, cpos, p.cap, nprobe};
+    hipLaunchKernelGGL(fbk, dim3((unsigned)p.ubB), dim3(p.waves * 64), 0, st, qi, xbh_ivf, meta_ivf, nq, n, 0, 0, 0, 1,
+                       nullptr, nullptr, nullptr, nullptr, isb);
+    NRK_CHECK_LAUNCH("screen_kernel (ivf collect)");
   }
 
   mark(2);
   {
-    const int P = host_pow2ceil(p.U), P2 = host_pow2ceil(p.KP);
-    const size_t smem = (size_t)P * 16 + (size_t)P2 * 16 + (size_t)d * 4;
-    if (smem > 150 * 1024) return fail(NRK_EUNSUPPORTED, "ivf_search: merge needs %zu B LDS", smem);
-    hipLaunchKernelGGL(merge_rescore_kernel, dim3((unsigned)nq), dim3(256), smem, st, ps, pi, pt, nprobe * p.cmax,
-                       p.M, p.KP, k, p.dp, xq, xb, n, d, l2, qmeta, stats, nullptr, D, I, S, id_offset, fb, pos2id);
-    NRK_CHECK_LAUNCH("merge_rescore_kernel (ivf)");
+    if (force_fb && n > 0 && hipMemsetAsync(ccnt, 0x7f, (size_t)nq * 4, st) != hipSuccess)  // testing: overflow all
+      return fail(NRK_ELAUNCH, "ivf_search: memset failed");
+    const size_t smem = (size_t)host_pow2ceil(p.cap) * 16 + (size_t)d * 4;
+    hipLaunchKernelGGL(collect_rescore_kernel, dim3((unsigned)nq), dim3(256), smem, st, ccnt, cpos, p.cap, pos2id, xq,
+                       xb, d, k, l2, lbg, lbi, D, I, S, id_offset, fb);
+    NRK_CHECK_LAUNCH("collect_rescore_kernel");
   }
 
   mark(3);
