@@ -12,6 +12,10 @@ searches its shard and the per-shard exact top-k lists are merged after ONE
 RCCL all_gather (newsrecommend_amd.dist).  value = queries answered / max-
 over-ranks wall time of the K timed steps.
 
+Secondary record `ivf` (configs[3] shape): IVF-Flat nlist=300, nprobe=32 over
+10M x 128 items (L2), rows split over the ranks, exact top-k per rank merged
+after one all_gather; recall@5 against the exact flat search.
+
 Secondary record `din` (configs[2]): DIN training, bf16 table of 2M items,
 5M synthetic click rows, L = 50, d = 128, A = 128, F = 32; one step = fwd +
 bwd + clip + Adam on a batch of --din-batch rows; data-parallel replicas with
@@ -180,6 +184,118 @@ def _pmc_traffic(args, world):
         return None
 
 
+# ------------------------------------------------------------------ IVF --
+def bench_ivf(args, rank, world, dev):
+    """configs[3]: IVF-Flat nlist=300, nprobe=32 over 10M x 128 (squared L2),
+    the corpus rows split over the ranks (every list partially on every rank),
+    per-rank exact top-k merged after one all_gather.  One step = one search
+    of a 4096-query batch INCLUDING the coarse quantizer."""
+    from newsrecommend_amd import _lib, faiss as nf
+    from newsrecommend_amd.data import clustered_corpus
+    from newsrecommend_amd.dist import ShardedIndexIVFFlat
+
+    d, k, nq, nlist, nprobe = args.d, args.k, args.nq, args.ivf_nlist, args.ivf_nprobe
+    xb = clustered_corpus(args.ivf_nb, d, seed=1234, device=dev)
+    xq = clustered_corpus(nq, d, seed=4321, device=dev)
+    barrier(world)
+    t0 = time.perf_counter()
+    index = ShardedIndexIVFFlat(d, nlist, nf.METRIC_L2, device=dev)
+    index.local.cp.niter = args.ivf_niter
+    index.train(xb)
+    index.add_full(xb)
+    index.nprobe = nprobe
+    barrier(world)
+    build_s = max_over_ranks(time.perf_counter() - t0, world, dev)
+    for _ in range(args.warmup):
+        D, I = index.search_device(xq, k)
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        D, I = index.search_device(xq, k)
+    barrier(world)
+    el = max_over_ranks(time.perf_counter() - t0, world, dev)
+    qps = nq * args.steps / el
+    # rank-local stage split (instrumented, outside the timed region)
+    _, probe = index.quantizer.search_device(xq, nprobe)
+    evs = [_lib.StageEvents() for _ in range(max(3, min(args.steps, 10)))]
+    for e in evs:
+        index.local.search_device(xq, k, probe=probe, stage_events=e)
+    torch.cuda.synchronize()
+    st = np.array([e.elapsed_ms() for e in evs]).mean(0)
+    sizes = torch.diff(index.local.list_off).cpu().numpy()
+    pr = probe.cpu().numpy()
+    flops = 2.0 * d * float(sizes[pr[pr >= 0]].sum())
+    achieved = flops / (st[1] * 1e-3) / 1e12
+    out = {
+        "metric": "IVF-Flat retrieval QPS", "value": qps, "unit": "queries/s", "ms_per_step": el / args.steps * 1e3,
+        "config": {"workload": f"configs[3]: IVF-Flat nlist={nlist} nprobe={nprobe}, {args.ivf_nb}x{d}, "
+                               f"batch={nq}, k={k}, L2", "parallelism": f"list-shard{world} + RCCL all_gather merge"
+                   if world > 1 else "single GPU", "kmeans_niter": args.ivf_niter},
+        "build_s": build_s,
+        "stages_ms": {"prepare+phaseA+grouping": float(st[0]), "collect_screen": float(st[1]),
+                      "exact_rescore": float(st[2]), "fallback": float(st[3])},
+        "fallback_queries": int(index.local.last_fallback.item()),
+        "roofline": {"bound": "mfma", "kernel": "screen_kernel MODE 3 (IVF collect, bf16 v_mfma_f32_32x32x16)",
+                     "achieved": achieved, "peak": BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / BF16_DENSE_TFLOPS, "traffic": None,
+                     "algorithmic": f"2*d*sum(probed local list sizes) = {flops:.4g} flop per launch"},
+    }
+    # recall@5 against the exact flat search over the whole corpus (our flat
+    # path is bit-exact vs the oracle, tests/test_knn_gpu.py)
+    if rank == 0:
+        flat = nf.IndexFlat(d, nf.METRIC_L2, device=dev)
+        flat.add(xb)
+        _, If = flat.search_device(xq, k)
+        Ig, Ie = I.cpu().numpy(), If.cpu().numpy()
+        out["recall_at_5"] = float(np.mean([len(set(a[:5]) & set(b[:5])) / min(5, k) for a, b in zip(Ig, Ie)]))
+        del flat
+        if world == 1:
+            out["oracle_match"] = _ivf_oracle_check(index, xb, xq, I, k, nprobe)
+            if not args.no_cpu_baseline:
+                out["cpu_baseline"] = _cpu_ivf(args, index, xb, xq, k, nprobe)
+    return out
+
+
+def _ivf_oracle_check(index, xb, xq, I, k, nprobe):
+    """A few queries against oracle/ivf_oracle.py on the full corpus."""
+    from oracle import ivf_oracle as io
+
+    sample = np.arange(0, xq.shape[0], xq.shape[0] // 4)
+    cent = index.quantizer._xb[: index.local.nlist].cpu().numpy()
+    assign = index.local._assign.cpu().numpy()
+    _, Io, _, _ = io.ivf_search(xq[sample].cpu().numpy(), xb.cpu().numpy(), cent, assign, nprobe, k, 1)
+    return bool(np.array_equal(I[sample].cpu().numpy(), Io))
+
+
+def _cpu_ivf(args, index, xb, xq, k, nprobe):
+    """faiss-cpu IndexIVFFlat's algorithm restated with numpy fp32 BLAS
+    (coarse GEMM, then one GEMV per query over its probed lists' rows + top-k),
+    on a bounded query sample."""
+    cent = index.quantizer._xb[: index.local.nlist].cpu().numpy()
+    assign = index.local._assign.cpu().numpy()
+    xbn = xb.cpu().numpy()
+    order = np.argsort(assign, kind="stable")
+    off = np.zeros(index.local.nlist + 1, np.int64)
+    np.cumsum(np.bincount(assign, minlength=index.local.nlist), out=off[1:])
+    lists = [order[off[l]:off[l + 1]] for l in range(index.local.nlist)]
+    norms = (xbn * xbn).sum(1)
+    q = xq.cpu().numpy()
+    t = time.perf_counter()
+    n = 0
+    while n < q.shape[0] and (time.perf_counter() - t < args.cpu_seconds / 2 or n < 8):
+        qq = q[n]
+        dc = (cent * cent).sum(1) - 2 * cent @ qq
+        probe = np.argpartition(dc, nprobe)[:nprobe]
+        ids = np.concatenate([lists[l] for l in probe])
+        dist_ = norms[ids] - 2 * (xbn[ids] @ qq)
+        top = ids[np.argpartition(dist_, k)[:k]]
+        n += 1
+    dt = time.perf_counter() - t
+    return {"value": n / dt, "unit": "queries/s", "cores": cpu_cores(), "kind": "port",
+            "sample": f"{n} queries (nprobe={nprobe}) over the {args.ivf_nb}x{args.d} IVF index, numpy fp32 BLAS "
+                      f"per query (faiss IndexIVFFlat scan restated), {dt:.1f} s"}
+
+
 # ------------------------------------------------------------------ DIN --
 def bench_din(args, rank, world, dev):
     from newsrecommend_amd.data import synthetic_click_rows
@@ -303,12 +419,16 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["flat", "din", "all"], default="all")
+    ap.add_argument("--workload", choices=["flat", "din", "ivf", "all"], default="all")
     ap.add_argument("--nb", type=int, default=1_000_000)
     ap.add_argument("--d", type=int, default=128)
     ap.add_argument("--nq", type=int, default=4096)
     ap.add_argument("--k", type=int, default=5)
     ap.add_argument("--metric", choices=["ip", "l2"], default="ip")
+    ap.add_argument("--ivf-nb", type=int, default=10_000_000)
+    ap.add_argument("--ivf-nlist", type=int, default=300)
+    ap.add_argument("--ivf-nprobe", type=int, default=32)
+    ap.add_argument("--ivf-niter", type=int, default=20)
     ap.add_argument("--din-rows", type=int, default=5_000_000)
     ap.add_argument("--din-items", type=int, default=2_000_000)
     ap.add_argument("--din-batch", type=int, default=4096)
@@ -331,6 +451,15 @@ def main():
         for k in ("roofline", "stages_ms", "fallback_queries", "recall_at_5", "exact_match", "cpu_baseline"):
             if k in r:
                 rec[k] = r[k]
+    if args.workload in ("ivf", "all"):
+        r = bench_ivf(args, rank, world, dev)
+        if args.workload == "ivf":
+            rec.update({"metric": r["metric"], "value": r["value"], "unit": r["unit"], "ms_per_step": r["ms_per_step"],
+                        "config": r["config"], "roofline": r["roofline"]})
+            if "cpu_baseline" in r:
+                rec["cpu_baseline"] = r["cpu_baseline"]
+        rec["ivf"] = r
+        torch.cuda.empty_cache()
     if args.workload in ("din", "all"):
         r = bench_din(args, rank, world, dev)
         if args.workload == "din":

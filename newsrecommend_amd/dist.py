@@ -72,3 +72,47 @@ class ShardedIndexFlat:
         S_all, I_all = all_gather_results(S, I, self.group)
         Dm, Im, _ = nf.topk_merge(S_all, I_all, k, self.metric)
         return Dm, Im
+
+
+class ShardedIndexIVFFlat:
+    """IndexIVFFlat whose inverted lists are split over the ranks by id block
+    (BASELINE configs[3]): the coarse centroids are replicated
+    (every rank runs the same deterministic k-means on the same subsample, so
+    no broadcast is needed), each rank holds its rows' entries of EVERY list,
+    probes the same nprobe lists, and the per-rank exact top-k lists are merged
+    after one all_gather — identical to a single-device IVF search."""
+
+    def __init__(self, d: int, nlist: int, metric: int = nf.METRIC_L2, group=None, device=None):
+        self.group = group
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.metric = metric
+        self.quantizer = nf.IndexFlatL2(d, device=device)
+        self.local = nf.IndexIVFFlat(self.quantizer, d, nlist, metric, device=device)
+        self.offset = 0
+        self.ntotal = 0
+
+    @property
+    def nprobe(self):
+        return self.local.nprobe
+
+    @nprobe.setter
+    def nprobe(self, v):
+        self.local.nprobe = int(v)
+
+    def train(self, x):
+        self.local.train(x)
+
+    def add_full(self, xb):
+        n = xb.shape[0]
+        lo, hi = shard_range(n, self.rank, self.world)
+        self.offset, self.ntotal = lo, n
+        self.local.add(xb[lo:hi])
+
+    def search_device(self, xq: torch.Tensor, k: int):
+        D, I, S = self.local.search_device(xq, k, exact_scores=True, id_offset=self.offset)
+        if self.world == 1:
+            return D, I
+        S_all, I_all = all_gather_results(S, I, self.group)
+        Dm, Im, _ = nf.topk_merge(S_all, I_all, k, self.metric)
+        return Dm, Im

@@ -52,3 +52,41 @@ def test_two_rank_exchange_and_merge(tmp_path):
         for r in range(world):
             ok, tie = np.load(tmp_path / f"ok_{metric}_{r}.npy")
             assert ok and tie
+
+
+def _ivf_worker(rank, world, port, out_dir):
+    """Sharded IVF (configs[3] layout): replicated centroids, each rank's rows
+    of every list, one exchange, merge == single-index IVF search."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from newsrecommend_amd.dist import all_gather_results, shard_range
+        from oracle import ivf_oracle as io
+        from oracle import knn_oracle as ko
+
+        rng = np.random.default_rng(5)
+        xb = rng.standard_normal((3001, 16)).astype(np.float32)
+        xq = rng.standard_normal((20, 16)).astype(np.float32)
+        cent, _ = io.kmeans(xb, 12, niter=3)  # identical on every rank (deterministic)
+        assign, _ = io.assign_nearest(xb, cent)
+        k, nprobe = 5, 3
+        lo, hi = shard_range(xb.shape[0], rank, world)
+        oks = []
+        for metric in (ko.METRIC_IP, ko.METRIC_L2):
+            _, I, S, _ = io.ivf_search(xq, xb[lo:hi], cent, assign[lo:hi], nprobe, k, metric)
+            I = np.where(I >= 0, I + lo, -1)
+            S_all, I_all = all_gather_results(torch.from_numpy(S), torch.from_numpy(I))
+            _, Im, Sm = ko.merge(S_all.numpy(), I_all.numpy(), k, metric)
+            _, Ig, Sg, _ = io.ivf_search(xq, xb, cent, assign, nprobe, k, metric)
+            oks.append(np.array_equal(Im, Ig) and np.array_equal(Sm, Sg))
+        np.save(os.path.join(out_dir, f"ivf_ok_{rank}.npy"), np.array(oks))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_sharded_ivf(tmp_path):
+    world = 2
+    mp.spawn(_ivf_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        assert np.load(tmp_path / f"ivf_ok_{r}.npy").all()
