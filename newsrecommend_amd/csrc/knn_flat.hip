@@ -242,9 +242,12 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
       }
       const int64_t lb = iv.list_off[lo], le = iv.list_off[lo + 1];
       const int nchl = (int)cdiv(le - lb, (int64_t)iv.ch);
+      // query tile innermost: the tiles sharing a chunk are consecutive work
+      // items, i.e. run together on one XCD and read the chunk through its L2
       const int local = logical - iv.work_off[lo];
-      qt = local / nchl;
-      c = local - qt * nchl;
+      const int nqtl = (iv.work_off[lo + 1] - iv.work_off[lo]) / nchl;
+      c = local / nqtl;
+      qt = local - c * nqtl;
       ibeg = lb + (int64_t)c * iv.ch;
       iend = ibeg + iv.ch < le ? ibeg + iv.ch : le;
       seg0 = iv.seg_off[lo];
