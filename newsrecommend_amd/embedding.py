@@ -1,0 +1,160 @@
+"""Article embedding model and corpus producer (embedding_generate.py:51-131),
+the producer side of the retrieval path.
+
+  ArticleEmbeddingModel   same layers, init order and state_dict keys as
+                          embedding_generate.py:51-65 (fc.0 Linear(253,512),
+                          fc.1 ReLU, fc.2 Dropout, fc.3 BatchNorm1d(512),
+                          fc.4 Linear(512,256)); a reference checkpoint
+                          (best_eg_model.pth) loads with weights_only=True
+  ArticleEmbeddingModel.embed   eval-mode inference for a whole corpus: the
+                          BatchNorm is folded into fc.4 (W' = W diag(s),
+                          b' = b + W t) so a batch is two GEMMs with a fused
+                          bias+ReLU — library GEMMs (hipBLASLt through torch),
+                          batches of 64K rows instead of the reference's
+                          364,047 batch-1 forwards (embedding_generate.py:118-121)
+  inference               embedding_generate.py:109-131 with typed outputs:
+                          ids int64 (N,) + embeddings float32 (N, 256) in one
+                          .npz instead of the pickled dict / object array
+                          (the object array cannot be read back by
+                          Retrieval.py:6 with allow_pickle=False)
+  load_article_table      Retrieval.py:6-9 for both the typed .npz and a plain
+                          numeric (N, d+1) table (ids in the last column)
+  ArticleTripletDataset / train_triplet   embedding_generate.py:25-49,67-107
+                          (TripletMarginLoss(margin=1, p=2), Adam with L2
+                          weight decay), features gathered on the device
+"""
+from __future__ import annotations
+
+import random
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+NUM_FEATURE = 253
+FC_DIM = 512
+EMBEDDING_DIM = 256
+DROPOUT = 0.13
+MARGIN = 1.0
+LR = 1e-3
+WEIGHT_DECAY = 5e-5
+
+
+class ArticleEmbeddingModel(nn.Module):
+    def __init__(self, input_dim=NUM_FEATURE, fc_dim=FC_DIM, embedding_dim=EMBEDDING_DIM, dropout_rate=DROPOUT):
+        super().__init__()
+        self.fc = nn.Sequential(
+            nn.Linear(input_dim, fc_dim),
+            nn.ReLU(),
+            nn.Dropout(dropout_rate),
+            nn.BatchNorm1d(fc_dim),
+            nn.Linear(fc_dim, embedding_dim),
+        )
+
+    def forward(self, x):
+        return self.fc(x)
+
+    def folded(self):
+        """(W1, b1, W2', b2') with the eval-mode BatchNorm folded into fc.4."""
+        l1, bn, l2 = self.fc[0], self.fc[3], self.fc[4]
+        s = bn.weight / torch.sqrt(bn.running_var + bn.eps)
+        t = bn.bias - bn.running_mean * s
+        return l1.weight, l1.bias, l2.weight * s[None, :], l2.bias + l2.weight @ t
+
+    @torch.no_grad()
+    def embed(self, x: torch.Tensor, batch: int = 65536) -> torch.Tensor:
+        """Eval-mode embeddings of x (n, input_dim) -> (n, embedding_dim) f32 on x's device."""
+        W1, b1, W2, b2 = (p.detach().float() for p in self.folded())
+        out = torch.empty((x.shape[0], W2.shape[0]), dtype=torch.float32, device=x.device)
+        for lo in range(0, x.shape[0], batch):
+            xb = x[lo:lo + batch].float()
+            h = torch.addmm(b1, xb, W1.t()).clamp_min_(0.0)
+            torch.addmm(b2, h, W2.t(), out=out[lo:lo + batch])
+        return out
+
+
+def inference(model: ArticleEmbeddingModel, article_features, device=None, out_path: str | None = None,
+              batch: int = 65536):
+    """embedding_generate.py:109-131.  `article_features` is the reference's
+    {article_id: feature(253)} dict or an (ids, features) pair.  Returns
+    (ids int64 (N,), emb float32 (N, 256)); with out_path, also writes them as
+    a typed .npz (keys "ids", "emb")."""
+    if isinstance(article_features, dict):
+        ids = np.fromiter(article_features.keys(), dtype=np.int64, count=len(article_features))
+        feats = np.stack([np.asarray(article_features[int(a)], dtype=np.float32) for a in ids])
+    else:
+        ids, feats = article_features
+        ids = np.asarray(ids, dtype=np.int64)
+        feats = np.ascontiguousarray(feats, dtype=np.float32)
+    if device is None:
+        device = next(model.parameters()).device
+    model = model.to(device).eval()
+    x = torch.from_numpy(feats).to(device)
+    emb = model.embed(x, batch=batch).cpu().numpy()
+    if out_path is not None:
+        np.savez(out_path, ids=ids, emb=emb)
+    return ids, emb
+
+
+def load_article_table(path: str):
+    """Retrieval.py:6-9 -> (ids int64 (N,), embeddings float32 (N, d))."""
+    if path.endswith(".npz"):
+        z = np.load(path)
+        return z["ids"].astype(np.int64), np.ascontiguousarray(z["emb"], dtype=np.float32)
+    table = np.load(path)  # numeric (N, d+1) table; object arrays are refused (allow_pickle=False)
+    return table[:, -1].astype(np.int64), np.ascontiguousarray(table[:, :-1], dtype=np.float32)
+
+
+class ArticleTripletDataset(torch.utils.data.Dataset):
+    """embedding_generate.py:25-49: for every user and every ordered pair of
+    clicks (i < j): (anchor = click i, positive = click j, negative = a random
+    article the user never clicked).  Items are ids; features are gathered on
+    the device by train_triplet."""
+
+    def __init__(self, user_clicks: dict, all_article_ids, rng=random):
+        all_ids = list(all_article_ids)
+        trip = []
+        for _, clicked_articles in user_clicks.items():
+            clicked = set(clicked_articles)
+            if len(clicked_articles) < 2:
+                continue
+            for i in range(len(clicked_articles) - 1):
+                for j in range(i + 1, len(clicked_articles)):
+                    neg = rng.choice(all_ids)
+                    while neg in clicked:
+                        neg = rng.choice(all_ids)
+                    trip.append((clicked_articles[i], clicked_articles[j], neg))
+        self.triplets = np.asarray(trip, dtype=np.int64).reshape(-1, 3)
+
+    def __len__(self):
+        return len(self.triplets)
+
+    def __getitem__(self, idx):
+        return self.triplets[idx]
+
+
+def train_triplet(model, triplets: np.ndarray, id_to_row: dict, features: torch.Tensor, optimizer,
+                  batch_size: int = 64, margin: float = MARGIN, shuffle_seed: int | None = 0):
+    """One epoch of embedding_generate.py:88-100 over id triplets; features
+    (N, 253) live on the device, rows looked up by id.  Returns the mean of
+    loss * batch rows, as the reference's running_loss / len(loader)."""
+    dev = features.device
+    rows = torch.from_numpy(np.vectorize(id_to_row.__getitem__)(triplets).astype(np.int64)).to(dev)
+    crit = nn.TripletMarginLoss(margin=margin, p=2)
+    order = np.arange(len(rows))
+    if shuffle_seed is not None:
+        np.random.default_rng(shuffle_seed).shuffle(order)
+    order = torch.from_numpy(order).to(dev)
+    model.train()
+    running = torch.zeros((), dtype=torch.float64, device=dev)
+    nb = 0
+    for lo in range(0, len(order), batch_size):
+        r = rows[order[lo:lo + batch_size]]
+        optimizer.zero_grad()
+        a, p, n = (model(features[r[:, c]]) for c in range(3))
+        loss = crit(a, p, n)
+        loss.backward()
+        optimizer.step()
+        running += loss.detach() * r.shape[0]
+        nb += 1
+    return (running / max(nb, 1)).item()

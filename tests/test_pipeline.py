@@ -1,0 +1,99 @@
+"""Retrieval -> DIN re-rank (SURVEY §8f rank 1, configs[4]).  CPU: candidate
+list semantics of Retrieval.py:28-34 / finialize_retrieval.py.  GPU: the
+batched re-rank reproduces the reference's per-user evaluate() (logits and
+NDCG@5 from the golden fixture made by DIN.py itself), and the end-to-end
+retrieve+rerank equals the oracle composition."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from tests.conftest import GOLDEN
+
+
+def test_finalize_candidates_appends_missing_ground_truth():
+    from newsrecommend_amd.pipeline import finalize_candidates
+
+    recs = {1: np.array([5, 6, 7]), 2: np.array([8, 9]), 3: np.arange(500)}
+    out = finalize_candidates(recs, {1: 6, 2: 4})
+    assert out[1].tolist() == [5, 6, 7] and out[2].tolist() == [8, 9, 4]
+    assert len(out[3]) == 500  # the reference's 400-cap line has no effect (its result is discarded)
+
+
+def test_pad_candidates():
+    from newsrecommend_amd.pipeline import pad_candidates
+
+    rows, mask = pad_candidates([[10, 11], [12], []], {10: 0, 11: 1, 12: 2})
+    assert rows.tolist() == [[0, 1], [2, -1], [-1, -1]]
+    assert mask.sum().item() == 3
+
+
+def _eval_world():
+    from newsrecommend_amd.din import DIN
+
+    z = np.load(os.path.join(GOLDEN, "din_dataset.npz"))
+    row = {int(a): i for i, a in enumerate(z["item_ids"])}
+    hist = np.vectorize(lambda a: row.get(int(a), -1))(z["ev_hist"]).astype(np.int32)
+    cands, o = [], 0
+    for n in z["ev_cand_len"]:
+        cands.append(z["ev_cand"][o:o + n])
+        o += n
+    m = DIN(int(z["d"]), 32, 32, 0.36)
+    m.load_state_dict({k[4:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("sd::")})
+    return z, row, hist, cands, m
+
+
+@pytest.mark.gpu
+def test_rerank_matches_reference_evaluate(gpu):
+    from newsrecommend_amd.pipeline import ndcg_at_k, pad_candidates, rerank
+
+    z, row, hist, cands, m = _eval_world()
+    m = m.cuda()
+    table = torch.from_numpy(z["table"]).cuda()
+    crow, mask = pad_candidates(cands, row, device="cuda")
+    logits = rerank(m, table, torch.from_numpy(hist).cuda(), crow)
+    flat = logits[mask].cpu().numpy()
+    np.testing.assert_allclose(flat, z["ev_logits"], atol=1e-4)
+    labs, o = torch.zeros_like(logits), 0
+    for i, n in enumerate(z["ev_cand_len"]):
+        labs[i, :n] = torch.from_numpy(z["ev_lab"][o:o + n].astype(np.float32))
+        o += n
+    nd = ndcg_at_k(logits, labs, 5)
+    assert abs(nd.mean().item() - float(z["ev_ndcg"])) < 1e-9
+
+
+@pytest.mark.gpu
+def test_retrieve_and_rerank_end_to_end(gpu):
+    from newsrecommend_amd import faiss as nf
+    from newsrecommend_amd.din import DIN
+    from newsrecommend_amd.pipeline import retrieve_and_rerank
+    from oracle import knn_oracle as ko
+
+    rng = np.random.default_rng(3)
+    n_items, d, U, L = 30_000, 64, 40, 12
+    table = (rng.standard_normal((n_items, d)) * 0.5).astype(np.float32)
+    hist = rng.integers(0, n_items, (U, L)).astype(np.int32)
+    hist[:, 9:] = -1
+    profiles = table[np.maximum(hist, 0)].mean(1).astype(np.float32)
+    gt = rng.integers(0, n_items, U).astype(np.int32)
+    idx = nf.IndexFlatIP(d)
+    idx.add(table)
+    torch.manual_seed(0)
+    m = DIN(d, 32, 32, 0.0).cuda().eval()
+    T = torch.from_numpy(table).cuda()
+    top, logits, cand, nd = retrieve_and_rerank(idx, m, T, torch.from_numpy(profiles).cuda(),
+                                                torch.from_numpy(hist).cuda(), 50, 5, torch.from_numpy(gt).cuda())
+    _, Io, _ = ko.exact_search(profiles, table, 50, ko.METRIC_IP)
+    np.testing.assert_array_equal(cand[:, :50].cpu().numpy(), Io)
+    for u in range(U):  # appended ground truth only when missing
+        assert (cand[u] == gt[u]).sum().item() == 1
+    # logits equal a plain per-user DIN forward
+    with torch.no_grad():
+        for u in (0, 17):
+            c = cand[u][cand[u] >= 0].long()
+            keys = torch.where(torch.from_numpy(hist[u]).cuda()[None, :, None] >= 0,
+                               T[torch.from_numpy(np.maximum(hist[u], 0)).cuda().long()][None], 0.0)
+            ref = m(T[c], keys.expand(len(c), -1, -1)).view(-1)
+            torch.testing.assert_close(logits[u][cand[u] >= 0], ref, atol=1e-5, rtol=1e-5)
+    assert nd.shape == (U,) and top.shape == (U, 5)
