@@ -16,6 +16,10 @@ Secondary record `ivf` (configs[3] shape): IVF-Flat nlist=300, nprobe=32 over
 10M x 128 items (L2), rows split over the ranks, exact top-k per rank merged
 after one all_gather; recall@5 against the exact flat search.
 
+Secondary record `e2e` (configs[4] shape): flat top-200 over 10M x 256 items
+(corpus sharded) -> ground truth appended -> DIN re-rank of this rank's users
+(users sharded) -> NDCG@5; value = users/s end to end.
+
 Secondary record `din` (configs[2]): DIN training, bf16 table of 2M items,
 5M synthetic click rows, L = 50, d = 128, A = 128, F = 32; one step = fwd +
 bwd + clip + Adam on a batch of --din-batch rows; data-parallel replicas with
@@ -296,6 +300,95 @@ def _cpu_ivf(args, index, xb, xq, k, nprobe):
                       f"per query (faiss IndexIVFFlat scan restated), {dt:.1f} s"}
 
 
+# ------------------------------------------------------------------ E2E --
+def bench_e2e(args, rank, world, dev):
+    """configs[4]: flat top-200 retrieval over 10M x 256 items (corpus rows
+    sharded, exact per-shard lists merged after one all_gather) for a batch of
+    user profiles, ground truth appended when missing (finialize_retrieval.py),
+    then DIN re-rank of the 201 candidates of this rank's share of the users
+    (users sharded: replicas) and NDCG@5.  One step = one batch of
+    --e2e-users users end to end."""
+    from newsrecommend_amd.data import clustered_corpus, zipf_ids
+    from newsrecommend_amd.din import DIN
+    from newsrecommend_amd.dist import ShardedIndexFlat, shard_range
+    from newsrecommend_amd.pipeline import ndcg_at_k, rerank
+
+    n, d, U, L, kr = args.e2e_nb, 256, args.e2e_users, 50, args.e2e_k
+    xb = clustered_corpus(n, d, seed=1234, device=dev)
+    index = ShardedIndexFlat(d, 0, device=dev)
+    index.add_full(xb)
+    table = xb.to(torch.bfloat16)  # the DIN item table: the same embeddings, bf16 (full copy on every rank)
+    del xb
+    torch.cuda.empty_cache()
+    g = torch.Generator(device=dev).manual_seed(11)
+    hist = zipf_ids(U * L, n, generator=g, device=dev).view(U, L).to(torch.int32)
+    lens = torch.randint(1, L + 1, (U,), generator=g, device=dev)
+    hist = torch.where(torch.arange(L, device=dev)[None] < lens[:, None], hist, torch.full_like(hist, -1))
+    valid = (hist >= 0).unsqueeze(-1)
+    profiles = (table[hist.clamp_min(0).long()].float() * valid).sum(1) / valid.sum(1)
+    gt = zipf_ids(U, n, generator=g, device=dev).to(torch.int32)
+    torch.manual_seed(42)
+    model = DIN(d, 128, 32, 0.36).to(dev).eval()
+    ulo, uhi = shard_range(U, rank, world)
+
+    def step():
+        _, I = index.search_device(profiles, kr)
+        cand = I[ulo:uhi].to(torch.int32)
+        g_ = gt[ulo:uhi]
+        hit = (cand == g_[:, None]).any(1)
+        cand = torch.cat([cand, torch.where(hit, torch.full_like(g_, -1), g_)[:, None]], 1)
+        logits = rerank(model, table, hist[ulo:uhi], cand)
+        labels = (cand == g_[:, None]) & (cand >= 0)
+        return cand, logits, ndcg_at_k(logits, labels, 5)
+
+    for _ in range(args.warmup):
+        step()
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        cand, logits, nd = step()
+    barrier(world)
+    el = max_over_ranks(time.perf_counter() - t0, world, dev)
+    # stage split (rank-local, outside the timed region)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(3):
+        index.search_device(profiles, kr)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    for _ in range(3):
+        rerank(model, table, hist[ulo:uhi], cand)
+    torch.cuda.synchronize()
+    t3 = time.perf_counter()
+    out = {
+        "metric": "end-to-end users/s (retrieve top-200 + DIN re-rank + NDCG@5)", "value": U * args.steps / el,
+        "unit": "users/s", "ms_per_step": el / args.steps * 1e3,
+        "config": {"workload": f"configs[4]: {n}x{d} flat IP top-{kr} -> DIN re-rank (d={d}, A=128, F=32, L={L}), "
+                               f"{U} users per step",
+                   "parallelism": f"corpus-shard{world} retrieval + user-shard{world} re-rank" if world > 1
+                   else "single GPU"},
+        "stages_ms": {"retrieve": (t2 - t1) / 3 * 1e3, "rerank": (t3 - t2) / 3 * 1e3},
+        "rerank_samples_per_step": int((uhi - ulo) * (kr + 1)),
+        "ndcg_at_5_mean_rank0": float(nd.mean().item()),
+        "fallback_queries": int(index.local.last_fallback.item()),
+    }
+    if rank == 0:
+        # re-rank parity on a few users: the reference's per-user forward
+        # (DIN.py:168-173: model(cand, his.expand(C, -1, -1))) on the same rows
+        errs = []
+        with torch.no_grad():
+            for u in range(0, uhi - ulo, max(1, (uhi - ulo) // 4)):
+                c = cand[u][cand[u] >= 0].long()
+                h = hist[ulo + u]
+                keys = torch.where(h[None, :, None] >= 0, table[h.clamp_min(0).long()][None].float(), 0.0)
+                ref = model(table[c].float(), keys.expand(len(c), -1, -1)).view(-1)
+                errs.append(float((logits[u][cand[u] >= 0] - ref).abs().max()))
+        out["rerank_vs_per_user_forward_max_abs"] = max(errs)
+    del index, table
+    torch.cuda.empty_cache()
+    return out
+
+
 # ------------------------------------------------------------------ DIN --
 def bench_din(args, rank, world, dev):
     from newsrecommend_amd.data import synthetic_click_rows
@@ -419,7 +512,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["flat", "din", "ivf", "all"], default="all")
+    ap.add_argument("--workload", choices=["flat", "din", "ivf", "e2e", "all"], default="all")
     ap.add_argument("--nb", type=int, default=1_000_000)
     ap.add_argument("--d", type=int, default=128)
     ap.add_argument("--nq", type=int, default=4096)
@@ -429,6 +522,9 @@ def main():
     ap.add_argument("--ivf-nlist", type=int, default=300)
     ap.add_argument("--ivf-nprobe", type=int, default=32)
     ap.add_argument("--ivf-niter", type=int, default=20)
+    ap.add_argument("--e2e-nb", type=int, default=10_000_000)
+    ap.add_argument("--e2e-users", type=int, default=4096)
+    ap.add_argument("--e2e-k", type=int, default=200)
     ap.add_argument("--din-rows", type=int, default=5_000_000)
     ap.add_argument("--din-items", type=int, default=2_000_000)
     ap.add_argument("--din-batch", type=int, default=4096)
@@ -460,6 +556,12 @@ def main():
                 rec["cpu_baseline"] = r["cpu_baseline"]
         rec["ivf"] = r
         torch.cuda.empty_cache()
+    if args.workload in ("e2e", "all"):
+        r = bench_e2e(args, rank, world, dev)
+        if args.workload == "e2e":
+            rec.update({"metric": r["metric"], "value": r["value"], "unit": r["unit"], "ms_per_step": r["ms_per_step"],
+                        "config": r["config"]})
+        rec["e2e"] = r
     if args.workload in ("din", "all"):
         r = bench_din(args, rank, world, dev)
         if args.workload == "din":
