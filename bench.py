@@ -405,16 +405,22 @@ def bench_din(args, rank, world, dev):
     B = args.din_batch
     perm = torch.randperm(rows, device=dev)
     nbatch = rows // B
-    graphed = world == 1 and not args.din_eager
-    opt = torch.optim.Adam(model.parameters(), lr=1.62e-3, weight_decay=8.96e-5, capturable=graphed)
-    if graphed:
-        from newsrecommend_amd.din import GraphedTrainStep
+    fused = not args.din_eager
+    graphed = fused and world == 1
+    opt = torch.optim.Adam(model.parameters(), lr=1.62e-3, weight_decay=8.96e-5)
+    if fused:
+        from newsrecommend_amd.din import FusedTrainStep
 
-        trainer = GraphedTrainStep(model, opt, crit, table, hist, tgt, lab, B)
+        def allreduce(G):
+            dist.all_reduce(G)
+            G.div_(world)
+
+        trainer = FusedTrainStep(model, table, hist, tgt, lab, B, lr=1.62e-3, weight_decay=8.96e-5, clip=1.0,
+                                 graph=graphed, grad_hook=allreduce if world > 1 else None)
 
     def step(s):
         idx = perm[(s % nbatch) * B:(s % nbatch + 1) * B]
-        if graphed:
+        if fused:
             return trainer.step(idx)
         logits = model.forward_ids(table, tgt[idx], hist[idx])
         loss = crit(logits, lab[idx])
@@ -459,8 +465,10 @@ def bench_din(args, rank, world, dev):
         "metric": "DIN train samples/s", "value": sps, "unit": "samples/s", "ms_per_step": el / args.steps * 1e3,
         "config": {"workload": "configs[2]: DIN train bf16, 5M synthetic click rows, seq_len=50, emb_dim=128",
                    "rows": rows, "items": n_items, "batch": B, "attn_units": A, "fc_units": F,
-                   "parallelism": f"dp{world}", "step": "hip graph" if graphed else "eager"},
-        "final_loss": float(loss.item()),
+                   "parallelism": f"dp{world}",
+                   "step": ("fused head/optimizer kernels, one hip graph" if graphed else
+                            "fused head/optimizer kernels + RCCL grad all_reduce") if fused else "eager torch"},
+        "final_loss": float(loss.reshape(-1)[0].item()),
         "kernels_ms": {"attn_fwd": fwd_ms, "attn_bwd+reduce": bwd_ms},
         "roofline_fwd": {"bound": "hbm", "achieved": fwd_gbs, "peak": HBM_GBS, "unit": "GB/s",
                          "frac": fwd_gbs / HBM_GBS, "traffic": None,

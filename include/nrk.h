@@ -177,6 +177,41 @@ int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe, int32_t np
                    int64_t id_offset, int32_t* n_fallback, void* ws, size_t ws_bytes,
                    void* const* stage_events, void* stream);
 
+/* ------------------------------------------------------------ DIN head --
+ * The MLP head of DIN in train mode, forward and backward (DIN.py:117-123,
+ * 130-133 with BCEWithLogitsLoss(mean), DIN.py:143-148):
+ *   x = [q | pooled] (B x 2d) -> BN0 -> Linear(2d,F) -> ReLU -> Dropout(p)
+ *     -> BN1 -> Linear(F,F/2) -> ReLU -> Dropout(p) -> BN2 -> Linear(F/2,1)
+ * Parameters in nn.Module order (fc.0 ... fc.9); running statistics and
+ * num_batches_tracked are updated as torch's train-mode BatchNorm1d does;
+ * gradients are WRITTEN (not accumulated).  Dropout masks are a counter-based
+ * hash of (seed, *step, layer, row, col).  Outputs: logits [B], loss [1]
+ * (mean BCE), dpooled [B][ld] (the gradient w.r.t. pooled, the attention
+ * backward's input; columns d..ld-1 zeroed).  B must be a multiple of 32,
+ * 2d <= 512, F even <= 64. */
+typedef struct {
+  const float *bn0_w, *bn0_b, *fc1_w, *fc1_b, *bn1_w, *bn1_b, *fc2_w, *fc2_b, *bn2_w, *bn2_b, *fc3_w, *fc3_b;
+  float *bn0_rm, *bn0_rv, *bn1_rm, *bn1_rv, *bn2_rm, *bn2_rv;
+  int64_t *bn0_nb, *bn1_nb, *bn2_nb;
+  float *g_bn0_w, *g_bn0_b, *g_fc1_w, *g_fc1_b, *g_bn1_w, *g_bn1_b, *g_fc2_w, *g_fc2_b, *g_bn2_w, *g_bn2_b,
+      *g_fc3_w, *g_fc3_b;
+} nrk_din_head_params;
+int nrk_din_head_workspace(int32_t B, int32_t d, int32_t F, size_t* ws_bytes);
+int nrk_din_head_train(const float* q, const float* pooled, int64_t ld_pooled, const float* labels,
+                       int32_t B, int32_t d, int32_t F, float momentum, float eps, float p_drop,
+                       uint64_t seed, const float* step, const nrk_din_head_params* params,
+                       float* logits, float* loss, float* dpooled, void* ws, size_t ws_bytes,
+                       void* stream);
+
+/* clip_grad_norm_(max_norm) + torch.optim.Adam (L2 weight decay) over one
+ * flat parameter buffer (DIN.py:150-151): *step (device f32) is incremented,
+ * grads are scaled in place by the clip coefficient, exp_avg / exp_avg_sq /
+ * params updated with torch's capturable-Adam formulas. */
+int nrk_clip_adam_workspace(int64_t n, size_t* ws_bytes);
+int nrk_clip_adam(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
+                  float* step, float lr, float beta1, float beta2, float eps, float weight_decay,
+                  float max_norm, void* ws, size_t ws_bytes, void* stream);
+
 /* Row gather (table [N][d] dtype -> out [n][d] f32), id < 0 -> zeros.
  * Replaces the per-sample dict lookups of DIN.py:47-50,83 (target and
  * candidate embeddings). */

@@ -1,0 +1,697 @@
+// din_head.hip — DIN's MLP head in train mode, forward + backward, and the
+// fused clip_grad_norm_ + Adam step (DIN.py:117-123,130-133,143-151).
+//
+// The head is tiny (2d -> F -> F/2 -> 1 per sample) but in torch it is ~150
+// latency-bound launches per step (three train-mode BatchNorms, Linear,
+// ReLU, Dropout, BCE and their backward).  Here it is 8 kernels over blocks
+// of 32 rows:
+//   stats0   per-block sums of x = [q | pooled] for BN0
+//   fwd1     BN0 -> Linear(2d,F) -> ReLU -> Dropout, BN1 sums
+//   fwd2     BN1 -> Linear(F,F/2) -> ReLU -> Dropout, BN2 sums
+//   fwd3     BN2 -> Linear(F/2,1) -> BCEWithLogits (mean); dlogit; BN2-bwd sums
+//   bwd2     BN2 bwd -> Dropout/ReLU bwd -> Linear(F,F/2) bwd; BN1-bwd sums
+//   bwd1     BN1 bwd -> Dropout/ReLU bwd -> Linear(2d,F) bwd; BN0-bwd sums
+//   bwd0     BN0 bwd -> dpooled (the attention backward's input)
+//   grads    parameter gradients = fixed-order sums of the block partials
+// Batch statistics are summed in fp64 per block and over blocks in a fixed
+// order (deterministic); every block recomputes the finalised statistics it
+// needs, and the first kernel that finalises a BatchNorm updates its running
+// statistics (momentum, unbiased variance) and num_batches_tracked.
+// Activations are recomputed in the backward kernels from the stored
+// pre-activations a1/a2 and the counter-based dropout masks.
+#include <math.h>
+
+#include "nrk_common.h"
+
+namespace nrk {
+
+constexpr int HR = 32;  // rows per block
+
+struct HeadArgs {
+  nrk_din_head_params p;
+  const float* q;
+  const float* pooled;
+  int64_t ld;  // row stride of pooled / dpooled
+  const float* y;
+  int B, d, D2, F, F2, nblk;
+  float momentum, eps, p_drop;
+  uint64_t seed;
+  const float* step;  // device step counter (dropout stream per step)
+  // workspace
+  double *part0, *part1, *part2, *part3, *part4, *part5;
+  double *sum0, *sum1, *sum2, *sum3, *sum4, *sum5, *sumw1;  // the partials summed over blocks
+  float *stat0, *stat1, *stat2;  // finalised {mean, invstd} per feature
+  float *a1, *a2, *dh2, *dh1, *dh0, *pw1;
+  float* logits;
+  float* loss;
+  float* dpooled;
+};
+
+__device__ __forceinline__ float hx(const HeadArgs& a, int64_t r, int c) {
+  return c < a.d ? a.q[r * a.d + c] : a.pooled[r * a.ld + (c - a.d)];
+}
+
+// counter-based dropout mask (splitmix64 of (seed, step, layer, row, col))
+__device__ __forceinline__ float keep_scale(const HeadArgs& a, int layer, int64_t r, int c) {
+  if (a.p_drop <= 0.f) return 1.f;
+  uint64_t z = a.seed ^ ((uint64_t)(int64_t)(*a.step) * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)layer << 58) ^
+               ((uint64_t)r << 20) ^ (uint64_t)c;
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  const float u = (float)(z >> 40) * (1.0f / 16777216.0f);
+  return u >= a.p_drop ? 1.f / (1.f - a.p_drop) : 0.f;
+}
+
+// Column sums over the blocks' partials, fixed order (deterministic): a
+// block covers 32 columns with 8 row groups; groups combined in LDS.
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ part, int nblk, int stride, int ncols,
+                                                     double* __restrict__ out) {
+  __shared__ double red[8][33];
+  const int cl = threadIdx.x & 31, g = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
+  double s = 0.0;
+  if (c < ncols) {
+#pragma unroll 4
+    for (int b = g; b < nblk; b += 8) s += (double)part[(int64_t)b * stride + c];
+  }
+  red[g][cl] = s;
+  __syncthreads();
+  if (g == 0 && c < ncols) {
+    double t = 0.0;
+    for (int i = 0; i < 8; ++i) t += red[i][cl];
+    out[c] = t;
+  }
+}
+
+// finalise BN batch statistics of C features (sums S[c], S[C + c]) into LDS;
+// the designated block also publishes them and updates the running statistics
+__device__ void bn_finalize(const HeadArgs& a, const double* sum, int C, float* s_mean, float* s_inv, float* stat,
+                            float* rm, float* rv, int64_t* nb, bool publish) {
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const double mean = sum[c] / a.B;
+    double var = sum[C + c] / a.B - mean * mean;
+    if (var < 0) var = 0;
+    const float inv = (float)(1.0 / sqrt(var + (double)a.eps));
+    s_mean[c] = (float)mean;
+    s_inv[c] = inv;
+    if (publish) {
+      stat[c] = (float)mean;
+      stat[C + c] = inv;
+      rm[c] = (1.f - a.momentum) * rm[c] + a.momentum * (float)mean;
+      rv[c] = (1.f - a.momentum) * rv[c] + a.momentum * (float)(var * a.B / (a.B - 1));
+    }
+  }
+  if (publish && threadIdx.x == 0 && nb) *nb += 1;
+}
+
+__device__ __forceinline__ void load_stat(const float* stat, int C, float* s_mean, float* s_inv) {
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    s_mean[c] = stat[c];
+    s_inv[c] = stat[C + c];
+  }
+}
+
+// dot product of n terms x[i*sx] * y[i*sy] with 4 independent chains (the
+// LDS loads of 4 terms are in flight together: these kernels run one wave
+// per SIMD, so a rolled loop waits out every ds_read latency)
+__device__ __forceinline__ float dot4(const float* x, int sx, const float* y, int sy, int n, float init) {
+  float c0 = init, c1 = 0.f, c2 = 0.f, c3 = 0.f;
+  int i = 0;
+  for (; i + 4 <= n; i += 4) {
+    c0 = fmaf(x[i * sx], y[i * sy], c0);
+    c1 = fmaf(x[(i + 1) * sx], y[(i + 1) * sy], c1);
+    c2 = fmaf(x[(i + 2) * sx], y[(i + 2) * sy], c2);
+    c3 = fmaf(x[(i + 3) * sx], y[(i + 3) * sy], c3);
+  }
+  for (; i < n; ++i) c0 = fmaf(x[i * sx], y[i * sy], c0);
+  return (c0 + c1) + (c2 + c3);
+}
+
+__global__ __launch_bounds__(256) void head_stats0(HeadArgs a) {
+  const int64_t r0 = (int64_t)blockIdx.x * HR;
+  for (int c = threadIdx.x; c < a.D2; c += 256) {
+    double s = 0.0, ss = 0.0;
+    for (int r = 0; r < HR; ++r) {
+      const double v = hx(a, r0 + r, c);
+      s += v;
+      ss += v * v;
+    }
+    a.part0[(int64_t)blockIdx.x * 2 * a.D2 + c] = s;
+    a.part0[(int64_t)blockIdx.x * 2 * a.D2 + a.D2 + c] = ss;
+  }
+}
+
+// LDS: h0 [HR][D2+1], W1 [F][D2+1], mean/inv [D2] x 2, d1 [HR][F]
+__global__ __launch_bounds__(256) void head_fwd1(HeadArgs a) {
+  extern __shared__ float sm[];
+  const int D2 = a.D2, F = a.F, ds = D2 + 1;
+  float* h0 = sm;
+  float* w1 = h0 + HR * ds;
+  float* mean = w1 + F * ds;
+  float* inv = mean + D2;
+  float* d1 = inv + D2;
+  const int64_t r0 = (int64_t)blockIdx.x * HR;
+  bn_finalize(a, a.sum0, D2, mean, inv, a.stat0, a.p.bn0_rm, a.p.bn0_rv, a.p.bn0_nb, blockIdx.x == 0);
+  for (int e = threadIdx.x; e < F * D2; e += 256) w1[(e / D2) * ds + e % D2] = a.p.fc1_w[e];
+  __syncthreads();
+  for (int e = threadIdx.x; e < HR * D2; e += 256) {
+    const int r = e / D2, c = e % D2;
+    h0[r * ds + c] = (hx(a, r0 + r, c) - mean[c]) * inv[c] * a.p.bn0_w[c] + a.p.bn0_b[c];
+  }
+  __syncthreads();
+  for (int o = threadIdx.x; o < HR * F; o += 256) {
+    const int r = o / F, j = o % F;
+    float acc = a.p.fc1_b[j];
+    acc = dot4(h0 + r * ds, 1, w1 + j * ds, 1, D2, acc);
+    a.a1[(r0 + r) * F + j] = acc;
+    d1[r * F + j] = fmaxf(acc, 0.f) * keep_scale(a, 1, r0 + r, j);
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < F; j += 256) {
+    double s = 0.0, ss = 0.0;
+    for (int r = 0; r < HR; ++r) {
+      const double v = d1[r * F + j];
+      s += v;
+      ss += v * v;
+    }
+    a.part1[(int64_t)blockIdx.x * 2 * F + j] = s;
+    a.part1[(int64_t)blockIdx.x * 2 * F + F + j] = ss;
+  }
+}
+
+// LDS: h1 [HR][F], W2 [F2][F], mean1/inv1 [F], d2 [HR][F2]
+__global__ __launch_bounds__(256) void head_fwd2(HeadArgs a) {
+  extern __shared__ float sm[];
+  const int F = a.F, F2 = a.F2;
+  float* h1 = sm;
+  float* w2 = h1 + HR * F;
+  float* mean = w2 + F2 * F;
+  float* inv = mean + F;
+  float* d2 = inv + F;
+  const int64_t r0 = (int64_t)blockIdx.x * HR;
+  bn_finalize(a, a.sum1, F, mean, inv, a.stat1, a.p.bn1_rm, a.p.bn1_rv, a.p.bn1_nb, blockIdx.x == 0);
+  for (int e = threadIdx.x; e < F2 * F; e += 256) w2[e] = a.p.fc2_w[e];
+  __syncthreads();
+  for (int e = threadIdx.x; e < HR * F; e += 256) {
+    const int r = e / F, j = e % F;
+    const float d1 = fmaxf(a.a1[(r0 + r) * F + j], 0.f) * keep_scale(a, 1, r0 + r, j);
+    h1[e] = (d1 - mean[j]) * inv[j] * a.p.bn1_w[j] + a.p.bn1_b[j];
+  }
+  __syncthreads();
+  for (int o = threadIdx.x; o < HR * F2; o += 256) {
+    const int r = o / F2, k = o % F2;
+    float acc = a.p.fc2_b[k];
+    acc = dot4(h1 + r * F, 1, w2 + k * F, 1, F, acc);
+    a.a2[(r0 + r) * F2 + k] = acc;
+    d2[o] = fmaxf(acc, 0.f) * keep_scale(a, 2, r0 + r, k);
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < F2; k += 256) {
+    double s = 0.0, ss = 0.0;
+    for (int r = 0; r < HR; ++r) {
+      const double v = d2[r * F2 + k];
+      s += v;
+      ss += v * v;
+    }
+    a.part2[(int64_t)blockIdx.x * 2 * F2 + k] = s;
+    a.part2[(int64_t)blockIdx.x * 2 * F2 + F2 + k] = ss;
+  }
+}
+
+// part3 per block: [F2] sum dh2, [F2] sum dh2*xhat2, [F2] dW3, [1] db3, [1] loss
+__global__ __launch_bounds__(256) void head_fwd3(HeadArgs a) {
+  extern __shared__ float sm[];
+  const int F2 = a.F2;
+  float* h2 = sm;            // [HR][F2]
+  float* xh = h2 + HR * F2;  // [HR][F2] xhat2
+  float* mean = xh + HR * F2;
+  float* inv = mean + F2;
+  float* dl = inv + F2;  // [HR]
+  float* lo = dl + HR;   // [HR]
+  const int64_t r0 = (int64_t)blockIdx.x * HR;
+  bn_finalize(a, a.sum2, F2, mean, inv, a.stat2, a.p.bn2_rm, a.p.bn2_rv, a.p.bn2_nb, blockIdx.x == 0);
+  __syncthreads();
+  for (int e = threadIdx.x; e < HR * F2; e += 256) {
+    const int r = e / F2, k = e % F2;
+    const float d2 = fmaxf(a.a2[(r0 + r) * F2 + k], 0.f) * keep_scale(a, 2, r0 + r, k);
+    const float x = (d2 - mean[k]) * inv[k];
+    xh[e] = x;
+    h2[e] = x * a.p.bn2_w[k] + a.p.bn2_b[k];
+  }
+  __syncthreads();
+  for (int r = threadIdx.x; r < HR; r += 256) {
+    float z = a.p.fc3_b[0];
+    for (int k = 0; k < F2; ++k) z = fmaf(h2[r * F2 + k], a.p.fc3_w[k], z);
+    const float y = a.y[r0 + r];
+    a.logits[r0 + r] = z;
+    lo[r] = fmaxf(z, 0.f) - z * y + log1pf(expf(-fabsf(z)));
+    dl[r] = (1.f / (1.f + expf(-z)) - y) / (float)a.B;
+  }
+  __syncthreads();
+  double* pp = a.part3 + (int64_t)blockIdx.x * (3 * F2 + 2);
+  for (int e = threadIdx.x; e < HR * F2; e += 256) {
+    const int r = e / F2, k = e % F2;
+    a.dh2[(r0 + r) * F2 + k] = dl[r] * a.p.fc3_w[k];
+  }
+  for (int k = threadIdx.x; k < F2; k += 256) {
+    double sb = 0.0, sg = 0.0, sw = 0.0;
+    for (int r = 0; r < HR; ++r) {
+      const double g = (double)dl[r] * a.p.fc3_w[k];
+      sb += g;
+      sg += g * xh[r * F2 + k];
+      sw += (double)dl[r] * h2[r * F2 + k];
+    }
+    pp[k] = sb;
+    pp[F2 + k] = sg;
+    pp[2 * F2 + k] = sw;
+  }
+  if (threadIdx.x == 0) {
+    double s = 0.0, l = 0.0;
+    for (int r = 0; r < HR; ++r) {
+      s += dl[r];
+      l += lo[r];
+    }
+    pp[3 * F2] = s;
+    pp[3 * F2 + 1] = l;
+  }
+}
+
+// part4 per block: [F] sum dh1, [F] sum dh1*xhat1, [F2*F] dW2, [F2] db2
+__global__ __launch_bounds__(256) void head_bwd2(HeadArgs a) {
+  extern __shared__ float sm[];
+  const int F = a.F, F2 = a.F2;
+  float* h1 = sm;             // [HR][F]
+  float* xh1 = h1 + HR * F;   // [HR][F]
+  float* da2 = xh1 + HR * F;  // [HR][F2]
+  float* dh1 = da2 + HR * F2; // [HR][F]
+  float* m1 = dh1 + HR * F;
+  float* i1 = m1 + F;
+  float* m2 = i1 + F;
+  float* i2 = m2 + F2;
+  float* sb2 = i2 + F2;  // sum dh2 over the batch
+  float* sg2 = sb2 + F2; // sum dh2*xhat2
+  const int64_t r0 = (int64_t)blockIdx.x * HR;
+  load_stat(a.stat1, F, m1, i1);
+  load_stat(a.stat2, F2, m2, i2);
+  for (int k = threadIdx.x; k < F2; k += 256) {
+    sb2[k] = (float)a.sum3[k];
+    sg2[k] = (float)a.sum3[F2 + k];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < HR * F; e += 256) {
+    const int r = e / F, j = e % F;
+    const float d1 = fmaxf(a.a1[(r0 + r) * F + j], 0.f) * keep_scale(a, 1, r0 + r, j);
+    const float x = (d1 - m1[j]) * i1[j];
+    xh1[e] = x;
+    h1[e] = x * a.p.bn1_w[j] + a.p.bn1_b[j];
+  }
+  const float invB = 1.f / (float)a.B;
+  for (int e = threadIdx.x; e < HR * F2; e += 256) {
+    const int r = e / F2, k = e % F2;
+    const float a2 = a.a2[(r0 + r) * F2 + k];
+    const float ks = keep_scale(a, 2, r0 + r, k);
+    const float xhat = (fmaxf(a2, 0.f) * ks - m2[k]) * i2[k];
+    const float g = a.p.bn2_w[k];
+    const float dd2 = i2[k] * g * (a.dh2[(r0 + r) * F2 + k] - sb2[k] * invB - xhat * sg2[k] * invB);
+    da2[e] = a2 > 0.f ? dd2 * ks : 0.f;
+  }
+  __syncthreads();
+  double* pp = a.part4 + (int64_t)blockIdx.x * (2 * F + F2 * F + F2);
+  for (int o = threadIdx.x; o < F2 * F; o += 256) {
+    const int k = o / F, j = o % F;
+    double s = 0.0;
+    for (int r = 0; r < HR; ++r) s += (double)da2[r * F2 + k] * h1[r * F + j];
+    pp[2 * F + o] = s;
+  }
+  for (int k = threadIdx.x; k < F2; k += 256) {
+    double s = 0.0;
+    for (int r = 0; r < HR; ++r) s += da2[r * F2 + k];
+    pp[2 * F + F2 * F + k] = s;
+  }
+  for (int e = threadIdx.x; e < HR * F; e += 256) {
+    const int r = e / F, j = e % F;
+    float s = 0.f;
+    s = dot4(da2 + r * F2, 1, a.p.fc2_w + j, F, F2, s);
+    dh1[e] = s;
+    a.dh1[(r0 + r) * F + j] = s;
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < F; j += 256) {
+    double sb = 0.0, sg = 0.0;
+    for (int r = 0; r < HR; ++r) {
+      sb += dh1[r * F + j];
+      sg += (double)dh1[r * F + j] * xh1[r * F + j];
+    }
+    pp[j] = sb;
+    pp[F + j] = sg;
+  }
+}
+
+// part5 per block: [D2] sum dh0, [D2] sum dh0*xhat0, [F] db1; pw1 per block [F*D2] (f32)
+__global__ __launch_bounds__(256) void head_bwd1(HeadArgs a) {
+  extern __shared__ float sm[];
+  const int D2 = a.D2, F = a.F, ds = D2 + 1;
+  float* h0 = sm;             // [HR][D2+1]
+  float* w1 = h0 + HR * ds;   // [F][D2+1]
+  float* da1 = w1 + F * ds;   // [HR][F]
+  float* m0 = da1 + HR * F;
+  float* i0 = m0 + D2;
+  float* m1 = i0 + D2;
+  float* i1 = m1 + F;
+  float* sb1 = i1 + F;
+  float* sg1 = sb1 + F;
+  const int64_t r0 = (int64_t)blockIdx.x * HR;
+  load_stat(a.stat0, D2, m0, i0);
+  load_stat(a.stat1, F, m1, i1);
+  for (int j = threadIdx.x; j < F; j += 256) {
+    sb1[j] = (float)a.sum4[j];
+    sg1[j] = (float)a.sum4[F + j];
+  }
+  for (int e = threadIdx.x; e < F * D2; e += 256) w1[(e / D2) * ds + e % D2] = a.p.fc1_w[e];
+  __syncthreads();
+  for (int e = threadIdx.x; e < HR * D2; e += 256) {  // h0 holds xhat0 here (h0 = xhat0 * w + b)
+    const int r = e / D2, c = e % D2;
+    h0[r * ds + c] = (hx(a, r0 + r, c) - m0[c]) * i0[c];
+  }
+  const float invB = 1.f / (float)a.B;
+  for (int e = threadIdx.x; e < HR * F; e += 256) {
+    const int r = e / F, j = e % F;
+    const float a1 = a.a1[(r0 + r) * F + j];
+    const float ks = keep_scale(a, 1, r0 + r, j);
+    const float xhat = (fmaxf(a1, 0.f) * ks - m1[j]) * i1[j];
+    const float dd1 = i1[j] * a.p.bn1_w[j] * (a.dh1[(r0 + r) * F + j] - sb1[j] * invB - xhat * sg1[j] * invB);
+    da1[e] = a1 > 0.f ? dd1 * ks : 0.f;
+  }
+  __syncthreads();
+  float* pw = a.pw1 + (int64_t)blockIdx.x * F * D2;
+  for (int o = threadIdx.x; o < F * D2; o += 256) {
+    const int j = o / D2, c = o % D2;
+    const float gw = a.p.bn0_w[c], gb = a.p.bn0_b[c];
+    float s = 0.f;
+    float s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll
+    for (int r = 0; r < HR; r += 4) {
+      s = fmaf(da1[r * F + j], fmaf(h0[r * ds + c], gw, gb), s);
+      s1 = fmaf(da1[(r + 1) * F + j], fmaf(h0[(r + 1) * ds + c], gw, gb), s1);
+      s2 = fmaf(da1[(r + 2) * F + j], fmaf(h0[(r + 2) * ds + c], gw, gb), s2);
+      s3 = fmaf(da1[(r + 3) * F + j], fmaf(h0[(r + 3) * ds + c], gw, gb), s3);
+    }
+    s = (s + s1) + (s2 + s3);
+    pw[o] = s;
+  }
+  double* pp = a.part5 + (int64_t)blockIdx.x * (2 * D2 + F);
+  for (int j = threadIdx.x; j < F; j += 256) {
+    double s = 0.0;
+    for (int r = 0; r < HR; ++r) s += da1[r * F + j];
+    pp[2 * D2 + j] = s;
+  }
+  // dh0 = da1 W1 and the BN0-backward sums over this block's rows
+  for (int c = threadIdx.x; c < D2; c += 256) {
+    double sb = 0.0, sg = 0.0;
+    for (int r = 0; r < HR; ++r) {
+      float s = 0.f;
+      s = dot4(da1 + r * F, 1, w1 + c, ds, F, s);
+      a.dh0[(r0 + r) * D2 + c] = s;
+      const float xhat = h0[r * ds + c];
+      sb += s;
+      sg += (double)s * xhat;
+    }
+    pp[c] = sb;
+    pp[D2 + c] = sg;
+  }
+}
+
+// dpooled = the pooled half of BN0's input gradient (padding columns zeroed);
+// one thread per (row, column), independent loads
+__global__ __launch_bounds__(256) void head_bwd0(HeadArgs a) {
+  const int64_t r0 = (int64_t)blockIdx.x * HR;
+  const int D2 = a.D2, d = a.d, ld = (int)a.ld;
+  const float invB = 1.f / (float)a.B;
+  for (int e = threadIdx.x; e < HR * ld; e += 256) {
+    const int r = e / ld, cc = e % ld, c = d + cc;
+    float v = 0.f;
+    if (cc < d) {
+      const float m = a.stat0[c], iv = a.stat0[D2 + c];
+      const float sb = (float)a.sum5[c], sg = (float)a.sum5[D2 + c];
+      const float xhat = (hx(a, r0 + r, c) - m) * iv;
+      v = iv * a.p.bn0_w[c] * (a.dh0[(r0 + r) * D2 + c] - sb * invB - xhat * sg * invB);
+    }
+    a.dpooled[(r0 + r) * a.ld + cc] = v;
+  }
+}
+
+// parameter gradients from the reduced sums (one thread per element)
+__global__ void head_grads(HeadArgs a) {
+  const int D2 = a.D2, F = a.F, F2 = a.F2;
+  const int n_w1 = F * D2;
+  const int total = n_w1 + F + D2 + F2 * F + F2 + F + F2 + 1 + F2;  // BN entries write weight and bias
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    int o = i;
+    if (o < n_w1) { a.p.g_fc1_w[o] = (float)a.sumw1[o]; continue; }
+    o -= n_w1;
+    if (o < F) { a.p.g_fc1_b[o] = (float)a.sum5[2 * D2 + o]; continue; }
+    o -= F;
+    if (o < D2) {  // BN0 weight: sum dh0 * xhat0; bias: sum dh0
+      a.p.g_bn0_w[o] = (float)a.sum5[D2 + o];
+      a.p.g_bn0_b[o] = (float)a.sum5[o];
+      continue;
+    }
+    o -= D2;
+    if (o < F2 * F) { a.p.g_fc2_w[o] = (float)a.sum4[2 * F + o]; continue; }
+    o -= F2 * F;
+    if (o < F2) { a.p.g_fc2_b[o] = (float)a.sum4[2 * F + F2 * F + o]; continue; }
+    o -= F2;
+    if (o < F) {
+      a.p.g_bn1_w[o] = (float)a.sum4[F + o];
+      a.p.g_bn1_b[o] = (float)a.sum4[o];
+      continue;
+    }
+    o -= F;
+    if (o < F2) { a.p.g_fc3_w[o] = (float)a.sum3[2 * F2 + o]; continue; }
+    o -= F2;
+    if (o < 1) {
+      a.p.g_fc3_b[0] = (float)a.sum3[3 * F2];
+      *a.loss = (float)(a.sum3[3 * F2 + 1] / a.B);
+      continue;
+    }
+    o -= 1;
+    if (o < F2) {
+      a.p.g_bn2_w[o] = (float)a.sum3[F2 + o];
+      a.p.g_bn2_b[o] = (float)a.sum3[o];
+    }
+  }
+}
+
+// ------------------------------------------------- clip_grad_norm_ + Adam --
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g, int64_t n, double* __restrict__ part,
+                                                    float* __restrict__ step) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const double v = g[i];
+    s += v * v;
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+  if (blockIdx.x == 0 && threadIdx.x == 0) *step += 1.f;  // Adam's step count, read by the next kernel
+}
+
+// torch.optim.Adam (L2 weight decay, capturable formulas) after clip_grad_norm_
+__global__ __launch_bounds__(256) void clip_adam_kernel(float* __restrict__ p, float* __restrict__ g,
+                                                        float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                        const double* __restrict__ part, int nparts,
+                                                        const float* __restrict__ step, float lr, float beta1,
+                                                        float beta2, float eps, float wd, float max_norm) {
+  __shared__ float s_coef;
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int i = 0; i < nparts; ++i) t += part[i];
+    const float norm = (float)sqrt(t);
+    const float c = max_norm / (norm + 1e-6f);
+    s_coef = c < 1.f ? c : 1.f;
+  }
+  __syncthreads();
+  const float coef = s_coef;
+  const float t = *step;
+  const float bc1 = 1.f - powf(beta1, t), bc2 = 1.f - powf(beta2, t);
+  const float step_size = lr / bc1, bc2_sqrt = sqrtf(bc2);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    float gi = g[i] * coef;
+    g[i] = gi;  // clip_grad_norm_ scales the stored gradients
+    gi = gi + wd * p[i];
+    const float mi = m[i] + (gi - m[i]) * (1.f - beta1);  // torch: exp_avg.lerp_(grad, 1 - beta1)
+    const float vi = v[i] * beta2 + (1.f - beta2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    p[i] = p[i] - step_size * (mi / denom);
+  }
+}
+
+}  // namespace nrk
+
+using namespace nrk;
+
+static void head_sizes(int B, int d, int F, int nblk, size_t* off, size_t* total) {
+  const int D2 = 2 * d, F2 = F / 2;
+  size_t o = 0;
+  auto take = [&](int i, size_t bytes) {
+    off[i] = o;
+    o = align_up(o + bytes, 256);
+  };
+  take(0, (size_t)nblk * 2 * D2 * 8);                  // part0
+  take(1, (size_t)nblk * 2 * F * 8);                   // part1
+  take(2, (size_t)nblk * 2 * F2 * 8);                  // part2
+  take(3, (size_t)nblk * (3 * F2 + 2) * 8);            // part3
+  take(4, (size_t)nblk * (2 * F + F2 * F + F2) * 8);   // part4
+  take(5, (size_t)nblk * (2 * D2 + F) * 8);            // part5
+  take(6, (size_t)2 * D2 * 4);                         // stat0
+  take(7, (size_t)2 * F * 4);                          // stat1
+  take(8, (size_t)2 * F2 * 4);                         // stat2
+  take(9, (size_t)B * F * 4);                          // a1
+  take(10, (size_t)B * F2 * 4);                        // a2
+  take(11, (size_t)B * F2 * 4);                        // dh2
+  take(12, (size_t)B * F * 4);                         // dh1
+  take(13, (size_t)B * D2 * 4);                        // dh0
+  take(14, (size_t)nblk * F * D2 * 4);                 // pw1
+  take(15, (size_t)(2 * D2 + 2 * F + 2 * F2 + (3 * F2 + 2) + (2 * F + F2 * F + F2) + (2 * D2 + F) + F * D2) * 8);
+  *total = o;
+}
+
+extern "C" int nrk_din_head_workspace(int32_t B, int32_t d, int32_t F, size_t* ws_bytes) {
+  NRK_CHECK_ARG(ws_bytes && B > 1 && d > 0 && F >= 2, "din_head_workspace: bad arguments");
+  size_t off[17];
+  head_sizes(B, d, F, (int)cdiv(B, HR), off, ws_bytes);
+  return NRK_OK;
+}
+
+extern "C" int nrk_din_head_train(const float* q, const float* pooled, int64_t ld_pooled, const float* labels,
+                                  int32_t B, int32_t d, int32_t F, float momentum, float eps, float p_drop,
+                                  uint64_t seed, const float* step, const nrk_din_head_params* prm, float* logits,
+                                  float* loss, float* dpooled, void* ws, size_t ws_bytes, void* stream) {
+  NRK_CHECK_ARG(B > 1 && B % HR == 0, "din_head_train: B=%d must be a positive multiple of %d", B, HR);
+  NRK_CHECK_ARG(d > 0 && 2 * d <= 512 && F >= 2 && F <= 64 && F % 2 == 0 && ld_pooled >= d,
+                "din_head_train: unsupported d=%d F=%d ld=%lld", d, F, (long long)ld_pooled);
+  NRK_CHECK_ARG(p_drop >= 0.f && p_drop < 1.f, "din_head_train: dropout %f", (double)p_drop);
+  NRK_CHECK_ARG(q && pooled && labels && step && prm && logits && loss && dpooled && ws, "din_head_train: null pointer");
+  const int nblk = B / HR;
+  size_t off[17], total = 0;
+  head_sizes(B, d, F, nblk, off, &total);
+  if (ws_bytes < total) return fail(NRK_EWORKSPACE, "din_head_train: workspace %zu < %zu", ws_bytes, total);
+  char* w = static_cast<char*>(ws);
+  HeadArgs a;
+  a.p = *prm;
+  a.q = q;
+  a.pooled = pooled;
+  a.ld = ld_pooled;
+  a.y = labels;
+  a.B = B;
+  a.d = d;
+  a.D2 = 2 * d;
+  a.F = F;
+  a.F2 = F / 2;
+  a.nblk = nblk;
+  a.momentum = momentum;
+  a.eps = eps;
+  a.p_drop = p_drop;
+  a.seed = seed;
+  a.step = step;
+  a.part0 = reinterpret_cast<double*>(w + off[0]);
+  a.part1 = reinterpret_cast<double*>(w + off[1]);
+  a.part2 = reinterpret_cast<double*>(w + off[2]);
+  a.part3 = reinterpret_cast<double*>(w + off[3]);
+  a.part4 = reinterpret_cast<double*>(w + off[4]);
+  a.part5 = reinterpret_cast<double*>(w + off[5]);
+  a.stat0 = reinterpret_cast<float*>(w + off[6]);
+  a.stat1 = reinterpret_cast<float*>(w + off[7]);
+  a.stat2 = reinterpret_cast<float*>(w + off[8]);
+  a.a1 = reinterpret_cast<float*>(w + off[9]);
+  a.a2 = reinterpret_cast<float*>(w + off[10]);
+  a.dh2 = reinterpret_cast<float*>(w + off[11]);
+  a.dh1 = reinterpret_cast<float*>(w + off[12]);
+  a.dh0 = reinterpret_cast<float*>(w + off[13]);
+  a.pw1 = reinterpret_cast<float*>(w + off[14]);
+  {
+    double* sb = reinterpret_cast<double*>(w + off[15]);
+    const int D2_ = 2 * d, F2_ = F / 2;
+    a.sum0 = sb;
+    a.sum1 = a.sum0 + 2 * D2_;
+    a.sum2 = a.sum1 + 2 * F;
+    a.sum3 = a.sum2 + 2 * F2_;
+    a.sum4 = a.sum3 + 3 * F2_ + 2;
+    a.sum5 = a.sum4 + 2 * F + F2_ * F + F2_;
+    a.sumw1 = a.sum5 + 2 * D2_ + F;
+  }
+  a.logits = logits;
+  a.loss = loss;
+  a.dpooled = dpooled;
+  hipStream_t st = (hipStream_t)stream;
+  const int D2 = 2 * d, F2 = F / 2;
+  const size_t lds1 = ((size_t)(HR + F) * (D2 + 1) + 2 * D2 + HR * F) * 4;
+  const size_t lds2 = ((size_t)HR * F + F2 * F + 2 * F + HR * F2) * 4;
+  const size_t lds3 = ((size_t)2 * HR * F2 + 2 * F2 + 2 * HR) * 4;
+  const size_t lds4 = ((size_t)3 * HR * F + HR * F2 + 2 * F + 4 * F2) * 4;
+  const size_t lds5 = ((size_t)(HR + F) * (D2 + 1) + HR * F + 2 * D2 + 4 * F) * 4;
+  auto colsum = [&](const double* part, int stride, double* out) {
+    hipLaunchKernelGGL(colsum_kernel<double>, dim3((unsigned)cdiv(stride, 32)), dim3(256), 0, st, part, nblk, stride,
+                       stride, out);
+  };
+  const int s3 = 3 * F2 + 2, s4 = 2 * F + F2 * F + F2, s5 = 2 * D2 + F;
+  hipLaunchKernelGGL(head_stats0, dim3(nblk), dim3(256), 0, st, a);
+  colsum(a.part0, 2 * D2, a.sum0);
+  NRK_CHECK_LAUNCH("head_stats0");
+  hipLaunchKernelGGL(head_fwd1, dim3(nblk), dim3(256), lds1, st, a);
+  colsum(a.part1, 2 * F, a.sum1);
+  NRK_CHECK_LAUNCH("head_fwd1");
+  hipLaunchKernelGGL(head_fwd2, dim3(nblk), dim3(256), lds2, st, a);
+  colsum(a.part2, 2 * F2, a.sum2);
+  NRK_CHECK_LAUNCH("head_fwd2");
+  hipLaunchKernelGGL(head_fwd3, dim3(nblk), dim3(256), lds3, st, a);
+  colsum(a.part3, s3, a.sum3);
+  NRK_CHECK_LAUNCH("head_fwd3");
+  hipLaunchKernelGGL(head_bwd2, dim3(nblk), dim3(256), lds4, st, a);
+  colsum(a.part4, s4, a.sum4);
+  NRK_CHECK_LAUNCH("head_bwd2");
+  hipLaunchKernelGGL(head_bwd1, dim3(nblk), dim3(256), lds5, st, a);
+  colsum(a.part5, s5, a.sum5);
+  hipLaunchKernelGGL(colsum_kernel<float>, dim3((unsigned)cdiv(F * D2, 32)), dim3(256), 0, st, a.pw1, nblk, F * D2,
+                     F * D2, a.sumw1);
+  NRK_CHECK_LAUNCH("head_bwd1");
+  hipLaunchKernelGGL(head_bwd0, dim3(nblk), dim3(256), 0, st, a);
+  NRK_CHECK_LAUNCH("head_bwd0");
+  const int ntot = F * D2 + F + D2 + F2 * F + F2 + F + F2 + 1 + F2;
+  hipLaunchKernelGGL(head_grads, dim3((unsigned)cdiv(ntot, 256)), dim3(256), 0, st, a);
+  NRK_CHECK_LAUNCH("head_grads");
+  return NRK_OK;
+}
+
+extern "C" int nrk_clip_adam_workspace(int64_t n, size_t* ws_bytes) {
+  NRK_CHECK_ARG(ws_bytes && n >= 0, "clip_adam_workspace: bad arguments");
+  *ws_bytes = 256 * 8;
+  return NRK_OK;
+}
+
+extern "C" int nrk_clip_adam(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, float* step,
+                             float lr, float beta1, float beta2, float eps, float weight_decay, float max_norm,
+                             void* ws, size_t ws_bytes, void* stream) {
+  NRK_CHECK_ARG(n > 0 && params && grads && exp_avg && exp_avg_sq && step && ws, "clip_adam: bad arguments");
+  if (ws_bytes < 256 * 8) return fail(NRK_EWORKSPACE, "clip_adam: workspace %zu < 2048", ws_bytes);
+  hipStream_t st = (hipStream_t)stream;
+  int nb = (int)cdiv(n, 256);
+  if (nb > 256) nb = 256;
+  double* part = static_cast<double*>(ws);
+  hipLaunchKernelGGL(sumsq_kernel, dim3(nb), dim3(256), 0, st, grads, n, part, step);
+  NRK_CHECK_LAUNCH("sumsq_kernel");
+  hipLaunchKernelGGL(clip_adam_kernel, dim3(nb), dim3(256), 0, st, params, grads, exp_avg, exp_avg_sq, n, part, nb,
+                     step, lr, beta1, beta2, eps, weight_decay, max_norm);
+  NRK_CHECK_LAUNCH("clip_adam_kernel");
+  return NRK_OK;
+}

@@ -19,6 +19,8 @@ restatement, for CPU checks).
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F  # noqa: F401  (parity with the reference's imports)
@@ -356,4 +358,155 @@ class GraphedTrainStep:
         """Run one step on rows `batch_index` (device int64, length batch_size); returns the device loss."""
         self.idx.copy_(batch_index, non_blocking=True)
         self.graph.replay()
+        return self.loss
+
+
+class _HeadParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in (
+        "bn0_w", "bn0_b", "fc1_w", "fc1_b", "bn1_w", "bn1_b", "fc2_w", "fc2_b", "bn2_w", "bn2_b", "fc3_w", "fc3_b",
+        "bn0_rm", "bn0_rv", "bn1_rm", "bn1_rv", "bn2_rm", "bn2_rv", "bn0_nb", "bn1_nb", "bn2_nb",
+        "g_bn0_w", "g_bn0_b", "g_fc1_w", "g_fc1_b", "g_bn1_w", "g_bn1_b", "g_fc2_w", "g_fc2_b", "g_bn2_w", "g_bn2_b",
+        "g_fc3_w", "g_fc3_b")]
+
+
+class FusedTrainStep:
+    """One DIN training step (DIN.py:143-151) as ~25 launches in one HIP graph:
+    gather + attention forward (libnrk), the whole train-mode MLP head forward
+    and backward (nrk_din_head_train: 8 kernels instead of ~150 torch ops),
+    attention backward (libnrk), and clip_grad_norm_ + Adam over ONE flat
+    parameter buffer (nrk_clip_adam).  The model's parameters and gradients
+    become views into flat buffers (state_dict keys and values unchanged).
+
+    Same semantics as `train()` with torch.optim.Adam(lr, betas, eps,
+    weight_decay) and clip_grad_norm_(clip): train-mode BatchNorm statistics,
+    BCEWithLogits mean loss.  Dropout masks come from a counter-based hash of
+    (seed, step, layer, row, col) instead of torch's Philox stream, so with
+    dropout > 0 the masks differ from torch's (identical distribution)."""
+
+    def __init__(self, model: "DIN", table, hist_ids, target_ids, labels, batch_size, lr=1.62e-3,
+                 betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, clip=1.0, seed=1234, graph=True,
+                 grad_hook=None):
+        dev = table.device
+        self.model, self.table = model, table
+        self.hist_all, self.tgt_all, self.lab_all = hist_ids, target_ids, labels
+        self.B = int(batch_size)
+        if self.B % 32:
+            raise ValueError("FusedTrainStep: batch_size must be a multiple of 32")
+        self.lr, self.betas, self.eps, self.wd, self.clip, self.seed = lr, betas, eps, weight_decay, clip, seed
+        self.grad_hook = grad_hook  # e.g. data-parallel all_reduce of the flat gradient buffer
+        attn0, attn2 = model.attn.attn[0], model.attn.attn[2]
+        self.d = attn0.weight.shape[1] // 2
+        self.A = attn0.weight.shape[0]
+        self.F = model.fc[1].weight.shape[0]
+        self.p_drop = float(model.fc[3].p)
+        self.Dk = _kernel_dim(self.d)
+        # flat parameter / gradient / moment buffers; parameters become views
+        params = list(model.parameters())
+        n = sum(p.numel() for p in params)
+        self.P = torch.empty(n, dtype=torch.float32, device=dev)
+        self.G = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.M = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.V = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.step_t = torch.zeros(1, dtype=torch.float32, device=dev)
+        o = 0
+        with torch.no_grad():
+            for p in params:
+                k = p.numel()
+                self.P[o:o + k].copy_(p.reshape(-1))
+                p.data = self.P[o:o + k].view_as(p)
+                p.grad = self.G[o:o + k].view_as(p)
+                o += k
+        fc = model.fc
+        self.hp = _HeadParams(*[_lib.ptr(t) for t in (
+            fc[0].weight, fc[0].bias, fc[1].weight, fc[1].bias, fc[4].weight, fc[4].bias, fc[5].weight, fc[5].bias,
+            fc[8].weight, fc[8].bias, fc[9].weight, fc[9].bias,
+            fc[0].running_mean, fc[0].running_var, fc[4].running_mean, fc[4].running_var, fc[8].running_mean,
+            fc[8].running_var, fc[0].num_batches_tracked, fc[4].num_batches_tracked, fc[8].num_batches_tracked,
+            fc[0].weight.grad, fc[0].bias.grad, fc[1].weight.grad, fc[1].bias.grad, fc[4].weight.grad,
+            fc[4].bias.grad, fc[5].weight.grad, fc[5].bias.grad, fc[8].weight.grad, fc[8].bias.grad,
+            fc[9].weight.grad, fc[9].bias.grad)])
+        B, d, A, Dk = self.B, self.d, self.A, self.Dk
+        L_ = _lib.load()
+        self.idx = torch.zeros(B, dtype=torch.long, device=dev)
+        self.pooled = torch.empty((B, Dk), dtype=torch.float32, device=dev)
+        self.alpha = torch.empty((B, hist_ids.shape[1]), dtype=torch.float32, device=dev)
+        self.logits = torch.empty(B, dtype=torch.float32, device=dev)
+        self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.dpooled = torch.empty((B, Dk), dtype=torch.float32, device=dev)
+        self.dU = torch.empty((B, A), dtype=torch.float32, device=dev)
+        self.dW1k = torch.empty((A, Dk), dtype=torch.float32, device=dev)
+        sz = _lib.c_size(0)
+        _lib.check(L_.nrk_din_head_workspace(B, d, self.F, sz), "din_head_workspace")
+        self.ws_head = torch.empty(max(sz.value, 1), dtype=torch.uint8, device=dev)
+        _lib.check(L_.nrk_din_attn_bwd_workspace(B, Dk, A, sz), "din_attn_bwd_workspace")
+        self.ws_attn = torch.empty(max(sz.value, 1), dtype=torch.uint8, device=dev)
+        _lib.check(L_.nrk_clip_adam_workspace(n, sz), "clip_adam_workspace")
+        self.ws_opt = torch.empty(max(sz.value, 1), dtype=torch.uint8, device=dev)
+        self.n = n
+        self.graph = None
+        if graph:
+            snap = [t.detach().clone() for t in (self.P, self.M, self.V, self.step_t)]
+            bufs = {k: v.detach().clone() for k, v in model.named_buffers()}
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                self._body()
+            torch.cuda.current_stream(dev).wait_stream(side)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self._body()
+            with torch.no_grad():  # capture ran real steps: restore the model and optimizer state
+                for t, s in zip((self.P, self.M, self.V, self.step_t), snap):
+                    t.copy_(s)
+                for k, v in model.named_buffers():
+                    v.copy_(bufs[k])
+
+    def _body(self):
+        L_ = _lib.load()
+        m = self.model
+        dev = self.table.device
+        st = _lib.stream(dev)
+        B, d, A, Dk = self.B, self.d, self.A, self.Dk
+        hist = self.hist_all.index_select(0, self.idx)
+        tgt = self.tgt_all.index_select(0, self.idx)
+        y = self.lab_all.index_select(0, self.idx).reshape(-1)
+        q = gather_rows(self.table, tgt)
+        W1, b1 = m.attn.attn[0].weight, m.attn.attn[0].bias
+        w2 = m.attn.attn[2].weight.reshape(-1)
+        U = torch.addmm(b1, q, W1[:, :d].t())
+        keys = _pad_last(self.table, Dk)
+        dtype = _dtype_code(keys)
+        W1k = _pad_last(W1[:, d:], Dk)
+        W1k = W1k.contiguous() if dtype == _lib.NRK_DTYPE_F32 else W1k.to(torch.bfloat16)
+        _lib.check(L_.nrk_din_attn_fwd(
+            _lib.ptr(keys), _lib.ptr(hist), keys.shape[0], dtype, _lib.ptr(U), _lib.ptr(W1k), _lib.ptr(w2), 0.0, B,
+            hist.shape[1], Dk, A, _lib.ptr(self.pooled), _lib.ptr(self.alpha), st), "din_attn_fwd")
+        _lib.check(L_.nrk_din_head_train(
+            _lib.ptr(q), _lib.ptr(self.pooled), Dk, _lib.ptr(y), B, d, self.F, 0.1, 1e-5, self.p_drop, self.seed,
+            _lib.ptr(self.step_t), ctypes.byref(self.hp), _lib.ptr(self.logits), _lib.ptr(self.loss),
+            _lib.ptr(self.dpooled), _lib.ptr(self.ws_head), self.ws_head.numel(), st), "din_head_train")
+        gW2, gb2 = m.attn.attn[2].weight.grad, m.attn.attn[2].bias.grad
+        _lib.check(L_.nrk_din_attn_bwd(
+            _lib.ptr(keys), _lib.ptr(hist), keys.shape[0], dtype, _lib.ptr(U), _lib.ptr(W1k), _lib.ptr(w2), 0.0, B,
+            hist.shape[1], Dk, A, _lib.ptr(self.dpooled), _lib.ptr(self.alpha), _lib.ptr(self.dU),
+            _lib.ptr(self.dW1k), _lib.ptr(gW2), _lib.ptr(gb2), _lib.ptr(self.ws_attn), self.ws_attn.numel(), st),
+            "din_attn_bwd")
+        gW1, gb1 = W1.grad, b1.grad
+        gW1[:, :d].copy_(self.dU.t() @ q)
+        gW1[:, d:].copy_(self.dW1k[:, :d])
+        torch.sum(self.dU, 0, out=gb1)
+        if self.grad_hook is not None:
+            self.grad_hook(self.G)
+        _lib.check(L_.nrk_clip_adam(
+            _lib.ptr(self.P), _lib.ptr(self.G), _lib.ptr(self.M), _lib.ptr(self.V), self.n, _lib.ptr(self.step_t),
+            self.lr, self.betas[0], self.betas[1], self.eps, self.wd, self.clip, _lib.ptr(self.ws_opt),
+            self.ws_opt.numel(), st), "clip_adam")
+
+    def step(self, batch_index: torch.Tensor):
+        """One training step on rows `batch_index` (device int64, length B); returns the device loss."""
+        self.idx.copy_(batch_index, non_blocking=True)
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self._body()
         return self.loss

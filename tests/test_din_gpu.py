@@ -208,3 +208,94 @@ def test_graphed_train_step_matches_eager(gpu):
         assert abs(la - lb.item()) < 1e-4, (s, la, lb.item())
     for (n, pa), (_, pb) in zip(ma.named_parameters(), mb.named_parameters()):
         assert torch.allclose(pa, pb, atol=1e-4), n
+
+
+def _setup_fused(p_drop, B=512, n_items=5000, d=64, L=20, seed=3):
+    from newsrecommend_amd.data import synthetic_click_rows
+    from newsrecommend_amd.din import DIN
+
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(seed)
+    table = (torch.randn((n_items, d), generator=g, device=dev) * 0.5).to(torch.bfloat16)
+    hist, tgt, lab = synthetic_click_rows(4096, n_items, L, seed=5, device=dev)
+    torch.manual_seed(0)
+    ma = DIN(d, 64, 32, p_drop).to(dev)
+    mb = DIN(d, 64, 32, p_drop).to(dev)
+    mb.load_state_dict(ma.state_dict())
+    return dev, table, hist, tgt, lab, ma, mb
+
+
+def test_fused_train_step_matches_eager(gpu):
+    """FusedTrainStep (head + clip + Adam fused kernels, one HIP graph) == the
+    eager torch loop (dropout 0): losses, parameters and BN running stats."""
+    from newsrecommend_amd.din import FusedTrainStep
+
+    dev, table, hist, tgt, lab, ma, mb = _setup_fused(0.0)
+    crit = torch.nn.BCEWithLogitsLoss()
+    B = 512
+    fused = FusedTrainStep(ma, table, hist, tgt, lab, B, lr=1e-3, weight_decay=1e-4, clip=1.0)
+    ob = torch.optim.Adam(mb.parameters(), lr=1e-3, weight_decay=1e-4)
+    mb.train()
+    for s in range(5):
+        idx = torch.arange(s * B, (s + 1) * B, device=dev)
+        la = fused.step(idx).item()
+        ob.zero_grad()
+        lb = crit(mb.forward_ids(table, tgt[idx], hist[idx]), lab[idx])
+        lb.backward()
+        torch.nn.utils.clip_grad_norm_(mb.parameters(), 1.0)
+        ob.step()
+        assert abs(la - lb.item()) < 1e-4, (s, la, lb.item())
+    sa, sb = ma.state_dict(), mb.state_dict()
+    for k in sb:
+        if "num_batches" in k:
+            assert int(sa[k]) == int(sb[k]) == 5, k
+        else:
+            assert torch.allclose(sa[k], sb[k], atol=2e-4, rtol=1e-3), (k, (sa[k] - sb[k]).abs().max().item())
+
+
+def _masks_np(seed, step, layer, B, C, p):
+    """The fused head's counter-based dropout masks (din_head.hip keep_scale), in numpy."""
+    M = np.uint64
+    r = np.arange(B, dtype=np.uint64)[:, None]
+    c = np.arange(C, dtype=np.uint64)[None, :]
+    with np.errstate(over="ignore"):
+        z = M(seed) ^ (M(step) * M(0x9E3779B97F4A7C15)) ^ (M(layer) << M(58)) ^ (r << M(20)) ^ c
+        z = z + M(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> M(30))) * M(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> M(27))) * M(0x94D049BB133111EB)
+        z = z ^ (z >> M(31))
+    u = (z >> M(40)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+    return np.where(u >= np.float32(p), np.float32(1.0 / (1.0 - p)), np.float32(0.0))
+
+
+def test_fused_head_with_dropout_matches_torch_with_same_masks(gpu):
+    """dropout 0.36: one fused step's loss and clipped gradients equal a torch
+    head applying the same (hash) masks."""
+    import torch.nn.functional as Fn
+    from newsrecommend_amd.din import FusedTrainStep
+
+    p = 0.36
+    dev, table, hist, tgt, lab, ma, mb = _setup_fused(p)
+    B = 512
+    fused = FusedTrainStep(ma, table, hist, tgt, lab, B, lr=1e-3, weight_decay=0.0, clip=1.0, seed=99, graph=False)
+    idx = torch.arange(B, device=dev)
+    la = fused.step(idx).item()
+    m1 = torch.from_numpy(_masks_np(99, 0, 1, B, 32, p)).to(dev)
+    m2 = torch.from_numpy(_masks_np(99, 0, 2, B, 16, p)).to(dev)
+    from newsrecommend_amd.din import gather_rows
+
+    mb.train()
+    q = gather_rows(table, tgt[idx])
+    x = torch.cat([q, mb.attn.forward_ids(q, table, hist[idx])], 1)
+    fc = mb.fc
+    h = fc[0](x)
+    h = fc[4](torch.relu(fc[1](h)) * m1)
+    h = fc[8](torch.relu(fc[5](h)) * m2)
+    lb = Fn.binary_cross_entropy_with_logits(fc[9](h), lab[idx])
+    lb.backward()
+    torch.nn.utils.clip_grad_norm_(mb.parameters(), 1.0)
+    assert abs(la - lb.item()) < 1e-4, (la, lb.item())
+    for (n, pa), (_, pb) in zip(ma.named_parameters(), mb.named_parameters()):
+        ref = pb.grad
+        assert torch.allclose(pa.grad, ref, atol=1e-6 + 1e-3 * ref.abs().max().item(), rtol=1e-3), \
+            (n, (pa.grad - ref).abs().max().item())
