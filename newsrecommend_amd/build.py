@@ -22,7 +22,8 @@ ORACLE_LIB = os.path.join(ROOT, "oracle", "liboracle_knn.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"]
-SOURCES = ["nrk_common.cpp", "knn_flat.hip", "din_attn.hip", "ivf_build.hip", "din_head.hip"]
+SOURCES = ["nrk_common.cpp", "knn_flat.hip", "din_attn.hip", "ivf_build.hip", "din_head.hip",
+           "screen_dp32.hip", "screen_dp64.hip", "screen_dp128.hip", "screen_dp256.hip"]
 
 
 def _run(cmd):
@@ -40,7 +41,7 @@ def _newer(target, deps):
 
 
 def build_lib(force: bool = False) -> str:
-    headers = [os.path.join(CSRC, "nrk_common.h"), os.path.join(ROOT, "include", "nrk.h")]
+    headers = [os.path.join(CSRC, "nrk_common.h"), os.path.join(CSRC, "screen.h"), os.path.join(ROOT, "include", "nrk.h")]
     objdir = os.path.join(CSRC, "build")
     os.makedirs(objdir, exist_ok=True)
     jobs = []

@@ -20,7 +20,7 @@
 
 #include <type_traits>
 
-#include "nrk_common.h"
+#include "screen.h"
 
 namespace nrk {
 
@@ -91,403 +91,6 @@ __global__ void query_prepare_kernel(const float* __restrict__ xq, int64_t nq, i
     qmeta[4 * row + 1] = sqrt(sr2) * (1.0 + 1e-9);
     qmeta[4 * row + 2] = sq2;
     qmeta[4 * row + 3] = 0.0;
-  }
-}
-
-// ================================================================ screen ==
-// LDS swizzle so that the ds_read_b128 A-fragment reads (32 rows, one 16-B
-// chunk each, 16-lane groups) hit 16 distinct bank slots.
-template <int CPR>
-__device__ __forceinline__ int swz(int row) {
-  if constexpr (CPR >= 16) return row & 15;
-  else return (row / (16 / CPR)) & (CPR - 1);
-}
-
-__device__ __forceinline__ float fmax_ieee(float a, float b) { return __builtin_elementwise_maximum(a, b); }
-
-// Buffer-descriptor LDS-DMA.  The AMDGPU buffer-resource builtins exist only in
-// the device compilation pass; the host pass (which only needs the kernel
-// stubs) silently drops every kernel whose body names them.
-struct BufRsrc {
-#if defined(__HIP_DEVICE_COMPILE__)
-  __amdgpu_buffer_rsrc_t r;
-#endif
-};
-__device__ __forceinline__ BufRsrc make_rsrc(const void* base, int bytes) {
-  BufRsrc b;
-#if defined(__HIP_DEVICE_COMPILE__)
-  b.r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
-#else
-  (void)base;
-  (void)bytes;
-#endif
-  return b;
-}
-#if defined(__HIP_DEVICE_COMPILE__)
-#define NRK_BUFFER_LOAD_LDS(SIZE)                                                                         \
-  __device__ __forceinline__ void buffer_load_lds##SIZE(const BufRsrc& b, void* lds_dst, int vo, int so) { \
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(b.r, (__attribute__((address_space(3))) void*)lds_dst, SIZE, vo, \
-                                             so, 0, 0);                                                  \
-  }
-#else
-#define NRK_BUFFER_LOAD_LDS(SIZE) \
-  __device__ __forceinline__ void buffer_load_lds##SIZE(const BufRsrc&, void*, int, int) {}
-#endif
-NRK_BUFFER_LOAD_LDS(16)
-NRK_BUFFER_LOAD_LDS(4)
-#undef NRK_BUFFER_LOAD_LDS
-
-// Sorted (descending) insertion into a register list of N entries.  Ties keep
-// the resident entry first (it has the lower id: a lane scans ids upward).
-template <int N>
-__device__ __forceinline__ void list_insert(float (&ls)[N], int (&li)[N], float v, int id) {
-#pragma unroll
-  for (int j = 0; j < N; ++j) {
-    bool gt = v > ls[j];
-    float ts = gt ? v : ls[j];
-    int ti = gt ? id : li[j];
-    v = gt ? ls[j] : v;
-    id = gt ? li[j] : id;
-    ls[j] = ts;
-    li[j] = ti;
-  }
-}
-
-// One workgroup = WAVES waves; wave w owns QT tiles of 32 queries; the
-// workgroup streams one corpus chunk in 64-item tiles, staged HBM -> LDS with
-// global_load_lds (double buffered; the XOR swizzle is applied to the SOURCE
-// address since the DMA writes LDS lane-linearly).  MFMA 32x32x16 bf16 with
-// A = items (rows), B = queries (cols): each lane holds ONE query (lane & 31)
-// and 16 items of each 32-item sub-tile.
-//
-// MODE 1 (threshold pre-pass): visits every TSTRIDE-th tile of its chunk and
-//   writes each lane's maximum screened score: many short, disjoint lane
-//   streams, so the R-th largest of a query's lane maxima (tau_select_kernel)
-//   is a proven lower bound on that query's global R-th best screened score.
-// MODE 0 (main pass): every lane keeps its top-(M+1) screened scores in
-//   registers, admitting only scores above max(its (M+1)-th, tau[q]); the
-//   pre-pass bound removes the warm-up insertions that otherwise dominate.
-//   The merge's certificate includes tau[q] in theta.
-//
-// MODE 2 (IVF list scan): the block's work item comes from a device table —
-//   (list l, tile of the queries probing l, chunk of l).  qh holds the probing
-//   queries gathered list-major (segments padded to WQ rows); slot_pair maps a
-//   gathered row back to its (query, probe) pair, whose candidates land at
-//   [(pair * cmax + chunk) * 2 + half].
-// MODE 3 (IVF collect): MODE 2's work items, no lane lists: every item whose
-//   screened score reaches the query's threshold is appended to the query's
-//   candidate buffer (rare: the threshold sits just below the k-th best).
-// MODE 4 (IVF lane maxima): MODE 2's work items, MODE 1's epilogue (each lane
-//   writes the maximum screened score of its stream).
-struct IvfScreen {
-  const int* work_off;     // [nlist + 1] prefix of work items per list
-  const int64_t* list_off; // [nlist + 1] list ranges in the list-major corpus
-  const int* seg_off;      // [nlist] first gathered query row of each list
-  const int* slot_pair;    // [slots] q * nprobe + p, or -1 for padding
-  int nlist, ch, cmax;
-  // MODE 3 (collect): append every item whose screened score >= thr_q[query]
-  const float* thr_q;
-  int* cand_cnt;           // [nq]
-  int* cand_pos;           // [nq][cap] list-major positions
-  int cap, nprobe;
-};
-
-// MODE 3 block-local candidate staging: hits are appended with LDS atomics and
-// flushed at the end of the work item with ONE global atomic per query row
-// (returning global atomics in the epilogue would stall the wave for ~1 us).
-template <int WQ>
-struct CollectLds {
-  static constexpr int CAP = 1024;
-  int n;
-  int qcnt[WQ];
-  int qid[WQ];
-  int base[WQ];
-  int2 ent[CAP];  // {row | rank << 8, position}
-};
-struct NoLds {};
-
-template <int DP, int QT, int M, int WAVES, bool L2, int MODE, int EPI = 0>
-__global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
-    const uint16_t* __restrict__ qh, const uint16_t* __restrict__ xbh, const float* __restrict__ xmeta,
-    int64_t nq, int64_t nb, int64_t chunk, int nch, int nqt, int tstride, float* __restrict__ part_s,
-    int* __restrict__ part_i, float* __restrict__ part_t, const float* __restrict__ tau_q, IvfScreen iv) {
-  constexpr int CPR = DP / 8;        // 16-B chunks per row
-  constexpr int TI = 64;  // items per tile (TI/32 sub-tiles of 32) between barriers
-  constexpr int TCH = TI * CPR;      // 16-B chunks per tile
-  constexpr int NT = WAVES * 64;
-  constexpr int GPT = TCH / NT;      // glds instructions per thread per tile
-  static_assert(TCH % NT == 0, "tile must split evenly over the workgroup");
-  constexpr int KS = DP / 16;
-  constexpr int WQ = WAVES * 32 * QT;
-  constexpr int BUF = TI * DP + 2 * TI;  // uint16 per buffer: rows + TI float norms
-  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BUF];
-  __shared__ std::conditional_t<MODE == 3, CollectLds<WQ>, NoLds> cl;
-
-  const int nblk = gridDim.x, b = blockIdx.x;
-  const int xg = b & 7, jj = b >> 3, q8 = nblk >> 3, r8 = nblk & 7;
-  const int logical0 = (xg < r8 ? xg * (q8 + 1) : r8 * (q8 + 1) + (xg - r8) * q8) + jj;
-  // IVF modes loop persistently over the device work table; flat modes run
-  // exactly one item per block
-  const int total = MODE >= 2 ? iv.work_off[iv.nlist] : nblk;
-  for (int logical = logical0; logical < total; logical += nblk) {
-    if (logical != logical0) __syncthreads();  // the previous item is done with the LDS buffers
-    int c, qt;
-    int64_t ibeg, iend, seg0 = 0;
-    if constexpr (MODE >= 2) {
-      int lo = 0, hi = iv.nlist;  // largest l with work_off[l] <= logical (empty lists own no items)
-      while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (iv.work_off[mid] <= logical) lo = mid;
-        else hi = mid;
-      }
-      const int64_t lb = iv.list_off[lo], le = iv.list_off[lo + 1];
-      const int nchl = (int)cdiv(le - lb, (int64_t)iv.ch);
-      // query tile innermost: the tiles sharing a chunk are consecutive work
-      // items, i.e. run together on one XCD and read the chunk through its L2
-      const int local = logical - iv.work_off[lo];
-      const int nqtl = (iv.work_off[lo + 1] - iv.work_off[lo]) / nchl;
-      c = local / nqtl;
-      qt = local - c * nqtl;
-      ibeg = lb + (int64_t)c * iv.ch;
-      iend = ibeg + iv.ch < le ? ibeg + iv.ch : le;
-      seg0 = iv.seg_off[lo];
-    } else {
-      c = logical / nqt;
-      qt = logical - c * nqt;
-      ibeg = (int64_t)c * chunk;
-      iend = ibeg + chunk < nb ? ibeg + chunk : nb;
-    }
-
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int r = lane & 31, h = lane >> 5;
-    const int ntiles = (int)cdiv(cdiv(iend - ibeg, TI), tstride);  // visited tiles
-
-    bf16x8 qf[QT][KS];
-    int64_t qidx[QT];
-  #pragma unroll
-    for (int t = 0; t < QT; ++t) {
-      qidx[t] = (int64_t)qt * WQ + (w * QT + t) * 32 + r;  // < nq_pad (zero rows)
-      const bf16x8* src = reinterpret_cast<const bf16x8*>(qh + (seg0 + qidx[t]) * DP + 8 * h);
-  #pragma unroll
-      for (int s = 0; s < KS; ++s) qf[t][s] = src[2 * s];
-    }
-    float ls[QT][M + 1];
-    int li[QT][M + 1];
-    float tau[QT];
-    float cthr[QT];  // MODE 3: collect threshold of the lane's query
-    int cq[QT];      // MODE 3: the lane's query (-1: padding row)
-  #pragma unroll
-    for (int t = 0; t < QT; ++t) {
-      tau[t] = (MODE == 0 && tau_q && qidx[t] < nq) ? tau_q[qidx[t]] : -INFINITY;
-      if constexpr (MODE == 3) {
-        const int pair = iv.slot_pair[seg0 + qidx[t]];
-        cq[t] = pair >= 0 ? pair / iv.nprobe : -1;
-        cthr[t] = pair >= 0 ? iv.thr_q[cq[t]] : INFINITY;
-        const int row = (w * QT + t) * 32 + r;
-        if (h == 0) {
-          cl.qid[row] = cq[t];
-          cl.qcnt[row] = 0;
-        }
-      }
-  #pragma unroll
-      for (int j = 0; j <= M; ++j) {
-        ls[t][j] = -INFINITY;
-        li[t][j] = -1;
-      }
-    }
-
-    // HBM -> LDS through chunk-relative buffer descriptors: rows past the chunk
-    // fall outside num_records and read as 0 (masked in the epilogue); each
-    // lane's inverse-swizzled 32-bit offset is fixed, only the scalar tile
-    // offset changes, so staging costs no per-tile vector address math.
-    typedef __attribute__((address_space(3))) void* lds_ptr;
-    const int64_t cnt = iend - ibeg > 0 ? iend - ibeg : 0;
-    const BufRsrc xrs = make_rsrc(xbh + ibeg * DP, (int)(cnt * DP * 2));
-    const BufRsrc nrs = make_rsrc(xmeta + 2 * ibeg, (int)(cnt * 8));
-    int voff[GPT];
-  #pragma unroll
-    for (int u = 0; u < GPT; ++u) {
-      const int p = u * NT + tid;
-      const int row = p / CPR, pc = p % CPR;
-      voff[u] = row * DP * 2 + 16 * (pc ^ swz<CPR>(row));
-    }
-    auto issue_tile = [&](int it, auto buf_c) {
-      constexpr int buf = decltype(buf_c)::value;
-      const int soff = it * tstride * TI * DP * 2;
-  #pragma unroll
-      for (int u = 0; u < GPT; ++u)
-        buffer_load_lds16(xrs, lds + buf * BUF + (u * NT + w * 64) * 8, voff[u], soff);
-      if constexpr (L2) {
-        if (w == 0)
-          buffer_load_lds4(nrs, lds + buf * BUF + TI * DP, lane * 8, it * tstride * TI * 8);
-      }
-    };
-
-    // one 64-item tile (buffer index is a compile-time constant: immediate LDS offsets)
-    auto tile = [&](int it, auto buf_c) {
-      constexpr int buf = decltype(buf_c)::value;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();  // tile `it` landed; everyone is done with the other buffer
-      if (it + 1 < ntiles) issue_tile(it + 1, std::integral_constant<int, buf ^ 1>{});
-
-      const uint16_t* tl = lds + buf * BUF;
-      const float* lnorm = reinterpret_cast<const float*>(tl + TI * DP);
-      const int64_t i0 = ibeg + (int64_t)it * tstride * TI;
-      const int nvalid = (int)((iend - i0) < TI ? (iend - i0) : TI);
-  #pragma unroll
-      for (int st = 0; st < TI / 32; ++st) {
-        f32x16 acc[QT];
-  #pragma unroll
-        for (int t = 0; t < QT; ++t)
-  #pragma unroll
-          for (int g = 0; g < 16; ++g) acc[t][g] = 0.f;
-        const int row = 32 * st + r;
-        const uint16_t* arow = tl + row * DP;
-        const int sw = swz<CPR>(row);
-  #pragma unroll
-        for (int s = 0; s < KS; ++s) {
-          const bf16x8 a = *reinterpret_cast<const bf16x8*>(arow + 8 * ((2 * s + h) ^ sw));
-  #pragma unroll
-          for (int t = 0; t < QT; ++t)
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[t][s], acc[t], 0, 0, 0);
-        }
-        if constexpr (EPI == 2) {  // ablation: MFMA only
-  #pragma unroll
-          for (int t = 0; t < QT; ++t) asm volatile("" ::"v"(acc[t][0]), "v"(acc[t][5]), "v"(acc[t][15]));
-          continue;
-        }
-        // Epilogue.  MASKED only for the (rare) partial last tile of a chunk: a
-        // wave-uniform branch, so full tiles carry no per-score selects.
-        auto epilogue = [&](auto masked_tag) {
-          constexpr bool MASKED = decltype(masked_tag)::value;
-  #pragma unroll
-          for (int t = 0; t < QT; ++t) {
-            float sc[16];
-  #pragma unroll
-            for (int g = 0; g < 16; ++g) {
-              const int ir = 32 * st + (g & 3) + 8 * (g >> 2) + 4 * h;
-              float v = acc[t][g];
-              if constexpr (L2) v = fmaf(2.f, v, -lnorm[ir]);
-              if constexpr (MASKED) v = ir < nvalid ? v : -INFINITY;
-              sc[g] = v;
-            }
-            // IEEE maximum (v_maximum3_f32): no canonicalising moves on MFMA outputs
-            float m4[4];
-  #pragma unroll
-            for (int j = 0; j < 4; ++j)
-              m4[j] = fmax_ieee(fmax_ieee(sc[4 * j], sc[4 * j + 1]), fmax_ieee(sc[4 * j + 2], sc[4 * j + 3]));
-            const float m = fmax_ieee(fmax_ieee(m4[0], m4[1]), fmax_ieee(m4[2], m4[3]));
-            if constexpr (MODE == 3) {  // collect: append every score at or above the threshold
-              if (__any(m >= cthr[t])) {
-  #pragma unroll
-                for (int g = 0; g < 16; ++g) {
-                  if (sc[g] >= cthr[t]) {
-                    const int ir = 32 * st + (g & 3) + 8 * (g >> 2) + 4 * h;
-                    const int e = atomicAdd(&cl.n, 1);
-                    if (e < CollectLds<WQ>::CAP) {
-                      const int row = (w * QT + t) * 32 + r;
-                      const int rank = atomicAdd(&cl.qcnt[row], 1);
-                      cl.ent[e] = make_int2(row | (rank << 8), (int)(i0 + ir));
-                    } else if (__builtin_nontemporal_load(&iv.cand_cnt[cq[t]]) <= iv.cap) {
-                      // staging full: append directly (stop once the query overflowed)
-                      const int pos = atomicAdd(&iv.cand_cnt[cq[t]], 1);
-                      if (pos < iv.cap) iv.cand_pos[(int64_t)cq[t] * iv.cap + pos] = (int)(i0 + ir);
-                    }
-                  }
-                }
-              }
-              continue;
-            }
-            if constexpr (MODE == 4) {  // lane maximum and its position (new maxima are rare)
-              if (__any(m > ls[t][0])) {
-  #pragma unroll
-                for (int g = 0; g < 16; ++g) {
-                  if (sc[g] > ls[t][0]) {
-                    ls[t][0] = sc[g];
-                    li[t][0] = (int)(i0 + 32 * st + (g & 3) + 8 * (g >> 2) + 4 * h);
-                  }
-                }
-              }
-              continue;
-            }
-            if constexpr (MODE == 1 || EPI == 1) {  // pre-pass (or ablation): lane maximum only
-              ls[t][0] = fmax_ieee(ls[t][0], m);
-              continue;
-            }
-            // rare path: descend only into 4-row groups that beat the threshold
-            if (__any(m > fmaxf(ls[t][M], tau[t]))) {
-  #pragma unroll
-              for (int j = 0; j < 4; ++j) {
-                if (__any(m4[j] > fmaxf(ls[t][M], tau[t]))) {
-  #pragma unroll
-                  for (int i = 0; i < 4; ++i) {
-                    const int g = 4 * j + i;
-                    const int ir = 32 * st + i + 8 * j + 4 * h;
-                    const float thr = fmaxf(ls[t][M], tau[t]);
-                    if (sc[g] > thr) list_insert<M + 1>(ls[t], li[t], sc[g], (int)(i0 + ir));
-                  }
-                }
-              }
-            }
-          }
-        };
-        if (nvalid >= 32 * (st + 1)) epilogue(std::false_type{});
-        else epilogue(std::true_type{});
-      }
-    };
-
-    if constexpr (MODE == 3) {
-      if (tid == 0) cl.n = 0;  // ordered before any append by the first tile's barrier
-    }
-    if (ntiles > 0) issue_tile(0, std::integral_constant<int, 0>{});
-    for (int it = 0; it < ntiles; it += 2) {
-      tile(it, std::integral_constant<int, 0>{});
-      if (it + 1 < ntiles) tile(it + 1, std::integral_constant<int, 1>{});
-    }
-
-    if constexpr (MODE == 3) {  // flush the staged candidates
-      __syncthreads();
-      for (int row = tid; row < WQ; row += NT) {
-        const int n_r = cl.qcnt[row];
-        cl.base[row] = n_r > 0 ? atomicAdd(&iv.cand_cnt[cl.qid[row]], n_r) : 0;
-      }
-      __syncthreads();
-      const int ne = cl.n < CollectLds<WQ>::CAP ? cl.n : CollectLds<WQ>::CAP;
-      for (int e = tid; e < ne; e += NT) {
-        const int2 en = cl.ent[e];
-        const int row = en.x & 255, dst = cl.base[row] + (en.x >> 8);
-        if (dst < iv.cap) iv.cand_pos[(int64_t)cl.qid[row] * iv.cap + dst] = en.y;
-      }
-      continue;
-    }
-
-  #pragma unroll
-    for (int t = 0; t < QT; ++t) {
-      const int64_t qi = qidx[t];
-      int64_t base = -1;
-      if constexpr (MODE == 3) {
-        continue;  // collect mode writes its candidates as it goes
-      } else if constexpr (MODE == 2 || MODE == 4) {
-        const int pair = iv.slot_pair[seg0 + qi];
-        if (pair >= 0) base = ((int64_t)pair * iv.cmax + c) * 2 + h;
-      } else if (qi < nq) {
-        base = (qi * nch + c) * 2 + h;
-      }
-      if (base >= 0) {
-        if constexpr (MODE == 1 || MODE == 4) {
-          part_t[base] = ls[t][0];
-          if constexpr (MODE == 4) part_i[base] = li[t][0];
-        } else {
-  #pragma unroll
-          for (int j = 0; j < M; ++j) {
-            part_s[base * M + j] = ls[t][j];
-            part_i[base * M + j] = li[t][j];
-          }
-          part_t[base] = ls[t][M];
-        }
-      }
-    }
-
   }
 }
 
@@ -1174,48 +777,6 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
   p.off_ovl = take((size_t)nq * 4);
   p.total = off;
   return p;
-}
-
-typedef void (*screen_fn)(const uint16_t*, const uint16_t*, const float*, int64_t, int64_t, int64_t, int, int, int,
-                          float*, int*, float*, const float*, IvfScreen);
-
-template <int DP, int QT, int M, bool L2, int MODE>
-static screen_fn pick3() {
-  if constexpr (DP == 128 && QT == 2 && M == 4 && !L2 && MODE == 0) {
-    const int epi = env_int("NRK_SCREEN_EPI", 0);
-    if (epi == 1) return screen_kernel<DP, QT, M, 4, L2, MODE, 1>;
-    if (epi == 2) return screen_kernel<DP, QT, M, 4, L2, MODE, 2>;
-  }
-  return screen_kernel<DP, QT, M, 4, L2, MODE>;
-}
-
-template <int DP, bool L2, int MODE>
-static screen_fn pick2(int qt, int M) {
-  constexpr int Q2 = DP == 256 ? 1 : 2;  // DP=256 always runs one query tile per wave
-  if (M == 4) return qt == 2 ? pick3<DP, Q2, 4, L2, MODE>() : pick3<DP, 1, 4, L2, MODE>();
-  if (M == 8) return pick3<DP, 1, 8, L2, MODE>();
-  return pick3<DP, 1, 16, L2, MODE>();
-}
-
-// mode: 0 main pass, 1 threshold pre-pass, 2 IVF list scan, 3 IVF collect, 4 IVF lane maxima
-template <int DP, bool L2>
-static screen_fn pick1(int qt, int M, int mode) {
-  constexpr int Q2 = DP == 256 ? 1 : 2;
-  if (mode == 1) return qt == 2 ? pick3<DP, Q2, 1, L2, 1>() : pick3<DP, 1, 1, L2, 1>();
-  if (mode == 2) return pick2<DP, L2, 2>(qt, M);
-  if (mode == 3) return qt == 2 ? pick3<DP, Q2, 1, L2, 3>() : pick3<DP, 1, 1, L2, 3>();
-  if (mode == 4) return qt == 2 ? pick3<DP, Q2, 1, L2, 4>() : pick3<DP, 1, 1, L2, 4>();
-  return pick2<DP, L2, 0>(qt, M);
-}
-
-static screen_fn pick_screen(int dp, int qt, int M, bool l2, int mode) {
-  switch (dp) {
-    case 32: return l2 ? pick1<32, true>(qt, M, mode) : pick1<32, false>(qt, M, mode);
-    case 64: return l2 ? pick1<64, true>(qt, M, mode) : pick1<64, false>(qt, M, mode);
-    case 128: return l2 ? pick1<128, true>(qt, M, mode) : pick1<128, false>(qt, M, mode);
-    case 256: return l2 ? pick1<256, true>(qt, M, mode) : pick1<256, false>(qt, M, mode);
-  }
-  return nullptr;
 }
 
 }  // namespace nrk
