@@ -133,6 +133,33 @@ int nrk_din_attn_bwd(const void* keys, const int32_t* hist_ids, int64_t n_table,
                      float* dU, float* dW1k, float* dw2, float* db2,
                      void* ws, size_t ws_bytes, void* stream);
 
+/* The same backward with the query half folded in (train step, id form, bf16
+ * table, d in {64, 128}): also accumulates dW1q = sum_b dU[b] q[b]^T and
+ * db1 = sum_b dU[b] per workgroup, and WRITES the layer's parameter gradients
+ * straight into the model's tensors: gW1 [A][2d] = [dW1q | dW1k], gb1 [A],
+ * gw2 [A], gb2 [1] (DIN.py:146 loss.backward() for attn.attn.{0,2}).
+ *   q [B][d] f32 (the query rows), dU [B][A] optional (NULL: not written).
+ *   ws as nrk_din_attn_bwd_workspace(B, d, A). */
+int nrk_din_attn_bwd_params(const void* table, const int32_t* hist_ids, int64_t n_table, int32_t dtype,
+                            const float* q, const float* U, const void* W1k, const float* w2,
+                            int32_t B, int32_t L, int32_t d, int32_t A,
+                            const float* dpooled, const float* alpha,
+                            float* gW1, float* gb1, float* gw2, float* gb2, float* dU,
+                            void* ws, size_t ws_bytes, void* stream);
+
+/* One train batch from a device-resident click log (replaces TrainDataset.
+ * __getitem__'s CPU gather, DIN.py:81-92, and the query GEMM of DIN.py:105-106):
+ *   idx [B] int64 rows of the log; hist_all [n_rows][L] int32, tgt_all [n_rows]
+ *   int32, lab_all [n_rows] f32; table [N][d] bf16; W1 [A][2d] f32, b1 [A] f32.
+ * Out: hist [B][L] int32, q [B][d] f32 (= table[target], id < 0 -> zeros),
+ *   y [B] f32, U [B][A] f32 = q W1[:, :d]^T + b1 (products exact in f32),
+ *   W1k_bf16 [A][d] = bf16(W1[:, d:]).  Rows outside [0, n_rows) give an
+ *   empty history, a zero query and label 0.  d in {64, 128}. */
+int nrk_din_batch(const int64_t* idx, int32_t B, const int32_t* hist_all, const int32_t* tgt_all,
+                  const float* lab_all, int64_t n_rows, int32_t L, const void* table, int64_t n_table,
+                  int32_t dtype, int32_t d, const float* W1, const float* b1, int32_t A, int32_t* hist,
+                  float* q, float* y, float* U, void* W1k_bf16, void* stream);
+
 /* ------------------------------------------------------ inverted lists --
  * faiss Clustering / IndexIVFFlat building blocks (Retrieval.py:11-23).
  *

@@ -55,6 +55,10 @@ SIGNATURES = {
     "nrk_din_attn_bwd_workspace": (ctypes.c_int, [c_i32, c_i32, c_i32, ctypes.POINTER(c_size)]),
     "nrk_din_attn_bwd": (ctypes.c_int, [c_p, c_p, c_i64, c_i32, c_p, c_p, c_p, c_f32, c_i32, c_i32, c_i32, c_i32,
                                         c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_size, c_p]),
+    "nrk_din_attn_bwd_params": (ctypes.c_int, [c_p, c_p, c_i64, c_i32, c_p, c_p, c_p, c_p, c_i32, c_i32, c_i32, c_i32,
+                                               c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_size, c_p]),
+    "nrk_din_batch": (ctypes.c_int, [c_p, c_i32, c_p, c_p, c_p, c_i64, c_i32, c_p, c_i64, c_i32, c_i32, c_p, c_p,
+                                     c_i32, c_p, c_p, c_p, c_p, c_p, c_p]),
     "nrk_gather_rows": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_i64, c_i32, c_p, c_p]),
 }
 

@@ -55,7 +55,7 @@ def build_lib(force: bool = False) -> str:
             jobs.append([HIPCC, *HIP_FLAGS, *lang, "-c", src, "-o", obj])
     with cf.ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
         list(ex.map(_run, jobs))
-    if jobs or not os.path.exists(LIB):
+    if jobs or not _newer(LIB, objs):
         _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", LIB])
     return LIB
 

@@ -389,22 +389,34 @@ __global__ __launch_bounds__(256, 2) void din_fwd_wave_kernel(const uint16_t* __
       if (h == 0 && c < nct && 32 * c + r < L) alpha[(int64_t)b * L + 32 * c + r] = e[c];
     }
     // ---- pooled = sum_rows alpha[row] K[row][:]
+    // rows in groups of 8 up to round_up(L, 8) <= Lp: rows >= L are zero rows
+    // with alpha 0, so the 8 LDS reads of a group issue back to back
     float acc2[DPL];
 #pragma unroll
     for (int j = 0; j < DPL; ++j) acc2[j] = 0.f;
-    for (int row = 0; row < L; ++row) {
-      const float ar = __builtin_amdgcn_readlane(__float_as_int(row < 32 ? e[0] : row < 64 ? e[1] : row < 96 ? e[2] : e[3]),
-                                                 row & 31);
-      const float al = __int_as_float(ar);
-      if constexpr (DPL == 2) {
-        const uint32_t u = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const unsigned char*>(img) +
-                                                              KImg<true, D>::off(row, 2 * lane));
-        acc2[0] = fmaf(al, __uint_as_float(u << 16), acc2[0]);
-        acc2[1] = fmaf(al, __uint_as_float(u & 0xFFFF0000u), acc2[1]);
-      } else {
-        const uint16_t u = *reinterpret_cast<const uint16_t*>(reinterpret_cast<const unsigned char*>(img) +
-                                                              KImg<true, D>::off(row, lane));
-        acc2[0] = fmaf(al, bf16_to_f32(u), acc2[0]);
+    const int L8 = (L + 7) & ~7;
+    for (int row0 = 0; row0 < L8; row0 += 8) {
+      const int c = row0 >> 5;
+      const float ec = c == 0 ? e[0] : c == 1 ? e[1] : c == 2 ? e[2] : e[3];
+      uint32_t u[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if constexpr (DPL == 2)
+          u[i] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const unsigned char*>(img) +
+                                                    KImg<true, D>::off(row0 + i, 2 * lane));
+        else
+          u[i] = *reinterpret_cast<const uint16_t*>(reinterpret_cast<const unsigned char*>(img) +
+                                                    KImg<true, D>::off(row0 + i, lane));
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float al = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ec), (row0 + i) & 31));
+        if constexpr (DPL == 2) {
+          acc2[0] = fmaf(al, __uint_as_float(u[i] << 16), acc2[0]);
+          acc2[1] = fmaf(al, __uint_as_float(u[i] & 0xFFFF0000u), acc2[1]);
+        } else {
+          acc2[0] = fmaf(al, bf16_to_f32((uint16_t)u[i]), acc2[0]);
+        }
       }
     }
     if constexpr (DPL == 2) {
@@ -425,7 +437,10 @@ __global__ __launch_bounds__(256, 2) void din_fwd_wave_kernel(const uint16_t* __
 
 // =============================================================== backward ==
 // Workgroup slab layout (floats): dW1k [A][D], then dw2 [A], then db2 [1].
-__host__ __device__ __forceinline__ size_t slab_floats(int A, int D) { return (size_t)A * D + A + 4; }
+// The pipelined backward with the query (nrk_din_attn_bwd_params) appends
+// dW1q [A][D] and db1 [A] at slab_q_off.
+__host__ __device__ __forceinline__ size_t slab_q_off(int A, int D) { return (size_t)A * D + A + 4; }
+__host__ __device__ __forceinline__ size_t slab_floats(int A, int D) { return 2 * ((size_t)A * D + A + 4); }
 
 template <bool BF16, int D>
 __global__ __launch_bounds__(256) void din_bwd_kernel(
@@ -575,7 +590,7 @@ __global__ __launch_bounds__(256, 1) void din_bwd_pipe_kernel(
     const uint16_t* __restrict__ table, const int32_t* __restrict__ ids, int64_t n_table, const float* __restrict__ U,
     const uint16_t* __restrict__ W1k, const float* __restrict__ w2, int B, int L, int A,
     const float* __restrict__ dpooled, const float* __restrict__ alpha, float* __restrict__ dU,
-    float* __restrict__ slabs) {
+    float* __restrict__ slabs, const float* __restrict__ q, int dq) {
   constexpr int CPR = D / 8, KS = D / 16, NCT = D / 32;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
@@ -599,6 +614,19 @@ __global__ __launch_bounds__(256, 1) void din_bwd_pipe_kernel(
 #pragma unroll
     for (int g = 0; g < 16; ++g) dw[c][g] = 0.f;
   float dw2_acc = 0.f, db2_acc = 0.f;
+  // query half of W1 (q != nullptr): dW1q = sum_b dU[b] q[b]^T on f32 MFMA,
+  // two samples per 32x32x2 step (lanes h = 0 / 1 carry the older / newer
+  // sample), and db1 = sum_b dU[b]
+  f32x16 dwq[NCT];
+#pragma unroll
+  for (int c = 0; c < NCT; ++c)
+#pragma unroll
+    for (int g = 0; g < 16; ++g) dwq[c][g] = 0.f;
+  float db1_acc = 0.f, du_prev = 0.f;
+  float qprev[NCT];
+#pragma unroll
+  for (int c = 0; c < NCT; ++c) qprev[c] = 0.f;
+  int npair = 0;
 
   // cooperative stage of sample b into slot sl (every thread issues its share)
   auto issue = [&](int64_t b, int sl) {
@@ -641,6 +669,11 @@ __global__ __launch_bounds__(256, 1) void din_bwd_pipe_kernel(
     const float* sdp = sp;
     const float* sal = sp + D;
     const unsigned char* img = reinterpret_cast<const unsigned char*>(sp + D + 128);
+    float qcur[NCT];
+    if (q != nullptr) {
+#pragma unroll
+      for (int c = 0; c < NCT; ++c) qcur[c] = 32 * c + r < dq ? q[b * dq + 32 * c + r] : 0.f;
+    }
     if (w < nsl) {
       // key-row fragments of every 32-row tile (rows 32c + r, k = 16s + 8h ..), reused twice
       // dalpha[row] = dpooled . K[row]  (halves over h combined)
@@ -728,10 +761,28 @@ __global__ __launch_bounds__(256, 1) void din_bwd_pipe_kernel(
         }
       }
       du += __shfl_xor(du, 32, 64);
-      if (h == 0) dU[b * A + 32 * w + r] = du;
+      if (h == 0 && dU != nullptr) dU[b * A + 32 * w + r] = du;
+      if (q != nullptr) {
+        db1_acc += du;
+        if (npair & 1) {
+          const float av = h ? du : du_prev;
+#pragma unroll
+          for (int c = 0; c < NCT; ++c)
+            dwq[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, h ? qcur[c] : qprev[c], dwq[c], 0, 0, 0);
+        }
+        du_prev = du;
+#pragma unroll
+        for (int c = 0; c < NCT; ++c) qprev[c] = qcur[c];
+        ++npair;
+      }
     }
     un = un_next;
     sl ^= 1;
+  }
+  if (q != nullptr && w < nsl && (npair & 1)) {  // odd tail: the newer-sample half is zero
+    const float av = h ? 0.f : du_prev;
+#pragma unroll
+    for (int c = 0; c < NCT; ++c) dwq[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, h ? 0.f : qprev[c], dwq[c], 0, 0, 0);
   }
 
   float* slab = slabs + (size_t)blockIdx.x * slab_floats(A, D);
@@ -742,10 +793,332 @@ __global__ __launch_bounds__(256, 1) void din_bwd_pipe_kernel(
       for (int g = 0; g < 16; ++g) slab[(size_t)(32 * w + acc_row(g, h)) * D + 32 * c + r] = dw[c][g];
     const float t = dw2_acc + __shfl_xor(dw2_acc, 32, 64);
     if (h == 0) slab[(size_t)A * D + 32 * w + r] = t;
+    if (q != nullptr) {
+      float* sq = slab + slab_q_off(A, D);
+#pragma unroll
+      for (int c = 0; c < NCT; ++c)
+#pragma unroll
+        for (int g = 0; g < 16; ++g) sq[(size_t)(32 * w + acc_row(g, h)) * D + 32 * c + r] = dwq[c][g];
+      if (h == 0) sq[(size_t)A * D + 32 * w + r] = db1_acc;
+    }
   }
   if (w == 0) {
     const float t = wave_sum(db2_acc);
     if (lane == 0) slab[(size_t)A * D + A] = t;
+  }
+}
+
+// Backward for the fused train step (query half folded in, no dU output),
+// pipelined TWO samples ahead with every per-sample input moved by LDS-DMA
+// issued from inline asm (hipcc neither sees nor waits for it, so no
+// conservative vmcnt(0) lands in front of the LDS reads of the current
+// sample): three LDS slots of {dpooled, alpha, U row, q row, key image} and
+// a per-wave ring of history ids one sample further ahead.  Each wave issues
+// the same N_D DMA ops per iteration (out-of-range samples / rows read
+// clamped addresses or the zero row), so the waits are counted vmcnt:
+//   top of iteration: vmcnt(N_D)  -> the DMA group of this sample landed,
+//   then s_waitcnt lgkmcnt(0) + raw s_barrier (never __syncthreads, whose
+//   fence would drain every DMA in flight);
+//   before issuing: vmcnt(N_D)    -> the ids of the sample being issued landed.
+// LP = padded history rows (32, 64 or 128; rows >= L are zero rows).
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_hw;
+__device__ __forceinline__ uint32_t lds_u32(const void* p) {
+  return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)p;
+}
+__device__ __forceinline__ void glds16_asm(const void* gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_dst)
+               : "memory");
+}
+__device__ __forceinline__ void glds4_asm(const void* gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_dst)
+               : "memory");
+}
+
+template <int D, int LP>
+__global__ __launch_bounds__(256, 1) void din_bwd_deep_kernel(
+    const uint16_t* __restrict__ table, const int32_t* __restrict__ ids, int64_t n_table, const float* __restrict__ U,
+    const uint16_t* __restrict__ W1k, const float* __restrict__ w2, int B, int L, int A,
+    const float* __restrict__ dpooled, const float* __restrict__ alpha, float* __restrict__ slabs,
+    const float* __restrict__ q, int dq) {
+  constexpr int CPR = D / 8, KS = D / 16, NCT = D / 32, NC = LP / 32;
+  constexpr int NPW = LP * CPR / 256;  // key-image DMA pieces per wave
+  constexpr int N_IDS = LP > 64 ? 2 : 1;
+  constexpr int N_D = NPW + 2 + N_IDS;  // per wave and iteration: keys, two small pieces, the ids pieces
+  static_assert(NPW >= 1 && 2 * N_D < 64, "vmcnt range");
+  // slot (floats): dpooled [128] | alpha [128] | U [128] | q [128] | key image [LP][D] bf16
+  constexpr int SLOT_F = 4 * 128 + LP * D / 2;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nsl = A >> 5;
+  float* slot0 = reinterpret_cast<float*>(smem);
+  int32_t* idring = reinterpret_cast<int32_t*>(slot0 + 3 * SLOT_F) + w * 2 * 128;  // [2][128] per wave
+  float* dsbuf = reinterpret_cast<float*>(reinterpret_cast<int32_t*>(slot0 + 3 * SLOT_F) + 4 * 2 * 128) + w * 128;
+  float* dabuf = reinterpret_cast<float*>(reinterpret_cast<int32_t*>(slot0 + 3 * SLOT_F) + 4 * 2 * 128) + 4 * 128;
+
+  WFrag<true, D> wf;
+  const int wu = w < nsl ? w : 0;
+  wf.load(W1k, 32 * wu + r, h);
+  const float w2n = w2[32 * wu + r];
+#pragma unroll
+  for (int s2 = 0; s2 < KS; ++s2) asm volatile("" ::"v"(wf.f[s2]));  // hipcc's waits for these land here
+  asm volatile("" ::"v"(w2n));
+  f32x16 dw[NCT], dwq[NCT];
+#pragma unroll
+  for (int c = 0; c < NCT; ++c)
+#pragma unroll
+    for (int g = 0; g < 16; ++g) dw[c][g] = dwq[c][g] = 0.f;
+  float dw2_acc = 0.f, db2_acc = 0.f, db1_acc = 0.f;
+
+  // ids of sample b (all LP rows; clamped) into ring entry e of this wave
+  auto issue_ids = [&](int64_t b, int e) {
+    const int64_t bc = b < B ? b : 0;
+    const int i = lane < LP ? lane : 0;
+    glds4_asm(ids + bc * L + (i < L ? i : 0), lds_u32(idring + e * 128));
+    if constexpr (LP > 64) glds4_asm(ids + bc * L + (64 + lane < L ? 64 + lane : 0), lds_u32(idring + e * 128 + 64));
+  };
+  // key rows + small pieces of sample b (its ids in ring entry e) into slot sl
+  auto issue_data = [&](int64_t b, int sl, int e) {
+    float* sp = slot0 + sl * SLOT_F;
+    uint16_t* img = reinterpret_cast<uint16_t*>(sp + 4 * 128);
+#pragma unroll
+    for (int k = 0; k < NPW; ++k) {
+      const int u = w + 4 * k;
+      const int p = u * 64 + lane;
+      const int row = p / CPR, pc = p % CPR;
+      const int cc = pc ^ kswz<CPR>(row);
+      const int32_t idv0 = idring[e * 128 + row];
+      const int32_t idr = row < L && b < B ? idv0 : -1;
+      const uint16_t* src = (idr >= 0 && idr < n_table) ? table + (int64_t)idr * D + cc * 8 : g_zero_row;
+      glds16_asm(src, lds_u32(img + u * 64 * 8));
+    }
+    const int64_t bc = b < B ? b : 0;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {  // small pieces 2w, 2w+1 of [dp0, dp1, al0, al1, u0, u1, q0, q1]
+      const int pc = 2 * w + k, kind = pc >> 1, part = pc & 1;
+      const int i = part * 64 + lane;
+      const float* base = kind == 0 ? dpooled + bc * D : kind == 1 ? alpha + bc * L : kind == 2 ? U + bc * A : q + bc * dq;
+      const int lim = kind == 0 ? D : kind == 1 ? L : kind == 2 ? A : dq;
+      glds4_asm(base + (i < lim ? i : 0), lds_u32(sp + kind * 128 + part * 64));
+    }
+  };
+
+  const int64_t grid = gridDim.x;
+  int64_t b = blockIdx.x;
+  issue_ids(b, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  issue_ids(b + grid, 1);
+  issue_data(b, 0, 0);
+  issue_ids(b + 2 * grid, 0);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_D) : "memory");  // ids of b + grid landed
+  issue_data(b + grid, 1, 1);
+  int sl = 0, e = 0;  // e: ring entry holding the ids of sample b + 2 grid
+  for (; b < B; b += grid) {
+    // this wave's DMA group of sample b landed; all waves' after the barrier; slot of b - grid is free
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N_D) : "memory");
+    issue_ids(b + 3 * grid, e ^ 1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_D) : "memory");  // ids of b + 2 grid landed
+    issue_data(b + 2 * grid, sl == 0 ? 2 : sl - 1, e);
+    e ^= 1;
+
+    const float* sp = slot0 + sl * SLOT_F;
+    const float* sdp = sp;
+    const float* sal = sp + 128;
+    const float* sU = sp + 256;
+    const float* sq = sp + 384;
+    const unsigned char* img = reinterpret_cast<const unsigned char*>(sp + 512);
+    {  // dalpha[row] = dpooled . K[row], split over the waves: wave w owns rows [w R, (w+1) R)
+      constexpr int R = LP / 4, LPR = 64 / R, CH = CPR / LPR;
+      const int row = w * R + lane / LPR, part = lane % LPR;
+      float acc = 0.f;
+#pragma unroll
+      for (int ch = 0; ch < CH; ++ch) {
+        const int cc = part * CH + ch;
+        const uint4 kv = *reinterpret_cast<const uint4*>(img + row * 2 * D + 16 * (cc ^ kswz<CPR>(row)));
+        const float4 d0 = *reinterpret_cast<const float4*>(sdp + 8 * cc);
+        const float4 d1 = *reinterpret_cast<const float4*>(sdp + 8 * cc + 4);
+        acc = fmaf(d0.x, __uint_as_float(kv.x << 16), acc);
+        acc = fmaf(d0.y, __uint_as_float(kv.x & 0xFFFF0000u), acc);
+        acc = fmaf(d0.z, __uint_as_float(kv.y << 16), acc);
+        acc = fmaf(d0.w, __uint_as_float(kv.y & 0xFFFF0000u), acc);
+        acc = fmaf(d1.x, __uint_as_float(kv.z << 16), acc);
+        acc = fmaf(d1.y, __uint_as_float(kv.z & 0xFFFF0000u), acc);
+        acc = fmaf(d1.z, __uint_as_float(kv.w << 16), acc);
+        acc = fmaf(d1.w, __uint_as_float(kv.w & 0xFFFF0000u), acc);
+      }
+#pragma unroll
+      for (int o = 1; o < LPR; o <<= 1) acc += __shfl_xor(acc, o, 64);
+      if (part == 0) dabuf[row] = acc;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (w < nsl) {
+      const float un = sU[32 * w + r];
+      float qcur[NCT];
+#pragma unroll
+      for (int c = 0; c < NCT; ++c) qcur[c] = 32 * c + r < dq ? sq[32 * c + r] : 0.f;
+      float da[NC];
+      bf16x8 kf[NC][KS];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int row = 32 * c + r;
+        da[c] = dabuf[row];
+#pragma unroll
+        for (int s2 = 0; s2 < KS; ++s2)
+          kf[c][s2] = *reinterpret_cast<const bf16x8*>(img + KImg<true, D>::off(row, 16 * s2 + 8 * h));
+      }
+      float t = 0.f;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int row = 32 * c + r;
+        t += (row < L && h == 0) ? sal[row] * da[c] : 0.f;
+      }
+      const float cdot = wave_sum(t);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int row = 32 * c + r;
+        if (h == 0) {
+          const float ds = row < L ? sal[row] * (da[c] - cdot) : 0.f;
+          dsbuf[row] = ds;
+          if (w == 0) db2_acc += ds;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      float du = 0.f;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        f32x16 acc;
+#pragma unroll
+        for (int g = 0; g < 16; ++g) acc[g] = un;
+#pragma unroll
+        for (int s2 = 0; s2 < KS; ++s2) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[c][s2], wf.f[s2], acc, 0, 0, 0);
+        f32x16 dz;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float4 d4 = *reinterpret_cast<const float4*>(dsbuf + 32 * c + 8 * j + 4 * h);
+          const float dsv[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int g = 4 * j + i;
+            const float z = acc[g];
+            dw2_acc = fmaf(dsv[i], fmaxf(z, 0.f), dw2_acc);
+            const float v = z > 0.f ? dsv[i] * w2n : 0.f;
+            dz[g] = v;
+            du += v;
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          bf16x8 af;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {  // v_cvt_pk_bf16_f32 (round to nearest even)
+            const bf16x2_hw pk = {(__bf16)dz[8 * s + 2 * j], (__bf16)dz[8 * s + 2 * j + 1]};
+            const uint32_t u = __builtin_bit_cast(uint32_t, pk);
+            af[2 * j] = (short)(u & 0xFFFF);
+            af[2 * j + 1] = (short)(u >> 16);
+          }
+          const int grp = lane >> 4, i16 = lane & 15;
+          const int rowq = 32 * c + 16 * s + 4 * h + (i16 >> 2);
+#pragma unroll
+          for (int cc = 0; cc < NCT; ++cc) {
+            const int col = 32 * cc + 16 * (grp & 1) + 4 * (i16 & 3);
+            typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+            const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(img + KImg<true, D>::off(rowq, col)));
+            const bf16x4 hi =
+                __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(img + KImg<true, D>::off(rowq + 8, col)));
+            const bf16x8 bfr = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+            dw[cc] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, dw[cc], 0, 0, 0);
+          }
+        }
+      }
+      du += __shfl_xor(du, 32, 64);
+      db1_acc += du;
+      // dW1q += dU q^T: one sample per 32x32x2 step (k = 1 half zero), no branch
+#pragma unroll
+      for (int c = 0; c < NCT; ++c)
+        dwq[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(h ? 0.f : du, h ? 0.f : qcur[c], dwq[c], 0, 0, 0);
+    }
+    sl = sl == 2 ? 0 : sl + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup exits
+  float* slab = slabs + (size_t)blockIdx.x * slab_floats(A, D);
+  if (w < nsl) {
+    float* sqs = slab + slab_q_off(A, D);
+#pragma unroll
+    for (int c = 0; c < NCT; ++c)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        slab[(size_t)(32 * w + acc_row(g, h)) * D + 32 * c + r] = dw[c][g];
+        sqs[(size_t)(32 * w + acc_row(g, h)) * D + 32 * c + r] = dwq[c][g];
+      }
+    const float t = dw2_acc + __shfl_xor(dw2_acc, 32, 64);
+    if (h == 0) {
+      slab[(size_t)A * D + 32 * w + r] = t;
+      sqs[(size_t)A * D + 32 * w + r] = db1_acc;
+    }
+  }
+  if (w == 0) {
+    const float t = wave_sum(db2_acc);
+    if (lane == 0) slab[(size_t)A * D + A] = t;
+  }
+}
+
+// Parameter gradients of the whole attention layer from the slabs (fixed
+// slab order, deterministic), written straight into the model's gradient
+// tensors: gW1 (A, 2d) = [dW1q | dW1k[:, :d]], gb1, gw2, gb2.  A block owns
+// 64 consecutive outputs of the layout {dW1q, dW1k, db1, dw2, db2}; its 8
+// waves each sum every 8th slab with 4 loads in flight, then combine.
+__global__ __launch_bounds__(512) void din_bwd_reduce_params_kernel(const float* __restrict__ slabs, int nslab, int A,
+                                                                    int D, int d, float* __restrict__ gW1,
+                                                                    float* __restrict__ gb1, float* __restrict__ gw2,
+                                                                    float* __restrict__ gb2) {
+  __shared__ float part[8][64];
+  const size_t n = slab_floats(A, D);
+  const size_t nw = (size_t)A * d;  // per half of W1
+  const size_t nout = 2 * nw + A + A + 1;
+  const int o = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const size_t i = (size_t)blockIdx.x * 64 + o;
+  size_t src = 0;
+  if (i < nout) {
+    if (i < 2 * nw) {
+      const size_t row = i / (2 * (size_t)d);
+      const int col = (int)(i % (2 * (size_t)d));
+      src = col < d ? slab_q_off(A, D) + row * D + col : row * D + (col - d);
+    } else if (i < 2 * nw + A) {
+      src = slab_q_off(A, D) + (size_t)A * D + (i - 2 * nw);
+    } else if (i < 2 * nw + 2 * A) {
+      src = (size_t)A * D + (i - 2 * nw - A);
+    } else {
+      src = (size_t)A * D + A;
+    }
+  }
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (i < nout) {
+    int j = g;
+    for (; j + 24 < nslab; j += 32) {
+      s0 += slabs[(size_t)j * n + src];
+      s1 += slabs[(size_t)(j + 8) * n + src];
+      s2 += slabs[(size_t)(j + 16) * n + src];
+      s3 += slabs[(size_t)(j + 24) * n + src];
+    }
+    for (; j < nslab; j += 8) s0 += slabs[(size_t)j * n + src];
+  }
+  part[g][o] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (g == 0 && i < nout) {
+    const float t = ((part[0][o] + part[1][o]) + (part[2][o] + part[3][o])) +
+                    ((part[4][o] + part[5][o]) + (part[6][o] + part[7][o]));
+    if (i < 2 * nw) gW1[i] = t;
+    else if (i < 2 * nw + A) gb1[i - 2 * nw] = t;
+    else if (i < 2 * nw + 2 * A) gw2[i - 2 * nw - A] = t;
+    else gb2[0] = t;
   }
 }
 
@@ -769,6 +1142,119 @@ __global__ __launch_bounds__(256) void din_bwd_reduce_kernel(const float* __rest
     if (i < (size_t)A * D) dW1k[i] = t;
     else if (i < (size_t)A * D + A) dw2[i - (size_t)A * D] = t;
     else db2[0] = t;
+  }
+}
+
+// ========================================================== train batch ==
+// One DIN train batch assembled from the device-resident click log, replacing
+// TrainDataset.__getitem__'s CPU gather (DIN.py:81-92) and the query half of
+// the attention MLP (DIN.py:105-106): for the 32 samples of a block,
+//   rows idx[b] -> history ids, target id, label;  q[b] = f32(table[target]);
+//   U[b] = W1q q[b] + b1  on bf16 MFMA.  q is exact in bf16 (a bf16 table row)
+//   and W1q is split three ways (hi + mid + lo bf16), so every product is the
+//   exact f32 product of the f32 weight and q, accumulated in f32;
+//   W1k (the key half of W1) -> bf16 for the attention kernels (grid-strided).
+template <int D>
+__global__ __launch_bounds__(256) void din_batch_kernel(const int64_t* __restrict__ idx, int B,
+                                                        const int32_t* __restrict__ hist_all,
+                                                        const int32_t* __restrict__ tgt_all,
+                                                        const float* __restrict__ lab_all, int64_t n_rows, int L,
+                                                        const uint16_t* __restrict__ table, int64_t n_table,
+                                                        const float* __restrict__ W1, const float* __restrict__ b1,
+                                                        int A, int32_t* __restrict__ hist, float* __restrict__ q,
+                                                        float* __restrict__ y, float* __restrict__ U,
+                                                        uint16_t* __restrict__ W1k_bf) {
+  constexpr int KS = D / 16;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int b0 = blockIdx.x * 32;
+  __shared__ int64_t s_row[32];
+  __shared__ int32_t s_tgt[32];
+  if (tid < 32) {
+    const int b = b0 + tid;
+    int64_t row = -1;
+    int32_t t = -1;
+    if (b < B) {
+      row = idx[b];
+      float lab = 0.f;
+      if (row >= 0 && row < n_rows) {
+        t = tgt_all[row];
+        lab = lab_all[row];
+      } else {
+        row = -1;
+      }
+      y[b] = lab;
+    }
+    s_row[tid] = row;
+    s_tgt[tid] = t;
+  }
+  for (int64_t e = (int64_t)blockIdx.x * 256 + tid; e < (int64_t)A * D; e += (int64_t)gridDim.x * 256) {
+    const int64_t n = e / D, k = e % D;
+    W1k_bf[e] = f32_to_bf16_rne(W1[n * 2 * D + D + k]);
+  }
+  __syncthreads();
+  for (int e = tid; e < 32 * L; e += 256) {
+    const int i = e / L, j = e % L, b = b0 + i;
+    if (b < B) hist[(int64_t)b * L + j] = s_row[i] >= 0 ? hist_all[s_row[i] * L + j] : -1;
+  }
+  const int b = b0 + r;
+  const int32_t t = s_tgt[r];
+  const bool ok = b < B && t >= 0 && t < n_table;
+  bf16x8 qf[KS];
+#pragma unroll
+  for (int s2 = 0; s2 < KS; ++s2) {
+    if (ok) {
+      qf[s2] = *reinterpret_cast<const bf16x8*>(table + (int64_t)t * D + 16 * s2 + 8 * h);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[s2][j] = 0;
+    }
+  }
+  if (b < B) {
+#pragma unroll
+    for (int s2 = 0; s2 < KS; ++s2) {
+      if ((s2 & 3) != w) continue;
+      float4 lo4, hi4;
+      lo4.x = bf16_to_f32((uint16_t)qf[s2][0]); lo4.y = bf16_to_f32((uint16_t)qf[s2][1]);
+      lo4.z = bf16_to_f32((uint16_t)qf[s2][2]); lo4.w = bf16_to_f32((uint16_t)qf[s2][3]);
+      hi4.x = bf16_to_f32((uint16_t)qf[s2][4]); hi4.y = bf16_to_f32((uint16_t)qf[s2][5]);
+      hi4.z = bf16_to_f32((uint16_t)qf[s2][6]); hi4.w = bf16_to_f32((uint16_t)qf[s2][7]);
+      float* o = q + (int64_t)b * D + 16 * s2 + 8 * h;
+      *reinterpret_cast<float4*>(o) = lo4;
+      *reinterpret_cast<float4*>(o + 4) = hi4;
+    }
+  }
+  for (int ws = w; ws < A / 32; ws += 4) {
+    f32x16 acc;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) acc[g] = 0.f;
+    const float* wrow = W1 + (int64_t)(32 * ws + r) * 2 * D;
+#pragma unroll
+    for (int s2 = 0; s2 < KS; ++s2) {
+      const float4 w0 = *reinterpret_cast<const float4*>(wrow + 16 * s2 + 8 * h);
+      const float4 w1 = *reinterpret_cast<const float4*>(wrow + 16 * s2 + 8 * h + 4);
+      const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      bf16x8 fh, fm, fl;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint16_t hb = f32_to_bf16_rne(wv[j]);
+        const float rem1 = wv[j] - bf16_to_f32(hb);
+        const uint16_t mb = f32_to_bf16_rne(rem1);
+        const uint16_t lb = f32_to_bf16_rne(rem1 - bf16_to_f32(mb));
+        fh[j] = (short)hb;
+        fm[j] = (short)mb;
+        fl[j] = (short)lb;
+      }
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fl, qf[s2], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fm, qf[s2], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fh, qf[s2], acc, 0, 0, 0);
+    }
+    if (b < B) {
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int n = 32 * ws + acc_row(g, h);
+        U[(int64_t)b * A + n] = acc[g] + b1[n];
+      }
+    }
   }
 }
 
@@ -863,10 +1349,14 @@ extern "C" int nrk_din_attn_fwd(const void* keys, const int32_t* hist_ids, int64
     const int Lp = (L + 31) & ~31;
     const size_t AP = (size_t)((A + 63) & ~63);
     const size_t slot = AP * 4 + (size_t)Lp * d * 2;
-    const bool dbl = AP * 4 + 4 * 2 * slot <= 150 * 1024;
+    const char* enb = getenv("NRK_DIN_FWD_NBUF");
+    // single-buffered slots (two workgroups per CU) measured faster than
+    // double-buffered ones (one per CU): 41 vs 51 us at B=4096, L=50, d=128
+    const bool dbl = AP * 4 + 4 * 2 * slot <= 150 * 1024 && enb && atoi(enb) == 2;
     const size_t wsm = AP * 4 + 4 * (dbl ? 2 : 1) * slot;
     int grid = (int)cdiv(B, 4);
-    const int cap = dbl ? 256 : 512;
+    const char* ecap = getenv("NRK_DIN_FWD_WGS");
+    const int cap = ecap && *ecap ? atoi(ecap) : dbl ? 256 : 512;
     if (grid > cap) grid = cap;
     const uint16_t* tb = static_cast<const uint16_t*>(keys);
     const uint16_t* wk = static_cast<const uint16_t*>(W1k);
@@ -936,10 +1426,12 @@ extern "C" int nrk_din_attn_bwd(const void* keys, const int32_t* hist_ids, int64
     NRK_CHECK_ARG(psm <= 160 * 1024, "din_bwd: L=%d d=%d needs %zu B LDS", L, d, psm);
     if (d == 128)
       hipLaunchKernelGGL(din_bwd_pipe_kernel<128>, dim3(grid), dim3(256), psm, st, static_cast<const uint16_t*>(keys),
-                         hist_ids, n_table, U, static_cast<const uint16_t*>(W1k), w2, B, L, A, dpooled, alpha, dU, slabs);
+                         hist_ids, n_table, U, static_cast<const uint16_t*>(W1k), w2, B, L, A, dpooled, alpha, dU, slabs,
+                         nullptr, 0);
     else
       hipLaunchKernelGGL(din_bwd_pipe_kernel<64>, dim3(grid), dim3(256), psm, st, static_cast<const uint16_t*>(keys),
-                         hist_ids, n_table, U, static_cast<const uint16_t*>(W1k), w2, B, L, A, dpooled, alpha, dU, slabs);
+                         hist_ids, n_table, U, static_cast<const uint16_t*>(W1k), w2, B, L, A, dpooled, alpha, dU, slabs,
+                         nullptr, 0);
   } else {
     NRK_DIN_DISPATCH(bf, d, {
       hipLaunchKernelGGL((din_bwd_kernel<kBF, kD>), dim3(grid), dim3(256), smem, st, keys, hist_ids, n_table, U, W1k,
@@ -968,5 +1460,83 @@ extern "C" int nrk_gather_rows(const void* table, int64_t n_table, int32_t dtype
     hipLaunchKernelGGL(gather_rows_kernel<false>, dim3(grid), dim3(256), 0, (hipStream_t)stream, table, n_table, ids,
                        n, d, out);
   NRK_CHECK_LAUNCH("gather_rows_kernel");
+  return NRK_OK;
+}
+
+extern "C" int nrk_din_batch(const int64_t* idx, int32_t B, const int32_t* hist_all, const int32_t* tgt_all,
+                             const float* lab_all, int64_t n_rows, int32_t L, const void* table, int64_t n_table,
+                             int32_t dtype, int32_t d, const float* W1, const float* b1, int32_t A, int32_t* hist,
+                             float* q, float* y, float* U, void* W1k_bf16, void* stream) {
+  NRK_CHECK_ARG(dtype == NRK_DTYPE_BF16, "din_batch: the table must be bf16");
+  NRK_CHECK_ARG(d == 64 || d == 128, "din_batch: emb_dim %d unsupported (64, 128)", d);
+  NRK_CHECK_ARG(A >= 32 && A <= 128 && A % 32 == 0, "din_batch: attn_units %d unsupported (32..128 step 32)", A);
+  NRK_CHECK_ARG(L >= 1 && L <= 128 && B >= 0, "din_batch: bad L=%d / B=%d", L, B);
+  if (B == 0) return NRK_OK;
+  NRK_CHECK_ARG(idx && hist_all && tgt_all && lab_all && table && W1 && b1 && hist && q && y && U && W1k_bf16,
+                "din_batch: null pointer");
+  const unsigned grid = (unsigned)cdiv(B, 32);
+  hipStream_t st = (hipStream_t)stream;
+  const uint16_t* tb = static_cast<const uint16_t*>(table);
+  uint16_t* wk = static_cast<uint16_t*>(W1k_bf16);
+  if (d == 128)
+    hipLaunchKernelGGL(din_batch_kernel<128>, dim3(grid), dim3(256), 0, st, idx, B, hist_all, tgt_all, lab_all, n_rows, L,
+                       tb, n_table, W1, b1, A, hist, q, y, U, wk);
+  else
+    hipLaunchKernelGGL(din_batch_kernel<64>, dim3(grid), dim3(256), 0, st, idx, B, hist_all, tgt_all, lab_all, n_rows, L,
+                       tb, n_table, W1, b1, A, hist, q, y, U, wk);
+  NRK_CHECK_LAUNCH("din_batch_kernel");
+  return NRK_OK;
+}
+
+extern "C" int nrk_din_attn_bwd_params(const void* table, const int32_t* hist_ids, int64_t n_table, int32_t dtype,
+                                       const float* q, const float* U, const void* W1k, const float* w2, int32_t B,
+                                       int32_t L, int32_t d, int32_t A, const float* dpooled, const float* alpha,
+                                       float* gW1, float* gb1, float* gw2, float* gb2, float* dU, void* ws,
+                                       size_t ws_bytes, void* stream) {
+  int rc = check_common(table, dtype, B, L, d, A);
+  if (rc) return rc;
+  NRK_CHECK_ARG(dtype == NRK_DTYPE_BF16 && hist_ids != nullptr && (d == 64 || d == 128),
+                "din_bwd_params: needs a bf16 table, history ids and emb_dim 64 or 128");
+  NRK_CHECK_ARG(B > 0, "din_bwd_params: empty batch");
+  NRK_CHECK_ARG(q && U && W1k && w2 && dpooled && alpha && gW1 && gb1 && gw2 && gb2 && ws,
+                "din_bwd_params: null pointer");
+  const int grid = din_grid(B, true);
+  const size_t need = (size_t)grid * slab_floats(A, d) * 4;
+  if (ws_bytes < need) return fail(NRK_EWORKSPACE, "din_bwd_params: workspace %zu < %zu", ws_bytes, need);
+  const int Lp = (L + 31) & ~31;
+  const size_t psm = (size_t)(2 * (d + 128 + Lp * d / 2) + 4 * 128) * 4;
+  NRK_CHECK_ARG(psm <= 160 * 1024, "din_bwd_params: L=%d d=%d needs %zu B LDS", L, d, psm);
+  hipStream_t st = (hipStream_t)stream;
+  float* slabs = static_cast<float*>(ws);
+  const uint16_t* tb = static_cast<const uint16_t*>(table);
+  const uint16_t* wk = static_cast<const uint16_t*>(W1k);
+  const char* ed = getenv("NRK_DIN_BWD_DEEP");
+  if (dU == nullptr && !(ed && atoi(ed) == 0)) {
+    const int LPk = Lp <= 32 ? 32 : Lp <= 64 ? 64 : 128;
+    const size_t dsm = (size_t)(3 * (4 * 128 + LPk * d / 2) + 4 * 2 * 128 + 5 * 128) * 4;
+    NRK_CHECK_ARG(dsm <= 160 * 1024, "din_bwd_params: L=%d d=%d needs %zu B LDS", L, d, dsm);
+#define NRK_BWD_DEEP(DD, LL)                                                                                     \
+  hipLaunchKernelGGL((din_bwd_deep_kernel<DD, LL>), dim3(grid), dim3(256), dsm, st, tb, hist_ids, n_table, U, wk, w2, B, \
+                     L, A, dpooled, alpha, slabs, q, d)
+    if (d == 128) {
+      if (LPk == 32) NRK_BWD_DEEP(128, 32); else if (LPk == 64) NRK_BWD_DEEP(128, 64); else NRK_BWD_DEEP(128, 128);
+    } else {
+      if (LPk == 32) NRK_BWD_DEEP(64, 32); else if (LPk == 64) NRK_BWD_DEEP(64, 64); else NRK_BWD_DEEP(64, 128);
+    }
+#undef NRK_BWD_DEEP
+    NRK_CHECK_LAUNCH("din_bwd_deep_kernel");
+  } else {
+    if (d == 128)
+      hipLaunchKernelGGL(din_bwd_pipe_kernel<128>, dim3(grid), dim3(256), psm, st, tb, hist_ids, n_table, U, wk, w2, B,
+                         L, A, dpooled, alpha, dU, slabs, q, d);
+    else
+      hipLaunchKernelGGL(din_bwd_pipe_kernel<64>, dim3(grid), dim3(256), psm, st, tb, hist_ids, n_table, U, wk, w2, B, L,
+                         A, dpooled, alpha, dU, slabs, q, d);
+    NRK_CHECK_LAUNCH("din_bwd_pipe_kernel");
+  }
+  const size_t nout = 2 * (size_t)A * d + 2 * (size_t)A + 1;
+  hipLaunchKernelGGL(din_bwd_reduce_params_kernel, dim3((unsigned)cdiv((int64_t)nout, 64)), dim3(512), 0, st, slabs,
+                     grid, A, d, d, gW1, gb1, gw2, gb2);
+  NRK_CHECK_LAUNCH("din_bwd_reduce_params_kernel");
   return NRK_OK;
 }

@@ -45,6 +45,8 @@ struct HeadArgs {
   float* logits;
   float* loss;
   float* dpooled;
+  int fast;  // F == 32 fast path: statistics reduced in each consumer's prologue
+  int nrg0;  // row groups of hf_stats0
 };
 
 __device__ __forceinline__ float hx(const HeadArgs& a, int64_t r, int c) {
@@ -112,6 +114,58 @@ __device__ __forceinline__ void load_stat(const float* stat, int C, float* s_mea
     s_mean[c] = stat[c];
     s_inv[c] = stat[C + c];
   }
+}
+
+// Fixed-order column sums of nblk partial rows (stride doubles apart) for
+// columns [0, ncol) into s_out (LDS), by every block of a consumer kernel
+// (the launch-boundary reduce: no separate colsum launch).  256 threads.
+__device__ void colsum_prologue(const double* __restrict__ part, int nblk, int stride, int ncol,
+                                double* s_tmp /*[256]*/, double* s_out) {
+  const int t = threadIdx.x;
+  if (ncol > 128) {
+    for (int c = t; c < ncol; c += 256) {
+      double acc = 0.0;
+      for (int b0 = 0; b0 < nblk; b0 += 16) {
+        double v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = b0 + u < nblk ? part[(int64_t)(b0 + u) * stride + c] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) acc += v[u];
+      }
+      s_out[c] = acc;
+    }
+    __syncthreads();
+    return;
+  }
+  const int nph = 256 / ncol;
+  const int c = t % ncol, ph = t / ncol;
+  if (ph < nph) {
+    double acc = 0.0;
+    for (int b0 = ph; b0 < nblk; b0 += 32 * nph) {  // 32 loads in flight, summed in block order
+      double v[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) {
+        const int b = b0 + u * nph;
+        v[u] = b < nblk ? part[(int64_t)b * stride + c] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 32; ++u) acc += v[u];
+    }
+    s_tmp[ph * ncol + c] = acc;
+  }
+  __syncthreads();
+  if (t < ncol) {
+    double acc = 0.0;
+    for (int q = 0; q < nph; ++q) acc += s_tmp[q * ncol + t];
+    s_out[t] = acc;
+  }
+  __syncthreads();
+}
+
+// x = [q | pooled] as float4 (d % 4 == 0): element 4*c4 .. of row r
+__device__ __forceinline__ float4 hx4(const HeadArgs& a, int64_t r, int c) {
+  return c < a.d ? *reinterpret_cast<const float4*>(a.q + r * a.d + c)
+                 : *reinterpret_cast<const float4*>(a.pooled + r * a.ld + (c - a.d));
 }
 
 // dot product of n terms x[i*sx] * y[i*sy] with 4 independent chains (the
@@ -192,7 +246,13 @@ __global__ __launch_bounds__(256) void head_fwd2(HeadArgs a) {
   float* inv = mean + F;
   float* d2 = inv + F;
   const int64_t r0 = (int64_t)blockIdx.x * HR;
-  bn_finalize(a, a.sum1, F, mean, inv, a.stat1, a.p.bn1_rm, a.p.bn1_rv, a.p.bn1_nb, blockIdx.x == 0);
+  __shared__ double pro_tmp[256], pro_sum[128];
+  const double* S1 = a.sum1;
+  if (a.fast) {
+    colsum_prologue(a.part1, a.nblk, 2 * F, 2 * F, pro_tmp, pro_sum);
+    S1 = pro_sum;
+  }
+  bn_finalize(a, S1, F, mean, inv, a.stat1, a.p.bn1_rm, a.p.bn1_rv, a.p.bn1_nb, blockIdx.x == 0);
   for (int e = threadIdx.x; e < F2 * F; e += 256) w2[e] = a.p.fc2_w[e];
   __syncthreads();
   for (int e = threadIdx.x; e < HR * F; e += 256) {
@@ -232,7 +292,13 @@ __global__ __launch_bounds__(256) void head_fwd3(HeadArgs a) {
   float* dl = inv + F2;  // [HR]
   float* lo = dl + HR;   // [HR]
   const int64_t r0 = (int64_t)blockIdx.x * HR;
-  bn_finalize(a, a.sum2, F2, mean, inv, a.stat2, a.p.bn2_rm, a.p.bn2_rv, a.p.bn2_nb, blockIdx.x == 0);
+  __shared__ double pro_tmp[256], pro_sum[64];
+  const double* S2 = a.sum2;
+  if (a.fast) {
+    colsum_prologue(a.part2, a.nblk, 2 * F2, 2 * F2, pro_tmp, pro_sum);
+    S2 = pro_sum;
+  }
+  bn_finalize(a, S2, F2, mean, inv, a.stat2, a.p.bn2_rm, a.p.bn2_rv, a.p.bn2_nb, blockIdx.x == 0);
   __syncthreads();
   for (int e = threadIdx.x; e < HR * F2; e += 256) {
     const int r = e / F2, k = e % F2;
@@ -296,9 +362,15 @@ __global__ __launch_bounds__(256) void head_bwd2(HeadArgs a) {
   const int64_t r0 = (int64_t)blockIdx.x * HR;
   load_stat(a.stat1, F, m1, i1);
   load_stat(a.stat2, F2, m2, i2);
+  __shared__ double pro_tmp[256], pro_sum[64];
+  const double* S3 = a.sum3;
+  if (a.fast) {
+    colsum_prologue(a.part3, a.nblk, 3 * F2 + 2, 2 * F2, pro_tmp, pro_sum);
+    S3 = pro_sum;
+  }
   for (int k = threadIdx.x; k < F2; k += 256) {
-    sb2[k] = (float)a.sum3[k];
-    sg2[k] = (float)a.sum3[F2 + k];
+    sb2[k] = (float)S3[k];
+    sg2[k] = (float)S3[F2 + k];
   }
   __syncthreads();
   for (int e = threadIdx.x; e < HR * F; e += 256) {
@@ -485,6 +557,373 @@ __global__ void head_grads(HeadArgs a) {
   }
 }
 
+// ============================================ fast head (fc_units == 32) ==
+// The same train-mode head in 8 launches instead of 15: every BatchNorm's
+// batch statistics are summed in the PROLOGUE of the kernel that needs them
+// (fixed block order, fp64) instead of by a separate colsum launch, and the
+// two 2d-wide layers run on f32 MFMA (v_mfma_f32_32x32x2_f32: exact f32
+// products, f32 accumulation):
+//   hf_stats0  BN0 partial sums over 8 row groups x 32-column groups
+//   hf_fwd1    BN0 -> Linear(2d,32) (MFMA, K split over the 4 waves) -> ReLU -> Dropout
+//   head_fwd2 / head_fwd3 / head_bwd2 (a.fast: prologue sums)
+//   hf_bwd1    BN1 bwd -> da1;  G = da1^T xhat0 per block (MFMA), sum da1
+//   hf_reduce  G, sum da1 and the small layers' partials -> every head gradient;
+//              BN0's backward sums follow from G: sum_r dh0 = W1^T sum da1,
+//              sum_r dh0 xhat0 = sum_j W1[j] G[j]  (dh0 = da1 W1, never stored)
+//   hf_bwd0    dh0 (pooled half) = da1 W1 (MFMA) -> BN0 bwd -> dpooled
+constexpr int HF = 32;  // fc_units of the fast path
+
+__device__ __forceinline__ int hacc_row(int g, int h) { return (g & 3) + 8 * (g >> 2) + 4 * h; }
+
+__global__ __launch_bounds__(256) void hf_stats0(HeadArgs a) {
+  const int ncg = a.D2 / 32;
+  const int cg = blockIdx.x % ncg, rg = blockIdx.x / ncg;
+  const int cl = threadIdx.x & 31, ph = threadIdx.x >> 5;
+  const int c = 32 * cg + cl;
+  const int rows = a.B / a.nrg0;
+  const int64_t r0 = (int64_t)rg * rows;
+  double sv = 0.0, ssv = 0.0;
+#pragma unroll 8
+  for (int r = ph; r < rows; r += 8) {
+    const double v = hx(a, r0 + r, c);
+    sv += v;
+    ssv += v * v;
+  }
+  __shared__ double red[2][8][32];
+  red[0][ph][cl] = sv;
+  red[1][ph][cl] = ssv;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int wch = threadIdx.x >> 5;
+    double t = 0.0;
+    for (int q = 0; q < 8; ++q) t += red[wch][q][cl];
+    a.part0[(int64_t)rg * 2 * a.D2 + wch * a.D2 + c] = t;
+  }
+}
+
+// LDS (floats): mean/inv [D2] x 2 | h0 [32][D2+4] | W1 [32][D2+4] | red [4][32][32] | d1 [32][33]
+__global__ __launch_bounds__(256) void hf_fwd1(HeadArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  __shared__ double pro_tmp[256], pro_sum[1024];
+  const int D2 = a.D2, hs = D2 + 4, t = threadIdx.x;
+  float* mean = sm;
+  float* inv = mean + D2;
+  float* h0 = inv + D2;
+  float* w1 = h0 + HR * hs;
+  float* red = w1 + HF * hs;
+  float* d1 = red + 4 * HR * HF;
+  const int64_t r0 = (int64_t)blockIdx.x * HR;
+  colsum_prologue(a.part0, a.nrg0, 2 * D2, 2 * D2, pro_tmp, pro_sum);
+  bn_finalize(a, pro_sum, D2, mean, inv, a.stat0, a.p.bn0_rm, a.p.bn0_rv, a.p.bn0_nb, blockIdx.x == 0);
+  {  // W1 and the block's x rows, 8 float4 loads in flight per thread
+    const int n4 = HF * D2 / 4, q4 = D2 / 4;
+    for (int e0 = t; e0 < n4; e0 += 8 * 256) {
+      float4 wv[8], xv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = e0 + u * 256;
+        if (e < n4) {
+          wv[u] = *reinterpret_cast<const float4*>(a.p.fc1_w + 4 * e);
+          xv[u] = hx4(a, r0 + e / q4, 4 * (e % q4));
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = e0 + u * 256;
+        if (e < n4) {
+          const int row = e / q4, c = 4 * (e % q4);
+          *reinterpret_cast<float4*>(w1 + row * hs + c) = wv[u];
+          xv[u].x = (xv[u].x - mean[c]) * inv[c] * a.p.bn0_w[c] + a.p.bn0_b[c];
+          xv[u].y = (xv[u].y - mean[c + 1]) * inv[c + 1] * a.p.bn0_w[c + 1] + a.p.bn0_b[c + 1];
+          xv[u].z = (xv[u].z - mean[c + 2]) * inv[c + 2] * a.p.bn0_w[c + 2] + a.p.bn0_b[c + 2];
+          xv[u].w = (xv[u].w - mean[c + 3]) * inv[c + 3] * a.p.bn0_w[c + 3] + a.p.bn0_b[c + 3];
+          *reinterpret_cast<float4*>(h0 + row * hs + c) = xv[u];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  {  // a1 = h0 W1^T: lane half h covers k in [h D2/2, (h+1) D2/2), wave w a quarter of that
+    const int lane = t & 63, w = t >> 6, i = lane & 31, h = lane >> 5;
+    const int kw = D2 / 8;
+    const float* ar = h0 + i * hs + h * (D2 / 2) + w * kw;
+    const float* br = w1 + i * hs + h * (D2 / 2) + w * kw;
+    f32x16 acc;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) acc[g] = 0.f;
+    for (int kk = 0; kk < kw; kk += 4) {
+      const float4 av = *reinterpret_cast<const float4*>(ar + kk);
+      const float4 bv = *reinterpret_cast<const float4*>(br + kk);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, bv.x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, bv.y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, bv.z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, bv.w, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int g = 0; g < 16; ++g) red[w * HR * HF + hacc_row(g, h) * HF + i] = acc[g];
+  }
+  __syncthreads();
+  for (int o = t; o < HR * HF; o += 256) {
+    const int r = o / HF, j = o % HF;
+    const float v = ((red[o] + red[HR * HF + o]) + (red[2 * HR * HF + o] + red[3 * HR * HF + o])) + a.p.fc1_b[j];
+    a.a1[(r0 + r) * HF + j] = v;
+    d1[r * (HF + 1) + j] = fmaxf(v, 0.f) * keep_scale(a, 1, r0 + r, j);
+  }
+  __syncthreads();
+  if (t < 2 * HF) {
+    const int j = t % HF, sq = t / HF;
+    double acc = 0.0;
+    for (int r = 0; r < HR; ++r) {
+      const double v = d1[r * (HF + 1) + j];
+      acc += sq ? v * v : v;
+    }
+    a.part1[(int64_t)blockIdx.x * 2 * HF + sq * HF + j] = acc;
+  }
+}
+
+// LDS (floats): m0/i0 [D2] x 2 | xhat0 [32][D2+4] | da1 [32][33] | m1/i1/sb1/sg1 [32] x 4
+__global__ __launch_bounds__(256) void hf_bwd1(HeadArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  __shared__ double pro_tmp[256], pro_sum[64];
+  const int D2 = a.D2, hs = D2 + 4, t = threadIdx.x;
+  float* m0 = sm;
+  float* i0 = m0 + D2;
+  float* xh = i0 + D2;
+  float* da = xh + HR * hs;
+  float* m1 = da + HR * (HF + 1);
+  float* i1 = m1 + HF;
+  float* sb1 = i1 + HF;
+  float* sg1 = sb1 + HF;
+  const int64_t r0 = (int64_t)blockIdx.x * HR;
+  const int s4 = 2 * HF + a.F2 * HF + a.F2;
+  colsum_prologue(a.part4, a.nblk, s4, 2 * HF, pro_tmp, pro_sum);
+  load_stat(a.stat0, D2, m0, i0);
+  load_stat(a.stat1, HF, m1, i1);
+  if (t < HF) {
+    sb1[t] = (float)pro_sum[t];
+    sg1[t] = (float)pro_sum[HF + t];
+  }
+  __syncthreads();
+  {
+    const int q4 = D2 / 4, n4 = HR * q4;
+    for (int e0 = t; e0 < n4; e0 += 8 * 256) {
+      float4 xv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = e0 + u * 256;
+        if (e < n4) xv[u] = hx4(a, r0 + e / q4, 4 * (e % q4));
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = e0 + u * 256;
+        if (e < n4) {
+          const int row = e / q4, c = 4 * (e % q4);
+          xv[u].x = (xv[u].x - m0[c]) * i0[c];
+          xv[u].y = (xv[u].y - m0[c + 1]) * i0[c + 1];
+          xv[u].z = (xv[u].z - m0[c + 2]) * i0[c + 2];
+          xv[u].w = (xv[u].w - m0[c + 3]) * i0[c + 3];
+          *reinterpret_cast<float4*>(xh + row * hs + c) = xv[u];
+        }
+      }
+    }
+  }
+  const float invB = 1.f / (float)a.B;
+  {
+    float a1v[HR * HF / 256], dhv[HR * HF / 256];
+#pragma unroll
+    for (int u = 0; u < HR * HF / 256; ++u) {
+      const int e = t + u * 256;
+      a1v[u] = a.a1[r0 * HF + e];
+      dhv[u] = a.dh1[r0 * HF + e];
+    }
+#pragma unroll
+    for (int u = 0; u < HR * HF / 256; ++u) {
+      const int e = t + u * 256, r = e / HF, j = e % HF;
+      const float ks = keep_scale(a, 1, r0 + r, j);
+      const float xhat = (fmaxf(a1v[u], 0.f) * ks - m1[j]) * i1[j];
+      const float dd1 = i1[j] * a.p.bn1_w[j] * (dhv[u] - sb1[j] * invB - xhat * sg1[j] * invB);
+      const float v = a1v[u] > 0.f ? dd1 * ks : 0.f;
+      da[r * (HF + 1) + j] = v;
+      a.dh1[(r0 + r) * HF + j] = v;  // da1 replaces dh1 (same thread, same element)
+    }
+  }
+  __syncthreads();
+  {  // G (32 x D2) = da1^T xhat0 over the block's 32 rows; wave w: column tiles w, w+4, ...
+    const int lane = t & 63, w = t >> 6, i = lane & 31, h = lane >> 5;
+    float* pg = a.pw1 + (int64_t)blockIdx.x * HF * D2;
+    for (int ct = w; ct < D2 / 32; ct += 4) {
+      f32x16 acc;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) acc[g] = 0.f;
+#pragma unroll 4
+      for (int kk = 0; kk < HR / 2; ++kk) {
+        const int row = 2 * kk + h;
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(da[row * (HF + 1) + i], xh[row * hs + 32 * ct + i], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int g = 0; g < 16; ++g) pg[(int64_t)hacc_row(g, h) * D2 + 32 * ct + i] = acc[g];
+    }
+  }
+  if (t < HF) {
+    double acc = 0.0;
+    for (int r = 0; r < HR; ++r) acc += da[r * (HF + 1) + t];
+    a.part5[(int64_t)blockIdx.x * HF + t] = acc;
+  }
+}
+
+// Every head gradient from the block partials (fixed order, fp64).
+// Blocks [0, D2/4): 4 columns c of G each (1024 threads = 8 phases x 32 j x 4 c):
+//   g_fc1_w[j][c] = bn0_w[c] G[j][c] + bn0_b[c] S[j]   (S = sum da1 = g_fc1_b)
+//   g_bn0_b[c] = sum_j W1[j][c] S[j],  g_bn0_w[c] = sum_j W1[j][c] G[j][c]
+//   (also kept in sum5 for hf_bwd0).  Blocks after: 64 columns each of the
+//   small layers' partials (part3: bn2, fc3, loss; part4: bn1, fc2).
+__global__ __launch_bounds__(1024) void hf_reduce(HeadArgs a) {
+  const int D2 = a.D2, F2 = a.F2, t = threadIdx.x, nblk = a.nblk;
+  const int nA = D2 / 4;
+  if ((int)blockIdx.x < nA) {
+    __shared__ double red[8][32][4];
+    __shared__ double sred[8][32];
+    __shared__ double Gt[32][4], St[32];
+    const int ph = t >> 7, j = (t >> 2) & 31, cl = t & 3;
+    const int c = 4 * blockIdx.x + cl;
+    double acc = 0.0;
+    for (int b0 = ph; b0 < nblk; b0 += 8 * 16) {
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int b = b0 + 8 * u;
+        v[u] = b < nblk ? a.pw1[(int64_t)b * HF * D2 + (int64_t)j * D2 + c] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) acc += (double)v[u];
+    }
+    red[ph][j][cl] = acc;
+    if (t < 256) {
+      const int j2 = t & 31, p2 = t >> 5;
+      double s2 = 0.0;
+      for (int b0 = p2; b0 < nblk; b0 += 8 * 16) {
+        double v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int b = b0 + 8 * u;
+          v[u] = b < nblk ? a.part5[(int64_t)b * HF + j2] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) s2 += v[u];
+      }
+      sred[p2][j2] = s2;
+    }
+    __syncthreads();
+    if (t < 128) {
+      const int jj = t >> 2, cc = t & 3;
+      double g = 0.0;
+      for (int q = 0; q < 8; ++q) g += red[q][jj][cc];
+      Gt[jj][cc] = g;
+    }
+    if (t < 32) {
+      double s2 = 0.0;
+      for (int q = 0; q < 8; ++q) s2 += sred[q][t];
+      St[t] = s2;
+    }
+    __syncthreads();
+    if (t < 128) {
+      const int jj = t >> 2, cc = t & 3, col = 4 * blockIdx.x + cc;
+      a.p.g_fc1_w[(int64_t)jj * D2 + col] = (float)(a.p.bn0_w[col] * Gt[jj][cc] + a.p.bn0_b[col] * St[jj]);
+    }
+    if (t < 4) {
+      const int col = 4 * blockIdx.x + t;
+      double sb = 0.0, sg = 0.0;
+      float wv[HF];
+#pragma unroll
+      for (int jj = 0; jj < HF; ++jj) wv[jj] = a.p.fc1_w[(int64_t)jj * D2 + col];
+#pragma unroll
+      for (int jj = 0; jj < HF; ++jj) {
+        sb += (double)wv[jj] * St[jj];
+        sg += (double)wv[jj] * Gt[jj][t];
+      }
+      a.p.g_bn0_b[col] = (float)sb;
+      a.p.g_bn0_w[col] = (float)sg;
+      a.sum5[col] = sb;
+      a.sum5[D2 + col] = sg;
+    }
+    if (blockIdx.x == 0 && t < HF) a.p.g_fc1_b[t] = (float)St[t];
+    return;
+  }
+  // small layers: column q of the concatenation [part3 (3F2+2) | part4 (2F + F2 F + F2)]
+  __shared__ double sr[16][64];
+  const int s3 = 3 * F2 + 2, s4 = 2 * HF + F2 * HF + F2;
+  const int cl = t & 63, ph = t >> 6;
+  const int q = ((int)blockIdx.x - nA) * 64 + cl;
+  const bool valid = q < s3 + s4;
+  double acc = 0.0;
+  if (valid) {
+    const double* src = q < s3 ? a.part3 + q : a.part4 + (q - s3);
+    const int stride = q < s3 ? s3 : s4;
+    for (int b0 = ph; b0 < nblk; b0 += 16 * 16) {
+      double v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int b = b0 + 16 * u;
+        v[u] = b < nblk ? src[(int64_t)b * stride] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) acc += v[u];
+    }
+  }
+  sr[ph][cl] = acc;
+  __syncthreads();
+  if (t < 64 && valid) {
+    double v = 0.0;
+    for (int p2 = 0; p2 < 16; ++p2) v += sr[p2][t];
+    if (q < s3) {
+      if (q < F2) a.p.g_bn2_b[q] = (float)v;
+      else if (q < 2 * F2) a.p.g_bn2_w[q - F2] = (float)v;
+      else if (q < 3 * F2) a.p.g_fc3_w[q - 2 * F2] = (float)v;
+      else if (q == 3 * F2) a.p.g_fc3_b[0] = (float)v;
+      else *a.loss = (float)(v / a.B);
+    } else {
+      const int o = q - s3;
+      if (o < HF) a.p.g_bn1_b[o] = (float)v;
+      else if (o < 2 * HF) a.p.g_bn1_w[o - HF] = (float)v;
+      else if (o < 2 * HF + F2 * HF) a.p.g_fc2_w[o - 2 * HF] = (float)v;
+      else a.p.g_fc2_b[o - 2 * HF - F2 * HF] = (float)v;
+    }
+  }
+}
+
+// dpooled = BN0 backward of dh0's pooled half, dh0 = da1 W1 on MFMA
+// (wave w: 32-column tiles w, w+4, ... of the pooled half).
+__global__ __launch_bounds__(256) void hf_bwd0(HeadArgs a) {
+  __shared__ float da[HR][HF + 1];
+  const int D2 = a.D2, d = a.d, ld = (int)a.ld, t = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * HR;
+  for (int e = t; e < HR * HF; e += 256) da[e / HF][e % HF] = a.dh1[(r0 + e / HF) * HF + e % HF];
+  for (int e = t; e < HR * (ld - d); e += 256) a.dpooled[(r0 + e / (ld - d)) * ld + d + e % (ld - d)] = 0.f;
+  __syncthreads();
+  const float invB = 1.f / (float)a.B;
+  const int lane = t & 63, w = t >> 6, i = lane & 31, h = lane >> 5;
+  for (int ct = w; ct < d / 32; ct += 4) {
+    const int c = d + 32 * ct + i;  // column of x (pooled half)
+    f32x16 acc;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) acc[g] = 0.f;
+    float wv[HF / 2];
+#pragma unroll
+    for (int kk = 0; kk < HF / 2; ++kk) wv[kk] = a.p.fc1_w[(int64_t)(2 * kk + h) * D2 + c];
+#pragma unroll
+    for (int kk = 0; kk < HF / 2; ++kk)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(da[i][2 * kk + h], wv[kk], acc, 0, 0, 0);
+    const float m = a.stat0[c], iv = a.stat0[D2 + c], gw = a.p.bn0_w[c];
+    const float sb = (float)a.sum5[c] * invB, sg = (float)a.sum5[D2 + c] * invB;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int64_t r = r0 + hacc_row(g, h);
+      const float xhat = (a.pooled[r * ld + (c - d)] - m) * iv;
+      a.dpooled[r * ld + (c - d)] = iv * gw * (acc[g] - sb - xhat * sg);
+    }
+  }
+}
+
 // ------------------------------------------------- clip_grad_norm_ + Adam --
 __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g, int64_t n, double* __restrict__ part,
                                                     float* __restrict__ step) {
@@ -635,6 +1074,27 @@ extern "C" int nrk_din_head_train(const float* q, const float* pooled, int64_t l
   a.dpooled = dpooled;
   hipStream_t st = (hipStream_t)stream;
   const int D2 = 2 * d, F2 = F / 2;
+  const char* ef = getenv("NRK_DIN_HEAD_FAST");
+  a.fast = F == HF && d % 32 == 0 && !(ef && atoi(ef) == 0);
+  a.nrg0 = nblk < 8 ? nblk : 8;
+  const size_t lds2_ = ((size_t)HR * F + F2 * F + 2 * F + HR * F2) * 4;
+  const size_t lds3_ = ((size_t)2 * HR * F2 + 2 * F2 + 2 * HR) * 4;
+  const size_t lds4_ = ((size_t)3 * HR * F + HR * F2 + 2 * F + 4 * F2) * 4;
+  if (a.fast) {
+    const size_t lf1 = ((size_t)2 * D2 + (size_t)(HR + HF) * (D2 + 4) + 4 * HR * HF + HR * (HF + 1)) * 4;
+    const size_t lb1 = ((size_t)2 * D2 + (size_t)HR * (D2 + 4) + HR * (HF + 1) + 4 * HF) * 4;
+    const int s3_ = 3 * F2 + 2, s4_ = 2 * F + F2 * F + F2;
+    hipLaunchKernelGGL(hf_stats0, dim3((unsigned)(D2 / 32 * a.nrg0)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(hf_fwd1, dim3(nblk), dim3(256), lf1, st, a);
+    hipLaunchKernelGGL(head_fwd2, dim3(nblk), dim3(256), lds2_, st, a);
+    hipLaunchKernelGGL(head_fwd3, dim3(nblk), dim3(256), lds3_, st, a);
+    hipLaunchKernelGGL(head_bwd2, dim3(nblk), dim3(256), lds4_, st, a);
+    hipLaunchKernelGGL(hf_bwd1, dim3(nblk), dim3(256), lb1, st, a);
+    hipLaunchKernelGGL(hf_reduce, dim3((unsigned)(D2 / 4 + cdiv(s3_ + s4_, 64))), dim3(1024), 0, st, a);
+    hipLaunchKernelGGL(hf_bwd0, dim3(nblk), dim3(256), 0, st, a);
+    NRK_CHECK_LAUNCH("din_head_train (fast)");
+    return NRK_OK;
+  }
   const size_t lds1 = ((size_t)(HR + F) * (D2 + 1) + 2 * D2 + HR * F) * 4;
   const size_t lds2 = ((size_t)HR * F + F2 * F + 2 * F + HR * F2) * 4;
   const size_t lds3 = ((size_t)2 * HR * F2 + 2 * F2 + 2 * HR) * 4;

@@ -443,6 +443,22 @@ class FusedTrainStep:
         _lib.check(L_.nrk_clip_adam_workspace(n, sz), "clip_adam_workspace")
         self.ws_opt = torch.empty(max(sz.value, 1), dtype=torch.uint8, device=dev)
         self.n = n
+        # fast path (bf16 table, emb_dim 64/128): one batch-assembly kernel
+        # (rows -> ids, labels, f32 query, U = q W1q^T + b1, bf16 W1k) and an
+        # attention backward that also forms dW1q / db1 and writes every
+        # attention gradient in place: no torch ops left inside the step
+        self.fast = (table.dtype == torch.bfloat16 and d in (64, 128) and Dk == d and hist_ids.dim() == 2
+                     and hist_ids.shape[1] <= 128)
+        if self.fast:
+            self.hist_all = hist_ids.to(torch.int32).contiguous()
+            self.tgt_all = target_ids.reshape(-1).to(torch.int32).contiguous()
+            self.lab_all = labels.reshape(-1).to(torch.float32).contiguous()
+            L = hist_ids.shape[1]
+            self.hist_b = torch.empty((B, L), dtype=torch.int32, device=dev)
+            self.q_b = torch.empty((B, d), dtype=torch.float32, device=dev)
+            self.y_b = torch.empty(B, dtype=torch.float32, device=dev)
+            self.U_b = torch.empty((B, A), dtype=torch.float32, device=dev)
+            self.W1k_b = torch.empty((A, d), dtype=torch.bfloat16, device=dev)
         self.graph = None
         if graph:
             snap = [t.detach().clone() for t in (self.P, self.M, self.V, self.step_t)]
@@ -462,6 +478,8 @@ class FusedTrainStep:
                     v.copy_(bufs[k])
 
     def _body(self):
+        if self.fast:
+            return self._body_fast()
         L_ = _lib.load()
         m = self.model
         dev = self.table.device
@@ -495,6 +513,40 @@ class FusedTrainStep:
         gW1[:, :d].copy_(self.dU.t() @ q)
         gW1[:, d:].copy_(self.dW1k[:, :d])
         torch.sum(self.dU, 0, out=gb1)
+        if self.grad_hook is not None:
+            self.grad_hook(self.G)
+        _lib.check(L_.nrk_clip_adam(
+            _lib.ptr(self.P), _lib.ptr(self.G), _lib.ptr(self.M), _lib.ptr(self.V), self.n, _lib.ptr(self.step_t),
+            self.lr, self.betas[0], self.betas[1], self.eps, self.wd, self.clip, _lib.ptr(self.ws_opt),
+            self.ws_opt.numel(), st), "clip_adam")
+
+    def _body_fast(self):
+        L_ = _lib.load()
+        m = self.model
+        st = _lib.stream(self.table.device)
+        B, d, A = self.B, self.d, self.A
+        L = self.hist_all.shape[1]
+        N = self.table.shape[0]
+        dt = _lib.NRK_DTYPE_BF16
+        W1, b1 = m.attn.attn[0].weight, m.attn.attn[0].bias
+        w2 = m.attn.attn[2].weight
+        _lib.check(L_.nrk_din_batch(
+            _lib.ptr(self.idx), B, _lib.ptr(self.hist_all), _lib.ptr(self.tgt_all), _lib.ptr(self.lab_all),
+            self.hist_all.shape[0], L, _lib.ptr(self.table), N, dt, d, _lib.ptr(W1), _lib.ptr(b1), A,
+            _lib.ptr(self.hist_b), _lib.ptr(self.q_b), _lib.ptr(self.y_b), _lib.ptr(self.U_b), _lib.ptr(self.W1k_b),
+            st), "din_batch")
+        _lib.check(L_.nrk_din_attn_fwd(
+            _lib.ptr(self.table), _lib.ptr(self.hist_b), N, dt, _lib.ptr(self.U_b), _lib.ptr(self.W1k_b), _lib.ptr(w2),
+            0.0, B, L, d, A, _lib.ptr(self.pooled), _lib.ptr(self.alpha), st), "din_attn_fwd")
+        _lib.check(L_.nrk_din_head_train(
+            _lib.ptr(self.q_b), _lib.ptr(self.pooled), d, _lib.ptr(self.y_b), B, d, self.F, 0.1, 1e-5, self.p_drop,
+            self.seed, _lib.ptr(self.step_t), ctypes.byref(self.hp), _lib.ptr(self.logits), _lib.ptr(self.loss),
+            _lib.ptr(self.dpooled), _lib.ptr(self.ws_head), self.ws_head.numel(), st), "din_head_train")
+        _lib.check(L_.nrk_din_attn_bwd_params(
+            _lib.ptr(self.table), _lib.ptr(self.hist_b), N, dt, _lib.ptr(self.q_b), _lib.ptr(self.U_b),
+            _lib.ptr(self.W1k_b), _lib.ptr(w2), B, L, d, A, _lib.ptr(self.dpooled), _lib.ptr(self.alpha),
+            _lib.ptr(W1.grad), _lib.ptr(b1.grad), _lib.ptr(w2.grad), _lib.ptr(m.attn.attn[2].bias.grad), None,
+            _lib.ptr(self.ws_attn), self.ws_attn.numel(), st), "din_attn_bwd_params")
         if self.grad_hook is not None:
             self.grad_hook(self.G)
         _lib.check(L_.nrk_clip_adam(
