@@ -263,7 +263,14 @@ __global__ __launch_bounds__(256) void din_fwd_kernel(const void* __restrict__ k
 // wave's LDS slice with global_load_lds (padding / invalid ids read a zero
 // row); z = U + W1k K^T on MFMA per (32-row, 32-unit) tile; softmax and the
 // alpha-weighted pool stay inside the wave.
-__device__ __attribute__((aligned(16))) uint16_t g_zero_row[256];  // zero-initialised code-object global
+// Zero rows for padding slots / invalid ids (zero-initialised code-object
+// global).  Padding is ~60% of the slots at L=50 with uniform history lengths;
+// reading ONE zero row from every CU serialises on one L2 channel per XCD, so
+// each (sample, row) picks one of 256 distinct zero rows.
+__device__ __attribute__((aligned(16))) uint16_t g_zero_rows[256 * 256];
+__device__ __forceinline__ const uint16_t* zero_row(int64_t b, int row) {
+  return g_zero_rows + (((int)b * 37 + row) & 255) * 256;
+}
 
 template <int D, int NA, int NBUF>
 __global__ __launch_bounds__(256, 2) void din_fwd_wave_kernel(const uint16_t* __restrict__ table,
@@ -311,7 +318,7 @@ __global__ __launch_bounds__(256, 2) void din_fwd_wave_kernel(const uint16_t* __
       const int cc = pc ^ kswz<CPR>(row);
       const int ida = __shfl(i0, row & 63, 64), idb = __shfl(i1, row & 63, 64);  // both: source lanes differ
       const int idr = row < 64 ? ida : idb;
-      const uint16_t* src = (row < L && idr >= 0 && idr < n_table) ? table + (int64_t)idr * D + cc * 8 : g_zero_row;
+      const uint16_t* src = (row < L && idr >= 0 && idr < n_table) ? table + (int64_t)idr * D + cc * 8 : zero_row(b, row) + cc * 8;
       __builtin_amdgcn_global_load_lds(src, (lds_ptr)(img + u * 64 * 8), 16, 0, 0);
     }
 #pragma unroll
@@ -638,7 +645,7 @@ __global__ __launch_bounds__(256, 1) void din_bwd_pipe_kernel(
       const int row = p / CPR, pc = p % CPR;
       const int cc = pc ^ kswz<CPR>(row);
       const int32_t idr = row < L ? ids[b * L + row] : -1;
-      const uint16_t* src = (idr >= 0 && idr < n_table) ? table + (int64_t)idr * D + cc * 8 : g_zero_row;
+      const uint16_t* src = (idr >= 0 && idr < n_table) ? table + (int64_t)idr * D + cc * 8 : zero_row(b, row) + cc * 8;
       __builtin_amdgcn_global_load_lds(src, (lds_ptr)(img + u * 64 * 8), 16, 0, 0);
     }
     if (w == 0) {
@@ -826,6 +833,7 @@ __device__ __forceinline__ uint32_t lds_u32(const void* p) {
   return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)p;
 }
 __device__ __forceinline__ void glds16_asm(const void* gsrc, uint32_t lds_dst) {
+  lds_dst = __builtin_amdgcn_readfirstlane(lds_dst);  // wave-uniform by construction
   unsigned keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
@@ -833,6 +841,7 @@ __device__ __forceinline__ void glds16_asm(const void* gsrc, uint32_t lds_dst) {
                : "memory");
 }
 __device__ __forceinline__ void glds4_asm(const void* gsrc, uint32_t lds_dst) {
+  lds_dst = __builtin_amdgcn_readfirstlane(lds_dst);  // wave-uniform by construction
   unsigned keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
@@ -840,17 +849,19 @@ __device__ __forceinline__ void glds4_asm(const void* gsrc, uint32_t lds_dst) {
                : "memory");
 }
 
-template <int D, int LP>
+template <int D, int LP, int NSLOT>
 __global__ __launch_bounds__(256, 1) void din_bwd_deep_kernel(
     const uint16_t* __restrict__ table, const int32_t* __restrict__ ids, int64_t n_table, const float* __restrict__ U,
     const uint16_t* __restrict__ W1k, const float* __restrict__ w2, int B, int L, int A,
     const float* __restrict__ dpooled, const float* __restrict__ alpha, float* __restrict__ slabs,
-    const float* __restrict__ q, int dq) {
+    const float* __restrict__ q, int dq, int dbg) {
   constexpr int CPR = D / 8, KS = D / 16, NCT = D / 32, NC = LP / 32;
   constexpr int NPW = LP * CPR / 256;  // key-image DMA pieces per wave
   constexpr int N_IDS = LP > 64 ? 2 : 1;
   constexpr int N_D = NPW + 2 + N_IDS;  // per wave and iteration: keys, two small pieces, the ids pieces
-  static_assert(NPW >= 1 && 2 * N_D < 64, "vmcnt range");
+  constexpr int P = NSLOT - 1;          // data groups in flight ahead of the sample computed
+  constexpr int X = 3, RING = X + 1;    // ids are fetched X iterations before their data group
+  static_assert(NPW >= 1 && P >= 2 && P <= X && X * N_D < 64, "vmcnt range");
   // slot (floats): dpooled [128] | alpha [128] | U [128] | q [128] | key image [LP][D] bf16
   constexpr int SLOT_F = 4 * 128 + LP * D / 2;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -858,9 +869,9 @@ __global__ __launch_bounds__(256, 1) void din_bwd_deep_kernel(
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nsl = A >> 5;
   float* slot0 = reinterpret_cast<float*>(smem);
-  int32_t* idring = reinterpret_cast<int32_t*>(slot0 + 3 * SLOT_F) + w * 2 * 128;  // [2][128] per wave
-  float* dsbuf = reinterpret_cast<float*>(reinterpret_cast<int32_t*>(slot0 + 3 * SLOT_F) + 4 * 2 * 128) + w * 128;
-  float* dabuf = reinterpret_cast<float*>(reinterpret_cast<int32_t*>(slot0 + 3 * SLOT_F) + 4 * 2 * 128) + 4 * 128;
+  int32_t* idring = reinterpret_cast<int32_t*>(slot0 + NSLOT * SLOT_F) + w * RING * 128;  // [RING][128] per wave
+  float* dsbuf = reinterpret_cast<float*>(reinterpret_cast<int32_t*>(slot0 + NSLOT * SLOT_F) + 4 * RING * 128) + w * 128;
+  float* dabuf = reinterpret_cast<float*>(reinterpret_cast<int32_t*>(slot0 + NSLOT * SLOT_F) + 4 * RING * 128) + 4 * 128;
 
   WFrag<true, D> wf;
   const int wu = w < nsl ? w : 0;
@@ -885,6 +896,7 @@ __global__ __launch_bounds__(256, 1) void din_bwd_deep_kernel(
   };
   // key rows + small pieces of sample b (its ids in ring entry e) into slot sl
   auto issue_data = [&](int64_t b, int sl, int e) {
+    if (dbg & 16) b = B;  // timing only: every key row from the zero rows
     float* sp = slot0 + sl * SLOT_F;
     uint16_t* img = reinterpret_cast<uint16_t*>(sp + 4 * 128);
 #pragma unroll
@@ -895,7 +907,7 @@ __global__ __launch_bounds__(256, 1) void din_bwd_deep_kernel(
       const int cc = pc ^ kswz<CPR>(row);
       const int32_t idv0 = idring[e * 128 + row];
       const int32_t idr = row < L && b < B ? idv0 : -1;
-      const uint16_t* src = (idr >= 0 && idr < n_table) ? table + (int64_t)idr * D + cc * 8 : g_zero_row;
+      const uint16_t* src = (idr >= 0 && idr < n_table) ? table + (int64_t)idr * D + cc * 8 : zero_row(b, row) + cc * 8;
       glds16_asm(src, lds_u32(img + u * 64 * 8));
     }
     const int64_t bc = b < B ? b : 0;
@@ -911,21 +923,27 @@ __global__ __launch_bounds__(256, 1) void din_bwd_deep_kernel(
 
   const int64_t grid = gridDim.x;
   int64_t b = blockIdx.x;
-  issue_ids(b, 0);
+#pragma unroll
+  for (int k = 0; k < X; ++k) issue_ids(b + k * grid, k);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  issue_ids(b + grid, 1);
-  issue_data(b, 0, 0);
-  issue_ids(b + 2 * grid, 0);
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_D) : "memory");  // ids of b + grid landed
-  issue_data(b + grid, 1, 1);
-  int sl = 0, e = 0;  // e: ring entry holding the ids of sample b + 2 grid
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    issue_ids(b + (k + X) * grid, (k + X) % RING);
+    issue_data(b + k * grid, k, k);
+  }
+  int sl = 0, e = P % RING;  // e: ring entry holding the ids of sample b + P grid
   for (; b < B; b += grid) {
     // this wave's DMA group of sample b landed; all waves' after the barrier; slot of b - grid is free
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N_D) : "memory");
-    issue_ids(b + 3 * grid, e ^ 1);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_D) : "memory");  // ids of b + 2 grid landed
-    issue_data(b + 2 * grid, sl == 0 ? 2 : sl - 1, e);
-    e ^= 1;
+    if (dbg & 32) {  // timing only: no DMA waits (results are garbage)
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      issue_ids(b + (P + X) * grid, e + X < RING ? e + X : e + X - RING);
+    } else {
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"((P - 1) * N_D) : "memory");
+      issue_ids(b + (P + X) * grid, e + X < RING ? e + X : e + X - RING);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(X * N_D) : "memory");  // ids of b + P grid landed
+    }
+    issue_data(b + P * grid, sl + P < NSLOT ? sl + P : sl + P - NSLOT, e);
+    e = e + 1 < RING ? e + 1 : 0;
 
     const float* sp = slot0 + sl * SLOT_F;
     const float* sdp = sp;
@@ -933,7 +951,7 @@ __global__ __launch_bounds__(256, 1) void din_bwd_deep_kernel(
     const float* sU = sp + 256;
     const float* sq = sp + 384;
     const unsigned char* img = reinterpret_cast<const unsigned char*>(sp + 512);
-    {  // dalpha[row] = dpooled . K[row], split over the waves: wave w owns rows [w R, (w+1) R)
+    if (!(dbg & 1)) {  // dalpha[row] = dpooled . K[row], split over the waves: wave w owns rows [w R, (w+1) R)
       constexpr int R = LP / 4, LPR = 64 / R, CH = CPR / LPR;
       const int row = w * R + lane / LPR, part = lane % LPR;
       float acc = 0.f;
@@ -957,21 +975,14 @@ __global__ __launch_bounds__(256, 1) void din_bwd_deep_kernel(
       if (part == 0) dabuf[row] = acc;
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (w < nsl) {
+    if (w < nsl && !(dbg & 2)) {
       const float un = sU[32 * w + r];
       float qcur[NCT];
 #pragma unroll
       for (int c = 0; c < NCT; ++c) qcur[c] = 32 * c + r < dq ? sq[32 * c + r] : 0.f;
       float da[NC];
-      bf16x8 kf[NC][KS];
 #pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        const int row = 32 * c + r;
-        da[c] = dabuf[row];
-#pragma unroll
-        for (int s2 = 0; s2 < KS; ++s2)
-          kf[c][s2] = *reinterpret_cast<const bf16x8*>(img + KImg<true, D>::off(row, 16 * s2 + 8 * h));
-      }
+      for (int c = 0; c < NC; ++c) da[c] = dabuf[32 * c + r];
       float t = 0.f;
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
@@ -998,7 +1009,10 @@ __global__ __launch_bounds__(256, 1) void din_bwd_deep_kernel(
 #pragma unroll
         for (int g = 0; g < 16; ++g) acc[g] = un;
 #pragma unroll
-        for (int s2 = 0; s2 < KS; ++s2) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[c][s2], wf.f[s2], acc, 0, 0, 0);
+        for (int s2 = 0; s2 < KS; ++s2) {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(img + KImg<true, D>::off(32 * c + r, 16 * s2 + 8 * h));
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, wf.f[s2], acc, 0, 0, 0);
+        }
         f32x16 dz;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -1026,6 +1040,7 @@ __global__ __launch_bounds__(256, 1) void din_bwd_deep_kernel(
           }
           const int grp = lane >> 4, i16 = lane & 15;
           const int rowq = 32 * c + 16 * s + 4 * h + (i16 >> 2);
+          if (dbg & 4) continue;
 #pragma unroll
           for (int cc = 0; cc < NCT; ++cc) {
             const int col = 32 * cc + 16 * (grp & 1) + 4 * (i16 & 3);
@@ -1045,11 +1060,11 @@ __global__ __launch_bounds__(256, 1) void din_bwd_deep_kernel(
       for (int c = 0; c < NCT; ++c)
         dwq[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(h ? 0.f : du, h ? 0.f : qcur[c], dwq[c], 0, 0, 0);
     }
-    sl = sl == 2 ? 0 : sl + 1;
+    sl = sl == NSLOT - 1 ? 0 : sl + 1;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup exits
   float* slab = slabs + (size_t)blockIdx.x * slab_floats(A, D);
-  if (w < nsl) {
+  if (w < nsl && !(dbg & 8)) {
     float* sqs = slab + slab_q_off(A, D);
 #pragma unroll
     for (int c = 0; c < NCT; ++c)
@@ -1070,6 +1085,310 @@ __global__ __launch_bounds__(256, 1) void din_bwd_deep_kernel(
   }
 }
 
+// 8-wave variant (two waves per SIMD): waves w and w + 4 own the same 32
+// units (us = w & 3) and split the sample's 32-row history tiles (rg = w >> 2
+// takes tiles rg, rg + 2, ...); each accumulates its rows' share of every
+// gradient, and the pairs are combined in a fixed order after the loop.
+template <int D, int LP, int NSLOT>
+__global__ __launch_bounds__(512, 1) void din_bwd_deep8_kernel(
+    const uint16_t* __restrict__ table, const int32_t* __restrict__ ids, int64_t n_table, const float* __restrict__ U,
+    const uint16_t* __restrict__ W1k, const float* __restrict__ w2, int B, int L, int A,
+    const float* __restrict__ dpooled, const float* __restrict__ alpha, float* __restrict__ slabs,
+    const float* __restrict__ q, int dq, float* __restrict__ dUp, float* __restrict__ dummy, int dbg) {
+  constexpr int CPR = D / 8, KS = D / 16, NCT = D / 32, NC = LP / 32;
+  constexpr int NPW = LP * CPR / 512;  // key-image DMA pieces per wave
+  constexpr int N_IDS = LP > 64 ? 2 : 1;
+  constexpr int N_D = 1 + NPW + 1 + N_IDS;  // per wave and iteration: the dU store, keys, one small piece, ids
+  constexpr int P = NSLOT - 1;          // data groups in flight ahead of the sample computed
+  constexpr int X = 3, RING = X + 1;    // ids are fetched X iterations before their data group
+  static_assert(NPW >= 0 && P >= 2 && P <= X && X * N_D < 64, "vmcnt range");
+  // slot (floats): dpooled [128] | alpha [128] | U [128] | q [128] | key image [LP][D] bf16
+  constexpr int SLOT_F = 4 * 128 + LP * D / 2;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int us = w & 3, rg = w >> 2;
+  const int nsl = A >> 5;
+  float* slot0 = reinterpret_cast<float*>(smem);
+  int32_t* idring = reinterpret_cast<int32_t*>(slot0 + NSLOT * SLOT_F) + w * RING * 128;  // [RING][128] per wave
+  float* dsbuf = reinterpret_cast<float*>(reinterpret_cast<int32_t*>(slot0 + NSLOT * SLOT_F) + 8 * RING * 128) + w * 128;
+  float* dabuf = reinterpret_cast<float*>(reinterpret_cast<int32_t*>(slot0 + NSLOT * SLOT_F) + 8 * RING * 128) + 8 * 128;
+
+  WFrag<true, D> wf;
+  const int wu = us < nsl ? us : 0;
+  wf.load(W1k, 32 * wu + r, h);
+  const float w2n = w2[32 * wu + r];
+#pragma unroll
+  for (int s2 = 0; s2 < KS; ++s2) asm volatile("" ::"v"(wf.f[s2]));  // hipcc's waits for these land here
+  asm volatile("" ::"v"(w2n));
+  f32x16 dw[NCT];
+#pragma unroll
+  for (int c = 0; c < NCT; ++c)
+#pragma unroll
+    for (int g = 0; g < 16; ++g) dw[c][g] = 0.f;
+  float dw2_acc = 0.f, db2_acc = 0.f, db1_acc = 0.f;
+  // this wave's rows' share of dU of the previous sample, stored (asm, counted
+  // in the vmcnt plan) at the top of the next iteration; dW1q = sum dU q^T is
+  // formed from these rows by din_dwq_kernel
+  float du_keep = 0.f;
+  int64_t b_keep = -1;
+  float* const dmy = dummy + (size_t)blockIdx.x * 512 + tid;
+  auto store_du = [&]() {
+    float* dst = (b_keep >= 0 && us < nsl && h == 0) ? dUp + ((size_t)rg * B + b_keep) * A + 32 * us + r : dmy;
+    asm volatile("global_store_dword %0, %1, off" ::"v"(dst), "v"(du_keep) : "memory");
+  };
+
+  // ids of sample b (all LP rows; clamped) into ring entry e of this wave
+  auto issue_ids = [&](int64_t b, int e) {
+    const int64_t bc = b < B ? b : 0;
+    const int i = lane < LP ? lane : 0;
+    glds4_asm(ids + bc * L + (i < L ? i : 0), lds_u32(idring + e * 128));
+    if constexpr (LP > 64) glds4_asm(ids + bc * L + (64 + lane < L ? 64 + lane : 0), lds_u32(idring + e * 128 + 64));
+  };
+  // key rows + small pieces of sample b (its ids in ring entry e) into slot sl
+  auto issue_data = [&](int64_t b, int sl, int e) {
+    if (dbg & 16) b = B;  // timing only: every key row from the zero rows
+    float* sp = slot0 + sl * SLOT_F;
+    uint16_t* img = reinterpret_cast<uint16_t*>(sp + 4 * 128);
+#pragma unroll
+    for (int k = 0; k < NPW; ++k) {
+      const int u = w + 8 * k;
+      const int p = u * 64 + lane;
+      const int row = p / CPR, pc = p % CPR;
+      const int cc = pc ^ kswz<CPR>(row);
+      const int32_t idv0 = idring[e * 128 + row];
+      const int32_t idr = row < L && b < B ? idv0 : -1;
+      const uint16_t* src = (idr >= 0 && idr < n_table) ? table + (int64_t)idr * D + cc * 8 : zero_row(b, row) + cc * 8;
+      glds16_asm(src, lds_u32(img + u * 64 * 8));
+    }
+    const int64_t bc = b < B ? b : 0;
+    {  // small piece w of [dp0, dp1, al0, al1, u0, u1, q0, q1]
+      const int pc = w, kind = pc >> 1, part = pc & 1;
+      const int i = part * 64 + lane;
+      const float* base = kind == 0 ? dpooled + bc * D : kind == 1 ? alpha + bc * L : kind == 2 ? U + bc * A : q + bc * dq;
+      const int lim = kind == 0 ? D : kind == 1 ? L : kind == 2 ? A : dq;
+      glds4_asm(base + (i < lim ? i : 0), lds_u32(sp + kind * 128 + part * 64));
+    }
+  };
+
+  const int64_t grid = gridDim.x;
+  int64_t b = blockIdx.x;
+#pragma unroll
+  for (int k = 0; k < X; ++k) issue_ids(b + k * grid, k);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    store_du();  // nothing to store yet: the dummy slot (keeps every group the same size)
+    issue_ids(b + (k + X) * grid, (k + X) % RING);
+    issue_data(b + k * grid, k, k);
+  }
+  int sl = 0, e = P % RING;  // e: ring entry holding the ids of sample b + P grid
+  for (; b < B; b += grid) {
+    // this wave's DMA group of sample b landed; all waves' after the barrier; slot of b - grid is free
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"((P - 1) * N_D) : "memory");
+    store_du();
+    issue_ids(b + (P + X) * grid, e + X < RING ? e + X : e + X - RING);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(X * N_D) : "memory");  // ids of b + P grid landed
+    issue_data(b + P * grid, sl + P < NSLOT ? sl + P : sl + P - NSLOT, e);
+    e = e + 1 < RING ? e + 1 : 0;
+
+    const float* sp = slot0 + sl * SLOT_F;
+    const float* sdp = sp;
+    const float* sal = sp + 128;
+    const float* sU = sp + 256;
+    
+    const unsigned char* img = reinterpret_cast<const unsigned char*>(sp + 512);
+    if (!(dbg & 1)) {  // dalpha[row] = dpooled . K[row], split over the waves: wave w owns rows [w R, (w+1) R)
+      constexpr int R = LP / 8, LPR = 64 / R, CH = CPR / LPR;
+      const int row = w * R + lane / LPR, part = lane % LPR;
+      float acc = 0.f;
+#pragma unroll
+      for (int ch = 0; ch < CH; ++ch) {
+        const int cc = part * CH + ch;
+        const uint4 kv = *reinterpret_cast<const uint4*>(img + row * 2 * D + 16 * (cc ^ kswz<CPR>(row)));
+        const float4 d0 = *reinterpret_cast<const float4*>(sdp + 8 * cc);
+        const float4 d1 = *reinterpret_cast<const float4*>(sdp + 8 * cc + 4);
+        acc = fmaf(d0.x, __uint_as_float(kv.x << 16), acc);
+        acc = fmaf(d0.y, __uint_as_float(kv.x & 0xFFFF0000u), acc);
+        acc = fmaf(d0.z, __uint_as_float(kv.y << 16), acc);
+        acc = fmaf(d0.w, __uint_as_float(kv.y & 0xFFFF0000u), acc);
+        acc = fmaf(d1.x, __uint_as_float(kv.z << 16), acc);
+        acc = fmaf(d1.y, __uint_as_float(kv.z & 0xFFFF0000u), acc);
+        acc = fmaf(d1.z, __uint_as_float(kv.w << 16), acc);
+        acc = fmaf(d1.w, __uint_as_float(kv.w & 0xFFFF0000u), acc);
+      }
+#pragma unroll
+      for (int o = 1; o < LPR; o <<= 1) acc += __shfl_xor(acc, o, 64);
+      if (part == 0) dabuf[row] = acc;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    float du = 0.f;
+    if (us < nsl && rg < NC && !(dbg & 2)) {
+      const float un = sU[32 * us + r];
+      float da[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) da[c] = dabuf[32 * c + r];
+      float t = 0.f;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int row = 32 * c + r;
+        t += (row < L && h == 0) ? sal[row] * da[c] : 0.f;
+      }
+      const float cdot = wave_sum(t);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int row = 32 * c + r;
+        if (h == 0 && (c & 1) == rg) {
+          const float ds = row < L ? sal[row] * (da[c] - cdot) : 0.f;
+          dsbuf[row] = ds;
+          if (us == 0) db2_acc += ds;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        if ((c & 1) != rg) continue;
+        f32x16 acc;
+#pragma unroll
+        for (int g = 0; g < 16; ++g) acc[g] = un;
+#pragma unroll
+        for (int s2 = 0; s2 < KS; ++s2) {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(img + KImg<true, D>::off(32 * c + r, 16 * s2 + 8 * h));
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, wf.f[s2], acc, 0, 0, 0);
+        }
+        f32x16 dz;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float4 d4 = *reinterpret_cast<const float4*>(dsbuf + 32 * c + 8 * j + 4 * h);
+          const float dsv[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int g = 4 * j + i;
+            const float z = acc[g];
+            dw2_acc = fmaf(dsv[i], fmaxf(z, 0.f), dw2_acc);
+            const float v = z > 0.f ? dsv[i] * w2n : 0.f;
+            dz[g] = v;
+            du += v;
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          bf16x8 af;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {  // v_cvt_pk_bf16_f32 (round to nearest even)
+            const bf16x2_hw pk = {(__bf16)dz[8 * s + 2 * j], (__bf16)dz[8 * s + 2 * j + 1]};
+            const uint32_t u = __builtin_bit_cast(uint32_t, pk);
+            af[2 * j] = (short)(u & 0xFFFF);
+            af[2 * j + 1] = (short)(u >> 16);
+          }
+          const int grp = lane >> 4, i16 = lane & 15;
+          const int rowq = 32 * c + 16 * s + 4 * h + (i16 >> 2);
+          if (dbg & 4) continue;
+#pragma unroll
+          for (int cc = 0; cc < NCT; ++cc) {
+            const int col = 32 * cc + 16 * (grp & 1) + 4 * (i16 & 3);
+            typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+            const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(img + KImg<true, D>::off(rowq, col)));
+            const bf16x4 hi =
+                __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(img + KImg<true, D>::off(rowq + 8, col)));
+            const bf16x8 bfr = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+            dw[cc] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, dw[cc], 0, 0, 0);
+          }
+        }
+      }
+      du += __shfl_xor(du, 32, 64);
+      db1_acc += du;
+    }
+    du_keep = du;
+    b_keep = b;
+    sl = sl == NSLOT - 1 ? 0 : sl + 1;
+  }
+  store_du();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup exits
+  // combine the row-group pairs (rg 1 into rg 0, fixed order) through LDS
+  float* xch = slot0;  // [4 unit slices][32][D] f32, reused for dW1k then dW1q
+  const bool act = us < nsl;
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  if (rg == 1 && act) {
+#pragma unroll
+    for (int c = 0; c < NCT; ++c)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) xch[(size_t)(32 * us + acc_row(g, h)) * D + 32 * c + r] = dw[c][g];
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  if (rg == 0 && act) {
+#pragma unroll
+    for (int c = 0; c < NCT; ++c)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) dw[c][g] += xch[(size_t)(32 * us + acc_row(g, h)) * D + 32 * c + r];
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  float* xs = slot0 + 4 * 32 * D;  // [4][32] dw2, [4][32] db1, [1] db2 of the rg = 1 waves
+  {
+    const float t2 = dw2_acc + __shfl_xor(dw2_acc, 32, 64);
+    const float tb2 = wave_sum(db2_acc);
+    if (rg == 1 && act && h == 0) {
+      xs[32 * us + r] = t2;
+      xs[128 + 32 * us + r] = db1_acc;
+    }
+    if (rg == 1 && us == 0 && lane == 0) xs[256] = tb2;
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    float* slab = slabs + (size_t)blockIdx.x * slab_floats(A, D);
+    if (rg == 0 && act && !(dbg & 8)) {
+      float* sqs = slab + slab_q_off(A, D);
+#pragma unroll
+      for (int c = 0; c < NCT; ++c)
+#pragma unroll
+        for (int g = 0; g < 16; ++g) slab[(size_t)(32 * us + acc_row(g, h)) * D + 32 * c + r] = dw[c][g];
+      if (h == 0) {
+        slab[(size_t)A * D + 32 * us + r] = t2 + xs[32 * us + r];
+        sqs[(size_t)A * D + 32 * us + r] = db1_acc + xs[128 + 32 * us + r];
+      }
+    }
+    if (rg == 0 && us == 0 && lane == 0) slab[(size_t)A * D + A] = tb2 + xs[256];
+  }
+}
+
+// dW1q partial tiles for nrk_din_attn_bwd_params (8-wave backward):
+//   part[kc][n][k] = sum over the samples b of chunk kc and both row groups
+//   of dUp[rg][b][n] q[b][k], on f32 MFMA (lane half h = row group).
+// grid (A/32 x D/32 tiles, KC chunks); 4 waves split a chunk's samples.
+__global__ __launch_bounds__(256) void din_dwq_kernel(const float* __restrict__ dUp, const float* __restrict__ q, int B,
+                                                      int A, int dq, int D, int kchunk, float* __restrict__ part) {
+  __shared__ float red[4][32][33];
+  const int nt = D / 32;
+  const int tn = blockIdx.x / nt, tk = blockIdx.x % nt, kc = blockIdx.y;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, i = lane & 31, h = lane >> 5;
+  f32x16 acc;
+#pragma unroll
+  for (int g = 0; g < 16; ++g) acc[g] = 0.f;
+  const int b0 = kc * kchunk, b1 = min(B, b0 + kchunk);
+  const int col = 32 * tk + i;
+  const bool colok = col < dq;
+  for (int bb = b0 + w; bb < b1; bb += 4 * 8) {
+    float av[8], bv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int b = bb + 4 * u;
+      const bool ok = b < b1;
+      av[u] = ok ? dUp[((size_t)h * B + b) * A + 32 * tn + i] : 0.f;
+      bv[u] = ok && colok ? q[(size_t)b * dq + col] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int g = 0; g < 16; ++g) red[w][acc_row(g, h)][i] = acc[g];
+  __syncthreads();
+  for (int o = threadIdx.x; o < 32 * 32; o += 256) {
+    const int rr = o >> 5, cc = o & 31;
+    const float v = (red[0][rr][cc] + red[1][rr][cc]) + (red[2][rr][cc] + red[3][rr][cc]);
+    part[((size_t)kc * A + 32 * tn + rr) * D + 32 * tk + cc] = v;
+  }
+}
+
 // Parameter gradients of the whole attention layer from the slabs (fixed
 // slab order, deterministic), written straight into the model's gradient
 // tensors: gW1 (A, 2d) = [dW1q | dW1k[:, :d]], gb1, gw2, gb2.  A block owns
@@ -1078,7 +1397,8 @@ __global__ __launch_bounds__(256, 1) void din_bwd_deep_kernel(
 __global__ __launch_bounds__(512) void din_bwd_reduce_params_kernel(const float* __restrict__ slabs, int nslab, int A,
                                                                     int D, int d, float* __restrict__ gW1,
                                                                     float* __restrict__ gb1, float* __restrict__ gw2,
-                                                                    float* __restrict__ gb2) {
+                                                                    float* __restrict__ gb2,
+                                                                    const float* __restrict__ qpart, int nkc) {
   __shared__ float part[8][64];
   const size_t n = slab_floats(A, D);
   const size_t nw = (size_t)A * d;  // per half of W1
@@ -1100,7 +1420,10 @@ __global__ __launch_bounds__(512) void din_bwd_reduce_params_kernel(const float*
     }
   }
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  if (i < nout) {
+  if (qpart != nullptr && i < 2 * nw && (int)(i % (2 * (size_t)d)) < d) {  // dW1q from din_dwq_kernel's chunks
+    const size_t row = i / (2 * (size_t)d), col = i % (2 * (size_t)d);
+    for (int kc = g; kc < nkc; kc += 8) s0 += qpart[((size_t)kc * A + row) * D + col];
+  } else if (i < nout) {
     int j = g;
     for (; j + 24 < nslab; j += 32) {
       s0 += slabs[(size_t)j * n + src];
@@ -1192,9 +1515,20 @@ __global__ __launch_bounds__(256) void din_batch_kernel(const int64_t* __restric
     W1k_bf[e] = f32_to_bf16_rne(W1[n * 2 * D + D + k]);
   }
   __syncthreads();
-  for (int e = tid; e < 32 * L; e += 256) {
-    const int i = e / L, j = e % L, b = b0 + i;
-    if (b < B) hist[(int64_t)b * L + j] = s_row[i] >= 0 ? hist_all[s_row[i] * L + j] : -1;
+  for (int e0 = tid; e0 < 32 * L; e0 += 8 * 256) {  // 8 loads in flight per thread
+    int32_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + u * 256;
+      const int i = e / L, j = e % L;
+      v[u] = (e < 32 * L && s_row[i < 32 ? i : 0] >= 0) ? hist_all[s_row[i] * L + j] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + u * 256;
+      const int i = e / L, j = e % L, b = b0 + i;
+      if (e < 32 * L && b < B) hist[(int64_t)b * L + j] = v[u];
+    }
   }
   const int b = b0 + r;
   const int32_t t = s_tgt[r];
@@ -1389,9 +1723,22 @@ extern "C" int nrk_din_attn_fwd(const void* keys, const int32_t* hist_ids, int64
   return NRK_OK;
 }
 
+constexpr int DWQ_KC = 64;  // sample chunks of din_dwq_kernel
+
+// workspace: slabs | dU rows of both row groups [2][B][A] | dW1q chunks [KC][A][d] | dummy store slots
+size_t bwd_ws_parts(int B, int d, int A, size_t off[4]) {
+  const int grid = B > 0 ? din_grid(B, true) : 1;
+  off[0] = 0;
+  off[1] = align_up((size_t)grid * slab_floats(A, d) * 4, 256);
+  off[2] = align_up(off[1] + (size_t)2 * B * A * 4, 256);
+  off[3] = align_up(off[2] + (size_t)DWQ_KC * A * d * 4, 256);
+  return off[3] + (size_t)grid * 512 * 4;
+}
+
 extern "C" int nrk_din_attn_bwd_workspace(int32_t B, int32_t d, int32_t A, size_t* ws_bytes) {
   NRK_CHECK_ARG(ws_bytes != nullptr, "din_bwd_workspace: null");
-  *ws_bytes = (size_t)(B > 0 ? din_grid(B, true) : 1) * slab_floats(A, d) * 4;
+  size_t off[4];
+  *ws_bytes = bwd_ws_parts(B, d, A, off);
   return NRK_OK;
 }
 
@@ -1501,8 +1848,13 @@ extern "C" int nrk_din_attn_bwd_params(const void* table, const int32_t* hist_id
   NRK_CHECK_ARG(q && U && W1k && w2 && dpooled && alpha && gW1 && gb1 && gw2 && gb2 && ws,
                 "din_bwd_params: null pointer");
   const int grid = din_grid(B, true);
-  const size_t need = (size_t)grid * slab_floats(A, d) * 4;
+  size_t woff[4];
+  const size_t need = bwd_ws_parts(B, d, A, woff);
   if (ws_bytes < need) return fail(NRK_EWORKSPACE, "din_bwd_params: workspace %zu < %zu", ws_bytes, need);
+  float* dUp = reinterpret_cast<float*>(static_cast<char*>(ws) + woff[1]);
+  float* qpart_w8 = reinterpret_cast<float*>(static_cast<char*>(ws) + woff[2]);
+  float* dmy = reinterpret_cast<float*>(static_cast<char*>(ws) + woff[3]);
+  const float* qpart = nullptr;
   const int Lp = (L + 31) & ~31;
   const size_t psm = (size_t)(2 * (d + 128 + Lp * d / 2) + 4 * 128) * 4;
   NRK_CHECK_ARG(psm <= 160 * 1024, "din_bwd_params: L=%d d=%d needs %zu B LDS", L, d, psm);
@@ -1512,12 +1864,32 @@ extern "C" int nrk_din_attn_bwd_params(const void* table, const int32_t* hist_id
   const uint16_t* wk = static_cast<const uint16_t*>(W1k);
   const char* ed = getenv("NRK_DIN_BWD_DEEP");
   if (dU == nullptr && !(ed && atoi(ed) == 0)) {
+    const char* edb = getenv("NRK_DIN_BWD_DBG");  // timing experiments only: skip parts of the math
+    const int dbg = edb ? atoi(edb) : 0;
     const int LPk = Lp <= 32 ? 32 : Lp <= 64 ? 64 : 128;
-    const size_t dsm = (size_t)(3 * (4 * 128 + LPk * d / 2) + 4 * 2 * 128 + 5 * 128) * 4;
+    const char* ens = getenv("NRK_DIN_BWD_SLOTS");
+    const int nslot = ens && atoi(ens) == 3 ? 3 : 4;
+    const char* e8 = getenv("NRK_DIN_BWD_8W");
+    const bool w8 = !(e8 && atoi(e8) == 0) && LPk * d >= 4096;  // >= 8 key-image pieces: one per wave
+    size_t dsm = (size_t)(nslot * (4 * 128 + LPk * d / 2) + 4 * 4 * 128 + 5 * 128) * 4;
+    if (w8) {
+      dsm = (size_t)(nslot * (4 * 128 + LPk * d / 2) + 8 * 4 * 128 + 9 * 128) * 4;
+      const size_t xneed = ((size_t)4 * 32 * d + 257) * 4;  // pair-combine exchange area (reuses the slots)
+      if (dsm < xneed) dsm = xneed;
+    }
     NRK_CHECK_ARG(dsm <= 160 * 1024, "din_bwd_params: L=%d d=%d needs %zu B LDS", L, d, dsm);
-#define NRK_BWD_DEEP(DD, LL)                                                                                     \
-  hipLaunchKernelGGL((din_bwd_deep_kernel<DD, LL>), dim3(grid), dim3(256), dsm, st, tb, hist_ids, n_table, U, wk, w2, B, \
-                     L, A, dpooled, alpha, slabs, q, d)
+#define NRK_BWD_DEEP(DD, LL)                                                                                          \
+  do {                                                                                                              \
+    if (w8)                                                                                                         \
+      hipLaunchKernelGGL((din_bwd_deep8_kernel<DD, LL, 3>), dim3(grid), dim3(512), dsm, st, tb, hist_ids, n_table, U, \
+                         wk, w2, B, L, A, dpooled, alpha, slabs, q, d, dUp, dmy, dbg);                                \
+    else if (nslot == 3)                                                                                            \
+      hipLaunchKernelGGL((din_bwd_deep_kernel<DD, LL, 3>), dim3(grid), dim3(256), dsm, st, tb, hist_ids, n_table, U, wk, \
+                         w2, B, L, A, dpooled, alpha, slabs, q, d, dbg);                                              \
+    else                                                                                                            \
+      hipLaunchKernelGGL((din_bwd_deep_kernel<DD, LL, 4>), dim3(grid), dim3(256), dsm, st, tb, hist_ids, n_table, U, wk, \
+                         w2, B, L, A, dpooled, alpha, slabs, q, d, dbg);                                              \
+  } while (0)
     if (d == 128) {
       if (LPk == 32) NRK_BWD_DEEP(128, 32); else if (LPk == 64) NRK_BWD_DEEP(128, 64); else NRK_BWD_DEEP(128, 128);
     } else {
@@ -1525,6 +1897,13 @@ extern "C" int nrk_din_attn_bwd_params(const void* table, const int32_t* hist_id
     }
 #undef NRK_BWD_DEEP
     NRK_CHECK_LAUNCH("din_bwd_deep_kernel");
+    if (w8) {
+      const int kchunk = (int)cdiv(B, DWQ_KC);
+      hipLaunchKernelGGL(din_dwq_kernel, dim3((unsigned)(A / 32 * (d / 32)), DWQ_KC), dim3(256), 0, st, dUp, q, B, A, d, d,
+                         kchunk, qpart_w8);
+      NRK_CHECK_LAUNCH("din_dwq_kernel");
+      qpart = qpart_w8;
+    }
   } else {
     if (d == 128)
       hipLaunchKernelGGL(din_bwd_pipe_kernel<128>, dim3(grid), dim3(256), psm, st, tb, hist_ids, n_table, U, wk, w2, B,
@@ -1536,7 +1915,7 @@ extern "C" int nrk_din_attn_bwd_params(const void* table, const int32_t* hist_id
   }
   const size_t nout = 2 * (size_t)A * d + 2 * (size_t)A + 1;
   hipLaunchKernelGGL(din_bwd_reduce_params_kernel, dim3((unsigned)cdiv((int64_t)nout, 64)), dim3(512), 0, st, slabs,
-                     grid, A, d, d, gW1, gb1, gw2, gb2);
+                     grid, A, d, d, gW1, gb1, gw2, gb2, qpart, qpart ? DWQ_KC : 0);
   NRK_CHECK_LAUNCH("din_bwd_reduce_params_kernel");
   return NRK_OK;
 }

@@ -359,6 +359,8 @@ __global__ __launch_bounds__(256) void head_bwd2(HeadArgs a) {
   float* i2 = m2 + F2;
   float* sb2 = i2 + F2;  // sum dh2 over the batch
   float* sg2 = sb2 + F2; // sum dh2*xhat2
+  float* w2s = sg2 + F2; // fc2 weight [F2][F]
+  for (int e = threadIdx.x; e < F2 * F; e += 256) w2s[e] = a.p.fc2_w[e];
   const int64_t r0 = (int64_t)blockIdx.x * HR;
   load_stat(a.stat1, F, m1, i1);
   load_stat(a.stat2, F2, m2, i2);
@@ -406,7 +408,7 @@ __global__ __launch_bounds__(256) void head_bwd2(HeadArgs a) {
   for (int e = threadIdx.x; e < HR * F; e += 256) {
     const int r = e / F, j = e % F;
     float s = 0.f;
-    s = dot4(da2 + r * F2, 1, a.p.fc2_w + j, F, F2, s);
+    s = dot4(da2 + r * F2, 1, w2s + j, F, F2, s);
     dh1[e] = s;
     a.dh1[(r0 + r) * F + j] = s;
   }
@@ -929,9 +931,15 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g,
                                                     float* __restrict__ step) {
   __shared__ double red[256];
   double s = 0.0;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const double v = g[i];
-    s += v * v;
+  for (int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x; i0 < n; i0 += (int64_t)gridDim.x * 256 * 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int64_t i = i0 + (int64_t)u * gridDim.x * 256;
+      v[u] = i < n ? g[i] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += (double)v[u] * v[u];
   }
   red[threadIdx.x] = s;
   __syncthreads();
@@ -950,12 +958,15 @@ __global__ __launch_bounds__(256) void clip_adam_kernel(float* __restrict__ p, f
                                                         const float* __restrict__ step, float lr, float beta1,
                                                         float beta2, float eps, float wd, float max_norm) {
   __shared__ float s_coef;
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 64) {  // fixed-order sum of the partials: lane-strided, then a fixed butterfly
     double t = 0.0;
-    for (int i = 0; i < nparts; ++i) t += part[i];
-    const float norm = (float)sqrt(t);
-    const float c = max_norm / (norm + 1e-6f);
-    s_coef = c < 1.f ? c : 1.f;
+    for (int i = threadIdx.x; i < nparts; i += 64) t += part[i];
+    t = wave_sum(t);
+    if (threadIdx.x == 0) {
+      const float norm = (float)sqrt(t);
+      const float c = max_norm / (norm + 1e-6f);
+      s_coef = c < 1.f ? c : 1.f;
+    }
   }
   __syncthreads();
   const float coef = s_coef;
@@ -1079,7 +1090,7 @@ extern "C" int nrk_din_head_train(const float* q, const float* pooled, int64_t l
   a.nrg0 = nblk < 8 ? nblk : 8;
   const size_t lds2_ = ((size_t)HR * F + F2 * F + 2 * F + HR * F2) * 4;
   const size_t lds3_ = ((size_t)2 * HR * F2 + 2 * F2 + 2 * HR) * 4;
-  const size_t lds4_ = ((size_t)3 * HR * F + HR * F2 + 2 * F + 4 * F2) * 4;
+  const size_t lds4_ = ((size_t)3 * HR * F + HR * F2 + 2 * F + 4 * F2 + F2 * F) * 4;
   if (a.fast) {
     const size_t lf1 = ((size_t)2 * D2 + (size_t)(HR + HF) * (D2 + 4) + 4 * HR * HF + HR * (HF + 1)) * 4;
     const size_t lb1 = ((size_t)2 * D2 + (size_t)HR * (D2 + 4) + HR * (HF + 1) + 4 * HF) * 4;
@@ -1098,7 +1109,7 @@ extern "C" int nrk_din_head_train(const float* q, const float* pooled, int64_t l
   const size_t lds1 = ((size_t)(HR + F) * (D2 + 1) + 2 * D2 + HR * F) * 4;
   const size_t lds2 = ((size_t)HR * F + F2 * F + 2 * F + HR * F2) * 4;
   const size_t lds3 = ((size_t)2 * HR * F2 + 2 * F2 + 2 * HR) * 4;
-  const size_t lds4 = ((size_t)3 * HR * F + HR * F2 + 2 * F + 4 * F2) * 4;
+  const size_t lds4 = ((size_t)3 * HR * F + HR * F2 + 2 * F + 4 * F2 + F2 * F) * 4;
   const size_t lds5 = ((size_t)(HR + F) * (D2 + 1) + HR * F + 2 * D2 + 4 * F) * 4;
   auto colsum = [&](const double* part, int stride, double* out) {
     hipLaunchKernelGGL(colsum_kernel<double>, dim3((unsigned)cdiv(stride, 32)), dim3(256), 0, st, part, nblk, stride,
@@ -1147,10 +1158,12 @@ extern "C" int nrk_clip_adam(float* params, float* grads, float* exp_avg, float*
   hipStream_t st = (hipStream_t)stream;
   int nb = (int)cdiv(n, 256);
   if (nb > 256) nb = 256;
+  int ns = (int)cdiv(n, 256 * 8);  // sumsq: 8 loads in flight per thread, few partials
+  if (ns > 256) ns = 256;
   double* part = static_cast<double*>(ws);
-  hipLaunchKernelGGL(sumsq_kernel, dim3(nb), dim3(256), 0, st, grads, n, part, step);
+  hipLaunchKernelGGL(sumsq_kernel, dim3(ns), dim3(256), 0, st, grads, n, part, step);
   NRK_CHECK_LAUNCH("sumsq_kernel");
-  hipLaunchKernelGGL(clip_adam_kernel, dim3(nb), dim3(256), 0, st, params, grads, exp_avg, exp_avg_sq, n, part, nb,
+  hipLaunchKernelGGL(clip_adam_kernel, dim3(nb), dim3(256), 0, st, params, grads, exp_avg, exp_avg_sq, n, part, ns,
                      step, lr, beta1, beta2, eps, weight_decay, max_norm);
   NRK_CHECK_LAUNCH("clip_adam_kernel");
   return NRK_OK;

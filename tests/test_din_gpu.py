@@ -225,12 +225,14 @@ def _setup_fused(p_drop, B=512, n_items=5000, d=64, L=20, seed=3):
     return dev, table, hist, tgt, lab, ma, mb
 
 
-def test_fused_train_step_matches_eager(gpu):
+@pytest.mark.parametrize("d,L", [(64, 20), (128, 50), (64, 64)])
+def test_fused_train_step_matches_eager(gpu, d, L):
     """FusedTrainStep (head + clip + Adam fused kernels, one HIP graph) == the
-    eager torch loop (dropout 0): losses, parameters and BN running stats."""
+    eager torch loop (dropout 0): losses, parameters and BN running stats.
+    (128, 50) and (64, 64) run the 8-wave attention backward + dW1q kernel."""
     from newsrecommend_amd.din import FusedTrainStep
 
-    dev, table, hist, tgt, lab, ma, mb = _setup_fused(0.0)
+    dev, table, hist, tgt, lab, ma, mb = _setup_fused(0.0, d=d, L=L)
     crit = torch.nn.BCEWithLogitsLoss()
     B = 512
     fused = FusedTrainStep(ma, table, hist, tgt, lab, B, lr=1e-3, weight_decay=1e-4, clip=1.0)
