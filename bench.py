@@ -448,17 +448,23 @@ def bench_din(args, rank, world, dev):
         loss = step(args.warmup + s)
     barrier(world)
     el = max_over_ranks(time.perf_counter() - t0, world, dev)
-    # attention kernel times: a few extra eager steps with event brackets
+    # attention kernel times: a few extra steps of the same path, outside the
+    # graph, with HIP events on the launch stream around the two attention calls
     with KernelTimer() as kt:
-        for s in range(3):
-            lg = model.forward_ids(table, tgt[perm[:B]], hist[perm[:B]])
-            crit(lg, lab[perm[:B]]).backward()
+        for s in range(4):
+            if fused:
+                trainer.idx.copy_(perm[s * B:(s + 1) * B])
+                trainer._body()
+            else:
+                lg = model.forward_ids(table, tgt[perm[:B]], hist[perm[:B]])
+                crit(lg, lab[perm[:B]]).backward()
         torch.cuda.synchronize()
-    model.zero_grad(set_to_none=True)
     sps = B * args.steps * world / el
-    fwd_ms, bwd_ms = kt.mean_ms("fwd"), kt.mean_ms("bwd")
-    fwd_bytes = B * (L * d * 2 + 4 * L + 4 * A + 4 * d + 4 * L)
-    bwd_bytes = B * (L * d * 2 + 4 * L + 4 * A + 4 * d + 4 * L + 4 * A)
+    fwd_ms, bwd_ms = kt.mean_ms("fwd", skip=1), kt.mean_ms("bwd", skip=1)
+    # algorithmic bytes per sample: history ids + bf16 key rows, the U row and
+    # outputs (fwd: pooled, alpha); bwd adds dpooled, alpha, q and the dU row
+    fwd_bytes = B * (4 * L + L * d * 2 + 4 * A + 4 * d + 4 * L)
+    bwd_bytes = B * (4 * L + L * d * 2 + 4 * A + 4 * d + 4 * L + 4 * d + 2 * 4 * A)
     fwd_gbs = fwd_bytes / (fwd_ms * 1e-3) / 1e9
     bwd_gbs = bwd_bytes / (bwd_ms * 1e-3) / 1e9
     out = {
@@ -469,7 +475,7 @@ def bench_din(args, rank, world, dev):
                    "step": ("fused head/optimizer kernels, one hip graph" if graphed else
                             "fused head/optimizer kernels + RCCL grad all_reduce") if fused else "eager torch"},
         "final_loss": float(loss.reshape(-1)[0].item()),
-        "kernels_ms": {"attn_fwd": fwd_ms, "attn_bwd+reduce": bwd_ms},
+        "kernels_ms": {"attn_fwd": fwd_ms, "attn_bwd (deep8 + dwq + reduce)" if fused else "attn_bwd+reduce": bwd_ms},
         "roofline_fwd": {"bound": "hbm", "achieved": fwd_gbs, "peak": HBM_GBS, "unit": "GB/s",
                          "frac": fwd_gbs / HBM_GBS, "traffic": None,
                          "algorithmic": f"{fwd_bytes // B} B/sample x {B} samples"},
@@ -477,9 +483,30 @@ def bench_din(args, rank, world, dev):
                          "frac": bwd_gbs / HBM_GBS, "traffic": None,
                          "algorithmic": f"{bwd_bytes // B} B/sample x {B} samples"},
     }
+    if fused and world == 1 and args.din_sweep:
+        out["batch_sweep"] = {str(bs): _din_rate(table, hist, tgt, lab, d, A, F, bs, dev) for bs in (16384, 65536)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = _cpu_din(args, n_items, L, d, A, F)
     return out
+
+
+def _din_rate(table, hist, tgt, lab, d, A, F, B, dev, steps=10):
+    """samples/s of the graphed fused train step at batch B (fresh model)."""
+    from newsrecommend_amd.din import DIN, FusedTrainStep
+
+    torch.manual_seed(43)
+    m = DIN(d, A, F, 0.36).to(dev)
+    tr = FusedTrainStep(m, table, hist, tgt, lab, B, lr=1.62e-3, weight_decay=8.96e-5, clip=1.0)
+    perm = torch.randperm(hist.shape[0], device=dev)
+    nb = hist.shape[0] // B
+    for s in range(3):
+        tr.step(perm[(s % nb) * B:(s % nb + 1) * B])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(steps):
+        tr.step(perm[(s % nb) * B:(s % nb + 1) * B])
+    torch.cuda.synchronize()
+    return B * steps / (time.perf_counter() - t0)
 
 
 def _cpu_din(args, n_items, L, d, A, F):
@@ -538,6 +565,7 @@ def main():
     ap.add_argument("--din-batch", type=int, default=4096)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--din-eager", action="store_true", help="no HIP-graph capture of the DIN train step")
+    ap.add_argument("--din-sweep", type=int, default=1, help="also report the fused step at B=16384, 65536")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 

@@ -160,6 +160,16 @@ int nrk_din_batch(const int64_t* idx, int32_t B, const int32_t* hist_all, const 
                   int32_t dtype, int32_t d, const float* W1, const float* b1, int32_t A, int32_t* hist,
                   float* q, float* y, float* U, void* W1k_bf16, void* stream);
 
+/* DIN attention for re-ranking (DIN.py:166-173: every candidate of a user
+ * attends over the same history): pooled [nU*C][d] f32 for candidates whose
+ * query rows give Uc [nU*C][A] f32 (= q W1[:, :d]^T + b1, caller GEMM), users'
+ * history ids hist [nU][L] int32 (-1 = zero row), table [N][d] bf16, W1k
+ * [A][d] bf16 = W1[:, d:], w2 [A].  P = K W1k^T is formed once per user.
+ * d in {64, 128, 256}, L <= 64. */
+int nrk_din_rerank_attn(const void* table, int64_t n_table, int32_t dtype, const int32_t* hist,
+                        int32_t nU, int32_t L, const float* Uc, int32_t C, int32_t d,
+                        const void* W1k_bf16, const float* w2, int32_t A, float* pooled, void* stream);
+
 /* ------------------------------------------------------ inverted lists --
  * faiss Clustering / IndexIVFFlat building blocks (Retrieval.py:11-23).
  *

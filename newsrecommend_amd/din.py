@@ -535,18 +535,22 @@ class FusedTrainStep:
             self.hist_all.shape[0], L, _lib.ptr(self.table), N, dt, d, _lib.ptr(W1), _lib.ptr(b1), A,
             _lib.ptr(self.hist_b), _lib.ptr(self.q_b), _lib.ptr(self.y_b), _lib.ptr(self.U_b), _lib.ptr(self.W1k_b),
             st), "din_batch")
+        t0 = KernelTimer.mark("fwd")
         _lib.check(L_.nrk_din_attn_fwd(
             _lib.ptr(self.table), _lib.ptr(self.hist_b), N, dt, _lib.ptr(self.U_b), _lib.ptr(self.W1k_b), _lib.ptr(w2),
             0.0, B, L, d, A, _lib.ptr(self.pooled), _lib.ptr(self.alpha), st), "din_attn_fwd")
+        KernelTimer.push("fwd", t0)
         _lib.check(L_.nrk_din_head_train(
             _lib.ptr(self.q_b), _lib.ptr(self.pooled), d, _lib.ptr(self.y_b), B, d, self.F, 0.1, 1e-5, self.p_drop,
             self.seed, _lib.ptr(self.step_t), ctypes.byref(self.hp), _lib.ptr(self.logits), _lib.ptr(self.loss),
             _lib.ptr(self.dpooled), _lib.ptr(self.ws_head), self.ws_head.numel(), st), "din_head_train")
+        t0 = KernelTimer.mark("bwd")
         _lib.check(L_.nrk_din_attn_bwd_params(
             _lib.ptr(self.table), _lib.ptr(self.hist_b), N, dt, _lib.ptr(self.q_b), _lib.ptr(self.U_b),
             _lib.ptr(self.W1k_b), _lib.ptr(w2), B, L, d, A, _lib.ptr(self.dpooled), _lib.ptr(self.alpha),
             _lib.ptr(W1.grad), _lib.ptr(b1.grad), _lib.ptr(w2.grad), _lib.ptr(m.attn.attn[2].bias.grad), None,
             _lib.ptr(self.ws_attn), self.ws_attn.numel(), st), "din_attn_bwd_params")
+        KernelTimer.push("bwd", t0)
         if self.grad_hook is not None:
             self.grad_hook(self.G)
         _lib.check(L_.nrk_clip_adam(

@@ -59,16 +59,51 @@ def pad_candidates(cand_lists, id_to_row: dict | None = None, device=None):
     return t, t >= 0
 
 
+def _rerank_shared(model, table, hist_rows, cand_rows, batch_samples):
+    """Shared-history path: U = q W1q^T + b1 for all candidates (one GEMM),
+    nrk_din_rerank_attn (P = K W1k^T once per user), the eval-mode head."""
+    from . import _lib
+    from .din import gather_rows
+
+    U, C = cand_rows.shape
+    L = hist_rows.shape[1]
+    d = table.shape[1]
+    W1, b1 = model.attn.attn[0].weight, model.attn.attn[0].bias
+    A = W1.shape[0]
+    W1k = W1[:, d:].to(torch.bfloat16).contiguous()
+    w2 = model.attn.attn[2].weight.reshape(-1).contiguous()
+    out = torch.empty((U, C), dtype=torch.float32, device=table.device)
+    ub = max(1, batch_samples // max(C, 1))
+    for lo in range(0, U, ub):
+        hi = min(U, lo + ub)
+        cr = cand_rows[lo:hi].reshape(-1).to(torch.int32).contiguous()
+        q = gather_rows(table, cr)
+        Uc = torch.addmm(b1, q, W1[:, :d].t())
+        pooled = torch.empty_like(q)
+        hr = hist_rows[lo:hi].to(torch.int32).contiguous()
+        _lib.check(_lib.load().nrk_din_rerank_attn(
+            _lib.ptr(table), table.shape[0], _lib.NRK_DTYPE_BF16, _lib.ptr(hr), hi - lo, L, _lib.ptr(Uc), C, d,
+            _lib.ptr(W1k), _lib.ptr(w2), A, _lib.ptr(pooled), _lib.stream(table.device)), "din_rerank_attn")
+        lg = model.fc(torch.cat([q, pooled], dim=1)).view(hi - lo, C)
+        out[lo:hi] = torch.where(cand_rows[lo:hi] >= 0, lg, torch.full_like(lg, -float("inf")))
+    return out
+
+
 @torch.no_grad()
 def rerank(model, table: torch.Tensor, hist_rows: torch.Tensor, cand_rows: torch.Tensor,
-           batch_samples: int = 1 << 18) -> torch.Tensor:
+           batch_samples: int = 1 << 18, shared: bool = True) -> torch.Tensor:
     """DIN logits (U, C) for candidate rows (U, C) (-1 = padding -> -inf) of
     users with history rows (U, L) (-1 = padding), all rows of `table` on the
     device.  Eval-mode BatchNorm is row-independent, so one forward over many
-    users equals the reference's per-user forwards."""
+    users equals the reference's per-user forwards.  With a bf16 table
+    (d in {64, 128, 256}, L <= 64) the attention runs shared per user
+    (nrk_din_rerank_attn); otherwise every candidate is a DIN sample."""
     model.eval()
     U, C = cand_rows.shape
     L = hist_rows.shape[1]
+    if (shared and table.dtype == torch.bfloat16 and table.shape[1] in (64, 128, 256) and L <= 64
+            and model.attn.attn[0].weight.shape[1] == 2 * table.shape[1]):
+        return _rerank_shared(model, table, hist_rows, cand_rows, batch_samples)
     out = torch.empty((U, C), dtype=torch.float32, device=table.device)
     ub = max(1, batch_samples // max(C, 1))
     for lo in range(0, U, ub):

@@ -97,3 +97,35 @@ def test_retrieve_and_rerank_end_to_end(gpu):
             ref = m(T[c], keys.expand(len(c), -1, -1)).view(-1)
             torch.testing.assert_close(logits[u][cand[u] >= 0], ref, atol=1e-5, rtol=1e-5)
     assert nd.shape == (U,) and top.shape == (U, 5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d,L,C", [(256, 50, 201), (64, 20, 37), (128, 64, 70)])
+def test_rerank_shared_history_matches_per_candidate(d, L, C):
+    """nrk_din_rerank_attn (P = K W1k^T once per user) == every candidate as
+    its own DIN sample (the generic attention kernel), eval mode, bf16 table;
+    padded histories and padded candidates included."""
+    from newsrecommend_amd.din import DIN
+    from newsrecommend_amd.pipeline import rerank
+
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(5)
+    N, U = 5000, 37
+    table = (torch.randn((N, d), generator=g, device=dev) * 0.5).to(torch.bfloat16)
+    hist = torch.randint(0, N, (U, L), generator=g, device=dev, dtype=torch.int32)
+    lens = torch.randint(1, L + 1, (U,), generator=g, device=dev)
+    hist = torch.where(torch.arange(L, device=dev)[None] < lens[:, None], hist, torch.full_like(hist, -1))
+    cand = torch.randint(0, N, (U, C), generator=g, device=dev, dtype=torch.int32)
+    cand[:, -3:] = -1
+    torch.manual_seed(0)
+    model = DIN(d, 128, 32, 0.0).to(dev).eval()
+    with torch.no_grad():  # non-trivial BN statistics
+        for bn in (model.fc[0], model.fc[4], model.fc[8]):
+            bn.running_mean.uniform_(-0.2, 0.2)
+            bn.running_var.uniform_(0.5, 1.5)
+    a = rerank(model, table, hist, cand, shared=True)
+    b = rerank(model, table, hist, cand, shared=False)
+    fin = torch.isfinite(b)
+    assert torch.equal(fin, torch.isfinite(a))
+    err = (a[fin] - b[fin]).abs().max().item()
+    assert err < 2e-3 * max(1.0, b[fin].abs().max().item()), err
