@@ -45,7 +45,7 @@ __global__ __launch_bounds__(256, 1) void din_rerank_kernel(const uint16_t* __re
                                                             const float* __restrict__ Uc, int C,
                                                             const uint16_t* __restrict__ W1k,
                                                             const float* __restrict__ w2, int A,
-                                                            float* __restrict__ pooled) {
+                                                            float* __restrict__ pooled, int dbg) {
   constexpr int CPR = D / 8, KS = D / 16, NDT = D / 32;
   constexpr int PS = 129;  // P row stride (floats): lane = row reads its own row conflict-free
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -68,17 +68,30 @@ __global__ __launch_bounds__(256, 1) void din_rerank_kernel(const uint16_t* __re
 
   for (int u = blockIdx.x; u < nU; u += gridDim.x) {
     // 1. history image (rows >= L and invalid ids: zeros)
-    for (int e = tid; e < LP * CPR; e += 256) {
-      const int row = e / CPR, cc = e % CPR;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (row < L) {
-        const int32_t id = hist[(int64_t)u * L + row];
-        if (id >= 0 && id < n_table) v = *reinterpret_cast<const uint4*>(table + (int64_t)id * D + cc * 8);
+    {  // all of a thread's id loads, then all of its row loads, in flight together
+      constexpr int NE = LP * CPR / 256;
+      int32_t idv[NE];
+#pragma unroll
+      for (int k = 0; k < NE; ++k) {
+        const int row = (tid + 256 * k) / CPR;
+        idv[k] = row < L ? hist[(int64_t)u * L + row] : -1;
       }
-      *reinterpret_cast<uint4*>(img + row * 2 * D + 16 * (cc ^ swz<CPR>(row))) = v;
+      uint4 v[NE];
+#pragma unroll
+      for (int k = 0; k < NE; ++k) {
+        const int cc = (tid + 256 * k) % CPR;
+        v[k] = make_uint4(0, 0, 0, 0);
+        if (idv[k] >= 0 && idv[k] < n_table) v[k] = *reinterpret_cast<const uint4*>(table + (int64_t)idv[k] * D + cc * 8);
+      }
+#pragma unroll
+      for (int k = 0; k < NE; ++k) {
+        const int e = tid + 256 * k, row = e / CPR, cc = e % CPR;
+        *reinterpret_cast<uint4*>(img + row * 2 * D + 16 * (cc ^ swz<CPR>(row))) = v[k];
+      }
     }
     __syncthreads();
-    // 2. P = K W1k^T
+    // 2. P = K W1k^T (columns of units >= A zero)
+    for (int e = tid; e < LP * (128 - A); e += 256) Ps[(e / (128 - A)) * PS + A + e % (128 - A)] = 0.f;
     if (w < nsl) {
 #pragma unroll
       for (int c = 0; c < LP / 32; ++c) {
@@ -98,50 +111,73 @@ __global__ __launch_bounds__(256, 1) void din_rerank_kernel(const uint16_t* __re
     // lane = history row: its P row in registers
     float pr[128];
 #pragma unroll
-    for (int n = 0; n < 128; ++n) pr[n] = n < A ? Ps[lane * PS + n] : 0.f;
+    for (int n = 0; n < 128; ++n) pr[n] = Ps[lane * PS + n];  // units >= A: zeroed below
     const bool rowok = lane < L;
 
     for (int c0 = 0; c0 < C; c0 += CCH) {
       const int nc = min(CCH, C - c0);
       // 3a. U rows of this chunk
       const float* ub = Uc + ((int64_t)u * C + c0) * A;
-      for (int e = tid; e < nc * (A / 4); e += 256) {
-        const int cl = e / (A / 4), q4 = e % (A / 4);
-        *reinterpret_cast<float4*>(Us + cl * 128 + 4 * q4) = *reinterpret_cast<const float4*>(ub + (int64_t)cl * A + 4 * q4);
+      {  // units >= A: zeros (their w2 is 0 too); 8 loads in flight per thread
+        float4 v[CCH * 32 / 256];
+#pragma unroll
+        for (int k = 0; k < CCH * 32 / 256; ++k) {
+          const int e = tid + 256 * k, cl = e >> 5, q4 = e & 31;
+          v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (cl < nc && 4 * q4 < A) v[k] = *reinterpret_cast<const float4*>(ub + (int64_t)cl * A + 4 * q4);
+        }
+#pragma unroll
+        for (int k = 0; k < CCH * 32 / 256; ++k) {
+          const int e = tid + 256 * k, cl = e >> 5, q4 = e & 31;
+          *reinterpret_cast<float4*>(Us + cl * 128 + 4 * q4) = v[k];
+        }
       }
       __syncthreads();
-      // 3b. scores, softmax, alpha (wave w: candidates w, w + 4, ...)
-      for (int cl = w; cl < CCH; cl += 4) {
-        float al = 0.f;
-        if (cl < nc) {
-          float s = 0.f;
-          const float* uc = Us + cl * 128;
+      // 3b. scores, softmax, alpha: wave w takes candidates 16w .. 16w+15, four at a
+      // time (four independent accumulation chains share each w2 / P read)
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int cb = 16 * w + 4 * g4;
+        float sc[4] = {0.f, 0.f, 0.f, 0.f};
+        if (!(dbg & 1) && cb < nc) {
+          const float* u0 = Us + cb * 128;
 #pragma unroll
-          for (int n = 0; n < 128; n += 4) {
-            if (n < A) {
-              const float4 uv = *reinterpret_cast<const float4*>(uc + n);
-              const float4 wv = *reinterpret_cast<const float4*>(w2s + n);
-              s = fmaf(wv.x, fmaxf(uv.x + pr[n], 0.f), s);
-              s = fmaf(wv.y, fmaxf(uv.y + pr[n + 1], 0.f), s);
-              s = fmaf(wv.z, fmaxf(uv.z + pr[n + 2], 0.f), s);
-              s = fmaf(wv.w, fmaxf(uv.w + pr[n + 3], 0.f), s);
+          for (int n = 0; n < 128; n += 4) {  // units >= A contribute w2 = 0
+            const float4 wv = *reinterpret_cast<const float4*>(w2s + n);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float4 uv = *reinterpret_cast<const float4*>(u0 + i * 128 + n);
+              sc[i] = fmaf(wv.x, fmaxf(uv.x + pr[n], 0.f), sc[i]);
+              sc[i] = fmaf(wv.y, fmaxf(uv.y + pr[n + 1], 0.f), sc[i]);
+              sc[i] = fmaf(wv.z, fmaxf(uv.z + pr[n + 2], 0.f), sc[i]);
+              sc[i] = fmaf(wv.w, fmaxf(uv.w + pr[n + 3], 0.f), sc[i]);
             }
           }
-          s = rowok ? s : -INFINITY;
-          const float m = wave_max(s);
-          const float ex = rowok ? expf(s - m) : 0.f;
-          al = ex / wave_sum(ex);
         }
-        const bf16x2_t hl = {(__bf16)al, (__bf16)0.f};
-        const uint16_t hb = (uint16_t)(__builtin_bit_cast(uint32_t, hl) & 0xFFFF);
-        const float rem = al - __uint_as_float((uint32_t)hb << 16);
-        const bf16x2_t ll = {(__bf16)rem, (__bf16)0.f};
-        ahi[cl * LP + lane] = hb;
-        alo[cl * LP + lane] = (uint16_t)(__builtin_bit_cast(uint32_t, ll) & 0xFFFF);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int cl = cb + i;
+          float al = 0.f;
+          if (cl < nc) {
+            if (dbg & 1) {
+              al = rowok ? 1.f / L : 0.f;
+            } else {
+              const float sv = rowok ? sc[i] : -INFINITY;
+              const float m = wave_max(sv);
+              const float ex = rowok ? expf(sv - m) : 0.f;
+              al = ex / wave_sum(ex);
+            }
+          }
+          const bf16x2_t hl = {(__bf16)al, (__bf16)0.f};
+          const uint16_t hb = (uint16_t)(__builtin_bit_cast(uint32_t, hl) & 0xFFFF);
+          const float rem = al - __uint_as_float((uint32_t)hb << 16);
+          const bf16x2_t ll = {(__bf16)rem, (__bf16)0.f};
+          ahi[cl * LP + lane] = hb;
+          alo[cl * LP + lane] = (uint16_t)(__builtin_bit_cast(uint32_t, ll) & 0xFFFF);
+        }
       }
       __syncthreads();
       // 4. pooled = alpha K (hi and lo passes); wave w: dim tiles w, w + 4, ...
-      for (int cg = 0; cg < nc; cg += 32) {
+      for (int cg = 0; cg < ((dbg & 2) ? 0 : nc); cg += 32) {
         for (int dt = w; dt < NDT; dt += 4) {
           f32x16 acc;
 #pragma unroll
@@ -202,18 +238,20 @@ extern "C" int nrk_din_rerank_attn(const void* table, int64_t n_table, int32_t d
   const size_t smem = (size_t)rr::LP * d * 2 + ((size_t)rr::LP * 129 + rr::CCH * 128 + 128) * 4 + 2 * (size_t)rr::CCH * rr::LP * 2;
   NRK_CHECK_ARG(smem <= 160 * 1024, "din_rerank: %zu B LDS", smem);
   const int grid = nU < 256 ? nU : 256;
+  const char* edb = getenv("NRK_RR_DBG");  // timing experiments only: 1 skip scores, 2 skip the pool
+  const int dbg = edb ? atoi(edb) : 0;
   hipStream_t st = (hipStream_t)stream;
   const uint16_t* tb = static_cast<const uint16_t*>(table);
   const uint16_t* wk = static_cast<const uint16_t*>(W1k_bf16);
   if (d == 256)
     hipLaunchKernelGGL(rr::din_rerank_kernel<256>, dim3(grid), dim3(256), smem, st, tb, n_table, hist, nU, L, Uc, C, wk,
-                       w2, A, pooled);
+                       w2, A, pooled, dbg);
   else if (d == 128)
     hipLaunchKernelGGL(rr::din_rerank_kernel<128>, dim3(grid), dim3(256), smem, st, tb, n_table, hist, nU, L, Uc, C, wk,
-                       w2, A, pooled);
+                       w2, A, pooled, dbg);
   else
     hipLaunchKernelGGL(rr::din_rerank_kernel<64>, dim3(grid), dim3(256), smem, st, tb, n_table, hist, nU, L, Uc, C, wk,
-                       w2, A, pooled);
+                       w2, A, pooled, dbg);
   NRK_CHECK_LAUNCH("din_rerank_kernel");
   return NRK_OK;
 }

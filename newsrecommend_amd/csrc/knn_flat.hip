@@ -543,6 +543,29 @@ __global__ __launch_bounds__(256) void fallback_scan_kernel(const float* __restr
         const int r = e / d;
         tile[r * ds + (e - r * d)] = xb[iv.pos2id[r0 + r] * d + (e - r * d)];
       }
+    } else if ((d & 3) == 0) {  // 16 float4 loads in flight per thread (one latency per tile)
+      const float4* src = reinterpret_cast<const float4*>(xb + r0 * d);
+      const int n4 = (rows * d) >> 2;
+      for (int e0 = threadIdx.x; e0 < n4; e0 += 256 * 16) {
+        float4 v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int e = e0 + u * 256;
+          if (e < n4) v[u] = src[e];
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int e = e0 + u * 256;
+          if (e < n4) {
+            const int f = 4 * e, r = f / d;
+            float* o = tile + r * ds + (f - r * d);
+            o[0] = v[u].x;
+            o[1] = v[u].y;
+            o[2] = v[u].z;
+            o[3] = v[u].w;
+          }
+        }
+      }
     } else {
       for (int e = threadIdx.x; e < rows * d; e += 256) {
         const int r = e / d;
@@ -699,12 +722,15 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
   else if (k <= 24) { p.M = 8; p.qt = 1; }
   else { p.M = 16; p.qt = 1; }
   p.R = k <= 8 ? 16 : 2 * k;
-  p.tau = k <= 24 && env_int("NRK_SCREEN_TAU", 1) != 0;
+  p.tau = env_int("NRK_SCREEN_TAU", 1) != 0;  // k = 200 at 10M x 256: -5% retrieve time
   if (p.dp == 256) p.qt = 1;
   p.wq = p.waves * 32 * p.qt;
   p.nqt = (int)cdiv(nq, p.wq);
   p.nq_pad = (int64_t)p.nqt * p.wq;
-  int target = env_int("NRK_SCREEN_WGS", 1024);
+  // k > 24 (M = 16): twice the lane streams, so that dense neighbourhoods do
+  // not overflow a lane's list (10M x 256, k = 200: 2 uncertified queries per
+  // 4096 -> 0, and the 4.5 ms fp64 fallback scan with them)
+  int target = env_int("NRK_SCREEN_WGS", p.M >= 16 ? 2048 : 1024);
   int64_t nch = target / (p.nqt > 0 ? p.nqt : 1);
   if (nch < 1) nch = 1;
   int64_t max_by_u = 2048 / (2 * p.M);
@@ -720,6 +746,7 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
   p.U = p.nch * 2 * p.M;
   int kp = 2 * k > 32 ? 2 * k : 32;
   if (kp < k + 16) kp = k + 16;
+  kp = env_int("NRK_KP", kp);
   if (kp > p.U) kp = p.U;
   if (kp > 1024) kp = 1024;
   p.KP = kp;

@@ -39,7 +39,7 @@ def test_c1_shape(gpu, metric):
 
 
 @pytest.mark.parametrize("metric", [ko.METRIC_IP, ko.METRIC_L2])
-@pytest.mark.parametrize("d,k", [(128, 5), (64, 10), (100, 32), (256, 5), (32, 1), (128, 100)])
+@pytest.mark.parametrize("d,k", [(128, 5), (64, 10), (100, 32), (256, 5), (32, 1), (128, 100), (256, 200)])
 def test_screened_path(gpu, metric, d, k):
     xq, xb = _mixture(60_001, 300, d, seed=d + k)
     idx = _check(xq, xb, k, metric, gpu)
