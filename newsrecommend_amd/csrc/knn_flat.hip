@@ -721,6 +721,10 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
   if (k <= 8) { p.M = 4; p.qt = 2; }
   else if (k <= 24) { p.M = 8; p.qt = 1; }
   else { p.M = 16; p.qt = 1; }
+  // DP = 256 with M = 16 (k > 24, e.g. configs[4]'s 10M x 256, k = 200): 8-wave
+  // workgroups, 256 queries per corpus pass; a chunk far larger than L2 is
+  // then re-read by half as many query tiles
+  if (p.dp == 256 && p.M == 16 && env_int("NRK_SCREEN_W8", 1)) p.waves = 8;
   p.R = k <= 8 ? 16 : 2 * k;
   p.tau = env_int("NRK_SCREEN_TAU", 1) != 0;  // k = 200 at 10M x 256: -5% retrieve time
   if (p.dp == 256) p.qt = 1;
@@ -910,7 +914,7 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
                      p.dp, qh, qmeta);
   NRK_CHECK_LAUNCH("query_prepare_kernel");
   if (p.tau) {
-    screen_fn pf = pick_screen(p.dp, p.qt, p.M, l2 != 0, 1);
+    screen_fn pf = p.waves == 8 ? pick_screen_dp256_w8(l2 != 0, 1) : pick_screen(p.dp, p.qt, p.M, l2 != 0, 1);
     if (!pf) return fail(NRK_EUNSUPPORTED, "knn_flat: no pre-pass kernel for dp=%d", p.dp);
     hipLaunchKernelGGL(pf, dim3(p.nqt * p.nch_pre), dim3(p.waves * 64), 0, st, qh, xb_bf16, xb_meta, nq, nb,
                        p.chunk_pre, p.nch_pre, p.nqt, p.tstride, nullptr, nullptr, pre, nullptr, IvfScreen{});
@@ -920,7 +924,7 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
     NRK_CHECK_LAUNCH("tau_select_kernel");
   }
 
-  screen_fn fn = pick_screen(p.dp, p.qt, p.M, l2 != 0, 0);
+  screen_fn fn = p.waves == 8 ? pick_screen_dp256_w8(l2 != 0, 0) : pick_screen(p.dp, p.qt, p.M, l2 != 0, 0);
   if (!fn) return fail(NRK_EUNSUPPORTED, "knn_flat: no screen kernel for dp=%d", p.dp);
   const int nblk = p.nqt * p.nch;
   mark(1);

@@ -427,6 +427,9 @@ screen_fn pick_screen_dp32(int qt, int M, bool l2, int mode);
 screen_fn pick_screen_dp64(int qt, int M, bool l2, int mode);
 screen_fn pick_screen_dp128(int qt, int M, bool l2, int mode);
 screen_fn pick_screen_dp256(int qt, int M, bool l2, int mode);
+// DP = 256, QT = 1, 8 waves (256 queries per workgroup and corpus pass):
+// the flat main pass with M = 16 (mode 0) and its pre-pass (mode 1)
+screen_fn pick_screen_dp256_w8(bool l2, int mode);
 
 inline screen_fn pick_screen(int dp, int qt, int M, bool l2, int mode) {
   switch (dp) {

@@ -47,4 +47,10 @@ screen_fn pick_screen_dp256(int qt, int M, bool l2, int mode) {
   return l2 ? pick1<256, true>(qt, M, mode) : pick1<256, false>(qt, M, mode);
 }
 
+screen_fn pick_screen_dp256_w8(bool l2, int mode) {
+  if (mode == 1)
+    return l2 ? screen_kernel<256, 1, 1, 8, true, 1, 0, false> : screen_kernel<256, 1, 1, 8, false, 1, 0, false>;
+  return l2 ? screen_kernel<256, 1, 16, 8, true, 0, 0, false> : screen_kernel<256, 1, 16, 8, false, 0, 0, false>;
+}
+
 }  // namespace nrk
