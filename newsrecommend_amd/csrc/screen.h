@@ -125,7 +125,14 @@ struct CollectLds {
 };
 struct NoLds {};
 
-template <int DP, int QT, int M, int WAVES, bool L2, int MODE, int EPI = 0, bool AFRAG_GROUP = true>
+// DEFER (flat modes 0 and 1): the epilogue of sub-tile s runs while the MFMA
+// chain of sub-tile s+1 is in flight.  Two accumulator sets alternate (A: even
+// sub-tiles, B: odd ones, whose epilogue falls into the next tile); the
+// straight-line part of the epilogue (L2 correction, max tree, threshold
+// test) is scheduled between the MFMAs, only the rare list insertions follow
+// the chain.  Without it every chain's results are waited for and reduced
+// before the next chain issues (the MFMA-only ablation, EPI 2, is 30 % faster).
+template <int DP, int QT, int M, int WAVES, bool L2, int MODE, int EPI = 0, bool AFRAG_GROUP = true, bool DEFER = false>
 __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
     const uint16_t* __restrict__ qh, const uint16_t* __restrict__ xbh, const float* __restrict__ xmeta,
     int64_t nq, int64_t nb, int64_t chunk, int nch, int nqt, int tstride, float* __restrict__ part_s,
@@ -139,6 +146,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
   constexpr int KS = DP / 16;
   constexpr int WQ = WAVES * 32 * QT;
   constexpr int BUF = TI * DP + 2 * TI;  // uint16 per buffer: rows + TI float norms
+  static_assert(!DEFER || (MODE <= 1 && EPI == 0), "deferred epilogue: flat modes only");
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BUF];
   __shared__ std::conditional_t<MODE == 3, CollectLds<WQ>, NoLds> cl;
 
@@ -243,12 +251,8 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
     };
 
     // one 64-item tile (buffer index is a compile-time constant: immediate LDS offsets)
-    auto tile = [&](int it, auto buf_c) {
+    auto compute = [&](int it, auto buf_c) {
       constexpr int buf = decltype(buf_c)::value;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();  // tile `it` landed; everyone is done with the other buffer
-      if (it + 1 < ntiles) issue_tile(it + 1, std::integral_constant<int, buf ^ 1>{});
-
       const uint16_t* tl = lds + buf * BUF;
       const float* lnorm = reinterpret_cast<const float*>(tl + TI * DP);
       const int64_t i0 = ibeg + (int64_t)it * tstride * TI;
@@ -362,14 +366,165 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
         else epilogue(std::true_type{});
       }
     };
-
+    // two buffers: tile it+1 in flight while tile it is computed
+    auto tile = [&](int it, auto buf_c) {
+      constexpr int buf = decltype(buf_c)::value;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // tile `it` landed; everyone is done with the other buffer
+      if (it + 1 < ntiles) issue_tile(it + 1, std::integral_constant<int, buf ^ 1>{});
+      compute(it, buf_c);
+    };
+    // ---- deferred epilogue (DEFER): see the comment at the template ----
+    static_assert(!DEFER || TI == 64, "two sub-tiles per tile");
+    f32x16 accA[QT], accB[QT];
+    int64_t baseA = -1, baseB = -1;  // item index of the pending sub-tile's row 0 (-1: nothing pending)
+    int nvA = 0, nvB = 0;            // its rows inside the chunk
+    float pnB[16];                   // L2: norms of sub-tile B's rows (its buffer is refilled before its epilogue)
+    // rows of a pending sub-tile past the chunk (only in a chunk's last tile)
+    auto mask_rows = [&](f32x16 (&pa)[QT], int nv) __attribute__((always_inline)) {
+  #pragma unroll
+      for (int t = 0; t < QT; ++t)
+  #pragma unroll
+        for (int g = 0; g < 16; ++g)
+          if ((g & 3) + 8 * (g >> 2) + 4 * h >= nv) pa[t][g] = -INFINITY;
+    };
+    // straight-line part: L2 scores 2 ip - |x|^2 (in place), 4-row maxima, lane maximum
+    auto tree = [&](f32x16 (&pa)[QT], const float (&n16)[16], float (&m4)[QT][4], float (&m)[QT]) __attribute__((always_inline)) {
+  #pragma unroll
+      for (int t = 0; t < QT; ++t) {
+        if constexpr (L2) {
+  #pragma unroll
+          for (int g = 0; g < 16; ++g) pa[t][g] = fmaf(2.f, pa[t][g], -n16[g]);
+        }
+  #pragma unroll
+        for (int j = 0; j < 4; ++j)
+          m4[t][j] = fmax_ieee(fmax_ieee(pa[t][4 * j], pa[t][4 * j + 1]), fmax_ieee(pa[t][4 * j + 2], pa[t][4 * j + 3]));
+        m[t] = fmax_ieee(fmax_ieee(m4[t][0], m4[t][1]), fmax_ieee(m4[t][2], m4[t][3]));
+      }
+    };
+    // rare part: lane-list insertions (MODE 0) or the lane maximum (MODE 1)
+    auto drain = [&](f32x16 (&pa)[QT], int64_t pbase, const float (&m4)[QT][4], const float (&m)[QT]) __attribute__((always_inline)) {
+      if constexpr (MODE == 1) {
+  #pragma unroll
+        for (int t = 0; t < QT; ++t) ls[t][0] = fmax_ieee(ls[t][0], m[t]);
+        return;
+      }
+      // one test for all query tiles (keeps every tile's max tree ahead of the branch)
+      bool hit = false;
+  #pragma unroll
+      for (int t = 0; t < QT; ++t) hit |= m[t] > fmaxf(ls[t][M], tau[t]);
+      if (!__any(hit)) return;
+  #pragma unroll
+      for (int t = 0; t < QT; ++t) {
+        if (__any(m[t] > fmaxf(ls[t][M], tau[t]))) {
+  #pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (__any(m4[t][j] > fmaxf(ls[t][M], tau[t]))) {
+  #pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const int g = 4 * j + i;
+                const float thr = fmaxf(ls[t][M], tau[t]);
+                if (pa[t][g] > thr) list_insert<M + 1>(ls[t], li[t], pa[t][g], (int)(pbase + i + 8 * j + 4 * h));
+              }
+            }
+          }
+        }
+      }
+    };
+    // one sub-tile: its MFMA chain with the pending sub-tile's straight-line
+    // epilogue scheduled between the MFMAs, then the pending one's rare part
+    auto sub_tile = [&](auto st_c, const uint16_t* tl, const float* lnorm, int64_t i0, int nvalid) __attribute__((always_inline)) {
+      constexpr int st = decltype(st_c)::value;
+      f32x16(&cur)[QT] = st ? accB : accA;
+      f32x16(&pend)[QT] = st ? accA : accB;
+      const int64_t pbase = st ? baseA : baseB;
+      const int pnv = st ? nvA : nvB;
+      const int row = 32 * st + r;
+      const uint16_t* arow = tl + row * DP;
+      const int sw = swz<CPR>(row);
+      bf16x8 af[KS];
+  #pragma unroll
+      for (int s = 0; s < KS; ++s) af[s] = *reinterpret_cast<const bf16x8*>(arow + 8 * ((2 * s + h) ^ sw));
+      if (pbase >= 0 && pnv < 32) mask_rows(pend, pnv);
+      float n16[16];
+      if constexpr (L2) {
+        if constexpr (st == 1) {  // pending A: rows 0..31 of this tile
+  #pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float4 v = *reinterpret_cast<const float4*>(lnorm + 8 * j + 4 * h);
+            n16[4 * j] = v.x; n16[4 * j + 1] = v.y; n16[4 * j + 2] = v.z; n16[4 * j + 3] = v.w;
+          }
+        } else {
+  #pragma unroll
+          for (int g = 0; g < 16; ++g) n16[g] = pnB[g];
+        }
+      }
+      const f32x16 zero = {};
+  #pragma unroll
+      for (int s = 0; s < KS; ++s)
+  #pragma unroll
+        for (int t = 0; t < QT; ++t)
+          cur[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], qf[t][s], s == 0 ? zero : cur[t], 0, 0, 0);
+      float m4[QT][4], m[QT];
+      tree(pend, n16, m4, m);
+  #pragma unroll
+      for (int t = 0; t < QT; ++t) m[t] = pbase >= 0 ? m[t] : -INFINITY;  // nothing pending: drain is a no-op
+      constexpr int NDS = KS + ((L2 && st == 1) ? 4 : 0), VPM = L2 ? 4 : 2;
+      __builtin_amdgcn_sched_group_barrier(0x100, NDS, 0);
+  #pragma unroll
+      for (int i = 0; i < KS * QT; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, VPM, 0);
+      }
+      drain(pend, pbase, m4, m);
+      if constexpr (st == 0) {
+        baseA = i0;
+        nvA = nvalid;
+      } else {
+        baseB = i0 + 32;
+        nvB = nvalid - 32;
+        if constexpr (L2) {
+  #pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float4 v = *reinterpret_cast<const float4*>(lnorm + 32 + 8 * j + 4 * h);
+            pnB[4 * j] = v.x; pnB[4 * j + 1] = v.y; pnB[4 * j + 2] = v.z; pnB[4 * j + 3] = v.w;
+          }
+        }
+      }
+    };
+    auto tile_d = [&](int it, auto buf_c) __attribute__((always_inline)) {
+      constexpr int buf = decltype(buf_c)::value;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // tile `it` landed; everyone is done with the other buffer
+      if (it + 1 < ntiles) issue_tile(it + 1, std::integral_constant<int, buf ^ 1>{});
+      const uint16_t* tl = lds + buf * BUF;
+      const float* lnorm = reinterpret_cast<const float*>(tl + TI * DP);
+      const int64_t i0 = ibeg + (int64_t)it * tstride * TI;
+      const int nvalid = (int)((iend - i0) < TI ? (iend - i0) : TI);
+      sub_tile(std::integral_constant<int, 0>{}, tl, lnorm, i0, nvalid);
+      sub_tile(std::integral_constant<int, 1>{}, tl, lnorm, i0, nvalid);
+    };
     if constexpr (MODE == 3) {
       if (tid == 0) cl.n = 0;  // ordered before any append by the first tile's barrier
     }
-    if (ntiles > 0) issue_tile(0, std::integral_constant<int, 0>{});
-    for (int it = 0; it < ntiles; it += 2) {
-      tile(it, std::integral_constant<int, 0>{});
-      if (it + 1 < ntiles) tile(it + 1, std::integral_constant<int, 1>{});
+    if constexpr (DEFER) {
+      if (ntiles > 0) issue_tile(0, std::integral_constant<int, 0>{});
+      for (int it = 0; it < ntiles; it += 2) {
+        tile_d(it, std::integral_constant<int, 0>{});
+        if (it + 1 < ntiles) tile_d(it + 1, std::integral_constant<int, 1>{});
+      }
+      if (baseB >= 0) {  // the last sub-tile's epilogue
+        if (nvB < 32) mask_rows(accB, nvB);
+        float m4[QT][4], m[QT];
+        tree(accB, pnB, m4, m);
+        drain(accB, baseB, m4, m);
+      }
+    } else {
+      if (ntiles > 0) issue_tile(0, std::integral_constant<int, 0>{});
+      for (int it = 0; it < ntiles; it += 2) {
+        tile(it, std::integral_constant<int, 0>{});
+        if (it + 1 < ntiles) tile(it + 1, std::integral_constant<int, 1>{});
+      }
     }
 
     if constexpr (MODE == 3) {  // flush the staged candidates

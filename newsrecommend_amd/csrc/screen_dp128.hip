@@ -16,6 +16,11 @@ static screen_fn pick3() {
     if (epi == 1) return screen_kernel<DP, QT, M, 4, L2, MODE, 1>;
     if (epi == 2) return screen_kernel<DP, QT, M, 4, L2, MODE, 2>;
   }
+  // flat modes: epilogue deferred into the next MFMA chain (screen.h); not for
+  // L2 with two query tiles or DP = 256 (the extra norm registers spill there)
+  if constexpr (MODE <= 1 && !(L2 && (QT == 2 || DP == 256))) {
+    if (env_int("NRK_SCREEN_DEFER", 1)) return screen_kernel<DP, QT, M, 4, L2, MODE, 0, false, true>;
+  }
   // grouped A-fragment reads: default on for the IVF modes (measured), env override
   const int grp = env_int("NRK_AFRAG_GROUP", -1);
   const bool g = grp < 0 ? (MODE >= 2) : grp != 0;

@@ -59,9 +59,27 @@ def pad_candidates(cand_lists, id_to_row: dict | None = None, device=None):
     return t, t >= 0
 
 
+def _fold_eval_head(fc):
+    """The eval-mode head DIN.py:200-204 (BN -> Linear -> ReLU -> Dropout, twice,
+    then BN -> Linear) with each BatchNorm folded into the Linear after it:
+    Linear(BN(x)) = x (W s)^T + (b + W t), s = gamma / sqrt(var + eps),
+    t = beta - mean s.  Returns [(W', b')] for the three Linears, or None when a
+    BatchNorm has no running statistics (eval then normalises per batch)."""
+    out = []
+    for bn, lin in ((fc[0], fc[1]), (fc[4], fc[5]), (fc[8], fc[9])):
+        if bn.running_mean is None:
+            return None
+        s = bn.weight / torch.sqrt(bn.running_var + bn.eps)
+        t = bn.bias - bn.running_mean * s
+        out.append(((lin.weight * s[None, :]).contiguous(), lin.bias + lin.weight @ t))
+    return out
+
+
 def _rerank_shared(model, table, hist_rows, cand_rows, batch_samples):
     """Shared-history path: U = q W1q^T + b1 for all candidates (one GEMM),
-    nrk_din_rerank_attn (P = K W1k^T once per user), the eval-mode head."""
+    nrk_din_rerank_attn (P = K W1k^T once per user), the eval-mode head with
+    its BatchNorms folded into the Linears (no [q, pooled] concatenation: the
+    first layer is two GEMMs accumulating into one output)."""
     from . import _lib
     from .din import gather_rows
 
@@ -72,6 +90,10 @@ def _rerank_shared(model, table, hist_rows, cand_rows, batch_samples):
     A = W1.shape[0]
     W1k = W1[:, d:].to(torch.bfloat16).contiguous()
     w2 = model.attn.attn[2].weight.reshape(-1).contiguous()
+    head = _fold_eval_head(model.fc)
+    if head is not None:
+        (H1, c1), (H2, c2), (H3, c3) = head
+        H1q, H1p = H1[:, :d].t(), H1[:, d:].t()
     out = torch.empty((U, C), dtype=torch.float32, device=table.device)
     ub = max(1, batch_samples // max(C, 1))
     for lo in range(0, U, ub):
@@ -84,7 +106,11 @@ def _rerank_shared(model, table, hist_rows, cand_rows, batch_samples):
         _lib.check(_lib.load().nrk_din_rerank_attn(
             _lib.ptr(table), table.shape[0], _lib.NRK_DTYPE_BF16, _lib.ptr(hr), hi - lo, L, _lib.ptr(Uc), C, d,
             _lib.ptr(W1k), _lib.ptr(w2), A, _lib.ptr(pooled), _lib.stream(table.device)), "din_rerank_attn")
-        lg = model.fc(torch.cat([q, pooled], dim=1)).view(hi - lo, C)
+        if head is None:
+            lg = model.fc(torch.cat([q, pooled], dim=1)).view(hi - lo, C)
+        else:
+            h1 = torch.addmm(c1, q, H1q).addmm_(pooled, H1p).relu_()
+            lg = torch.addmm(c3, torch.addmm(c2, h1, H2.t()).relu_(), H3.t()).view(hi - lo, C)
         out[lo:hi] = torch.where(cand_rows[lo:hi] >= 0, lg, torch.full_like(lg, -float("inf")))
     return out
 

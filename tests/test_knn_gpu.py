@@ -46,6 +46,18 @@ def test_screened_path(gpu, metric, d, k):
     assert idx.last_fallback is not None
 
 
+@pytest.mark.parametrize("defer", ["0", "1"])
+@pytest.mark.parametrize("metric", [ko.METRIC_IP, ko.METRIC_L2])
+@pytest.mark.parametrize("d,k", [(128, 5), (64, 10), (100, 32), (256, 5), (32, 1)])
+def test_screen_deferred_epilogue(gpu, monkeypatch, defer, metric, d, k):
+    """Both screen epilogues (reduced right after each MFMA chain; deferred into
+    the next chain, with the last sub-tile flushed after the loop) give the
+    oracle's exact results, including the short last tile of each chunk."""
+    monkeypatch.setenv("NRK_SCREEN_DEFER", defer)
+    xq, xb = _mixture(70_003, 300, d, seed=d + k + 1)
+    _check(xq, xb, k, metric, gpu)
+
+
 def test_gaussian_unstructured(gpu):
     rng = np.random.default_rng(7)
     xb = rng.standard_normal((50_000, 128)).astype(np.float32)

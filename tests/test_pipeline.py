@@ -29,6 +29,27 @@ def test_pad_candidates():
     assert mask.sum().item() == 3
 
 
+def test_folded_eval_head_equals_module():
+    """The re-rank head with each eval-mode BatchNorm folded into the next
+    Linear equals DIN.fc (DIN.py:200-204) in eval mode."""
+    from newsrecommend_amd.din import DIN
+    from newsrecommend_amd.pipeline import _fold_eval_head
+
+    torch.manual_seed(0)
+    m = DIN(32, 16, 32, 0.36).eval()
+    with torch.no_grad():
+        for bn in (m.fc[0], m.fc[4], m.fc[8]):
+            bn.running_mean.uniform_(-0.3, 0.3)
+            bn.running_var.uniform_(0.5, 1.5)
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.2, 0.2)
+        x = torch.randn(257, 64)
+        (H1, c1), (H2, c2), (H3, c3) = _fold_eval_head(m.fc)
+        h = torch.relu(x[:, :32] @ H1[:, :32].t() + x[:, 32:] @ H1[:, 32:].t() + c1)
+        y = torch.relu(h @ H2.t() + c2) @ H3.t() + c3
+        torch.testing.assert_close(y, m.fc(x), atol=1e-5, rtol=1e-5)
+
+
 def _eval_world():
     from newsrecommend_amd.din import DIN
 
