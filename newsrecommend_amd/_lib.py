@@ -13,7 +13,7 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libnrk.so")
+LIB_PATH = os.environ.get("NRK_LIB") or os.path.join(_HERE, "libnrk.so")  # NRK_LIB: A/B builds only
 
 NRK_METRIC_INNER_PRODUCT = 0
 NRK_METRIC_L2 = 1

@@ -431,50 +431,47 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
         }
       }
     };
-    // one sub-tile: its MFMA chain with the pending sub-tile's straight-line
-    // epilogue scheduled between the MFMAs, then the pending one's rare part
-    auto sub_tile = [&](auto st_c, const uint16_t* tl, const float* lnorm, int64_t i0, int nvalid) __attribute__((always_inline)) {
+    // one sub-tile: its MFMA chain with, scheduled between the MFMAs, the
+    // pending sub-tile's straight-line epilogue and the LDS reads of the NEXT
+    // sub-tile's A fragments (af[s] is refilled right after its last MFMA, so
+    // the chain never waits on LDS); then the pending one's rare part
+    bf16x8 af[KS];  // A fragments of the sub-tile computed next
+    float pnA[16];  // L2: norms of sub-tile A's rows
+    auto sub_tile = [&](auto st_c, int64_t i0, int nvalid, const uint16_t* next_tl) __attribute__((always_inline)) {
       constexpr int st = decltype(st_c)::value;
       f32x16(&cur)[QT] = st ? accB : accA;
       f32x16(&pend)[QT] = st ? accA : accB;
       const int64_t pbase = st ? baseA : baseB;
       const int pnv = st ? nvA : nvB;
-      const int row = 32 * st + r;
-      const uint16_t* arow = tl + row * DP;
-      const int sw = swz<CPR>(row);
-      bf16x8 af[KS];
-  #pragma unroll
-      for (int s = 0; s < KS; ++s) af[s] = *reinterpret_cast<const bf16x8*>(arow + 8 * ((2 * s + h) ^ sw));
       if (pbase >= 0 && pnv < 32) mask_rows(pend, pnv);
       float n16[16];
       if constexpr (L2) {
-        if constexpr (st == 1) {  // pending A: rows 0..31 of this tile
   #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float4 v = *reinterpret_cast<const float4*>(lnorm + 8 * j + 4 * h);
-            n16[4 * j] = v.x; n16[4 * j + 1] = v.y; n16[4 * j + 2] = v.z; n16[4 * j + 3] = v.w;
-          }
-        } else {
-  #pragma unroll
-          for (int g = 0; g < 16; ++g) n16[g] = pnB[g];
-        }
+        for (int g = 0; g < 16; ++g) n16[g] = st ? pnA[g] : pnB[g];
       }
+      // next sub-tile: rows 32..63 of this tile (st 0) or rows 0..31 of the next tile (st 1);
+      // past the last tile the reads hit the idle buffer and are never used
+      const int nrow = (st == 0 ? 32 : 0) + r;
+      const uint16_t* narow = next_tl + nrow * DP;
+      const int nsw = swz<CPR>(nrow);
       const f32x16 zero = {};
   #pragma unroll
-      for (int s = 0; s < KS; ++s)
+      for (int s = 0; s < KS; ++s) {
   #pragma unroll
         for (int t = 0; t < QT; ++t)
           cur[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], qf[t][s], s == 0 ? zero : cur[t], 0, 0, 0);
+        af[s] = *reinterpret_cast<const bf16x8*>(narow + 8 * ((2 * s + h) ^ nsw));
+      }
       float m4[QT][4], m[QT];
       tree(pend, n16, m4, m);
   #pragma unroll
       for (int t = 0; t < QT; ++t) m[t] = pbase >= 0 ? m[t] : -INFINITY;  // nothing pending: drain is a no-op
-      constexpr int NDS = KS + ((L2 && st == 1) ? 4 : 0), VPM = L2 ? 4 : 2;
-      __builtin_amdgcn_sched_group_barrier(0x100, NDS, 0);
+      constexpr int VPM = L2 ? 4 : 2;
   #pragma unroll
-      for (int i = 0; i < KS * QT; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, VPM, 0);
+      for (int s = 0; s < KS; ++s) {
+        __builtin_amdgcn_sched_group_barrier(0x008, QT, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, VPM * QT, 0);
       }
       drain(pend, pbase, m4, m);
       if constexpr (st == 0) {
@@ -483,32 +480,47 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
       } else {
         baseB = i0 + 32;
         nvB = nvalid - 32;
-        if constexpr (L2) {
-  #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float4 v = *reinterpret_cast<const float4*>(lnorm + 32 + 8 * j + 4 * h);
-            pnB[4 * j] = v.x; pnB[4 * j + 1] = v.y; pnB[4 * j + 2] = v.z; pnB[4 * j + 3] = v.w;
-          }
-        }
       }
     };
+    // tile it (buffer buf): sub-tile 0; then the tile barrier (tile it+1 landed,
+    // every wave is done with buffer buf: its fragments and norms are all in
+    // registers) and the DMA of tile it+2 into buf; then sub-tile 1, which
+    // reads tile it+1's first fragments
     auto tile_d = [&](int it, auto buf_c) __attribute__((always_inline)) {
       constexpr int buf = decltype(buf_c)::value;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();  // tile `it` landed; everyone is done with the other buffer
-      if (it + 1 < ntiles) issue_tile(it + 1, std::integral_constant<int, buf ^ 1>{});
       const uint16_t* tl = lds + buf * BUF;
-      const float* lnorm = reinterpret_cast<const float*>(tl + TI * DP);
       const int64_t i0 = ibeg + (int64_t)it * tstride * TI;
       const int nvalid = (int)((iend - i0) < TI ? (iend - i0) : TI);
-      sub_tile(std::integral_constant<int, 0>{}, tl, lnorm, i0, nvalid);
-      sub_tile(std::integral_constant<int, 1>{}, tl, lnorm, i0, nvalid);
+      sub_tile(std::integral_constant<int, 0>{}, i0, nvalid, tl);
+      if constexpr (L2) {
+        const float* lnorm = reinterpret_cast<const float*>(tl + TI * DP);
+  #pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float4 va = *reinterpret_cast<const float4*>(lnorm + 8 * j + 4 * h);
+          const float4 vb = *reinterpret_cast<const float4*>(lnorm + 32 + 8 * j + 4 * h);
+          pnA[4 * j] = va.x; pnA[4 * j + 1] = va.y; pnA[4 * j + 2] = va.z; pnA[4 * j + 3] = va.w;
+          pnB[4 * j] = vb.x; pnB[4 * j + 1] = vb.y; pnB[4 * j + 2] = vb.z; pnB[4 * j + 3] = vb.w;
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (it + 2 < ntiles) issue_tile(it + 2, buf_c);
+      sub_tile(std::integral_constant<int, 1>{}, i0, nvalid, lds + (buf ^ 1) * BUF);
     };
     if constexpr (MODE == 3) {
       if (tid == 0) cl.n = 0;  // ordered before any append by the first tile's barrier
     }
     if constexpr (DEFER) {
-      if (ntiles > 0) issue_tile(0, std::integral_constant<int, 0>{});
+      if (ntiles > 0) {
+        issue_tile(0, std::integral_constant<int, 0>{});
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // tile 0 landed
+        if (ntiles > 1) issue_tile(1, std::integral_constant<int, 1>{});
+        const uint16_t* arow = lds + r * DP;
+        const int sw = swz<CPR>(r);
+  #pragma unroll
+        for (int s = 0; s < KS; ++s) af[s] = *reinterpret_cast<const bf16x8*>(arow + 8 * ((2 * s + h) ^ sw));
+      }
       for (int it = 0; it < ntiles; it += 2) {
         tile_d(it, std::integral_constant<int, 0>{});
         if (it + 1 < ntiles) tile_d(it + 1, std::integral_constant<int, 1>{});

@@ -17,8 +17,9 @@ static screen_fn pick3() {
     if (epi == 2) return screen_kernel<DP, QT, M, 4, L2, MODE, 2>;
   }
   // flat modes: epilogue deferred into the next MFMA chain (screen.h); not for
-  // L2 with two query tiles or DP = 256 (the extra norm registers spill there)
-  if constexpr (MODE <= 1 && !(L2 && (QT == 2 || DP == 256))) {
+  // DP = 256, L2 with two query tiles, and the DP = 128 two-tile pre-pass
+  // (the second accumulator set and the fragment prefetch spill there)
+  if constexpr (MODE <= 1 && DP < 256 && !(L2 && QT == 2) && !(DP == 128 && QT == 2 && MODE == 1)) {
     if (env_int("NRK_SCREEN_DEFER", 1)) return screen_kernel<DP, QT, M, 4, L2, MODE, 0, false, true>;
   }
   // grouped A-fragment reads: default on for the IVF modes (measured), env override
