@@ -132,13 +132,16 @@ struct NoLds {};
 // test) is scheduled between the MFMAs, only the rare list insertions follow
 // the chain.  Without it every chain's results are waited for and reduced
 // before the next chain issues (the MFMA-only ablation, EPI 2, is 30 % faster).
-template <int DP, int QT, int M, int WAVES, bool L2, int MODE, int EPI = 0, bool AFRAG_GROUP = true, bool DEFER = false>
+// TIL: items per tile (deferred IP main pass may use 128: half the barriers).
+template <int DP, int QT, int M, int WAVES, bool L2, int MODE, int EPI = 0, bool AFRAG_GROUP = true, bool DEFER = false,
+          int TIL = 64>
 __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
     const uint16_t* __restrict__ qh, const uint16_t* __restrict__ xbh, const float* __restrict__ xmeta,
     int64_t nq, int64_t nb, int64_t chunk, int nch, int nqt, int tstride, float* __restrict__ part_s,
     int* __restrict__ part_i, float* __restrict__ part_t, const float* __restrict__ tau_q, IvfScreen iv) {
   constexpr int CPR = DP / 8;        // 16-B chunks per row
-  constexpr int TI = 64;  // items per tile (TI/32 sub-tiles of 32) between barriers
+  constexpr int TI = TIL;  // items per tile (TI/32 sub-tiles of 32) between barriers
+  static_assert(TIL == 64 || (TIL == 128 && DEFER && !L2 && MODE == 0), "128-item tiles: deferred IP main pass");
   constexpr int TCH = TI * CPR;      // 16-B chunks per tile
   constexpr int NT = WAVES * 64;
   constexpr int GPT = TCH / NT;      // glds instructions per thread per tile
@@ -146,7 +149,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
   constexpr int KS = DP / 16;
   constexpr int WQ = WAVES * 32 * QT;
   constexpr int BUF = TI * DP + 2 * TI;  // uint16 per buffer: rows + TI float norms
-  static_assert(!DEFER || (MODE <= 1 && EPI == 0), "deferred epilogue: flat modes only");
+  static_assert(!DEFER || (MODE <= 1 && (EPI == 0 || EPI == 3)), "deferred epilogue: flat modes only (EPI 3: no epilogue)");
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BUF];
   __shared__ std::conditional_t<MODE == 3, CollectLds<WQ>, NoLds> cl;
 
@@ -375,7 +378,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
       compute(it, buf_c);
     };
     // ---- deferred epilogue (DEFER): see the comment at the template ----
-    static_assert(!DEFER || TI == 64, "two sub-tiles per tile");
+    constexpr int NSUB = TI / 32;  // sub-tiles per tile (2 or 4)
     f32x16 accA[QT], accB[QT];
     int64_t baseA = -1, baseB = -1;  // item index of the pending sub-tile's row 0 (-1: nothing pending)
     int nvA = 0, nvB = 0;            // its rows inside the chunk
@@ -439,19 +442,20 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
     float pnA[16];  // L2: norms of sub-tile A's rows
     auto sub_tile = [&](auto st_c, int64_t i0, int nvalid, const uint16_t* next_tl) __attribute__((always_inline)) {
       constexpr int st = decltype(st_c)::value;
-      f32x16(&cur)[QT] = st ? accB : accA;
-      f32x16(&pend)[QT] = st ? accA : accB;
-      const int64_t pbase = st ? baseA : baseB;
-      const int pnv = st ? nvA : nvB;
+      constexpr int par = st & 1;  // even sub-tiles accumulate into A, odd ones into B
+      f32x16(&cur)[QT] = par ? accB : accA;
+      f32x16(&pend)[QT] = par ? accA : accB;
+      const int64_t pbase = par ? baseA : baseB;
+      const int pnv = par ? nvA : nvB;
       if (pbase >= 0 && pnv < 32) mask_rows(pend, pnv);
       float n16[16];
       if constexpr (L2) {
   #pragma unroll
-        for (int g = 0; g < 16; ++g) n16[g] = st ? pnA[g] : pnB[g];
+        for (int g = 0; g < 16; ++g) n16[g] = par ? pnA[g] : pnB[g];
       }
-      // next sub-tile: rows 32..63 of this tile (st 0) or rows 0..31 of the next tile (st 1);
-      // past the last tile the reads hit the idle buffer and are never used
-      const int nrow = (st == 0 ? 32 : 0) + r;
+      // next sub-tile: the next 32 rows of this tile, or rows 0..31 of the next tile
+      // (last sub-tile); past the last tile the reads hit the idle buffer, unused
+      const int nrow = (st + 1 < NSUB ? 32 * (st + 1) : 0) + r;
       const uint16_t* narow = next_tl + nrow * DP;
       const int nsw = swz<CPR>(nrow);
       const f32x16 zero = {};
@@ -463,9 +467,14 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
         af[s] = *reinterpret_cast<const bf16x8*>(narow + 8 * ((2 * s + h) ^ nsw));
       }
       float m4[QT][4], m[QT];
-      tree(pend, n16, m4, m);
+      if constexpr (EPI == 3) {  // ablation: keep the chain alive, no epilogue
   #pragma unroll
-      for (int t = 0; t < QT; ++t) m[t] = pbase >= 0 ? m[t] : -INFINITY;  // nothing pending: drain is a no-op
+        for (int t = 0; t < QT; ++t) asm volatile("" ::"v"(cur[t][0]), "v"(cur[t][5]), "v"(cur[t][15]));
+      } else {
+        tree(pend, n16, m4, m);
+      }
+  #pragma unroll
+      for (int t = 0; t < QT; ++t) m[t] = (EPI != 3 && pbase >= 0) ? m[t] : -INFINITY;  // drain is a no-op
       constexpr int VPM = L2 ? 4 : 2;
   #pragma unroll
       for (int s = 0; s < KS; ++s) {
@@ -473,13 +482,13 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
         __builtin_amdgcn_sched_group_barrier(0x002, VPM * QT, 0);
       }
-      drain(pend, pbase, m4, m);
-      if constexpr (st == 0) {
-        baseA = i0;
-        nvA = nvalid;
+      if constexpr (EPI != 3) drain(pend, pbase, m4, m);
+      if constexpr (par == 0) {
+        baseA = i0 + 32 * st;
+        nvA = nvalid - 32 * st;
       } else {
-        baseB = i0 + 32;
-        nvB = nvalid - 32;
+        baseB = i0 + 32 * st;
+        nvB = nvalid - 32 * st;
       }
     };
     // tile it (buffer buf): sub-tile 0; then the tile barrier (tile it+1 landed,
@@ -492,7 +501,11 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
       const int64_t i0 = ibeg + (int64_t)it * tstride * TI;
       const int nvalid = (int)((iend - i0) < TI ? (iend - i0) : TI);
       sub_tile(std::integral_constant<int, 0>{}, i0, nvalid, tl);
-      if constexpr (L2) {
+      if constexpr (NSUB == 4) {
+        sub_tile(std::integral_constant<int, 1>{}, i0, nvalid, tl);
+        sub_tile(std::integral_constant<int, 2>{}, i0, nvalid, tl);
+      }
+      if constexpr (L2) {  // (NSUB == 2)
         const float* lnorm = reinterpret_cast<const float*>(tl + TI * DP);
   #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -505,7 +518,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (it + 2 < ntiles) issue_tile(it + 2, buf_c);
-      sub_tile(std::integral_constant<int, 1>{}, i0, nvalid, lds + (buf ^ 1) * BUF);
+      sub_tile(std::integral_constant<int, NSUB - 1>{}, i0, nvalid, lds + (buf ^ 1) * BUF);
     };
     if constexpr (MODE == 3) {
       if (tid == 0) cl.n = 0;  // ordered before any append by the first tile's barrier
@@ -525,7 +538,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
         tile_d(it, std::integral_constant<int, 0>{});
         if (it + 1 < ntiles) tile_d(it + 1, std::integral_constant<int, 1>{});
       }
-      if (baseB >= 0) {  // the last sub-tile's epilogue
+      if (EPI != 3 && baseB >= 0) {  // the last sub-tile's epilogue
         if (nvB < 32) mask_rows(accB, nvB);
         float m4[QT][4], m[QT];
         tree(accB, pnB, m4, m);

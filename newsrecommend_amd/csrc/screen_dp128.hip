@@ -15,12 +15,18 @@ static screen_fn pick3() {
     const int epi = env_int("NRK_SCREEN_EPI", 0);
     if (epi == 1) return screen_kernel<DP, QT, M, 4, L2, MODE, 1>;
     if (epi == 2) return screen_kernel<DP, QT, M, 4, L2, MODE, 2>;
+    if (epi == 3) return screen_kernel<DP, QT, M, 4, L2, MODE, 3, false, true>;  // deferred path, no epilogue
   }
   // flat modes: epilogue deferred into the next MFMA chain (screen.h); not for
   // DP = 256, L2 with two query tiles, and the DP = 128 two-tile pre-pass
   // (the second accumulator set and the fragment prefetch spill there)
   if constexpr (MODE <= 1 && DP < 256 && !(L2 && QT == 2) && !(DP == 128 && QT == 2 && MODE == 1)) {
-    if (env_int("NRK_SCREEN_DEFER", 1)) return screen_kernel<DP, QT, M, 4, L2, MODE, 0, false, true>;
+    if (env_int("NRK_SCREEN_DEFER", 1)) {
+      if constexpr (MODE == 0 && !L2) {  // 128-item tiles: half the barriers (measured +9 %)
+        if (env_int("NRK_SCREEN_TI", 128) == 128) return screen_kernel<DP, QT, M, 4, L2, MODE, 0, false, true, 128>;
+      }
+      return screen_kernel<DP, QT, M, 4, L2, MODE, 0, false, true>;
+    }
   }
   // grouped A-fragment reads: default on for the IVF modes (measured), env override
   const int grp = env_int("NRK_AFRAG_GROUP", -1);
