@@ -213,33 +213,63 @@ __global__ __launch_bounds__(256) void merge_rescore_kernel(
   int64_t* id2 = reinterpret_cast<int64_t*>(g2 + P2);
   float* qs = reinterpret_cast<float*>(id2 + P2);
   __shared__ float red[256];
-  __shared__ int s_valid;
 
   const float* ps = part_s + (int64_t)qi * U;
   const int* pi = part_i + (int64_t)qi * U;
-  for (int i = tid; i < P; i += 256) {
-    float v = i < U ? ps[i] : -INFINITY;
+  // the union (U <= 2048: at most 8 entries per thread) -> registers; only the
+  // valid entries (with the pre-pass bound: a few hundred at k = 200, of 2048)
+  // are compacted to the front and sorted
+  constexpr int EPT = 8;
+  double rg[EPT];
+  int64_t ri[EPT];
+  bool rv[EPT];
+  int nv = 0;
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    const int i = tid + 256 * e;
+    const float v = i < U ? ps[i] : -INFINITY;
     const int64_t item = i < U ? (int64_t)pi[i] : -1;
-    const bool ok = v != -INFINITY && item >= 0 && item < nb;  // never dereference an unset slot
-    g[i] = ok ? (double)v : -INFINITY;
-    id[i] = ok ? (pos2id ? pos2id[item] : item) : INT64_MAX;  // IVF: list position -> id
+    rv[e] = v != -INFINITY && item >= 0 && item < nb;  // never dereference an unset slot
+    rg[e] = (double)v;
+    ri[e] = rv[e] ? (pos2id ? pos2id[item] : item) : INT64_MAX;  // IVF: list position -> id
+    nv += rv[e] ? 1 : 0;
   }
+  const int lane = tid & 63, w = tid >> 6;
+  int incl = nv;  // inclusive prefix of the valid counts within the wave
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  __shared__ int wsum[4];
+  if (lane == 63) wsum[w] = incl;
   float th = -INFINITY;
   for (int i = tid; i < nch * 2; i += 256) th = fmaxf(th, part_t[(int64_t)qi * nch * 2 + i]);
   red[tid] = th;
   for (int i = tid; i < d; i += 256) qs[i] = xq[(int64_t)qi * d + i];
-  if (tid == 0) s_valid = 0;
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (tid < o) red[tid] = fmaxf(red[tid], red[tid + o]);
-    __syncthreads();
+  const int V = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  int off = incl - nv;
+  for (int j = 0; j < w; ++j) off += wsum[j];
+#pragma unroll
+  for (int e = 0; e < EPT; ++e)
+    if (rv[e]) {
+      g[off] = rg[e];
+      id[off] = ri[e];
+      ++off;
+    }
+  const int PS = pow2ceil(V > 1 ? V : 1);
+  for (int i = V + tid; i < PS; i += 256) {
+    g[i] = -INFINITY;
+    id[i] = INT64_MAX;
   }
-  const float theta_lanes = red[0];
-  block_bitonic_sort(g, id, P);
-  for (int i = tid; i < P; i += 256)
-    if (id[i] != INT64_MAX) atomicAdd(&s_valid, 1);
+  for (int o = 128; o > 0; o >>= 1) {  // (its first barrier also publishes the compaction)
+    __syncthreads();
+    if (tid < o) red[tid] = fmaxf(red[tid], red[tid + o]);
+  }
   __syncthreads();
-  const int V = s_valid;
+  const float theta_lanes = red[0];
+  block_bitonic_sort(g, id, PS);
   const int kp = KP < V ? KP : V;
   double theta = fmax((double)theta_lanes, kp < V ? g[kp] : -INFINITY);
   if (tau_q) theta = fmax(theta, (double)tau_q[qi]);  // items below the bound were never kept
@@ -748,6 +778,12 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
   p.chunk = (int64_t)align_up((size_t)cdiv(nb, nch), 64);
   p.nch = (int)cdiv(nb, p.chunk);
   p.U = p.nch * 2 * p.M;
+  if (p.U > 2048) {  // the merge holds the union in registers (8 entries per thread)
+    p.exact_only = true;
+    p.off_fbc = 0;
+    p.total = 256;
+    return p;
+  }
   int kp = 2 * k > 32 ? 2 * k : 32;
   if (kp < k + 16) kp = k + 16;
   kp = env_int("NRK_KP", kp);
