@@ -63,8 +63,10 @@ screen_fn pick_screen_dp256_w8(bool l2, int mode) {
   // retrieve 21.7 -> 19.8 ms), 64-item tiles (128 spills 460 B here)
   if (mode == 0 && !l2 && env_int("NRK_SCREEN_W8_DEFER", 1))
     return screen_kernel<256, 1, 16, 8, false, 0, 0, false, true, 64>;
-  if (mode == 1)
+  if (mode == 1) {
+    if (!l2 && env_int("NRK_SCREEN_W8_DEFER", 1)) return screen_kernel<256, 1, 1, 8, false, 1, 0, false, true, 64>;
     return l2 ? screen_kernel<256, 1, 1, 8, true, 1, 0, false> : screen_kernel<256, 1, 1, 8, false, 1, 0, false>;
+  }
   return l2 ? screen_kernel<256, 1, 16, 8, true, 0, 0, false> : screen_kernel<256, 1, 16, 8, false, 0, 0, false>;
 }
 
