@@ -1207,6 +1207,7 @@ __global__ __launch_bounds__(256) void collect_rescore_kernel(
 
 struct IvfPlan {
   int dp, qt, M, waves, wq, nqt;
+  int qtA, wqA;             // phase A query tiles per wave / queries per work item
   int nA, chA, cmaxA, R;    // phase A: lane maxima (+positions) over the nA nearest lists, R seeds
   int chB, cmaxB, cap;      // phase B: all probed lists, collect above e_k - B
   int fb_slots, fb_cap;
@@ -1225,7 +1226,13 @@ static IvfPlan make_ivf_plan(int64_t nq, int nprobe, int nlist, int64_t max_list
   else if (k <= 24) { p.M = 8; p.qt = 1; }
   else { p.M = 16; p.qt = 1; }
   if (p.dp == 256) p.qt = 1;
+  if (env_int("NRK_IVF_QT", 0) == 1) p.qt = 1;  // A/B: one query tile per wave (the deferred IVF screens)
   p.wq = p.waves * 32 * p.qt;
+  // phase A (lane maxima over the nA nearest lists) runs one query tile per
+  // wave: half the work-item padding of the grouped queries and a lighter
+  // epilogue.  Phase B keeps p.qt (two tiles share each A fragment).
+  p.qtA = env_int("NRK_IVF_QTA", 1) == 1 ? 1 : p.qt;
+  p.wqA = p.waves * 32 * p.qtA;
   p.nqt = (int)cdiv(nq, p.wq);
   p.nq_pad = (int64_t)p.nqt * p.wq;
   const int64_t ml = max_list > 0 ? max_list : 1;
@@ -1260,7 +1267,7 @@ static IvfPlan make_ivf_plan(int64_t nq, int nprobe, int nlist, int64_t max_list
   p.max_rows = (p.max_rows + p.wq - 1) / p.wq * p.wq;
   // persistent grids over the device work tables (upper bound on the items)
   const int64_t gcap = env_int("NRK_IVF_GRID", 2048);
-  p.ubA = (cdiv(nq * p.nA, (int64_t)p.wq) + nlist) * p.cmaxA;
+  p.ubA = (cdiv(nq * p.nA, (int64_t)p.wqA) + nlist) * p.cmaxA;
   p.ubB = (cdiv(npairs, (int64_t)p.wq) + nlist) * p.cmaxB;
   if (p.ubA > gcap) p.ubA = gcap;
   if (p.ubB > gcap) p.ubB = gcap;
@@ -1409,9 +1416,9 @@ extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe,
         hipMemsetAsync(ccnt, 0, (size_t)nq * 4, st) != hipSuccess)
       return fail(NRK_ELAUNCH, "ivf_search: copy/memset failed");
     int rc =
-        ivf_group(p0, nq, p.nA, nlist, list_off, p.wq, p.chA, p.dp, p.max_rows, qh, cnt, fill, seg, work, sp, qi, st);
+        ivf_group(p0, nq, p.nA, nlist, list_off, p.wqA, p.chA, p.dp, p.max_rows, qh, cnt, fill, seg, work, sp, qi, st);
     if (rc != NRK_OK) return rc;
-    screen_fn fa = pick_screen(p.dp, p.qt, p.M, l2 != 0, 4);
+    screen_fn fa = pick_screen(p.dp, p.qtA, p.M, l2 != 0, 4);
     if (!fa) return fail(NRK_EUNSUPPORTED, "ivf_search: no screen kernel for dp=%d", p.dp);
     IvfScreen isa{work, list_off, seg, sp, nlist, p.chA, p.cmaxA, nullptr, nullptr, nullptr, 0, p.nA};
     hipLaunchKernelGGL(fa, dim3((unsigned)p.ubA), dim3(p.waves * 64), 0, st, qi, xbh_ivf, meta_ivf, nq, n, 0, 0, 0, 1,

@@ -149,7 +149,8 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
   constexpr int KS = DP / 16;
   constexpr int WQ = WAVES * 32 * QT;
   constexpr int BUF = TI * DP + 2 * TI;  // uint16 per buffer: rows + TI float norms
-  static_assert(!DEFER || (MODE <= 1 && (EPI == 0 || EPI == 3)), "deferred epilogue: flat modes only (EPI 3: no epilogue)");
+  static_assert(!DEFER || ((MODE <= 1 || MODE == 3 || MODE == 4) && (EPI == 0 || EPI == 3)),
+                "deferred epilogue: flat modes, IVF collect / lane maxima (EPI 3: no epilogue)");
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BUF];
   __shared__ std::conditional_t<MODE == 3, CollectLds<WQ>, NoLds> cl;
 
@@ -407,6 +408,44 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
     };
     // rare part: lane-list insertions (MODE 0) or the lane maximum (MODE 1)
     auto drain = [&](f32x16 (&pa)[QT], int64_t pbase, const float (&m4)[QT][4], const float (&m)[QT]) __attribute__((always_inline)) {
+      if constexpr (MODE == 3) {  // IVF collect: append every score at or above the query's threshold
+  #pragma unroll
+        for (int t = 0; t < QT; ++t) {
+          if (__any(m[t] >= cthr[t])) {
+  #pragma unroll
+            for (int g = 0; g < 16; ++g) {
+              if (pa[t][g] >= cthr[t]) {
+                const int pos = (int)(pbase + (g & 3) + 8 * (g >> 2) + 4 * h);
+                const int e = atomicAdd(&cl.n, 1);
+                if (e < CollectLds<WQ>::CAP) {
+                  const int row = (w * QT + t) * 32 + r;
+                  const int rank = atomicAdd(&cl.qcnt[row], 1);
+                  cl.ent[e] = make_int2(row | (rank << 8), pos);
+                } else if (__builtin_nontemporal_load(&iv.cand_cnt[cq[t]]) <= iv.cap) {
+                  const int slot = atomicAdd(&iv.cand_cnt[cq[t]], 1);
+                  if (slot < iv.cap) iv.cand_pos[(int64_t)cq[t] * iv.cap + slot] = pos;
+                }
+              }
+            }
+          }
+        }
+        return;
+      }
+      if constexpr (MODE == 4) {  // IVF lane maximum and its position
+  #pragma unroll
+        for (int t = 0; t < QT; ++t) {
+          if (__any(m[t] > ls[t][0])) {
+  #pragma unroll
+            for (int g = 0; g < 16; ++g) {
+              if (pa[t][g] > ls[t][0]) {
+                ls[t][0] = pa[t][g];
+                li[t][0] = (int)(pbase + (g & 3) + 8 * (g >> 2) + 4 * h);
+              }
+            }
+          }
+        }
+        return;
+      }
       if constexpr (MODE == 1) {
   #pragma unroll
         for (int t = 0; t < QT; ++t) ls[t][0] = fmax_ieee(ls[t][0], m[t]);

@@ -20,6 +20,9 @@ static screen_fn pick3() {
   // flat modes: epilogue deferred into the next MFMA chain (screen.h); not for
   // DP = 256, L2 with two query tiles, and the DP = 128 two-tile pre-pass
   // (the second accumulator set and the fragment prefetch spill there)
+  if constexpr ((MODE == 3 || MODE == 4) && QT == 1 && DP < 256) {  // IVF collect / lane maxima
+    if (env_int("NRK_IVF_DEFER", 0)) return screen_kernel<DP, QT, M, 4, L2, MODE, 0, false, true>;
+  }
   if constexpr (MODE <= 1 && DP < 256 && !(L2 && QT == 2) && !(DP == 128 && QT == 2 && MODE == 1)) {
     if (env_int("NRK_SCREEN_DEFER", 1)) {
       if constexpr (MODE == 0 && !L2) {  // 128-item tiles: half the barriers (measured +9 %)
