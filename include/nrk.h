@@ -243,10 +243,12 @@ int nrk_din_head_train(const float* q, const float* pooled, int64_t ld_pooled, c
 /* clip_grad_norm_(max_norm) + torch.optim.Adam (L2 weight decay) over one
  * flat parameter buffer (DIN.py:150-151): *step (device f32) is incremented,
  * grads are scaled in place by the clip coefficient, exp_avg / exp_avg_sq /
- * params updated with torch's capturable-Adam formulas. */
+ * params updated with torch's capturable-Adam formulas.  lr_dev (device f32,
+ * optional) overrides lr when non-null, so ReduceLROnPlateau (DIN.py:246,254)
+ * can change the rate of a captured step between graph replays. */
 int nrk_clip_adam_workspace(int64_t n, size_t* ws_bytes);
 int nrk_clip_adam(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
-                  float* step, float lr, float beta1, float beta2, float eps, float weight_decay,
+                  float* step, float lr, const float* lr_dev, float beta1, float beta2, float eps, float weight_decay,
                   float max_norm, void* ws, size_t ws_bytes, void* stream);
 
 /* Row gather (table [N][d] dtype -> out [n][d] f32), id < 0 -> zeros.

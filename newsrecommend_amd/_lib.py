@@ -48,8 +48,8 @@ SIGNATURES = {
     "nrk_din_head_train": (ctypes.c_int, [c_p, c_p, c_i64, c_p, c_i32, c_i32, c_i32, c_f32, c_f32, c_f32,
                                           ctypes.c_uint64, c_p, c_p, c_p, c_p, c_p, c_p, c_size, c_p]),
     "nrk_clip_adam_workspace": (ctypes.c_int, [c_i64, ctypes.POINTER(c_size)]),
-    "nrk_clip_adam": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_i64, c_p, c_f32, c_f32, c_f32, c_f32, c_f32, c_f32, c_p,
-                                     c_size, c_p]),
+    "nrk_clip_adam": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_i64, c_p, c_f32, c_p, c_f32, c_f32, c_f32, c_f32, c_f32,
+                                     c_p, c_size, c_p]),
     "nrk_din_attn_fwd": (ctypes.c_int, [c_p, c_p, c_i64, c_i32, c_p, c_p, c_p, c_f32, c_i32, c_i32, c_i32, c_i32,
                                         c_p, c_p, c_p]),
     "nrk_din_attn_bwd_workspace": (ctypes.c_int, [c_i32, c_i32, c_i32, ctypes.POINTER(c_size)]),

@@ -955,7 +955,8 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g,
 __global__ __launch_bounds__(256) void clip_adam_kernel(float* __restrict__ p, float* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                         const double* __restrict__ part, int nparts,
-                                                        const float* __restrict__ step, float lr, float beta1,
+                                                        const float* __restrict__ step, float lr,
+                                                        const float* __restrict__ lr_dev, float beta1,
                                                         float beta2, float eps, float wd, float max_norm) {
   __shared__ float s_coef;
   if (threadIdx.x < 64) {  // fixed-order sum of the partials: lane-strided, then a fixed butterfly
@@ -971,6 +972,7 @@ __global__ __launch_bounds__(256) void clip_adam_kernel(float* __restrict__ p, f
   __syncthreads();
   const float coef = s_coef;
   const float t = *step;
+  if (lr_dev) lr = *lr_dev;  // device-resident lr: a scheduler updates it between graph replays
   const float bc1 = 1.f - powf(beta1, t), bc2 = 1.f - powf(beta2, t);
   const float step_size = lr / bc1, bc2_sqrt = sqrtf(bc2);
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
@@ -1151,7 +1153,7 @@ extern "C" int nrk_clip_adam_workspace(int64_t n, size_t* ws_bytes) {
 }
 
 extern "C" int nrk_clip_adam(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, float* step,
-                             float lr, float beta1, float beta2, float eps, float weight_decay, float max_norm,
+                             float lr, const float* lr_dev, float beta1, float beta2, float eps, float weight_decay, float max_norm,
                              void* ws, size_t ws_bytes, void* stream) {
   NRK_CHECK_ARG(n > 0 && params && grads && exp_avg && exp_avg_sq && step && ws, "clip_adam: bad arguments");
   if (ws_bytes < 256 * 8) return fail(NRK_EWORKSPACE, "clip_adam: workspace %zu < 2048", ws_bytes);
@@ -1164,7 +1166,7 @@ extern "C" int nrk_clip_adam(float* params, float* grads, float* exp_avg, float*
   hipLaunchKernelGGL(sumsq_kernel, dim3(ns), dim3(256), 0, st, grads, n, part, step);
   NRK_CHECK_LAUNCH("sumsq_kernel");
   hipLaunchKernelGGL(clip_adam_kernel, dim3(nb), dim3(256), 0, st, params, grads, exp_avg, exp_avg_sq, n, part, ns,
-                     step, lr, beta1, beta2, eps, weight_decay, max_norm);
+                     step, lr, lr_dev, beta1, beta2, eps, weight_decay, max_norm);
   NRK_CHECK_LAUNCH("clip_adam_kernel");
   return NRK_OK;
 }

@@ -545,6 +545,170 @@ __global__ __launch_bounds__(256) void exact_topk_kernel(
   }
 }
 
+// ============================================================ small corpus ==
+// Exact search over a SMALL corpus (nb <= SMALL_NB: the coarse quantizer's
+// centroids, k-means assignment, IndexIVFFlat.add): the (query, item) scores
+// are computed EXACTLY in fp64 with the oracle's operation order (sequential d,
+// fma) as a 64 x 64 tile GEMM on the VALU — one tile per workgroup, a 4 x 4
+// register micro-tile per thread, f32 operands staged d-major through LDS —
+// so no certificate is needed.  k = 1 fuses the arg-best into the tile loop
+// (a workgroup walks all items for its 64 queries); larger k writes the
+// goodness matrix of a query chunk and selects per query with a block bitonic
+// sort (P = pow2ceil(nb) <= SMALL_NB entries in LDS).
+constexpr int SM_T = 64;          // queries and items per tile
+constexpr int SM_DC = 32;         // dimensions staged per LDS step
+constexpr int SM_LD = SM_T + 4;   // LDS row stride (floats): conflict-light transposed stores
+constexpr int SMALL_NB = 4096;
+
+template <bool L2>
+__device__ __forceinline__ void small_tile(const float* __restrict__ xq, int64_t q0, int64_t nq,
+                                           const float* __restrict__ xb, int64_t j0, int64_t nb, int d,
+                                           float* __restrict__ Qs, float* __restrict__ Xs, double (&acc)[4][4]) {
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[r][c] = 0.0;
+  for (int dc = 0; dc < d; dc += SM_DC) {
+    const int w = d - dc < SM_DC ? d - dc : SM_DC;
+    __syncthreads();  // previous step's readers are done
+#pragma unroll
+    for (int u = 0; u < (SM_T * SM_DC) / 256; ++u) {
+      const int e = tid + u * 256;
+      const int r = e / SM_DC, c = e % SM_DC;  // consecutive threads: consecutive dims of one row
+      const int64_t qi = q0 + r, xi = j0 + r;
+      Qs[c * SM_LD + r] = (c < w && qi < nq) ? xq[qi * d + dc + c] : 0.f;
+      Xs[c * SM_LD + r] = (c < w && xi < nb) ? xb[xi * d + dc + c] : 0.f;
+    }
+    __syncthreads();
+    for (int j = 0; j < w; ++j) {
+      const float4 qv = *reinterpret_cast<const float4*>(Qs + j * SM_LD + ty * 4);
+      const float4 xv = *reinterpret_cast<const float4*>(Xs + j * SM_LD + tx * 4);
+      const double qd[4] = {(double)qv.x, (double)qv.y, (double)qv.z, (double)qv.w};
+      const double xd[4] = {(double)xv.x, (double)xv.y, (double)xv.z, (double)xv.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if (L2) {
+            const double t = qd[r] - xd[c];
+            acc[r][c] = fma(t, t, acc[r][c]);
+          } else {
+            acc[r][c] = fma(qd[r], xd[c], acc[r][c]);
+          }
+        }
+    }
+  }
+}
+
+// k = 1: grid = query tiles; each workgroup walks every item tile.
+template <bool L2>
+__global__ __launch_bounds__(256) void small_best_kernel(const float* __restrict__ xq, int64_t nq,
+                                                         const float* __restrict__ xb, int64_t nb, int d,
+                                                         float* __restrict__ D, int64_t* __restrict__ I,
+                                                         double* __restrict__ S, int64_t id_offset) {
+  __shared__ __attribute__((aligned(16))) float Qs[SM_DC * SM_LD];
+  __shared__ __attribute__((aligned(16))) float Xs[SM_DC * SM_LD];
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  const int64_t q0 = (int64_t)blockIdx.x * SM_T;
+  double bg[4];
+  int64_t bi[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    bg[r] = -INFINITY;
+    bi[r] = INT64_MAX;
+  }
+  for (int64_t j0 = 0; j0 < nb; j0 += SM_T) {
+    double acc[4][4];
+    small_tile<L2>(xq, q0, nq, xb, j0, nb, d, Qs, Xs, acc);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int64_t j = j0 + tx * 4 + c;
+      if (j < nb) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const double g = L2 ? -acc[r][c] : acc[r][c];
+          if (better(g, j, bg[r], bi[r])) {
+            bg[r] = g;
+            bi[r] = j;
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {  // arg-best over the 16 lanes sharing these rows
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) {
+      const double og = __shfl_xor(bg[r], o, 64);
+      const int64_t oi = __shfl_xor(bi[r], o, 64);
+      if (better(og, oi, bg[r], bi[r])) {
+        bg[r] = og;
+        bi[r] = oi;
+      }
+    }
+    const int64_t qi = q0 + ty * 4 + r;
+    if (tx == 0 && qi < nq) {
+      const bool valid = bi[r] != INT64_MAX;
+      const double sc = valid ? (L2 ? -bg[r] : bg[r]) : (L2 ? DBL_MAX : -DBL_MAX);
+      D[qi] = valid ? (float)sc : (L2 ? FLT_MAX : -FLT_MAX);
+      I[qi] = valid ? bi[r] + id_offset : -1;
+      if (S) S[qi] = sc;
+    }
+  }
+}
+
+// k > 1, pass 1: goodness G[q - q0][j] for one query chunk; grid = (item tiles, query tiles).
+template <bool L2>
+__global__ __launch_bounds__(256) void small_scores_kernel(const float* __restrict__ xq, int64_t q0, int64_t nq,
+                                                           const float* __restrict__ xb, int64_t nb, int d,
+                                                           double* __restrict__ G, int64_t ldg) {
+  __shared__ __attribute__((aligned(16))) float Qs[SM_DC * SM_LD];
+  __shared__ __attribute__((aligned(16))) float Xs[SM_DC * SM_LD];
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  const int64_t j0 = (int64_t)blockIdx.x * SM_T;
+  const int64_t qt = q0 + (int64_t)blockIdx.y * SM_T;
+  double acc[4][4];
+  small_tile<L2>(xq, qt, nq, xb, j0, nb, d, Qs, Xs, acc);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int64_t qi = qt + ty * 4 + r;
+    if (qi >= nq) continue;
+    double* row = G + (qi - q0) * ldg + j0 + tx * 4;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (j0 + tx * 4 + c < nb) row[c] = L2 ? -acc[r][c] : acc[r][c];
+  }
+}
+
+// k > 1, pass 2: one workgroup per query of the chunk sorts its nb goodness values.
+__global__ __launch_bounds__(256) void small_select_kernel(const double* __restrict__ G, int64_t ldg, int64_t q0,
+                                                           int64_t nq, int64_t nb, int k, int l2, int P,
+                                                           float* __restrict__ D, int64_t* __restrict__ I,
+                                                           double* __restrict__ S, int64_t id_offset) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* g = reinterpret_cast<double*>(smem);
+  int64_t* id = reinterpret_cast<int64_t*>(g + P);
+  const int64_t qi = q0 + blockIdx.x;
+  if (qi >= nq) return;
+  const double* row = G + (int64_t)blockIdx.x * ldg;
+  for (int i = threadIdx.x; i < P; i += 256) {
+    const bool ok = i < nb;
+    g[i] = ok ? row[i] : -INFINITY;
+    id[i] = ok ? (int64_t)i : INT64_MAX;
+  }
+  __syncthreads();
+  block_bitonic_sort(g, id, P);
+  for (int j = threadIdx.x; j < k; j += 256) {
+    const int64_t o = qi * k + j;
+    const bool valid = j < P && id[j] != INT64_MAX;
+    const double sc = valid ? (l2 ? -g[j] : g[j]) : (l2 ? DBL_MAX : -DBL_MAX);
+    D[o] = valid ? (float)sc : (l2 ? FLT_MAX : -FLT_MAX);
+    I[o] = valid ? id[j] + id_offset : -1;
+    if (S) S[o] = sc;
+  }
+}
+
 // ========================================================= tiled fallback ==
 // Chip-wide fp64 scan for the fallback slots: 64-row fp32 tiles staged in LDS
 // (row stride d+1, so lane = row reads are bank-conflict free), each wave
@@ -708,6 +872,10 @@ __global__ void topk_merge_kernel(const double* __restrict__ Sp, const int64_t* 
 // ================================================================== plan ==
 struct FlatPlan {
   bool exact_only, tau;
+  bool cliff;  // exact_only forced by a shape the screen cannot plan (reported as nq fallbacks)
+  bool small;  // nb <= SMALL_NB: exact fp64 tile GEMM (small_best / small_scores + small_select)
+  int small_P;
+  int64_t small_ld, small_chunk;
   int dp, qt, M, waves, wq, nqt, nch, U, KP;
   int R, nch_pre, tstride;  // threshold pre-pass: bound rank, chunks, tile stride
   int fb_slots, fb_cap;     // tiled fallback: slots with candidate storage, candidates per slot
@@ -739,6 +907,18 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
   FlatPlan p;
   memset(&p, 0, sizeof(p));
   p.dp = padded_dim(d);
+  if (nb <= SMALL_NB && k <= SMALL_NB && nq > 0) {  // exact fp64 tile GEMM, no screening
+    p.small = true;
+    p.exact_only = true;
+    const int64_t P = host_pow2ceil(nb > 0 ? (int)nb : 1);
+    p.small_ld = align_up((size_t)(nb > 0 ? nb : 1), SM_T);
+    const int64_t want = ((int64_t)64 << 20) / (p.small_ld * 8);  // <= 64 MB of goodness per chunk
+    p.small_chunk = want < SM_T ? SM_T : want / SM_T * SM_T;
+    if (p.small_chunk > (int64_t)align_up((size_t)nq, SM_T)) p.small_chunk = align_up((size_t)nq, SM_T);
+    p.small_P = (int)P;
+    p.total = k == 1 ? 256 : align_up((size_t)p.small_chunk * p.small_ld * 8, 256);
+    return p;
+  }
   p.exact_only = nb < env_int("NRK_EXACT_BELOW", 16384) || d > 256 || k > 256 || nb >= (1ll << 31) || nq == 0;
   if (p.exact_only) {
     p.off_fbc = 0;
@@ -780,6 +960,7 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
   p.U = p.nch * 2 * p.M;
   if (p.U > 2048) {  // the merge holds the union in registers (8 entries per thread)
     p.exact_only = true;
+    p.cliff = true;
     p.off_fbc = 0;
     p.total = 256;
     return p;
@@ -792,6 +973,7 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
   p.KP = kp;
   if (p.KP < k) {
     p.exact_only = true;
+    p.cliff = true;
     p.off_fbc = 0;
     p.total = 256;
     return p;
@@ -850,6 +1032,37 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
 
 using namespace nrk;
 
+
+static int small_launch(const FlatPlan& p, const float* xq, int64_t nq, const float* xb, int64_t nb, int d, int k,
+                        int l2, float* D, int64_t* I, double* S, int64_t id_offset, void* ws, hipStream_t st) {
+  if (k == 1) {
+    const unsigned grid = (unsigned)cdiv(nq, SM_T);
+    if (l2)
+      hipLaunchKernelGGL(small_best_kernel<true>, dim3(grid), dim3(256), 0, st, xq, nq, xb, nb, d, D, I, S, id_offset);
+    else
+      hipLaunchKernelGGL(small_best_kernel<false>, dim3(grid), dim3(256), 0, st, xq, nq, xb, nb, d, D, I, S,
+                         id_offset);
+    NRK_CHECK_LAUNCH("small_best_kernel");
+    return NRK_OK;
+  }
+  double* G = static_cast<double*>(ws);
+  const size_t smem = (size_t)p.small_P * 16;
+  for (int64_t q0 = 0; q0 < nq; q0 += p.small_chunk) {
+    const int64_t nc = nq - q0 < p.small_chunk ? nq - q0 : p.small_chunk;
+    if (nb > 0) {
+      const dim3 grid((unsigned)cdiv(nb, SM_T), (unsigned)cdiv(nc, SM_T));
+      if (l2)
+        hipLaunchKernelGGL(small_scores_kernel<true>, grid, dim3(256), 0, st, xq, q0, nq, xb, nb, d, G, p.small_ld);
+      else
+        hipLaunchKernelGGL(small_scores_kernel<false>, grid, dim3(256), 0, st, xq, q0, nq, xb, nb, d, G, p.small_ld);
+      NRK_CHECK_LAUNCH("small_scores_kernel");
+    }
+    hipLaunchKernelGGL(small_select_kernel, dim3((unsigned)nc), dim3(256), smem, st, G, p.small_ld, q0, nq, nb, k, l2,
+                       p.small_P, D, I, S, id_offset);
+    NRK_CHECK_LAUNCH("small_select_kernel");
+  }
+  return NRK_OK;
+}
 
 static int exact_launch(const float* xq, int64_t nq, const float* xb, int64_t nb, int d, int k, int l2,
                         const int* qlist, const int* qcount, int64_t max_work, float* D, int64_t* I,
@@ -918,7 +1131,13 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
   if (nq == 0) return NRK_OK;
   NRK_CHECK_ARG(xq && D && I && (xb || nb == 0), "knn_flat: null pointer");
   const int l2 = metric == NRK_METRIC_L2;
+  if (p.small) return small_launch(p, xq, nq, xb, nb, d, k, l2, D, I, S, id_offset, ws, st);
   if (p.exact_only) {
+    // a shape the screen cannot plan (merge union > 2048, d or k > 256) runs the
+    // fp64 brute force for every query: say so through the fallback count
+    if (n_fallback && (p.cliff || d > 256 || k > 256) &&
+        hipMemsetD32Async(n_fallback, (int)nq, 1, st) != hipSuccess)
+      return fail(NRK_ELAUNCH, "knn_flat: memset failed");
     return exact_launch(xq, nq, xb, nb, d, k, l2, nullptr, nullptr, nq, D, I, S, id_offset, st);
   }
   NRK_CHECK_ARG(xb_bf16 && xb_meta && stats, "knn_flat: index not prepared (null bf16/meta/stats)");

@@ -369,6 +369,21 @@ class _HeadParams(ctypes.Structure):
         "g_fc3_w", "g_fc3_b")]
 
 
+class FusedAdam(torch.optim.Optimizer):
+    """The optimizer facade of a FusedTrainStep: torch.optim.Adam's
+    hyper-parameters in one param group, so torch's LR schedulers
+    (ReduceLROnPlateau, DIN.py:246,254) can read and set `lr`.  The update
+    itself runs inside the fused step (nrk_clip_adam reads the rate from a
+    device scalar the step refreshes whenever the group's lr changed), so a
+    captured HIP graph follows the schedule without re-capture."""
+
+    def __init__(self, params, lr, betas, eps, weight_decay):
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+
+    def step(self, closure=None):  # noqa: D401
+        raise RuntimeError("FusedAdam is stepped by FusedTrainStep.step(); call that instead")
+
+
 class FusedTrainStep:
     """One DIN training step (DIN.py:143-151) as ~25 launches in one HIP graph:
     gather + attention forward (libnrk), the whole train-mode MLP head forward
@@ -387,12 +402,28 @@ class FusedTrainStep:
                  betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, clip=1.0, seed=1234, graph=True,
                  grad_hook=None):
         dev = table.device
+        _lib.require_device(table, hist_ids, target_ids, labels, what="FusedTrainStep")
         self.model, self.table = model, table
-        self.hist_all, self.tgt_all, self.lab_all = hist_ids, target_ids, labels
+        # the kernels read int32 ids and f32 labels: normalise whatever the caller passes
+        # (torch's default int64 ids, (n, 1) or float64 labels)
+        if hist_ids.dim() != 2:
+            raise ValueError(f"FusedTrainStep: hist_ids must be (rows, L), got {tuple(hist_ids.shape)}")
+        self.hist_all = hist_ids.to(torch.int32).contiguous()
+        self.tgt_all = target_ids.reshape(-1).to(torch.int32).contiguous()
+        self.lab_all = labels.reshape(-1).to(torch.float32).contiguous()
+        if not (self.tgt_all.numel() == self.lab_all.numel() == self.hist_all.shape[0]):
+            raise ValueError("FusedTrainStep: hist_ids, target_ids and labels must have one entry per row")
         self.B = int(batch_size)
         if self.B % 32:
             raise ValueError("FusedTrainStep: batch_size must be a multiple of 32")
-        self.lr, self.betas, self.eps, self.wd, self.clip, self.seed = lr, betas, eps, weight_decay, clip, seed
+        self.betas, self.eps, self.wd, self.clip, self.seed = betas, eps, weight_decay, clip, seed
+        bns = (model.fc[0], model.fc[4], model.fc[8])
+        mom = {bn.momentum for bn in bns}
+        bn_eps = {bn.eps for bn in bns}
+        if len(mom) != 1 or len(bn_eps) != 1 or None in mom or not all(bn.track_running_stats for bn in bns):
+            raise ValueError("FusedTrainStep: the fused head needs one BatchNorm momentum (not None) and eps "
+                             "shared by fc.0/fc.4/fc.8, with running statistics")
+        self.bn_momentum, self.bn_eps = float(mom.pop()), float(bn_eps.pop())
         self.grad_hook = grad_hook  # e.g. data-parallel all_reduce of the flat gradient buffer
         attn0, attn2 = model.attn.attn[0], model.attn.attn[2]
         self.d = attn0.weight.shape[1] // 2
@@ -416,6 +447,9 @@ class FusedTrainStep:
                 p.data = self.P[o:o + k].view_as(p)
                 p.grad = self.G[o:o + k].view_as(p)
                 o += k
+        self.optimizer = FusedAdam(params, lr, betas, eps, weight_decay)
+        self.lr_t = torch.full((1,), float(lr), dtype=torch.float32, device=dev)  # read by nrk_clip_adam
+        self._lr_host = float(lr)
         fc = model.fc
         self.hp = _HeadParams(*[_lib.ptr(t) for t in (
             fc[0].weight, fc[0].bias, fc[1].weight, fc[1].bias, fc[4].weight, fc[4].bias, fc[5].weight, fc[5].bias,
@@ -447,12 +481,8 @@ class FusedTrainStep:
         # (rows -> ids, labels, f32 query, U = q W1q^T + b1, bf16 W1k) and an
         # attention backward that also forms dW1q / db1 and writes every
         # attention gradient in place: no torch ops left inside the step
-        self.fast = (table.dtype == torch.bfloat16 and d in (64, 128) and Dk == d and hist_ids.dim() == 2
-                     and hist_ids.shape[1] <= 128)
+        self.fast = (table.dtype == torch.bfloat16 and d in (64, 128) and Dk == d and hist_ids.shape[1] <= 128)
         if self.fast:
-            self.hist_all = hist_ids.to(torch.int32).contiguous()
-            self.tgt_all = target_ids.reshape(-1).to(torch.int32).contiguous()
-            self.lab_all = labels.reshape(-1).to(torch.float32).contiguous()
             L = hist_ids.shape[1]
             self.hist_b = torch.empty((B, L), dtype=torch.int32, device=dev)
             self.q_b = torch.empty((B, d), dtype=torch.float32, device=dev)
@@ -500,7 +530,8 @@ class FusedTrainStep:
             _lib.ptr(keys), _lib.ptr(hist), keys.shape[0], dtype, _lib.ptr(U), _lib.ptr(W1k), _lib.ptr(w2), 0.0, B,
             hist.shape[1], Dk, A, _lib.ptr(self.pooled), _lib.ptr(self.alpha), st), "din_attn_fwd")
         _lib.check(L_.nrk_din_head_train(
-            _lib.ptr(q), _lib.ptr(self.pooled), Dk, _lib.ptr(y), B, d, self.F, 0.1, 1e-5, self.p_drop, self.seed,
+            _lib.ptr(q), _lib.ptr(self.pooled), Dk, _lib.ptr(y), B, d, self.F, self.bn_momentum, self.bn_eps, self.p_drop,
+            self.seed,
             _lib.ptr(self.step_t), ctypes.byref(self.hp), _lib.ptr(self.logits), _lib.ptr(self.loss),
             _lib.ptr(self.dpooled), _lib.ptr(self.ws_head), self.ws_head.numel(), st), "din_head_train")
         gW2, gb2 = m.attn.attn[2].weight.grad, m.attn.attn[2].bias.grad
@@ -517,7 +548,8 @@ class FusedTrainStep:
             self.grad_hook(self.G)
         _lib.check(L_.nrk_clip_adam(
             _lib.ptr(self.P), _lib.ptr(self.G), _lib.ptr(self.M), _lib.ptr(self.V), self.n, _lib.ptr(self.step_t),
-            self.lr, self.betas[0], self.betas[1], self.eps, self.wd, self.clip, _lib.ptr(self.ws_opt),
+            self._lr_host, _lib.ptr(self.lr_t), self.betas[0], self.betas[1], self.eps, self.wd, self.clip,
+            _lib.ptr(self.ws_opt),
             self.ws_opt.numel(), st), "clip_adam")
 
     def _body_fast(self):
@@ -541,7 +573,8 @@ class FusedTrainStep:
             0.0, B, L, d, A, _lib.ptr(self.pooled), _lib.ptr(self.alpha), st), "din_attn_fwd")
         KernelTimer.push("fwd", t0)
         _lib.check(L_.nrk_din_head_train(
-            _lib.ptr(self.q_b), _lib.ptr(self.pooled), d, _lib.ptr(self.y_b), B, d, self.F, 0.1, 1e-5, self.p_drop,
+            _lib.ptr(self.q_b), _lib.ptr(self.pooled), d, _lib.ptr(self.y_b), B, d, self.F, self.bn_momentum,
+            self.bn_eps, self.p_drop,
             self.seed, _lib.ptr(self.step_t), ctypes.byref(self.hp), _lib.ptr(self.logits), _lib.ptr(self.loss),
             _lib.ptr(self.dpooled), _lib.ptr(self.ws_head), self.ws_head.numel(), st), "din_head_train")
         t0 = KernelTimer.mark("bwd")
@@ -555,11 +588,27 @@ class FusedTrainStep:
             self.grad_hook(self.G)
         _lib.check(L_.nrk_clip_adam(
             _lib.ptr(self.P), _lib.ptr(self.G), _lib.ptr(self.M), _lib.ptr(self.V), self.n, _lib.ptr(self.step_t),
-            self.lr, self.betas[0], self.betas[1], self.eps, self.wd, self.clip, _lib.ptr(self.ws_opt),
+            self._lr_host, _lib.ptr(self.lr_t), self.betas[0], self.betas[1], self.eps, self.wd, self.clip,
+            _lib.ptr(self.ws_opt),
             self.ws_opt.numel(), st), "clip_adam")
+
+    @property
+    def lr(self) -> float:
+        return float(self.optimizer.param_groups[0]["lr"])
+
+    @lr.setter
+    def lr(self, v: float):
+        self.optimizer.param_groups[0]["lr"] = float(v)
+
+    def _sync_lr(self):
+        lr = self.lr
+        if lr != self._lr_host:  # a scheduler changed the group's lr: refresh the device scalar
+            self.lr_t.fill_(lr)
+            self._lr_host = lr
 
     def step(self, batch_index: torch.Tensor):
         """One training step on rows `batch_index` (device int64, length B); returns the device loss."""
+        self._sync_lr()
         self.idx.copy_(batch_index, non_blocking=True)
         if self.graph is not None:
             self.graph.replay()

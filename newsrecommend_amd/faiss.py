@@ -96,6 +96,19 @@ class IndexFlat:
             raise AssertionError(f"expected (n, {self.d}) input, got {a.shape}")
         return torch.from_numpy(a).to(self.device, non_blocking=False), True
 
+    def _as_query(self, xq) -> torch.Tensor:
+        """Device-path query check: a GPU tensor on this index's device, (nq, d),
+        converted to contiguous float32 (bf16/f16/f64 or strided views are
+        converted, a host tensor or a wrong shape raises)."""
+        if not isinstance(xq, torch.Tensor):
+            raise TypeError("search_device takes a torch tensor on the GPU (use search() for numpy input)")
+        _lib.require_device(xq, what="search_device")
+        if xq.device != self.device:
+            raise _lib.NrkError(f"search_device: queries on {xq.device}, index on {self.device}")
+        if xq.dim() != 2 or xq.shape[1] != self.d:
+            raise AssertionError(f"expected (n, {self.d}) queries, got {tuple(xq.shape)}")
+        return xq.detach().to(torch.float32).contiguous()
+
     def add(self, x):
         """Append vectors (ids continue from ntotal), faiss Index.add."""
         xt, _ = self._as_input(x)
@@ -126,6 +139,7 @@ class IndexFlat:
         k = int(k)
         if k <= 0:
             raise ValueError("k must be positive")
+        xq = self._as_query(xq)
         nq = xq.shape[0]
         L = _lib.load()
         D = torch.empty((nq, k), dtype=torch.float32, device=self.device)
@@ -330,7 +344,11 @@ class IndexIVFFlat:
         self.nlist = int(nlist)
         self.metric_type = int(metric)
         self.nprobe = 1
+        # faiss's IndexIVF constructor: cp.niter = 10 (Level1Quantizer) and
+        # spherical k-means for inner-product indexes
         self.cp = Clustering(d, nlist)
+        self.cp.niter = 10
+        self.cp.spherical = self.metric_type == METRIC_INNER_PRODUCT
         self.device = quantizer.device if device is None else torch.device(device)
         self.is_trained = quantizer.ntotal == self.nlist
         self.flat = IndexFlat(d, metric, device=self.device)  # id-order rows, bf16 copy, norms, stats
@@ -416,11 +434,20 @@ class IndexIVFFlat:
         if k <= 0:
             raise ValueError("k must be positive")
         L = _lib.load()
+        xq = self.flat._as_query(xq)
         nq = xq.shape[0]
         nprobe = max(1, min(int(self.nprobe), self.nlist))
+        dev = self.device
         if probe is None:
             _, probe = self.quantizer.search_device(xq, nprobe)
-        dev = self.device
+        else:
+            _lib.require_device(probe, what="IndexIVFFlat.search_device")
+            if probe.shape != (nq, nprobe):
+                raise AssertionError(f"probe must be ({nq}, {nprobe}), got {tuple(probe.shape)}")
+            probe = probe.to(device=dev, dtype=torch.int64)
+            if int(probe.max().item()) >= self.nlist:
+                raise ValueError("probe holds a list number >= nlist")
+        probe = probe.contiguous()
         D = torch.empty((nq, k), dtype=torch.float32, device=dev)
         I = torch.empty((nq, k), dtype=torch.int64, device=dev)
         S = torch.empty((nq, k), dtype=torch.float64, device=dev) if exact_scores else None
@@ -434,7 +461,7 @@ class IndexIVFFlat:
                        "ivf_search_workspace")
             ws = self._workspace(sz.value)
             _lib.check(L.nrk_ivf_search(
-                _lib.ptr(xq), nq, _lib.ptr(probe.contiguous()), nprobe, _lib.ptr(f._xb[:n]) if n else None,
+                _lib.ptr(xq), nq, _lib.ptr(probe), nprobe, _lib.ptr(f._xb[:n]) if n else None,
                 _lib.ptr(self.xbh_ivf) if n else None, _lib.ptr(self.meta_ivf) if n else None, _lib.ptr(f._stats),
                 _lib.ptr(self.list_off), _lib.ptr(self.pos2id) if n else None,
                 _lib.ptr(self.pos2list) if n else None, self.nlist, n, self.max_list, self.d, k, self.metric_type,

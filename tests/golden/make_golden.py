@@ -239,6 +239,65 @@ def din_dataset_fixture(name, seed):
         )
 
 
+def din_rerank_fixture(name, seed, d=256, L=50, n_users=24, n_cand=201, n_items=1200):
+    """configs[4]'s re-rank shape through the reference's own EvalDataset +
+    evaluate() (DIN.py:21-57,155-193): d = 256, L = 50, 201 candidates per
+    user, DIN(256, 128, 32, 0.36) in eval mode with non-trivial BN statistics.
+    The item table is rounded to bf16-representable values so the same numbers
+    feed the reference's fp32 forward and the bf16-table GPU path."""
+    with tempfile.TemporaryDirectory() as wd:
+        rng = np.random.default_rng(seed)
+        ids = rng.choice(np.arange(1000, 1000 + 10 * n_items), size=n_items, replace=False)
+        table = torch.from_numpy(rng.standard_normal((n_items, d)).astype(np.float32) * 0.5)
+        table = table.to(torch.bfloat16).float().numpy()
+        emb = {int(a): table[i] for i, a in enumerate(ids)}
+        test_clicks, test_recs = {}, {}
+        for u in range(n_users):
+            n = int(rng.integers(2, L + 12))  # histories of 1..L+10 clicks: short, full and truncated
+            clicks = [int(x) for x in rng.choice(ids, size=n, replace=False)]
+            cands = rng.choice(ids, size=n_cand, replace=False).astype(np.int64)
+            if u % 4 != 3 and clicks[-1] not in set(cands.tolist()):
+                cands[int(rng.integers(0, n_cand))] = clicks[-1]
+            test_clicks[7000 + u] = clicks
+            test_recs[7000 + u] = cands
+        _write_news(wd, emb, {1: [int(ids[0]), int(ids[1])]}, test_clicks, test_recs)
+        ref = _import_ref("DIN", wd)
+        torch.manual_seed(seed)
+        model = ref.DIN(d, 128, 32, 0.36)
+        _random_bn_stats(model, torch.Generator().manual_seed(seed + 1))
+        ev = ref.EvalDataset(L)
+        loader = torch.utils.data.DataLoader(ev, batch_size=8, shuffle=False, num_workers=0,
+                                             collate_fn=ref.custom_collate_fn)
+        ev_loss, ev_ndcg = ref.evaluate(model, loader, torch.nn.BCEWithLogitsLoss(), torch.device("cpu"), 5)
+        per_logits, per_ndcg = [], []
+        model.eval()
+        with torch.no_grad():
+            for b in loader:
+                for i in range(len(b["uid"])):
+                    c = b["cand_embs"][i]
+                    lg = model(c, b["history_emb"][i].unsqueeze(0).expand(c.size(0), -1, -1)).view(-1)
+                    per_logits.append(lg.numpy())
+                    probs = torch.sigmoid(lg).numpy()
+                    labs = b["labels"][i].numpy()
+                    nd = 0.0
+                    for rank, idx in enumerate(np.argsort(-probs)[:5], start=1):  # DIN.py:183-188
+                        if labs[idx] == 1:
+                            nd = 1 / np.log2(rank + 1)
+                            break
+                    per_ndcg.append(nd)
+        assert abs(float(np.mean(per_ndcg)) - ev_ndcg) < 1e-12
+        np.savez_compressed(
+            os.path.join(OUT, f"{name}.npz"),
+            d=d, L=L, A=128, F=32, item_ids=ids.astype(np.int64), table=table,
+            ev_uid=np.array([s["uid"] for s in ev.data], np.int64),
+            ev_hist=_pad_hist([s["history"] for s in ev.data], L),
+            ev_cand=np.stack([np.asarray(s["candidates"], np.int64) for s in ev.data]),
+            ev_lab=np.stack([np.asarray(s["labels"], np.int64) for s in ev.data]),
+            ev_loss=np.float64(ev_loss), ev_ndcg=np.float64(ev_ndcg),
+            ev_logits=np.stack(per_logits), ev_ndcg_user=np.array(per_ndcg, np.float64), **_sd(model),
+        )
+
+
 def embedding_fixture(name, seed, n_articles=48):
     """ArticleEmbeddingModel + inference() (embedding_generate.py:51-65,109-131)."""
     with tempfile.TemporaryDirectory() as wd:
@@ -280,6 +339,7 @@ def main():
     din_train_fixture("din_train_c3", d=128, A=128, F=32, B=32, L=50, n_items=400, seed=14)
     din_dataset_fixture("din_dataset", seed=15)
     embedding_fixture("embedding_infer", seed=16)
+    din_rerank_fixture("din_rerank_c5", seed=17)
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))

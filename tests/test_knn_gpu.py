@@ -181,3 +181,74 @@ def test_forced_fallback_paths(gpu, monkeypatch, cap):
         for k in (1, 5, 40):
             idx = _check(xq, xb, k, metric, gpu)
             assert int(idx.last_fallback.item()) == 200
+
+
+@pytest.mark.parametrize("metric", [ko.METRIC_IP, ko.METRIC_L2])
+@pytest.mark.parametrize("nb,nq,d,k", [(300, 4100, 128, 32), (300, 777, 256, 1), (1, 70, 32, 3), (63, 65, 100, 63),
+                                       (4096, 5000, 32, 10), (2048, 300, 300, 200), (500, 129, 64, 700)])
+def test_small_corpus_exact_path(gpu, metric, nb, nq, d, k):
+    """nb <= 4096 (the coarse quantizer, k-means assignment, IndexIVFFlat.add):
+    the fp64 tile-GEMM path (k = 1: fused arg-best; k > 1: goodness chunks +
+    per-query bitonic select, several chunks at nb = 4096) equals the oracle
+    bit for bit, including k > nb padding, d > 256 and exact duplicates."""
+    xq, xb = _mixture(nb, nq, d, seed=nb + nq + d + k)
+    if nb > 10:
+        xb[nb // 2] = xb[3]
+        xq[0] = xb[3]
+    from newsrecommend_amd import faiss as nf
+
+    idx = nf.IndexFlat(d, metric)
+    idx.add(xb)
+    D, I, S = idx.search_device(torch.from_numpy(xq).cuda(), k, exact_scores=True)
+    Do, Io, So = ko.exact_search(xq, xb, k, metric)
+    np.testing.assert_array_equal(I.cpu().numpy(), Io)
+    np.testing.assert_array_equal(D.cpu().numpy(), Do)
+    np.testing.assert_array_equal(S.cpu().numpy(), So)
+    assert int(idx.last_fallback.item()) == 0
+
+
+def test_small_corpus_assignment_at_scale(gpu):
+    """IndexIVFFlat.add's assignment shape: 200k rows x 300 centroids, k = 1."""
+    from newsrecommend_amd import faiss as nf
+
+    xq, xb = _mixture(300, 200_000, 128, seed=77)
+    idx = nf.IndexFlatL2(128)
+    idx.add(xb)
+    D, I = idx.search(xq, 1)
+    Do, Io, _ = ko.exact_search(xq, xb, 1, ko.METRIC_L2)
+    np.testing.assert_array_equal(I, Io)
+    np.testing.assert_array_equal(D, Do)
+
+
+def test_search_device_input_checks(gpu):
+    """search_device converts bf16 / strided queries and refuses host tensors
+    and wrong widths; probes are normalised to int64."""
+    from newsrecommend_amd import _lib, faiss as nf
+
+    xq, xb = _mixture(20_000, 64, 64, seed=12)
+    idx = nf.IndexFlatIP(64)
+    idx.add(xb)
+    q = torch.from_numpy(xq).cuda()
+    _, I_ref = idx.search_device(q, 5)
+    wide = torch.zeros((64, 128), device="cuda")
+    wide[:, ::2] = q
+    _, I_view = idx.search_device(wide[:, ::2], 5)  # non-contiguous view
+    assert torch.equal(I_view, I_ref)
+    _, I_bf = idx.search_device(q.to(torch.bfloat16), 5)  # converted to f32 (bf16 values)
+    _, I_bf_ref = idx.search_device(q.to(torch.bfloat16).float(), 5)
+    assert torch.equal(I_bf, I_bf_ref)
+    with pytest.raises(_lib.NrkError):
+        idx.search_device(q.cpu(), 5)
+    with pytest.raises(AssertionError):
+        idx.search_device(q[:, :32], 5)
+    ivf = nf.IndexIVFFlat(nf.IndexFlatL2(64), 64, 16, nf.METRIC_L2)
+    ivf.cp.niter = 2
+    ivf.train(xb)
+    ivf.add(xb)
+    ivf.nprobe = 4
+    _, probe = ivf.quantizer.search_device(q, 4)
+    _, I1 = ivf.search_device(q, 5, probe=probe)
+    _, I2 = ivf.search_device(q, 5, probe=probe.to(torch.int32))
+    assert torch.equal(I1, I2)
+    with pytest.raises(AssertionError):
+        ivf.search_device(q, 5, probe=probe[:, :2])
