@@ -155,25 +155,37 @@ def _recall(args, xq, xb_host, D, I, metric):
     return rec, bool(np.array_equal(Ig, Io))
 
 
-def _cpu_flat(args, xq, xb_host, metric):
-    """oracle.knn_oracle.faiss_port (faiss-cpu's blocked-BLAS flat search,
-    restated) on a bounded query sample against the FULL corpus."""
-    from oracle import knn_oracle as ko
+def _timed_sample(fn, n_total, n0, budget_s, align=64):
+    """Run fn(n) on a first sample of n0 units, then scale n so the second run
+    takes about budget_s; returns (n, seconds) of the second run."""
+    t = time.perf_counter()
+    fn(n0)
+    dt = max(time.perf_counter() - t, 1e-3)
+    n = int(min(n_total, max(n0, n0 * budget_s / dt)))
+    n = max(n0, (n // align) * align)
+    t = time.perf_counter()
+    fn(n)
+    return n, time.perf_counter() - t
 
-    q = xq.cpu().numpy()
-    n = 64
-    t = time.perf_counter()
-    ko.faiss_port(q[:n], xb_host, args.k, metric)
-    dt = time.perf_counter() - t
-    budget = args.cpu_seconds
-    n2 = int(min(args.nq, max(n, n * budget / max(dt, 1e-3))))
-    n2 = max(n, (n2 // 64) * 64)
-    t = time.perf_counter()
-    ko.faiss_port(q[:n2], xb_host, args.k, metric)
-    dt = time.perf_counter() - t
-    return {"value": n2 / dt, "unit": "queries/s", "cores": cpu_cores(), "kind": "port",
-            "sample": f"{n2} of the {args.nq} queries x full {args.nb}x{args.d} corpus, k={args.k}, "
-                      f"oracle.knn_oracle.faiss_port (numpy fp32 BLAS blocks + top-k), {dt:.1f} s"}
+
+def _cpu_flat(args, xq, xb_host, metric, nb=None, d=None, k=None):
+    """faiss-cpu IndexFlat's blocked-sgemm search restated on all host cores
+    (oracle/cpu_baselines.flat_search, torch CPU kernels), on a bounded query
+    sample against the FULL corpus."""
+    from oracle import cpu_baselines as cb
+
+    cores = cpu_cores()
+    torch.set_num_threads(cores)
+    q = xq.cpu()
+    xb = torch.from_numpy(xb_host)
+    norms = (xb * xb).sum(1) if metric == 1 else None
+    k = args.k if k is None else k
+    n, dt = _timed_sample(lambda n: cb.flat_search(q[:n], xb, k, metric, xb_norms=norms), q.shape[0], 64,
+                          args.cpu_seconds)
+    return {"value": n / dt, "unit": "queries/s", "cores": cores, "kind": "port",
+            "sample": f"{n} of the {q.shape[0]} queries x full {xb.shape[0]}x{xb.shape[1]} corpus, k={k}, "
+                      f"oracle.cpu_baselines.flat_search (faiss exhaustive_*_blas restated: torch-CPU fp32 sgemm "
+                      f"blocks + running top-k, {cores} threads), {dt:.1f} s"}
 
 
 def _pmc_traffic(args, world):
@@ -252,12 +264,38 @@ def bench_ivf(args, rank, world, dev):
         _, If = flat.search_device(xq, k)
         Ig, Ie = I.cpu().numpy(), If.cpu().numpy()
         out["recall_at_5"] = float(np.mean([len(set(a[:5]) & set(b[:5])) / min(5, k) for a, b in zip(Ig, Ie)]))
+        if not args.no_flat_l2:
+            out["flat_l2_10m"] = _flat_l2_leg(args, flat, xq, k)
         del flat
         if world == 1:
             out["oracle_match"] = _ivf_oracle_check(index, xb, xq, I, k, nprobe)
             if not args.no_cpu_baseline:
                 out["cpu_baseline"] = _cpu_ivf(args, index, xb, xq, k, nprobe)
     return out
+
+
+def _flat_l2_leg(args, flat, xq, k):
+    """IndexFlatL2 over the same 10M x 128 corpus (exact flat L2, single GPU):
+    QPS, stage split and the number of queries the L2 certificate could not
+    cover (they take the fp64 fallback scan)."""
+    from newsrecommend_amd import _lib
+
+    for _ in range(2):
+        flat.search_device(xq, k)
+    torch.cuda.synchronize()
+    steps = max(3, min(args.steps, 10))
+    evs = [_lib.StageEvents() for _ in range(steps)]
+    t0 = time.perf_counter()
+    for e in evs:
+        flat.search_device(xq, k, stage_events=e)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    st = np.array([e.elapsed_ms() for e in evs]).mean(0)
+    return {"metric": "IndexFlatL2 QPS", "value": xq.shape[0] * steps / el, "unit": "queries/s",
+            "ms_per_step": el / steps * 1e3, "config": f"flat L2 {flat.ntotal}x{flat.d}, batch={xq.shape[0]}, k={k}",
+            "stages_ms": {"query_prepare+tau_prepass": float(st[0]), "screen": float(st[1]),
+                          "merge_rescore": float(st[2]), "exact_fallback": float(st[3])},
+            "fallback_queries": int(flat.last_fallback.item())}
 
 
 def _ivf_oracle_check(index, xb, xq, I, k, nprobe):
@@ -272,32 +310,77 @@ def _ivf_oracle_check(index, xb, xq, I, k, nprobe):
 
 
 def _cpu_ivf(args, index, xb, xq, k, nprobe):
-    """faiss-cpu IndexIVFFlat's algorithm restated with numpy fp32 BLAS
-    (coarse GEMM, then one GEMV per query over its probed lists' rows + top-k),
+    """faiss-cpu IndexIVFFlat.search restated on all host cores
+    (oracle/cpu_baselines.ivf_search: coarse sgemm top-nprobe, then each
+    probed list scanned in place from a list-major copy, batched per list),
     on a bounded query sample."""
-    cent = index.quantizer._xb[: index.local.nlist].cpu().numpy()
-    assign = index.local._assign.cpu().numpy()
-    xbn = xb.cpu().numpy()
-    order = np.argsort(assign, kind="stable")
-    off = np.zeros(index.local.nlist + 1, np.int64)
-    np.cumsum(np.bincount(assign, minlength=index.local.nlist), out=off[1:])
-    lists = [order[off[l]:off[l + 1]] for l in range(index.local.nlist)]
-    norms = (xbn * xbn).sum(1)
-    q = xq.cpu().numpy()
-    t = time.perf_counter()
-    n = 0
-    while n < q.shape[0] and (time.perf_counter() - t < args.cpu_seconds / 2 or n < 8):
-        qq = q[n]
-        dc = (cent * cent).sum(1) - 2 * cent @ qq
-        probe = np.argpartition(dc, nprobe)[:nprobe]
-        ids = np.concatenate([lists[l] for l in probe])
-        dist_ = norms[ids] - 2 * (xbn[ids] @ qq)
-        top = ids[np.argpartition(dist_, k)[:k]]
-        n += 1
-    dt = time.perf_counter() - t
-    return {"value": n / dt, "unit": "queries/s", "cores": cpu_cores(), "kind": "port",
-            "sample": f"{n} queries (nprobe={nprobe}) over the {args.ivf_nb}x{args.d} IVF index, numpy fp32 BLAS "
-                      f"per query (faiss IndexIVFFlat scan restated), {dt:.1f} s"}
+    from oracle import cpu_baselines as cb
+
+    cores = cpu_cores()
+    torch.set_num_threads(cores)
+    lists = cb.IvfLists(xb.cpu().numpy(), index.local._assign.cpu().numpy(),
+                        index.quantizer._xb[: index.local.nlist].cpu().numpy())
+    q = xq.cpu()
+    n, dt = _timed_sample(lambda n: cb.ivf_search(q[:n], lists, nprobe, k, 1), q.shape[0], 64, args.cpu_seconds)
+    return {"value": n / dt, "unit": "queries/s", "cores": cores, "kind": "port",
+            "sample": f"{n} of the {q.shape[0]} queries (nprobe={nprobe}) over the {xb.shape[0]}x{xb.shape[1]} IVF "
+                      f"index, oracle.cpu_baselines.ivf_search (faiss IndexIVFFlat restated: in-place list scans, "
+                      f"torch-CPU sgemm per list, {cores} threads), {dt:.1f} s"}
+
+
+# -------------------------------------------------- N1 (north_star) --
+def bench_n1(args, rank, world, dev, index, xb):
+    """north_star's target workload: exact flat IP retrieval, k = 5, over the
+    10M x 256 corpus (configs[4]'s corpus, sharded over the ranks), 4096-query
+    batches from the same mixture.  One step = one batch.  Recall@5 and exact
+    match on a query sample vs the oracle; cpu_baseline = the faiss-cpu
+    IndexFlatIP port on all host cores over a bounded query sample."""
+    from newsrecommend_amd import _lib
+    from newsrecommend_amd.data import clustered_corpus
+
+    n, d, nq, k = xb.shape[0], xb.shape[1], args.nq, 5
+    xq = clustered_corpus(nq, d, seed=4321, device=dev)
+    for _ in range(args.warmup):
+        index.search_device(xq, k)
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        D, I = index.search_device(xq, k)
+    barrier(world)
+    el = max_over_ranks(time.perf_counter() - t0, world, dev)
+    evs = [_lib.StageEvents() for _ in range(min(args.steps, 10))]
+    for e in evs:
+        index.local.search_device(xq, k, id_offset=index.offset, stage_events=e)
+    torch.cuda.synchronize()
+    st = np.array([e.elapsed_ms() for e in evs]).mean(0)
+    flops = 2.0 * nq * index.local.ntotal * d
+    achieved = flops / (st[1] * 1e-3) / 1e12
+    out = {
+        "metric": "retrieval QPS @ recall@5 (north_star target: 10M x 256, k = 5)", "value": nq * args.steps / el,
+        "unit": "queries/s", "ms_per_step": el / args.steps * 1e3,
+        "config": {"workload": f"north_star: flat IP {n}x{d}, batch={nq}, k={k}",
+                   "parallelism": f"corpus-shard{world} + all_gather merge" if world > 1 else "single GPU"},
+        "stages_ms": {"query_prepare+tau_prepass": float(st[0]), "screen": float(st[1]),
+                      "merge_rescore": float(st[2]), "exact_fallback": float(st[3])},
+        "fallback_queries": int(index.local.last_fallback.item()),
+        "roofline": {"bound": "mfma", "kernel": "screen_kernel (bf16 v_mfma_f32_32x32x16, dp 256)",
+                     "achieved": achieved, "peak": BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / BF16_DENSE_TFLOPS, "traffic": None,
+                     "algorithmic": f"2*nq*nb_local*d = {flops:.4g} flop per launch"},
+    }
+    if rank == 0:
+        from oracle import knn_oracle as ko
+
+        xb_host = xb.cpu().numpy()
+        sample = np.arange(0, nq, nq // 16)
+        _, Io, _ = ko.exact_search(xq[sample].cpu().numpy(), xb_host, k, 0)
+        Ig = I[sample].cpu().numpy()
+        out["recall_at_5"] = float(np.mean([len(set(a) & set(b)) / k for a, b in zip(Ig, Io)]))
+        out["exact_match_sample"] = bool(np.array_equal(Ig, Io))
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = _cpu_flat(args, xq, xb_host, 0, k=k)
+        del xb_host
+    return out
 
 
 # ------------------------------------------------------------------ E2E --
@@ -318,6 +401,7 @@ def bench_e2e(args, rank, world, dev):
     index = ShardedIndexFlat(d, 0, device=dev)
     index.add_full(xb)
     table = xb.to(torch.bfloat16)  # the DIN item table: the same embeddings, bf16 (full copy on every rank)
+    n1 = bench_n1(args, rank, world, dev, index, xb) if not args.no_n1 else None
     del xb
     torch.cuda.empty_cache()
     g = torch.Generator(device=dev).manual_seed(11)
@@ -372,6 +456,8 @@ def bench_e2e(args, rank, world, dev):
         "ndcg_at_5_mean_rank0": float(nd.mean().item()),
         "fallback_queries": int(index.local.last_fallback.item()),
     }
+    if n1 is not None:
+        out["n1_retrieval_10m_256_k5"] = n1
     if rank == 0:
         # re-rank parity on a few users: the reference's per-user forward
         # (DIN.py:168-173: model(cand, his.expand(C, -1, -1))) on the same rows
@@ -465,6 +551,8 @@ def bench_din(args, rank, world, dev):
     # outputs (fwd: pooled, alpha); bwd adds dpooled, alpha, q and the dU row
     fwd_bytes = B * (4 * L + L * d * 2 + 4 * A + 4 * d + 4 * L)
     bwd_bytes = B * (4 * L + L * d * 2 + 4 * A + 4 * d + 4 * L + 4 * d + 2 * 4 * A)
+    STEP_BYTES = L * d * 2 + d * 2 + 4 * (L + 1) + 4
+    step_gbs = STEP_BYTES * B * args.steps / el / 1e9  # per GPU
     fwd_gbs = fwd_bytes / (fwd_ms * 1e-3) / 1e9
     bwd_gbs = bwd_bytes / (bwd_ms * 1e-3) / 1e9
     out = {
@@ -476,6 +564,10 @@ def bench_din(args, rank, world, dev):
                             "fused head/optimizer kernels + RCCL grad all_reduce") if fused else "eager torch"},
         "final_loss": float(loss.reshape(-1)[0].item()),
         "kernels_ms": {"attn_fwd": fwd_ms, "attn_bwd (deep8 + dwq + reduce)" if fused else "attn_bwd+reduce": bwd_ms},
+        "roofline_step": {"bound": "hbm", "achieved": step_gbs, "peak": HBM_GBS, "unit": "GB/s",
+                          "frac": step_gbs / HBM_GBS, "traffic": None,
+                          "algorithmic": f"{STEP_BYTES} B/sample (SURVEY.md 8d: L*d*2 + d*2 + 4*(L+1) + 4) x "
+                                         f"samples/s over the whole step"},
         "roofline_fwd": {"bound": "hbm", "achieved": fwd_gbs, "peak": HBM_GBS, "unit": "GB/s",
                          "frac": fwd_gbs / HBM_GBS, "traffic": None,
                          "algorithmic": f"{fwd_bytes // B} B/sample x {B} samples"},
@@ -509,37 +601,37 @@ def _din_rate(table, hist, tgt, lab, d, A, F, B, dev, steps=10):
     return B * steps / (time.perf_counter() - t0)
 
 
-def _cpu_din(args, n_items, L, d, A, F):
-    """oracle.din_oracle (numpy float64 restatement of DIN.py's train step:
-    forward, backward, clip, Adam) on a bounded sample of rows."""
-    from oracle import din_oracle as o
-    from newsrecommend_amd.din import DIN
+def _cpu_din(args, n_items, L, d, A, F, B=4096):
+    """The reference's PyTorch-CPU fp32 train step (oracle/din_torch_ref,
+    pinned to DIN.py's own train() by tests/test_oracle_din.py) on all host
+    cores, batch B, including the history gather from a host table
+    (TrainDataset.__getitem__, DIN.py:81-92), on a bounded number of steps."""
+    from oracle.din_torch_ref import TorchDIN, train_step
 
-    rng = np.random.default_rng(0)
-    Bc = 1024
-    table = (rng.standard_normal((20000, d)) * 0.5).astype(np.float32)
-    m = DIN(d, A, F, 0.0)
-    p = {k: v.numpy().astype(np.float64) for k, v in m.state_dict().items() if "num_batches" not in k}
-    params = {k: v for k, v in p.items() if "running" not in k}
-    state = {}
-    t = time.perf_counter()
-    n = 0
-    while time.perf_counter() - t < args.cpu_seconds / 2 or n < 2:
-        ln = rng.integers(1, L + 1, Bc)
-        idx = np.where(np.arange(L)[None] < ln[:, None], rng.integers(0, 20000, (Bc, L)), -1)
-        keys = np.where(idx[..., None] >= 0, table[np.maximum(idx, 0)], 0.0)
-        q = table[rng.integers(0, 20000, Bc)]
-        y = (rng.random((Bc, 1)) < 0.5).astype(np.float64)
-        full = dict(p)
-        full.update(params)
-        lg, _, _, c = o.din_forward(full, q, keys, train=True)
-        g = o.din_backward(full, c, lg, y)
-        g, _ = o.clip_grad_norm(g, 1.0)
-        params = o.adam_step(params, g, state, 1.62e-3, 8.96e-5)
-        n += 1
-    dt = time.perf_counter() - t
-    return {"value": n * Bc / dt, "unit": "samples/s", "cores": cpu_cores(), "kind": "port",
-            "sample": f"{n} train steps x {Bc} rows (L={L}, d={d}), oracle.din_oracle numpy fp64, {dt:.1f} s"}
+    cores = cpu_cores()
+    torch.set_num_threads(cores)
+    g = torch.Generator().manual_seed(0)
+    n_tab = min(n_items, 200_000)
+    table = torch.randn((n_tab, d), generator=g) * 0.5
+    torch.manual_seed(42)
+    m = TorchDIN(d, A, F, 0.36).train()
+    opt = torch.optim.Adam(m.parameters(), lr=1.62e-3, weight_decay=8.96e-5)
+    crit = torch.nn.BCEWithLogitsLoss()
+
+    def steps(n):
+        for _ in range(n):
+            ln = torch.randint(1, L + 1, (B, 1), generator=g)
+            ids = torch.randint(0, n_tab, (B, L), generator=g)
+            keys = table[ids] * (torch.arange(L)[None, :] < ln).unsqueeze(-1)
+            q = table[torch.randint(0, n_tab, (B,), generator=g)]
+            y = (torch.rand((B, 1), generator=g) < 0.5).float()
+            train_step(m, opt, crit, q, keys, y)
+
+    n, dt = _timed_sample(steps, 10**9, 2, args.cpu_seconds / 2, align=1)
+    return {"value": n * B / dt, "unit": "samples/s", "cores": cores, "kind": "port",
+            "sample": f"{n} train steps x {B} rows (L={L}, d={d}, A={A}, F={F}), oracle.din_torch_ref "
+                      f"(the reference's DIN train step in PyTorch-CPU fp32, {cores} threads, gather included), "
+                      f"{dt:.1f} s"}
 
 
 def main():
@@ -567,6 +659,8 @@ def main():
     ap.add_argument("--din-eager", action="store_true", help="no HIP-graph capture of the DIN train step")
     ap.add_argument("--din-sweep", type=int, default=1, help="also report the fused step at B=16384, 65536")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-n1", action="store_true", help="skip the north_star 10M x 256 k=5 retrieval record")
+    ap.add_argument("--no-flat-l2", action="store_true", help="skip the IndexFlatL2 10M x 128 record")
     args = ap.parse_args()
 
     rank, world, dev = setup(args)

@@ -615,3 +615,52 @@ class FusedTrainStep:
         else:
             self._body()
         return self.loss
+
+
+def fit(model, table, hist_ids, target_ids, labels, eval_loader, epochs=10, batch_size=64, lr=1.62e-3,
+        weight_decay=8.96e-5, clip=1.0, k=5, checkpoint=None, scheduler=None, seed=42, graph=True, log=None):
+    """DIN.py:225-257 (main()) on the fused train step: per epoch, shuffle the
+    rows (DataLoader(shuffle=True) -> torch.randperm from a generator seeded
+    with `seed`), train on every FULL batch (the fused step has a fixed batch;
+    the reference's last partial batch of n % batch_size rows is dropped),
+    report the mean of the per-batch losses (DIN.py:153), evaluate
+    (DIN.py:155-193), step the scheduler — by default
+    ReduceLROnPlateau(mode='min', factor=0.5, patience=1) on the validation
+    loss (DIN.py:246,254), any other LR scheduler with step() — and save the
+    state_dict whenever NDCG@k beats the best so far (DIN.py:255-257).
+    Returns one dict per epoch (train_loss, val_loss, ndcg, lr)."""
+    dev = table.device
+    trainer = FusedTrainStep(model, table, hist_ids, target_ids, labels, batch_size, lr=lr,
+                             weight_decay=weight_decay, clip=clip, graph=graph)
+    opt = trainer.optimizer
+    plateau = scheduler is None
+    sched = (torch.optim.lr_scheduler.ReduceLROnPlateau(opt, mode="min", factor=0.5, patience=1) if plateau
+             else scheduler(opt))
+    crit = nn.BCEWithLogitsLoss()
+    gen = torch.Generator(device=dev).manual_seed(seed)
+    n, B = trainer.hist_all.shape[0], trainer.B
+    nb = n // B
+    best, history = 0.0, []
+    for epoch in range(epochs):
+        lr_epoch = trainer.lr
+        model.train()
+        perm = torch.randperm(n, generator=gen, device=dev)
+        total = torch.zeros((), dtype=torch.float64, device=dev)
+        for b in range(nb):
+            total += trainer.step(perm[b * B:(b + 1) * B])[0]
+        train_loss = (total / max(nb, 1)).item()
+        val_loss, ndcg = evaluate(model, eval_loader, crit, dev, k)
+        if plateau:
+            sched.step(val_loss)
+        else:
+            opt._opt_called = True  # the fused step is the optimizer step (silences torch's order check)
+            sched.step()
+        history.append({"epoch": epoch + 1, "train_loss": train_loss, "val_loss": val_loss, "ndcg": ndcg,
+                        "lr": lr_epoch})
+        if log is not None:
+            log(f"Epoch {epoch + 1}: Train {train_loss}, Validate {val_loss}, NDCG {ndcg}")
+        if ndcg > best:
+            best = ndcg
+            if checkpoint is not None:
+                torch.save({k_: v.detach().clone() for k_, v in model.state_dict().items()}, checkpoint)
+    return history

@@ -34,15 +34,33 @@ def unpack_results(buf: torch.Tensor, k: int):
 
 
 def all_gather_results(S: torch.Tensor, I: torch.Tensor, group=None):
-    """One collective for all shards' lists.  Works on nccl (RCCL) and gloo."""
+    """One collective for all shards' lists.  RCCL gathers device buffers in
+    place; gloo (CPU tests, or GPU ranks sharing one card in tests) gathers
+    host copies of them."""
     world = dist.get_world_size(group)
     local = pack_results(S, I)
-    out = torch.empty((world, *local.shape), dtype=local.dtype, device=local.device)
     if dist.get_backend(group) == "nccl":
+        out = torch.empty((world, *local.shape), dtype=local.dtype, device=local.device)
         dist.all_gather_into_tensor(out, local, group=group)
     else:
-        dist.all_gather(list(out.unbind(0)), local, group=group)
+        host = local.cpu()
+        out = torch.empty((world, *host.shape), dtype=host.dtype)
+        dist.all_gather(list(out.unbind(0)), host, group=group)
+        out = out.to(local.device)
     return unpack_results(out, S.shape[1])
+
+
+def all_reduce_mean_(t: torch.Tensor, group=None) -> torch.Tensor:
+    """In-place mean over the ranks of `group` (the data-parallel gradient
+    hook of FusedTrainStep): RCCL on device buffers, a host copy on gloo."""
+    world = dist.get_world_size(group)
+    if dist.get_backend(group) == "nccl":
+        dist.all_reduce(t, group=group)
+    else:
+        h = t.cpu()
+        dist.all_reduce(h, group=group)
+        t.copy_(h)
+    return t.div_(world)
 
 
 class ShardedIndexFlat:

@@ -1,0 +1,250 @@
+"""GPU parity of the bf16 DIN kernels the benchmark records time, against the
+float64 oracle (oracle/din_oracle.py, pinned to the reference's own DIN.py by
+tests/test_oracle_din.py) and against the reference's evaluate() fixture.
+
+  * FusedTrainStep fast path at configs[2]'s shape (d = 128, A = 128, F = 32,
+    L = 50, bf16 table, B = 512, dropout 0): loss, every clipped gradient, the
+    BatchNorm running statistics and the parameters after two clip + Adam steps
+    (DIN.py:143-151).
+  * nrk_din_rerank_attn (the shared-history re-rank configs[4] runs) at
+    d = 256, L = 50, C = 201: logits and NDCG@5 (DIN.py:155-193).
+
+Two oracles per check:
+  "emulated" — the oracle fed exactly the kernel's inputs: the bf16 table
+      (upcast, exact) AND W1[:, d:] rounded to bf16 the way the kernels round
+      it.  What remains is fp32 accumulation order, so tolerances are tight.
+  "reference" — the oracle with the model's f32 W1 (the reference's exact
+      arithmetic).  The gap adds the bf16 rounding of W1k (relative 2^-9).
+Tolerances (written here and in DESIGN.md "Parity"):
+  train, emulated (each of 2 steps checked from the kernel's state before
+      it): loss 2e-5 abs; each clipped gradient tensor max-abs error
+      <= 2e-3 * its max |g| + 1e-7; parameters after the clip + Adam step
+      5e-5 abs, except entries whose new first moment lies within the
+      gradient error of 0 (Adam's sign-normalised step: bound 2 lr);
+      BN running stats 1e-5 abs.
+  train, reference: loss 2e-3 abs.
+  re-rank, emulated: logits 1e-3 abs;  reference: 2e-2 abs.  NDCG@5 per user
+      equal wherever the positive's logit is more than 2x the tolerance away
+      from every other candidate's logit (rank well defined under the bound).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from tests.conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf16_round(a: np.ndarray) -> np.ndarray:
+    return torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(torch.bfloat16).float().numpy()
+
+
+def _params_f64(model, emulate: bool):
+    d = model.attn.attn[0].weight.shape[1] // 2
+    p = {k: v.detach().cpu().numpy().astype(np.float64) for k, v in model.state_dict().items()
+         if "num_batches" not in k}
+    if emulate:
+        W1 = p["attn.attn.0.weight"].copy()
+        W1[:, d:] = _bf16_round(W1[:, d:].astype(np.float32))
+        p["attn.attn.0.weight"] = W1
+    return p
+
+
+def _keys(table_f32, hist):
+    return np.where(hist[..., None] >= 0, table_f32[np.maximum(hist, 0)], 0.0)
+
+
+def _bn_inputs(cache, pooled, q):
+    """Inputs of the three train-mode BatchNorms (dropout 0), from the oracle cache."""
+    return [np.concatenate([q, pooled], 1), np.maximum(cache["pre.relu1"], 0), np.maximum(cache["pre.relu2"], 0)]
+
+
+def test_fused_train_step_fast_path_vs_oracle_c3_shape(gpu):
+    from newsrecommend_amd.data import synthetic_click_rows
+    from newsrecommend_amd.din import DIN, FusedTrainStep
+    from oracle import din_oracle as o
+
+    dev = torch.device("cuda")
+    d, A, F, L, B, N = 128, 128, 32, 50, 512, 6000
+    lr, wd = 1.62e-3, 8.96e-5
+    g = torch.Generator(device=dev).manual_seed(21)
+    table = (torch.randn((N, d), generator=g, device=dev) * 0.5).to(torch.bfloat16)
+    hist, tgt, lab = synthetic_click_rows(4 * B, N, L, seed=9, device=dev)
+    torch.manual_seed(3)
+    model = DIN(d, A, F, 0.0).to(dev)
+    fused = FusedTrainStep(model, table, hist, tgt, lab, B, lr=lr, weight_decay=wd, clip=1.0, graph=False)
+    assert fused.fast
+    T = table.float().cpu().numpy().astype(np.float64)
+    H, Tg, Y = hist.cpu().numpy(), tgt.cpu().numpy(), lab.cpu().numpy().reshape(-1, 1).astype(np.float64)
+    shapes = [(n, prm.shape, prm.numel()) for n, prm in model.named_parameters()]
+
+    def unflat(buf):  # flat fused buffer -> {name: f64 array}, model.parameters() order
+        out, o_ = {}, 0
+        v = buf.detach().cpu().numpy().astype(np.float64)
+        for n, shp, k in shapes:
+            out[n] = v[o_:o_ + k].reshape(shp)
+            o_ += k
+        return out
+
+    # Each step is checked from the kernel's own state (parameters, Adam
+    # moments, BN statistics before the step): a multi-step trajectory is not
+    # comparable entry by entry, because Adam's sign-normalised first steps turn
+    # gradient rounding in near-zero entries into +-lr parameter differences.
+    for s in range(2):
+        params = unflat(fused.P)
+        state = {"step": s}
+        for n, m_ in unflat(fused.M).items():
+            state[f"m.{n}"] = m_.copy()
+        for n, v_ in unflat(fused.V).items():
+            state[f"v.{n}"] = v_.copy()
+        run = {k: v.detach().cpu().numpy().astype(np.float64) for k, v in model.state_dict().items() if "running" in k}
+        rows = np.arange(s * B, (s + 1) * B)
+        loss = fused.step(torch.from_numpy(rows).to(dev)).item()
+        q, keys, y = T[Tg[rows]], _keys(T, H[rows]), Y[rows]
+        full = {**run, **params}
+        emu = dict(full)  # the kernels' inputs: W1k rounded to bf16
+        W1 = emu["attn.attn.0.weight"].copy()
+        W1[:, d:] = _bf16_round(W1[:, d:].astype(np.float32))
+        emu["attn.attn.0.weight"] = W1
+        lo, pooled, _, cache = o.din_forward(emu, q, keys, train=True)
+        g_cl, _ = o.clip_grad_norm(o.din_backward(emu, cache, lo, y), 1.0)
+        print(f"step {s} loss err (emulated) {abs(loss - o.bce_with_logits(lo, y)):.3g}")
+        assert abs(loss - o.bce_with_logits(lo, y)) < 2e-5, (s, loss, o.bce_with_logits(lo, y))
+        lo_ref, _, _, _ = o.din_forward(full, q, keys, train=True)
+        assert abs(loss - o.bce_with_logits(lo_ref, y)) < 2e-3
+        flip = {}
+        for n, prm in model.named_parameters():  # clipped gradients (what clip_grad_norm_ leaves in .grad)
+            ref = g_cl[n].reshape(prm.shape)
+            err = np.abs(prm.grad.detach().cpu().numpy() - ref).max()
+            print(f"step {s} grad {n}: max abs err {err:.3g} (rel {err / max(np.abs(ref).max(), 1e-30):.3g})")
+            assert err <= 2e-3 * np.abs(ref).max() + 1e-7, (s, n, err, np.abs(ref).max())
+            # an entry whose new first moment is within the gradient error of 0
+            # may get the opposite Adam step (+-lr)
+            m_new = 0.9 * state[f"m.{n}"] + 0.1 * (ref + 8.96e-5 * params[n])
+            flip[n] = np.abs(m_new) <= 0.1 * 2 * err
+        sd = model.state_dict()
+        for bn, x in zip(("fc.0", "fc.4", "fc.8"), _bn_inputs(cache, pooled, q)):
+            n_ = x.shape[0]  # torch BatchNorm1d: momentum 0.1, unbiased running variance
+            for st, val in (("running_mean", 0.9 * run[f"{bn}.running_mean"] + 0.1 * x.mean(0)),
+                            ("running_var", 0.9 * run[f"{bn}.running_var"] + 0.1 * x.var(0) * n_ / (n_ - 1))):
+                assert np.abs(sd[f"{bn}.{st}"].cpu().numpy() - val).max() < 1e-5, (s, bn, st)
+        expect = o.adam_step(params, g_cl, state, lr, wd)
+        for n, prm in model.named_parameters():
+            got = prm.detach().cpu().numpy()
+            err = np.abs(got - expect[n].reshape(prm.shape))
+            tiny = flip[n]
+            print(f"step {s} param {n}: err {err[~tiny].max(initial=0):.3g}, {int(tiny.sum())} sign-ambiguous")
+            assert err[~tiny].max(initial=0) < 5e-5, (s, n, err[~tiny].max(initial=0))
+            assert err[tiny].max(initial=0) <= 2 * lr + 1e-6, (s, n)
+
+
+def _rerank_oracle(p, T, hist_u, cand_u):
+    from oracle import din_oracle as o
+
+    c = cand_u[cand_u >= 0]
+    keys = np.broadcast_to(_keys(T, hist_u[None, :]), (len(c), hist_u.shape[0], T.shape[1]))
+    lo, _, _, _ = o.din_forward(p, T[c], keys, train=False)
+    return lo.reshape(-1)
+
+
+def _rank_ambiguous(ref_logits_u, lab_u, tol):
+    """True when the positive's logit lies within 2 tol of another candidate's
+    (its rank is then not determined under the stated tolerance)."""
+    pos = np.flatnonzero(lab_u == 1)
+    if pos.size == 0:
+        return False
+    others = np.delete(ref_logits_u, pos[0])
+    return bool(np.abs(others - ref_logits_u[pos[0]]).min(initial=np.inf) <= 2 * tol)
+
+
+def test_rerank_shared_vs_oracle_c5_shape(gpu):
+    """nrk_din_rerank_attn at configs[4]'s shape (d 256, L 50, C 201) vs the oracle."""
+    from newsrecommend_amd.din import DIN
+    from newsrecommend_amd.pipeline import ndcg_at_k, rerank
+    from oracle import din_oracle as o
+
+    dev = torch.device("cuda")
+    d, L, C, U, N = 256, 50, 201, 40, 8000
+    g = torch.Generator(device=dev).manual_seed(31)
+    table = (torch.randn((N, d), generator=g, device=dev) * 0.5).to(torch.bfloat16)
+    hist = torch.randint(0, N, (U, L), generator=g, device=dev, dtype=torch.int32)
+    lens = torch.randint(1, L + 1, (U,), generator=g, device=dev)
+    lens[0], lens[1] = 1, L
+    hist = torch.where(torch.arange(L, device=dev)[None] < lens[:, None], hist, torch.full_like(hist, -1))
+    cand = torch.randint(0, N, (U, C), generator=g, device=dev, dtype=torch.int32)
+    cand[::5, -1] = -1  # users without an appended ground truth: one padded slot
+    gt_col = torch.randint(0, C - 1, (U,), generator=g, device=dev)
+    labels = torch.zeros((U, C), dtype=torch.bool, device=dev)
+    labels[torch.arange(U, device=dev), gt_col] = True
+    torch.manual_seed(4)
+    model = DIN(d, 128, 32, 0.36).to(dev).eval()
+    with torch.no_grad():
+        for bn in (model.fc[0], model.fc[4], model.fc[8]):
+            bn.running_mean.uniform_(-0.3, 0.3)
+            bn.running_var.uniform_(0.4, 1.6)
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.1, 0.1)
+    logits = rerank(model, table, hist, cand)
+    nd = ndcg_at_k(logits, labels, 5).cpu().numpy()
+    T = table.float().cpu().numpy().astype(np.float64)
+    H, Cn, Lg, Lb = hist.cpu().numpy(), cand.cpu().numpy(), logits.cpu().numpy(), labels.cpu().numpy()
+    p_emu, p_ref = _params_f64(model, True), _params_f64(model, False)
+    worst_emu = worst_ref = 0.0
+    for u in range(U):
+        valid = Cn[u] >= 0
+        assert np.isneginf(Lg[u][~valid]).all()
+        got = Lg[u][valid]
+        emu = _rerank_oracle(p_emu, T, H[u], Cn[u])
+        ref = _rerank_oracle(p_ref, T, H[u], Cn[u])
+        worst_emu = max(worst_emu, np.abs(got - emu).max())
+        worst_ref = max(worst_ref, np.abs(got - ref).max())
+        lab_u = Lb[u][valid].astype(np.int64)
+        nd_ref = o.ndcg_single(1 / (1 + np.exp(-ref)), lab_u, 5)
+        assert nd[u] == nd_ref or _rank_ambiguous(ref, lab_u, 2e-2), (u, nd[u], nd_ref)
+    print(f"rerank logits max abs err: emulated {worst_emu:.3g}, reference {worst_ref:.3g}")
+    assert worst_emu < 1e-3, worst_emu
+    assert worst_ref < 2e-2, worst_ref
+
+
+def test_rerank_matches_reference_evaluate_fixture_c5(gpu):
+    """The reference's own evaluate() at configs[4]'s re-rank shape (fixture
+    din_rerank_c5: d 256, L 50, 201 candidates, made by DIN.py): the shared
+    bf16 re-rank's logits and NDCG@5, and the fp32 generic evaluate() path's
+    loss and NDCG, against the reference's numbers."""
+    from newsrecommend_amd.din import DIN, evaluate
+    from newsrecommend_amd.pipeline import ndcg_at_k, rerank
+
+    z = np.load(os.path.join(GOLDEN, "din_rerank_c5.npz"))
+    dev = torch.device("cuda")
+    d, L = int(z["d"]), int(z["L"])
+    row = {int(a): i for i, a in enumerate(z["item_ids"])}
+    to_rows = np.vectorize(lambda a: row.get(int(a), -1))
+    hist = torch.from_numpy(to_rows(z["ev_hist"]).astype(np.int32)).to(dev)
+    cand = torch.from_numpy(to_rows(z["ev_cand"]).astype(np.int32)).to(dev)
+    lab = z["ev_lab"]
+    model = DIN(d, int(z["A"]), int(z["F"]), 0.36)
+    model.load_state_dict({k[4:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("sd::")})
+    model = model.to(dev).eval()
+    table32 = torch.from_numpy(z["table"]).to(dev)
+    # (1) bf16 shared-history re-rank (the configs[4] path); the table is bf16-exact
+    logits = rerank(model, table32.to(torch.bfloat16), hist, cand).cpu().numpy()
+    err = np.abs(logits - z["ev_logits"]).max()
+    print(f"fixture c5: shared re-rank logits max abs err {err:.3g}")
+    assert err < 2e-2, err
+    nd = ndcg_at_k(torch.from_numpy(logits).to(dev), torch.from_numpy(lab).to(dev) > 0, 5).cpu().numpy()
+    for u in range(len(nd)):
+        assert nd[u] == z["ev_ndcg_user"][u] or _rank_ambiguous(z["ev_logits"][u], lab[u], 2e-2), u
+    # (2) the fp32 generic evaluate() (every candidate its own DIN sample)
+    hist_emb = torch.where(hist[..., None] >= 0, table32[hist.clamp_min(0).long()], 0.0)
+    batches = []
+    for lo in range(0, hist.shape[0], 8):
+        hi = min(lo + 8, hist.shape[0])
+        batches.append({"uid": list(range(lo, hi)), "history_emb": hist_emb[lo:hi],
+                        "cand_embs": [table32[cand[u].long()] for u in range(lo, hi)],
+                        "labels": [torch.from_numpy(lab[u].astype(np.float32)) for u in range(lo, hi)]})
+    loss, ndcg = evaluate(model, batches, torch.nn.BCEWithLogitsLoss(), dev, 5)
+    assert abs(loss - float(z["ev_loss"])) < 1e-5, (loss, float(z["ev_loss"]))
+    assert abs(ndcg - float(z["ev_ndcg"])) < 1e-9, (ndcg, float(z["ev_ndcg"]))

@@ -375,3 +375,75 @@ def test_fused_train_step_generic_path_matches_eager(gpu):
             assert (pa - pb).abs().max().item() <= 2 * 3 * 1e-3 + 1e-6, n
         else:
             assert torch.allclose(pa, pb, atol=2e-4, rtol=1e-3), n
+
+
+def _eval_batches(table32, n_users, L, C, seed, dev):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    N = table32.shape[0]
+    hist = torch.randint(0, N, (n_users, L), generator=g, device=dev)
+    lens = torch.randint(1, L + 1, (n_users,), generator=g, device=dev)
+    hist = torch.where(torch.arange(L, device=dev)[None] < lens[:, None], hist, torch.full_like(hist, -1))
+    hemb = torch.where(hist[..., None] >= 0, table32[hist.clamp_min(0)], 0.0)
+    out = []
+    for lo in range(0, n_users, 8):
+        cands = [table32[torch.randint(0, N, (C,), generator=g, device=dev)] for _ in range(lo, min(lo + 8, n_users))]
+        labs = []
+        for _ in cands:
+            lab = torch.zeros(C)
+            lab[int(torch.randint(0, C, (1,), generator=g, device=dev))] = 1.0
+            labs.append(lab)
+        out.append({"uid": list(range(lo, lo + len(cands))), "history_emb": hemb[lo:lo + len(cands)],
+                    "cand_embs": cands, "labels": labs})
+    return out
+
+
+@pytest.mark.parametrize("sched", ["plateau", "step"])
+def test_fit_epoch_driver_matches_eager_main_loop(gpu, tmp_path, sched):
+    """din.fit (DIN.py:225-257 on the fused step, lr read from a device scalar)
+    == the reference's main() loop run eagerly with torch.optim.Adam and the
+    same scheduler, batch order (drop_last) and evaluate(): per-epoch losses,
+    NDCG and lr, final parameters; the best-NDCG checkpoint loads with
+    weights_only=True.  StepLR(gamma 0.5) forces an lr change every epoch."""
+    from newsrecommend_amd.din import DIN, evaluate, fit
+
+    dev, table, hist, tgt, lab, ma, mb = _setup_fused(0.0, d=64, L=20)
+    rows = 1100  # 17 full batches of 64, 12 rows dropped
+    hist, tgt, lab = hist[:rows], tgt[:rows], lab[:rows]
+    ev = _eval_batches(table.float(), 20, 20, 30, seed=8, dev=dev)
+    factory = None if sched == "plateau" else (lambda o: torch.optim.lr_scheduler.StepLR(o, 1, gamma=0.5))
+    ck = str(tmp_path / "DIN_model.pth")
+    hist_f = fit(ma, table, hist, tgt, lab, ev, epochs=3, batch_size=64, lr=5e-3, weight_decay=1e-4, checkpoint=ck,
+                 scheduler=factory, seed=7)
+    # eager restatement of main()
+    crit = torch.nn.BCEWithLogitsLoss()
+    opt = torch.optim.Adam(mb.parameters(), lr=5e-3, weight_decay=1e-4)
+    sch = (torch.optim.lr_scheduler.ReduceLROnPlateau(opt, mode="min", factor=0.5, patience=1) if factory is None
+           else factory(opt))
+    gen = torch.Generator(device=dev).manual_seed(7)
+    for e in range(3):
+        lr_e = opt.param_groups[0]["lr"]
+        mb.train()
+        perm = torch.randperm(rows, generator=gen, device=dev)
+        losses = []
+        for b in range(rows // 64):
+            idx = perm[b * 64:(b + 1) * 64]
+            opt.zero_grad()
+            loss = crit(mb.forward_ids(table, tgt[idx], hist[idx]), lab[idx])
+            loss.backward()
+            torch.nn.utils.clip_grad_norm_(mb.parameters(), 1.0)
+            opt.step()
+            losses.append(loss.item())
+        vl, nd = evaluate(mb, ev, crit, dev, 5)
+        sch.step(vl) if factory is None else sch.step()
+        h = hist_f[e]
+        assert h["lr"] == pytest.approx(lr_e, rel=1e-7), (e, h["lr"], lr_e)
+        assert abs(h["train_loss"] - float(np.mean(losses))) < 2e-3, (e, h, np.mean(losses))
+        assert abs(h["val_loss"] - vl) < 2e-3, (e, h, vl)
+    if sched == "step":
+        assert [h["lr"] for h in hist_f] == pytest.approx([5e-3, 2.5e-3, 1.25e-3])
+    for (n, pa), (_, pb) in zip(ma.named_parameters(), mb.named_parameters()):
+        if n != "attn.attn.2.bias":
+            assert torch.allclose(pa, pb, atol=5e-3, rtol=5e-2), (n, (pa - pb).abs().max().item())
+    assert max(h["ndcg"] for h in hist_f) > 0
+    m2 = DIN(64, 64, 32, 0.0)
+    m2.load_state_dict(torch.load(ck, weights_only=True))  # the reference's checkpoint format

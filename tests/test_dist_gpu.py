@@ -1,0 +1,44 @@
+"""World-2 run of the product's multi-GPU code on the GPU box (one card, two
+ranks on cuda:0, gloo): ShardedIndexFlat / ShardedIndexIVFFlat equal one index
+over the whole corpus, and FusedTrainStep's data-parallel gradient hook
+produces the rank-mean gradient with replicas staying identical.  The RCCL
+branch (all_gather_into_tensor / all_reduce on device buffers) is the
+driver's 8-GPU scaling run; here gloo carries host copies of the same
+buffers.  The ranks run as child processes of torch.distributed.run."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_world2_sharded_search_and_dp_hook(gpu, tmp_path):
+    env = dict(os.environ, PYTHONPATH=ROOT, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "tests", "dist_gpu_worker.py"), str(tmp_path)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = [json.load(open(tmp_path / f"rank{i}.json")) for i in range(2)]
+    for x in res:
+        assert x["world"] == 2
+        for m in (0, 1):
+            assert x[f"flat{m}_I_equal"] and x[f"flat{m}_D_equal"], (m, x)
+        assert x["ivf_centroids_equal"] and x["ivf_I_equal"] and x["ivf_D_equal"], x
+        assert x["dp_grad_rel_err"] < 1e-6, x
+        assert x["dp_replica_param_diff"] == 0.0, x
+    assert res[0]["flat0_local_rows"] + res[1]["flat0_local_rows"] == 50_001

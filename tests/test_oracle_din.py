@@ -79,3 +79,55 @@ def test_evaluate_ndcg():
         ls.append(o.bce_with_logits(lg, lb))
     assert abs(np.mean(nd) - z["ev_ndcg"]) < 1e-9
     assert abs(np.mean(ls) - z["ev_loss"]) < 1e-6
+
+
+@pytest.mark.parametrize("name", ["din_train_c1", "din_train_c3"])
+def test_torch_cpu_restatement_pinned(name):
+    """oracle/din_torch_ref (the PyTorch-CPU baseline the bench times) equals
+    the reference's own two train() steps (DIN.py:139-153)."""
+    import torch
+
+    from oracle.din_torch_ref import TorchDIN, train_step
+
+    z = _load(name)
+    m = TorchDIN(int(z["d"]), int(z["A"]), int(z["F"]), 0.0)
+    m.load_state_dict({k[4:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("sd::")})
+    opt = torch.optim.Adam(m.parameters(), lr=1.62e-3, weight_decay=8.96e-5)
+    crit = torch.nn.BCEWithLogitsLoss()
+    m.train()
+    losses = []
+    for s in range(2):
+        keys = torch.from_numpy(_keys(z["table"], z[f"hist_idx{s}"]))
+        q = torch.from_numpy(z["table"][z[f"tgt_idx{s}"]].astype(np.float32))
+        losses.append(train_step(m, opt, crit, q, keys, torch.from_numpy(z[f"label{s}"])).item())
+    assert abs(losses[0] - float(z["loss0"])) < 1e-6
+    assert abs(np.mean(losses) - float(z["mean_loss"])) < 1e-6
+    for k, v in m.state_dict().items():
+        if f"after::{k}" in z.files and "num_batches" not in k:
+            # b2's gradient is 0 up to rounding (softmax shift invariance): Adam moves it by +-lr
+            tol = 2 * 1.62e-3 if k == "attn.attn.2.bias" else 5e-5
+            np.testing.assert_allclose(v.numpy(), z[f"after::{k}"], atol=tol, err_msg=k)
+
+
+def test_cpu_baseline_ports_agree_with_exact_oracle():
+    """oracle/cpu_baselines (the faiss-cpu stand-ins the bench times) return
+    the exact oracle's neighbours on well-separated data."""
+    import torch
+
+    from oracle import cpu_baselines as cb, ivf_oracle as io, knn_oracle as ko
+
+    rng = np.random.default_rng(0)
+    c = rng.standard_normal((20, 24)).astype(np.float32) * 3
+    xb = (c[rng.integers(0, 20, 3000)] + rng.standard_normal((3000, 24))).astype(np.float32)
+    xq = (c[rng.integers(0, 20, 50)] + rng.standard_normal((50, 24))).astype(np.float32)
+    for metric in (ko.METRIC_IP, ko.METRIC_L2):
+        _, I = cb.flat_search(torch.from_numpy(xq), torch.from_numpy(xb), 5, metric, block=700)
+        _, Io, _ = ko.exact_search(xq, xb, 5, metric)
+        assert (I.numpy() == Io).mean() > 0.99
+    cent = xb[:16].copy()
+    assign, _ = io.assign_nearest(xb, cent)
+    lists = cb.IvfLists(xb, assign, cent)
+    for metric in (ko.METRIC_IP, ko.METRIC_L2):
+        _, I = cb.ivf_search(torch.from_numpy(xq), lists, 4, 5, metric)
+        _, Io, _, _ = io.ivf_search(xq, xb, cent, assign, 4, 5, metric)
+        assert (I.numpy() == Io).mean() > 0.99
