@@ -115,31 +115,35 @@ def test_fused_train_step_fast_path_vs_oracle_c3_shape(gpu):
         assert abs(loss - o.bce_with_logits(lo, y)) < 2e-5, (s, loss, o.bce_with_logits(lo, y))
         lo_ref, _, _, _ = o.din_forward(full, q, keys, train=True)
         assert abs(loss - o.bce_with_logits(lo_ref, y)) < 2e-3
-        flip = {}
+        g_k = {}
         for n, prm in model.named_parameters():  # clipped gradients (what clip_grad_norm_ leaves in .grad)
             ref = g_cl[n].reshape(prm.shape)
-            err = np.abs(prm.grad.detach().cpu().numpy() - ref).max()
+            g_k[n] = prm.grad.detach().cpu().numpy().astype(np.float64)
+            err = np.abs(g_k[n] - ref).max()
             print(f"step {s} grad {n}: max abs err {err:.3g} (rel {err / max(np.abs(ref).max(), 1e-30):.3g})")
             assert err <= 2e-3 * np.abs(ref).max() + 1e-7, (s, n, err, np.abs(ref).max())
-            # an entry whose new first moment is within the gradient error of 0
-            # may get the opposite Adam step (+-lr)
-            m_new = 0.9 * state[f"m.{n}"] + 0.1 * (ref + 8.96e-5 * params[n])
-            flip[n] = np.abs(m_new) <= 0.1 * 2 * err
         sd = model.state_dict()
         for bn, x in zip(("fc.0", "fc.4", "fc.8"), _bn_inputs(cache, pooled, q)):
             n_ = x.shape[0]  # torch BatchNorm1d: momentum 0.1, unbiased running variance
             for st, val in (("running_mean", 0.9 * run[f"{bn}.running_mean"] + 0.1 * x.mean(0)),
                             ("running_var", 0.9 * run[f"{bn}.running_var"] + 0.1 * x.var(0) * n_ / (n_ - 1))):
                 assert np.abs(sd[f"{bn}.{st}"].cpu().numpy() - val).max() < 1e-5, (s, bn, st)
-        expect = o.adam_step(params, g_cl, state, lr, wd)
+        # Adam (DIN.py:151, torch.optim.Adam with L2 weight decay) checked as
+        # its own stage: the oracle's update applied to the kernel's clipped
+        # gradients (checked above) must reproduce the new parameters to fp32
+        # rounding.  Feeding the oracle's gradients instead is not comparable
+        # entry by entry: where v is tiny, Adam's normalised step amplifies the
+        # gradient tolerance up to +-lr.
+        cp = lambda st: {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in st.items()}
+        expect = o.adam_step(params, g_k, cp(state), lr, wd)
+        expect_o = o.adam_step(params, {n: g_cl[n].reshape(g_k[n].shape) for n in g_k}, cp(state), lr, wd)
         for n, prm in model.named_parameters():
             got = prm.detach().cpu().numpy()
             err = np.abs(got - expect[n].reshape(prm.shape))
-            tiny = flip[n]
-            print(f"step {s} param {n}: err {err[~tiny].max(initial=0):.3g}, {int(tiny.sum())} sign-ambiguous")
-            assert err[~tiny].max(initial=0) < 5e-5, (s, n, err[~tiny].max(initial=0))
-            assert err[tiny].max(initial=0) <= 2 * lr + 1e-6, (s, n)
-
+            lim = 1e-6 + 4e-7 * np.abs(expect[n]).reshape(prm.shape)
+            print(f"step {s} param {n}: err {err.max():.3g} (oracle-gradient Adam: {np.abs(got - expect_o[n]).max():.3g})")
+            assert (err <= lim).all(), (s, n, err.max())
+            assert np.abs(got - expect_o[n]).max() <= 2 * lr + 1e-6, (s, n)
 
 def _rerank_oracle(p, T, hist_u, cand_u):
     from oracle import din_oracle as o
