@@ -125,13 +125,13 @@ def bench_flat(args, rank, world, dev):
     screen_ms = float(stage_ms[1])
     flops = 2.0 * args.nq * nb_local * args.d
     achieved = flops / (screen_ms * 1e-3) / 1e12
-    fallback = int(index.local.last_fallback.item())
+    fallback = index.local.fallback_counts.tolist()
 
     out = {
         "value": qps, "unit": "queries/s", "ms_per_step": el / args.steps * 1e3,
         "stages_ms": {"query_prepare+tau_prepass": float(stage_ms[0]), "screen": screen_ms,
                       "merge_rescore": float(stage_ms[2]), "exact_fallback": float(stage_ms[3])},
-        "fallback_queries": fallback,
+        "fallback_queries": fallback[0], "exact_scan_queries": fallback[1],
         "roofline": {"bound": "mfma", "kernel": "screen_kernel (bf16 v_mfma_f32_32x32x16)",
                      "achieved": achieved, "peak": BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / BF16_DENSE_TFLOPS, "traffic": _pmc_traffic(args, world),
@@ -251,6 +251,7 @@ def bench_ivf(args, rank, world, dev):
         "stages_ms": {"prepare+phaseA+grouping": float(st[0]), "collect_screen": float(st[1]),
                       "exact_rescore": float(st[2]), "fallback": float(st[3])},
         "fallback_queries": int(index.local.last_fallback.item()),
+        "exact_scan_queries": int(index.local.last_exact_scan.item()),
         "roofline": {"bound": "mfma", "kernel": "screen_kernel MODE 3 (IVF collect, bf16 v_mfma_f32_32x32x16)",
                      "achieved": achieved, "peak": BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / BF16_DENSE_TFLOPS, "traffic": None,
@@ -295,7 +296,8 @@ def _flat_l2_leg(args, flat, xq, k):
             "ms_per_step": el / steps * 1e3, "config": f"flat L2 {flat.ntotal}x{flat.d}, batch={xq.shape[0]}, k={k}",
             "stages_ms": {"query_prepare+tau_prepass": float(st[0]), "screen": float(st[1]),
                           "merge_rescore": float(st[2]), "exact_fallback": float(st[3])},
-            "fallback_queries": int(flat.last_fallback.item())}
+            "fallback_queries": int(flat.last_fallback.item()),
+            "exact_scan_queries": int(flat.last_exact_scan.item())}
 
 
 def _ivf_oracle_check(index, xb, xq, I, k, nprobe):
@@ -363,6 +365,7 @@ def bench_n1(args, rank, world, dev, index, xb):
         "stages_ms": {"query_prepare+tau_prepass": float(st[0]), "screen": float(st[1]),
                       "merge_rescore": float(st[2]), "exact_fallback": float(st[3])},
         "fallback_queries": int(index.local.last_fallback.item()),
+        "exact_scan_queries": int(index.local.last_exact_scan.item()),
         "roofline": {"bound": "mfma", "kernel": "screen_kernel (bf16 v_mfma_f32_32x32x16, dp 256)",
                      "achieved": achieved, "peak": BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / BF16_DENSE_TFLOPS, "traffic": None,
@@ -455,6 +458,7 @@ def bench_e2e(args, rank, world, dev):
         "rerank_samples_per_step": int((uhi - ulo) * (kr + 1)),
         "ndcg_at_5_mean_rank0": float(nd.mean().item()),
         "fallback_queries": int(index.local.last_fallback.item()),
+        "exact_scan_queries": int(index.local.last_exact_scan.item()),
     }
     if n1 is not None:
         out["n1_retrieval_10m_256_k5"] = n1

@@ -74,8 +74,12 @@ int nrk_knn_flat_workspace(int64_t nq, int64_t nb, int32_t d, int32_t k, size_t*
  *   I  [nq][k] int64 (global id = local row + id_offset; -1 padding)
  *   S  [nq][k] f64 exact scores (optional, may be NULL): the values D rounds;
  *      used by the multi-shard merge so ties break exactly as on one device.
- *   n_fallback (optional, device int32[1]): number of queries that needed the
- *      exact scan (diagnostic).
+ *   n_fallback (optional, device int32[2], diagnostic): [0] queries the
+ *      screening certificate did not cover (answered by the collect pass: one
+ *      more bf16 screen over the corpus for these queries only, keeping every
+ *      item within the error bound of the merge's exact k-th, then exact
+ *      rescoring); [1] of those, queries whose collect buffer overflowed and
+ *      that the fp64 corpus scan answered.
  *   stage_events (optional, host array of NRK_KNN_STAGES+1 hipEvent_t created by
  *      the caller): recorded on `stream` before each stage and after the last,
  *      so a benchmark can time the screening kernel alone.  NULL in production. */
@@ -203,7 +207,9 @@ int nrk_kmeans_update(const float* x, int32_t d, const int64_t* list_off, const 
  *   list_off / pos2id / pos2list from nrk_group_by_list; max_list = largest list.
  * Result: the exact top-k (same order and ties as nrk_knn_flat) among the
  * items of the probed lists.  Outputs and stage_events as nrk_knn_flat
- * (stage 0 = query prepare + grouping by list). */
+ * (stage 0 = query prepare + grouping by list); n_fallback[0] = n_fallback[1] =
+ * queries whose collect buffer overflowed (or that had fewer than k seeds),
+ * answered by the fp64 scan of their probed lists. */
 int nrk_ivf_search_workspace(int64_t nq, int32_t nprobe, int32_t nlist, int64_t max_list,
                              int32_t d, int32_t k, size_t* ws_bytes);
 int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe, int32_t nprobe,

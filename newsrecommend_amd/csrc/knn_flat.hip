@@ -319,152 +319,6 @@ __global__ __launch_bounds__(256) void merge_rescore_kernel(
   }
 }
 
-// Wave-per-query variant (used when the pre-pass bound is active, so only a
-// few dozen union entries are valid): compact the valid entries with
-// ballot/mbcnt into this wave's LDS slice, select the top KP by rank
-// counting, rescore them exactly, rank again, certify.  No block barriers.
-// Queries whose union holds more than WCAP valid entries defer to the
-// fallback list (exact scan), which keeps the result exact.
-template <int WCAP>
-__global__ __launch_bounds__(256) void merge_rescore_wave_kernel(
-    const float* __restrict__ part_s, const int* __restrict__ part_i, const float* __restrict__ part_t, int nch,
-    int M, int KP, int k, int dp, const float* __restrict__ xq, const float* __restrict__ xb, int64_t nb, int d, int l2,
-    const double* __restrict__ qmeta, const float* __restrict__ stats, const float* __restrict__ tau_q,
-    float* __restrict__ D, int64_t* __restrict__ I, double* __restrict__ S, int64_t id_offset, FbState fb,
-    int nq) {
-  __shared__ float cs[4][WCAP];   // screened score of compacted candidates
-  __shared__ int ci[4][WCAP];     // their ids
-  __shared__ double es[4][64];    // exact goodness of the rescored top-KP
-  __shared__ int64_t ei[4][64];
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int qi = blockIdx.x * 4 + wv;
-  if (qi >= nq) return;
-  const int U = nch * 2 * M;
-  const float* ps = part_s + (int64_t)qi * U;
-  const int* pi = part_i + (int64_t)qi * U;
-
-  // 1. compact valid entries
-  int V = 0;
-  bool overflow = false;
-  for (int base = 0; base < U; base += 64) {
-    const int i = base + lane;
-    const float v = i < U ? ps[i] : -INFINITY;
-    const int item = i < U ? pi[i] : -1;
-    const bool ok = v != -INFINITY && item >= 0 && item < nb;
-    const unsigned long long bal = __ballot(ok);
-    const int pos = V + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
-    if (ok && pos < WCAP) {
-      cs[wv][pos] = v;
-      ci[wv][pos] = item;
-    }
-    V += __popcll(bal);
-  }
-  if (V > WCAP) overflow = true;
-  float th = -INFINITY;
-  for (int i = lane; i < nch * 2; i += 64) th = fmaxf(th, part_t[(int64_t)qi * nch * 2 + i]);
-  th = wave_max(th);
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const int Vc = V < WCAP ? V : WCAP;
-
-  // 2. rank each candidate (screened score desc, lower id first); keep top kp
-  const int kp = KP < Vc ? KP : Vc;
-  double theta = fmax((double)th, tau_q ? (double)tau_q[qi] : -INFINITY);
-  int my_rank[WCAP / 64];
-#pragma unroll
-  for (int u = 0; u < WCAP / 64; ++u) {
-    const int e = u * 64 + lane;
-    int rk = 1 << 30;
-    if (e < Vc) {
-      const float ve = cs[wv][e];
-      const int ie = ci[wv][e];
-      rk = 0;
-      for (int j = 0; j < Vc; ++j) {
-        const float vj = cs[wv][j];
-        rk += (vj > ve) || (vj == ve && ci[wv][j] < ie);
-      }
-    }
-    my_rank[u] = rk;
-  }
-  // theta gets the (kp+1)-th screened score when candidates were cut
-  float cut = -INFINITY;
-#pragma unroll
-  for (int u = 0; u < WCAP / 64; ++u)
-    if (my_rank[u] == kp) cut = cs[wv][u * 64 + lane];
-  theta = fmax(theta, (double)wave_max(cut));
-
-  // 3. exact rescoring of the kp survivors -> es/ei[rank]
-  const float* q = xq + (int64_t)qi * d;
-#pragma unroll
-  for (int u = 0; u < WCAP / 64; ++u) {
-    const int rk = my_rank[u];
-    if (rk < kp) {
-      const int64_t item = ci[wv][u * 64 + lane];
-      const double sc = exact_score(q, xb + item * d, d, l2 != 0);
-      es[wv][rk] = l2 ? -sc : sc;
-      ei[wv][rk] = item;
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-  // 4. exact ranks (kp <= 64: one entry per lane)
-  int er = 1 << 30;
-  double eg = -INFINITY;
-  int64_t eid = INT64_MAX;
-  if (lane < kp) {
-    eg = es[wv][lane];
-    eid = ei[wv][lane];
-    er = 0;
-    for (int j = 0; j < kp; ++j) {
-      const double gj = es[wv][j];
-      er += better(gj, ei[wv][j], eg, eid);
-    }
-  }
-  // k-th exact goodness for the certificate
-  double kth = -INFINITY;
-  {
-    double cand = (er == k - 1) ? eg : -INFINITY;
-    for (int o = 32; o > 0; o >>= 1) cand = fmax(cand, __shfl_xor(cand, o, 64));
-    kth = cand;
-  }
-  bool ok = !overflow && kp >= k;
-  if (ok && theta != -INFINITY) {
-    const double nqh = qmeta[4 * qi + 0], nrq = qmeta[4 * qi + 1], qn2 = qmeta[4 * qi + 2];
-    const double Xh = stats[0], R = stats[1], NX = stats[2];
-    const double gam = (double)dp * 0x1p-22;
-    const double bip = gam * nqh * Xh + nqh * R + nrq * Xh + nrq * R;
-    if (!l2) {
-      const double lim = theta + bip;
-      ok = kth - lim > 1e-12 * (fabs(lim) + fabs(kth));
-    } else {
-      const double B = 2.0 * bip + 0x1p-21 * (NX + nqh * Xh);
-      const double lo = qn2 - theta - B;
-      ok = lo - (-kth) > 1e-12 * (fabs(lo) + fabs(kth) + qn2);
-    }
-  }
-  if (fb.force) ok = false;
-  const unsigned long long kb = __ballot(er == k - 1);
-  const int64_t kid = kb ? __shfl(eid, __ffsll((long long)kb) - 1, 64) : (int64_t)-1;
-  if (lane == 0 && !ok) fb.push(qi, kb ? kth : -INFINITY, kid);
-  // 5. outputs: lane with exact rank j writes slot j
-  if (er < k) {
-    const int64_t o = (int64_t)qi * k + er;
-    const double sc = l2 ? -eg : eg;
-    D[o] = (float)sc;
-    I[o] = eid + id_offset;
-    if (S) S[o] = sc;
-  }
-  for (int j = kp + lane; j < k; j += 64) {  // fewer than k candidates: pad (the fallback rewrites)
-    const int64_t o = (int64_t)qi * k + j;
-    D[o] = l2 ? FLT_MAX : -FLT_MAX;
-    I[o] = -1;
-    if (S) S[o] = l2 ? DBL_MAX : -DBL_MAX;
-  }
-}
-
 // ============================================================ exact top-k ==
 // Workgroups loop over a query list (fallback) or over all queries (direct
 // exact mode).  Block top-k kept in LDS: list [0,k), staged candidates
@@ -559,6 +413,7 @@ constexpr int SM_T = 64;          // queries and items per tile
 constexpr int SM_DC = 32;         // dimensions staged per LDS step
 constexpr int SM_LD = SM_T + 4;   // LDS row stride (floats): conflict-light transposed stores
 constexpr int SMALL_NB = 4096;
+constexpr int64_t EXACT_BELOW = 16384;  // nb in (SMALL_NB, EXACT_BELOW): block-per-query fp64 scan
 
 template <bool L2>
 __device__ __forceinline__ void small_tile(const float* __restrict__ xq, int64_t q0, int64_t nq,
@@ -869,6 +724,297 @@ __global__ void topk_merge_kernel(const double* __restrict__ Sp, const int64_t* 
   }
 }
 
+// ============================================================== IVF-Flat ==
+// faiss IndexIVFFlat.search (BASELINE configs[3]; the inverted lists of
+// Retrieval.py:21-23).  The caller supplies the probed lists (the coarse
+// quantizer's top-nprobe, a flat search over the centroids).  List-major
+// batching: every (query, probe) pair is grouped under its list, each list's
+// probing queries are gathered into a padded bf16 segment, and the screen
+// kernel (MODE 2) runs (list, query tile, list chunk) work items, so each list
+// chunk is streamed once per 32*QT*WAVES queries.  Merge, certificate and the
+// exact fallback are the flat path's, restricted to the probed lists.
+
+__global__ void ivf_count_kernel(const int64_t* __restrict__ probe, int64_t npairs, int nlist, int* __restrict__ cnt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npairs) return;
+  const int64_t l = probe[i];
+  if (l >= 0 && l < nlist) atomicAdd(&cnt[l], 1);
+}
+
+// One block: per-list query segments (padded to wq rows) and work-item prefix.
+__global__ __launch_bounds__(1024) void ivf_plan_kernel(const int* __restrict__ cnt,
+                                                        const int64_t* __restrict__ list_off, int nlist, int wq,
+                                                        int ch, int* __restrict__ seg_off, int* __restrict__ work_off,
+                                                        int* __restrict__ fill) {
+  __shared__ int s_seg[1024], s_work[1024];
+  const int t = threadIdx.x;
+  const int per = (nlist + 1023) / 1024;
+  const int lo = t * per < nlist ? t * per : nlist, hi = lo + per < nlist ? lo + per : nlist;
+  int ss = 0, sw = 0;
+  for (int l = lo; l < hi; ++l) {
+    const int rows = (cnt[l] + wq - 1) / wq * wq;
+    const int nchl = (int)cdiv(list_off[l + 1] - list_off[l], (int64_t)ch);
+    ss += rows;
+    sw += rows / wq * nchl;
+  }
+  s_seg[t] = ss;
+  s_work[t] = sw;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const int a = t >= o ? s_seg[t - o] : 0, b = t >= o ? s_work[t - o] : 0;
+    __syncthreads();
+    s_seg[t] += a;
+    s_work[t] += b;
+    __syncthreads();
+  }
+  int es = s_seg[t] - ss, ew = s_work[t] - sw;
+  for (int l = lo; l < hi; ++l) {
+    const int rows = (cnt[l] + wq - 1) / wq * wq;
+    const int nchl = (int)cdiv(list_off[l + 1] - list_off[l], (int64_t)ch);
+    seg_off[l] = es;
+    work_off[l] = ew;
+    fill[l] = 0;
+    es += rows;
+    ew += rows / wq * nchl;
+  }
+  if (t == 1023) {
+    seg_off[nlist] = s_seg[1023];
+    work_off[nlist] = s_work[1023];
+  }
+}
+
+__global__ void ivf_scatter_kernel(const int64_t* __restrict__ probe, int64_t npairs, int nlist,
+                                   const int* __restrict__ seg_off, int* __restrict__ fill,
+                                   int* __restrict__ slot_pair) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npairs) return;
+  const int64_t l = probe[i];
+  if (l < 0 || l >= nlist) return;
+  slot_pair[seg_off[l] + atomicAdd(&fill[l], 1)] = (int)i;
+}
+
+// gathered query rows: one wave per slot row (padding rows are zeroed)
+__global__ void ivf_gather_kernel(const uint16_t* __restrict__ qh, int dp, int nprobe,
+                                  const int* __restrict__ slot_pair, const int* __restrict__ seg_off, int nlist,
+                                  int64_t max_rows, uint16_t* __restrict__ qh_ivf) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= max_rows || row >= seg_off[nlist]) return;
+  const int pair = slot_pair[row];
+  const int64_t q = pair >= 0 ? pair / nprobe : 0;
+  for (int j = lane * 4; j < dp; j += 256) {
+    uint2 v = make_uint2(0u, 0u);
+    if (pair >= 0) v = *reinterpret_cast<const uint2*>(qh + q * dp + j);
+    *reinterpret_cast<uint2*>(qh_ivf + row * dp + j) = v;
+  }
+}
+
+// Collect threshold in screened units.  e_k is the exact goodness of a real
+// item ranked k-th among exactly scored real items, so the true k-th best is at
+// least e_k; every true top-k item x then has screened(x) >= exact(x) - B_q >=
+// e_k - B_q (IP), resp. screened = 2 q^.x^ - |x|^2 >= e_k + |q|^2 - B_q (L2,
+// goodness = -|q - x|^2), with the flat certificate's error bound B_q.  Rounded
+// down to f32 with slack for the fp64 evaluation of the bound itself.
+__device__ __forceinline__ float collect_threshold(double ek, const double* __restrict__ qm,
+                                                   const float* __restrict__ stats, int dp, int l2) {
+  const double nqh = qm[0], nrq = qm[1], qn2 = qm[2];
+  const double Xh = stats[0], Rr = stats[1], NX = stats[2];
+  const double gam = (double)dp * 0x1p-22;
+  const double bip = gam * nqh * Xh + nqh * Rr + nrq * Xh + nrq * Rr;
+  const double B = l2 ? 2.0 * bip + 0x1p-21 * (NX + nqh * Xh) : bip;
+  double t = (l2 ? qn2 + ek : ek) - B;
+  t -= 1e-9 * (fabs(t) + fabs(ek) + qn2 + B);
+  float f = (float)t;
+  if ((double)f > t) f = nextafterf(f, -INFINITY);
+  return f < -FLT_MAX ? -FLT_MAX : f;
+}
+
+// IVF phase A seed: exact rescoring of the R best lane maxima of the nearest
+// list (distinct real items) -> e_k = their k-th best exact (goodness, id),
+// a lower bound on the true k-th best s_k.  Every true top-k item x then has
+// screened(x) >= exact(x) - B >= e_k - B =: T (screened units, rounded down;
+// same error bound B_q as the flat certificate), and (e_k, id) is the
+// fallback threshold.  Fewer than k seeds: the query goes to the fallback.
+__global__ __launch_bounds__(256) void ivf_seed_kernel(const int* __restrict__ seed_pos, int R, int k,
+                                                       const int64_t* __restrict__ pos2id,
+                                                       const float* __restrict__ xq, const float* __restrict__ xb,
+                                                       int d, int l2, const double* __restrict__ qmeta,
+                                                       const float* __restrict__ stats, int dp,
+                                                       float* __restrict__ thr, double* __restrict__ lb_g,
+                                                       int64_t* __restrict__ lb_i, int* __restrict__ cand_cnt,
+                                                       int cap) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int q = blockIdx.x, tid = threadIdx.x;
+  const int P = pow2ceil(R);
+  double* g = reinterpret_cast<double*>(smem);
+  int64_t* id = reinterpret_cast<int64_t*>(g + P);
+  float* qs = reinterpret_cast<float*>(id + P);
+  __shared__ int s_valid;
+  if (tid == 0) s_valid = 0;
+  for (int i = tid; i < d; i += 256) qs[i] = xq[(int64_t)q * d + i];
+  __syncthreads();
+  for (int i = tid; i < P; i += 256) {
+    const int pos = i < R ? seed_pos[(int64_t)q * R + i] : -1;
+    if (pos >= 0) {
+      const int64_t item = pos2id[pos];
+      const double sc = exact_score(qs, xb + item * d, d, l2 != 0);
+      g[i] = l2 ? -sc : sc;
+      id[i] = item;
+      atomicAdd(&s_valid, 1);
+    } else {
+      g[i] = -INFINITY;
+      id[i] = INT64_MAX;
+    }
+  }
+  __syncthreads();
+  block_bitonic_sort(g, id, P);
+  if (tid != 0) return;
+  if (s_valid < k) {  // too few seeds for a bound: no collection, straight to the fallback
+    thr[q] = INFINITY;
+    lb_g[q] = -INFINITY;
+    lb_i[q] = -1;
+    cand_cnt[q] = cap + 1;
+    return;
+  }
+  const double ek = g[k - 1];
+  thr[q] = collect_threshold(ek, qmeta + 4 * q, stats, dp, l2);
+  lb_g[q] = ek;
+  lb_i[q] = id[k - 1];
+}
+
+// IVF phase B: exact rescoring of every collected candidate, top-k.  Queries
+// whose buffer overflowed go to the fallback with threshold (e_k, id).
+__global__ __launch_bounds__(256) void collect_rescore_kernel(
+    const int* __restrict__ cand_cnt, const int* __restrict__ cand_pos, int cap, const int64_t* __restrict__ pos2id,
+    const float* __restrict__ xq, const float* __restrict__ xb, int d, int k, int l2,
+    const double* __restrict__ lb_g, const int64_t* __restrict__ lb_i, float* __restrict__ D,
+    int64_t* __restrict__ I, double* __restrict__ S, int64_t id_offset, FbState fb,
+    const int* __restrict__ qlist = nullptr, const int* __restrict__ qcount = nullptr) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  // IVF: slot = query.  Flat collect pass: slot b holds query qlist[b], if any.
+  const int sl = blockIdx.x;
+  if (qlist && sl >= *qcount) return;
+  const int qi = qlist ? qlist[sl] : sl;
+  const int c = cand_cnt[sl];
+  if (c > cap) {
+    if (tid == 0) fb.push(qi, lb_g[sl], lb_i[sl]);
+    return;
+  }
+  const int P = pow2ceil(c > 0 ? c : 1);
+  double* g = reinterpret_cast<double*>(smem);
+  int64_t* id = reinterpret_cast<int64_t*>(g + P);
+  float* qs = reinterpret_cast<float*>(id + P);
+  for (int i = tid; i < d; i += 256) qs[i] = xq[(int64_t)qi * d + i];
+  __syncthreads();
+  for (int i = tid; i < P; i += 256) {
+    if (i < c) {
+      const int pos = cand_pos[(int64_t)sl * cap + i];
+      const int64_t item = pos2id ? pos2id[pos] : (int64_t)pos;
+      const double sc = exact_score(qs, xb + item * d, d, l2 != 0);
+      g[i] = l2 ? -sc : sc;
+      id[i] = item;
+    } else {
+      g[i] = -INFINITY;
+      id[i] = INT64_MAX;
+    }
+  }
+  __syncthreads();
+  block_bitonic_sort(g, id, P);
+  for (int j = tid; j < k; j += 256) {
+    const int64_t o = (int64_t)qi * k + j;
+    const bool valid = j < c;
+    const double sc = valid ? (l2 ? -g[j] : g[j]) : (l2 ? DBL_MAX : -DBL_MAX);
+    D[o] = valid ? (float)sc : (l2 ? FLT_MAX : -FLT_MAX);
+    I[o] = valid ? id[j] + id_offset : -1;
+    if (S) S[o] = sc;
+  }
+}
+
+// ====================================================== flat collect pass ==
+// Queries the flat merge could not certify (dense neighbourhoods: the exact
+// k-th best lies within the screening error bound of theta) get a second,
+// exact-by-construction pass instead of an fp64 corpus scan: the IVF collect
+// screen (MODE 3) over the whole corpus as ONE list, probed only by these
+// queries, appends every item whose screened score reaches the query's collect
+// threshold (from the merge's exact k-th e_k, collect_threshold), and
+// collect_rescore ranks the candidates exactly.  Only a buffer overflow (more
+// than `cap` items within the bound) goes on to the tiled fp64 fallback.
+//
+// Collect storage is indexed by slot s (the merge's fallback order; the first
+// fb.slots uncertified queries, which are also the ones with a stored e_k).
+// One block: turns the merge's fallback list into the one-list work table
+// (list_off, seg_off, work_off, slot_pair = s) and the per-slot thresholds,
+// saves the slot -> query map for the gather and collect_rescore, and empties
+// the fallback list, which the overflowing queries refill.  Entries past the
+// storage (nq > 4096 only) stay in the fallback list, moved to its front,
+// with threshold -inf (they were pushed without one).
+__global__ __launch_bounds__(1024) void flat_collect_plan_kernel(
+    FbState fb, int64_t nq, int64_t nb, int wq, int ch, const double* __restrict__ qmeta,
+    const float* __restrict__ stats, int dp, int l2, int cap, int force_overflow, int64_t* __restrict__ list_off,
+    int* __restrict__ seg_off, int* __restrict__ work_off, int* __restrict__ slot_pair, float* __restrict__ thr,
+    double* __restrict__ lb_g, int64_t* __restrict__ lb_i, int* __restrict__ cand_cnt, int* __restrict__ clist,
+    int* __restrict__ ccount) {
+  const int t = threadIdx.x, nt = blockDim.x;
+  const int n = (int)min((int64_t)fb.count[0], nq);
+  const int nc = n < fb.slots ? n : fb.slots;  // collected slots
+  const int rows = (nc + wq - 1) / wq * wq;
+  for (int s = t; s < rows; s += nt) slot_pair[s] = s < nc ? s : -1;
+  for (int s = t; s < nc; s += nt) {
+    const int q = fb.list[s];
+    clist[s] = q;
+    const bool has = fb.thr_i[s] >= 0;  // the merge rescored >= k candidates
+    thr[s] = has ? collect_threshold(fb.thr_g[s], qmeta + 4 * q, stats, dp, l2) : INFINITY;
+    lb_g[s] = has ? fb.thr_g[s] : -INFINITY;
+    lb_i[s] = has ? fb.thr_i[s] : -1;
+    cand_cnt[s] = (has && !force_overflow) ? 0 : cap + 1;
+  }
+  if (t == 0) {
+    list_off[0] = 0;
+    list_off[1] = nb;
+    seg_off[0] = 0;
+    seg_off[1] = rows;
+    work_off[0] = 0;
+    work_off[1] = rows / wq * (int)cdiv(nb, (int64_t)ch);
+    ccount[0] = nc;
+    ccount[1] = n;  // queries the certificate did not cover (reported as n_fallback[0])
+  }
+  __syncthreads();  // every thread has read fb.count and the collected part of fb.list
+  // the rest (s >= slots >= 1024 > nt): move to the front in rounds of nt;
+  // each round reads above everything written so far
+  for (int base = 0; base < n - nc; base += nt) {
+    const int src = nc + base + t;
+    const int q = src < n ? fb.list[src] : -1;
+    __syncthreads();
+    if (src < n) {
+      fb.list[base + t] = q;
+      if (base + t < fb.slots) {
+        fb.thr_g[base + t] = -INFINITY;
+        fb.thr_i[base + t] = -1;
+        fb.n[base + t] = 0;
+      }
+    }
+    __syncthreads();
+  }
+  if (t == 0) fb.count[0] = n - nc;
+}
+
+// collected slot rows of the bf16 queries: one wave per row (padding rows zeroed)
+__global__ void flat_collect_gather_kernel(const uint16_t* __restrict__ qh, int dp, const int* __restrict__ clist,
+                                           const int* __restrict__ ccount, int64_t max_rows, int wq,
+                                           uint16_t* __restrict__ qc) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int nc = *ccount;
+  if (row >= max_rows || row >= (int64_t)(nc + wq - 1) / wq * wq) return;
+  const int64_t q = row < nc ? clist[row] : -1;
+  for (int j = lane * 4; j < dp; j += 256) {
+    uint2 v = make_uint2(0u, 0u);
+    if (q >= 0) v = *reinterpret_cast<const uint2*>(qh + q * dp + j);
+    *reinterpret_cast<uint2*>(qc + row * dp + j) = v;
+  }
+}
+
 // ================================================================== plan ==
 struct FlatPlan {
   bool exact_only, tau;
@@ -882,6 +1028,11 @@ struct FlatPlan {
   int64_t nq_pad, chunk, chunk_pre;
   size_t off_qh, off_qmeta, off_ps, off_pi, off_pt, off_fbl, off_fbc, off_tau, off_pre, total;
   size_t off_fbt, off_fbi, off_fbn, off_fcg, off_fci, off_ovl;
+  // collect pass for uncertified queries (flat_collect_plan_kernel)
+  int cwq, cch, ccap, cgrid;
+  int64_t crows;
+  size_t off_clo, off_cseg, off_cwork, off_csp, off_cqi, off_cthr, off_clbg, off_clbi, off_ccnt, off_cpos, off_clist,
+      off_ccount;
 };
 
 static int padded_dim(int d) {
@@ -898,7 +1049,14 @@ static int host_pow2ceil(int n) {
   return p;
 }
 
-static int env_int(const char* name, int dflt) {
+// Test hooks (tests/test_knn_gpu.py, tests/test_ivf_gpu.py) that drive the
+// rare exact paths on ordinary data; nothing else reads the environment.
+//   NRK_FORCE_FALLBACK=1  certify nothing (flat: the collect pass answers)
+//   NRK_FORCE_FALLBACK=2  certify nothing and overflow every collect buffer
+//                         (the tiled fp64 fallback answers)
+//   NRK_FB_CAP=n          tiled-fallback candidates per slot (tiny: the
+//                         block-per-query exact kernel answers)
+static int test_hook(const char* name, int dflt) {
   const char* v = getenv(name);
   return v && *v ? atoi(v) : dflt;
 }
@@ -919,7 +1077,7 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
     p.total = k == 1 ? 256 : align_up((size_t)p.small_chunk * p.small_ld * 8, 256);
     return p;
   }
-  p.exact_only = nb < env_int("NRK_EXACT_BELOW", 16384) || d > 256 || k > 256 || nb >= (1ll << 31) || nq == 0;
+  p.exact_only = nb < EXACT_BELOW || d > 256 || k > 256 || nb >= (1ll << 31) || nq == 0;
   if (p.exact_only) {
     p.off_fbc = 0;
     p.total = 256;
@@ -934,9 +1092,9 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
   // DP = 256 with M = 16 (k > 24, e.g. configs[4]'s 10M x 256, k = 200): 8-wave
   // workgroups, 256 queries per corpus pass; a chunk far larger than L2 is
   // then re-read by half as many query tiles
-  if (p.dp == 256 && p.M == 16 && env_int("NRK_SCREEN_W8", 1)) p.waves = 8;
+  if (p.dp == 256 && p.M == 16) p.waves = 8;
   p.R = k <= 8 ? 16 : 2 * k;
-  p.tau = env_int("NRK_SCREEN_TAU", 1) != 0;  // k = 200 at 10M x 256: -5% retrieve time
+  p.tau = true;  // k = 200 at 10M x 256: -5% retrieve time
   if (p.dp == 256) p.qt = 1;
   p.wq = p.waves * 32 * p.qt;
   p.nqt = (int)cdiv(nq, p.wq);
@@ -944,7 +1102,7 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
   // k > 24 (M = 16): twice the lane streams, so that dense neighbourhoods do
   // not overflow a lane's list (10M x 256, k = 200: 2 uncertified queries per
   // 4096 -> 0, and the 4.5 ms fp64 fallback scan with them)
-  int target = env_int("NRK_SCREEN_WGS", p.M >= 16 ? 2048 : 1024);
+  int target = p.M >= 16 ? 2048 : 1024;
   int64_t nch = target / (p.nqt > 0 ? p.nqt : 1);
   if (nch < 1) nch = 1;
   int64_t max_by_u = 2048 / (2 * p.M);
@@ -967,7 +1125,6 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
   }
   int kp = 2 * k > 32 ? 2 * k : 32;
   if (kp < k + 16) kp = k + 16;
-  kp = env_int("NRK_KP", kp);
   if (kp > p.U) kp = p.U;
   if (kp > 1024) kp = 1024;
   p.KP = kp;
@@ -980,7 +1137,7 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
   }
   // pre-pass: every tstride-th 64-item tile, chunks small enough that each
   // query gets >= 8R short lane streams (their maxima are distinct items)
-  p.tstride = env_int("NRK_PRE_STRIDE", 8);
+  p.tstride = 8;
   {
     const int TI = 64;  // must equal screen_kernel TI
     int64_t tiles = cdiv(nb, TI);
@@ -1015,7 +1172,7 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
   p.fb_slots = (int)(nq < 4096 ? nq : 4096);
   p.fb_cap = host_pow2ceil(2 * k + 64);
   if (p.fb_cap < 512) p.fb_cap = 512;
-  p.fb_cap = env_int("NRK_FB_CAP", p.fb_cap);
+  p.fb_cap = test_hook("NRK_FB_CAP", p.fb_cap);
   if (p.fb_cap < 1) p.fb_cap = 1;
   if (p.fb_cap > 8192) p.fb_cap = 8192;  // select kernel sorts cap x 16 B in LDS
   p.off_fbt = take((size_t)p.fb_slots * 8);
@@ -1024,6 +1181,29 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
   p.off_fcg = take((size_t)p.fb_slots * p.fb_cap * 8);
   p.off_fci = take((size_t)p.fb_slots * p.fb_cap * 8);
   p.off_ovl = take((size_t)nq * 4);
+  // collect pass: one query tile per wave (128 queries per work item), 4096-row
+  // chunks (each chunk's query tiles run back to back on one XCD), storage for
+  // the fb_slots uncertified queries that carry an e_k
+  p.cwq = 4 * 32;
+  p.cch = 4096;
+  p.ccap = 2048;
+  p.crows = cdiv(p.fb_slots, p.cwq) * p.cwq;
+  {
+    const int64_t items = (p.crows / p.cwq) * cdiv(nb, (int64_t)p.cch);
+    p.cgrid = (int)(items < 2048 ? items : 2048);
+  }
+  p.off_clo = take(16);
+  p.off_cseg = take(8);
+  p.off_cwork = take(8);
+  p.off_csp = take((size_t)p.crows * 4);
+  p.off_cqi = take((size_t)p.crows * p.dp * 2);
+  p.off_cthr = take((size_t)p.fb_slots * 4);
+  p.off_clbg = take((size_t)p.fb_slots * 8);
+  p.off_clbi = take((size_t)p.fb_slots * 8);
+  p.off_ccnt = take((size_t)p.fb_slots * 4);
+  p.off_cpos = take((size_t)p.fb_slots * p.ccap * 4);
+  p.off_clist = take((size_t)p.fb_slots * 4);
+  p.off_ccount = take(16);
   p.total = off;
   return p;
 }
@@ -1126,7 +1306,7 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
   char* w = static_cast<char*>(ws);
   int* fbc = reinterpret_cast<int*>(w + p.off_fbc);
   if (hipMemsetAsync(fbc, 0, 16, st) != hipSuccess) return fail(NRK_ELAUNCH, "knn_flat: memset failed");
-  if (n_fallback && hipMemsetAsync(n_fallback, 0, 4, st) != hipSuccess)
+  if (n_fallback && hipMemsetAsync(n_fallback, 0, 8, st) != hipSuccess)
     return fail(NRK_ELAUNCH, "knn_flat: memset failed");
   if (nq == 0) return NRK_OK;
   NRK_CHECK_ARG(xq && D && I && (xb || nb == 0), "knn_flat: null pointer");
@@ -1136,7 +1316,7 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
     // a shape the screen cannot plan (merge union > 2048, d or k > 256) runs the
     // fp64 brute force for every query: say so through the fallback count
     if (n_fallback && (p.cliff || d > 256 || k > 256) &&
-        hipMemsetD32Async(n_fallback, (int)nq, 1, st) != hipSuccess)
+        hipMemsetD32Async(n_fallback, (int)nq, 2, st) != hipSuccess)
       return fail(NRK_ELAUNCH, "knn_flat: memset failed");
     return exact_launch(xq, nq, xb, nb, d, k, l2, nullptr, nullptr, nq, D, I, S, id_offset, st);
   }
@@ -1157,7 +1337,7 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
   fb.thr_g = reinterpret_cast<double*>(w + p.off_fbt);
   fb.thr_i = reinterpret_cast<int64_t*>(w + p.off_fbi);
   fb.n = reinterpret_cast<int*>(w + p.off_fbn);
-  fb.force = env_int("NRK_FORCE_FALLBACK", 0);
+  fb.force = test_hook("NRK_FORCE_FALLBACK", 0);
   double* fcg = reinterpret_cast<double*>(w + p.off_fcg);
   int64_t* fci = reinterpret_cast<int64_t*>(w + p.off_fci);
   int* ovl = reinterpret_cast<int*>(w + p.off_ovl);
@@ -1188,11 +1368,7 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
   NRK_CHECK_LAUNCH("screen_kernel");
 
   mark(2);
-  if (p.tau && p.KP <= 64 && env_int("NRK_MERGE_WAVE", 0)) {
-    hipLaunchKernelGGL(merge_rescore_wave_kernel<256>, dim3((unsigned)cdiv(nq, 4)), dim3(256), 0, st, ps, pi, pt,
-                       p.nch, p.M, p.KP, k, p.dp, xq, xb, nb, d, l2, qmeta, stats, tau, D, I, S, id_offset, fb, (int)nq);
-    NRK_CHECK_LAUNCH("merge_rescore_wave_kernel");
-  } else {
+  {
     const int P = host_pow2ceil(p.U), P2 = host_pow2ceil(p.KP);
     const size_t smem = (size_t)P * 16 + (size_t)P2 * 16 + (size_t)d * 4;
     if (smem > 150 * 1024) return fail(NRK_EUNSUPPORTED, "knn_flat: merge needs %zu B LDS", smem);
@@ -1202,6 +1378,37 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
   }
 
   mark(3);
+  {  // collect pass for the uncertified queries (normally none: every launch exits at once)
+    int64_t* clo = reinterpret_cast<int64_t*>(w + p.off_clo);
+    int* cseg = reinterpret_cast<int*>(w + p.off_cseg);
+    int* cwork = reinterpret_cast<int*>(w + p.off_cwork);
+    int* csp = reinterpret_cast<int*>(w + p.off_csp);
+    uint16_t* cqi = reinterpret_cast<uint16_t*>(w + p.off_cqi);
+    float* cthr = reinterpret_cast<float*>(w + p.off_cthr);
+    double* clbg = reinterpret_cast<double*>(w + p.off_clbg);
+    int64_t* clbi = reinterpret_cast<int64_t*>(w + p.off_clbi);
+    int* ccnt = reinterpret_cast<int*>(w + p.off_ccnt);
+    int* cpos = reinterpret_cast<int*>(w + p.off_cpos);
+    int* clist = reinterpret_cast<int*>(w + p.off_clist);
+    int* ccount = reinterpret_cast<int*>(w + p.off_ccount);
+    hipLaunchKernelGGL(flat_collect_plan_kernel, dim3(1), dim3(1024), 0, st, fb, nq, nb, p.cwq, p.cch, qmeta, stats,
+                       p.dp, l2, p.ccap, fb.force >= 2 ? 1 : 0, clo, cseg, cwork, csp, cthr, clbg, clbi, ccnt, clist,
+                       ccount);
+    NRK_CHECK_LAUNCH("flat_collect_plan_kernel");
+    hipLaunchKernelGGL(flat_collect_gather_kernel, dim3((unsigned)cdiv(p.crows, 4)), dim3(256), 0, st, qh, p.dp, clist,
+                       ccount, p.crows, p.cwq, cqi);
+    NRK_CHECK_LAUNCH("flat_collect_gather_kernel");
+    screen_fn fc = pick_screen(p.dp, 1, p.M, l2 != 0, 3);
+    if (!fc) return fail(NRK_EUNSUPPORTED, "knn_flat: no collect kernel for dp=%d", p.dp);
+    IvfScreen isc{cwork, clo, cseg, csp, 1, p.cch, (int)cdiv(nb, (int64_t)p.cch), cthr, ccnt, cpos, p.ccap, 1};
+    hipLaunchKernelGGL(fc, dim3((unsigned)p.cgrid), dim3(4 * 64), 0, st, cqi, xb_bf16, xb_meta, (int64_t)p.fb_slots, nb,
+                       0, 0, 0, 1, nullptr, nullptr, nullptr, nullptr, isc);
+    NRK_CHECK_LAUNCH("screen_kernel (flat collect)");
+    const size_t smem = (size_t)host_pow2ceil(p.ccap) * 16 + (size_t)d * 4;
+    hipLaunchKernelGGL(collect_rescore_kernel, dim3((unsigned)p.fb_slots), dim3(256), smem, st, ccnt, cpos, p.ccap,
+                       nullptr, xq, xb, d, k, l2, clbg, clbi, D, I, S, id_offset, fb, clist, ccount);
+    NRK_CHECK_LAUNCH("collect_rescore_kernel (flat)");
+  }
   {
     const int64_t ntiles = cdiv(nb, (int64_t)FB_TR);
     const int grid = (int)(ntiles < 2048 ? ntiles : 2048);
@@ -1215,8 +1422,9 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
   int rc = exact_launch(xq, nq, xb, nb, d, k, l2, ovl, fbc + 1, 256, D, I, S, id_offset, st);
   if (rc != NRK_OK) return rc;
   mark(4);
-  if (n_fallback && hipMemcpyAsync(n_fallback, fbc, 4, hipMemcpyDeviceToDevice, st) != hipSuccess)
-    return fail(NRK_ELAUNCH, "knn_flat: copy of fallback count failed");
+  if (n_fallback && (hipMemcpyAsync(n_fallback, w + p.off_ccount + 4, 4, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+                     hipMemcpyAsync(n_fallback + 1, fbc, 4, hipMemcpyDeviceToDevice, st) != hipSuccess))
+    return fail(NRK_ELAUNCH, "knn_flat: copy of fallback counts failed");
   return NRK_OK;
 }
 
@@ -1233,197 +1441,7 @@ extern "C" int nrk_topk_merge(const double* S_parts, const int64_t* I_parts, int
   return NRK_OK;
 }
 
-// ============================================================== IVF-Flat ==
-// faiss IndexIVFFlat.search (BASELINE configs[3]; the inverted lists of
-// Retrieval.py:21-23).  The caller supplies the probed lists (the coarse
-// quantizer's top-nprobe, a flat search over the centroids).  List-major
-// batching: every (query, probe) pair is grouped under its list, each list's
-// probing queries are gathered into a padded bf16 segment, and the screen
-// kernel (MODE 2) runs (list, query tile, list chunk) work items, so each list
-// chunk is streamed once per 32*QT*WAVES queries.  Merge, certificate and the
-// exact fallback are the flat path's, restricted to the probed lists.
 namespace nrk {
-
-__global__ void ivf_count_kernel(const int64_t* __restrict__ probe, int64_t npairs, int nlist, int* __restrict__ cnt) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= npairs) return;
-  const int64_t l = probe[i];
-  if (l >= 0 && l < nlist) atomicAdd(&cnt[l], 1);
-}
-
-// One block: per-list query segments (padded to wq rows) and work-item prefix.
-__global__ __launch_bounds__(1024) void ivf_plan_kernel(const int* __restrict__ cnt,
-                                                        const int64_t* __restrict__ list_off, int nlist, int wq,
-                                                        int ch, int* __restrict__ seg_off, int* __restrict__ work_off,
-                                                        int* __restrict__ fill) {
-  __shared__ int s_seg[1024], s_work[1024];
-  const int t = threadIdx.x;
-  const int per = (nlist + 1023) / 1024;
-  const int lo = t * per < nlist ? t * per : nlist, hi = lo + per < nlist ? lo + per : nlist;
-  int ss = 0, sw = 0;
-  for (int l = lo; l < hi; ++l) {
-    const int rows = (cnt[l] + wq - 1) / wq * wq;
-    const int nchl = (int)cdiv(list_off[l + 1] - list_off[l], (int64_t)ch);
-    ss += rows;
-    sw += rows / wq * nchl;
-  }
-  s_seg[t] = ss;
-  s_work[t] = sw;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
-    const int a = t >= o ? s_seg[t - o] : 0, b = t >= o ? s_work[t - o] : 0;
-    __syncthreads();
-    s_seg[t] += a;
-    s_work[t] += b;
-    __syncthreads();
-  }
-  int es = s_seg[t] - ss, ew = s_work[t] - sw;
-  for (int l = lo; l < hi; ++l) {
-    const int rows = (cnt[l] + wq - 1) / wq * wq;
-    const int nchl = (int)cdiv(list_off[l + 1] - list_off[l], (int64_t)ch);
-    seg_off[l] = es;
-    work_off[l] = ew;
-    fill[l] = 0;
-    es += rows;
-    ew += rows / wq * nchl;
-  }
-  if (t == 1023) {
-    seg_off[nlist] = s_seg[1023];
-    work_off[nlist] = s_work[1023];
-  }
-}
-
-__global__ void ivf_scatter_kernel(const int64_t* __restrict__ probe, int64_t npairs, int nlist,
-                                   const int* __restrict__ seg_off, int* __restrict__ fill,
-                                   int* __restrict__ slot_pair) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= npairs) return;
-  const int64_t l = probe[i];
-  if (l < 0 || l >= nlist) return;
-  slot_pair[seg_off[l] + atomicAdd(&fill[l], 1)] = (int)i;
-}
-
-// gathered query rows: one wave per slot row (padding rows are zeroed)
-__global__ void ivf_gather_kernel(const uint16_t* __restrict__ qh, int dp, int nprobe,
-                                  const int* __restrict__ slot_pair, const int* __restrict__ seg_off, int nlist,
-                                  int64_t max_rows, uint16_t* __restrict__ qh_ivf) {
-  const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (row >= max_rows || row >= seg_off[nlist]) return;
-  const int pair = slot_pair[row];
-  const int64_t q = pair >= 0 ? pair / nprobe : 0;
-  for (int j = lane * 4; j < dp; j += 256) {
-    uint2 v = make_uint2(0u, 0u);
-    if (pair >= 0) v = *reinterpret_cast<const uint2*>(qh + q * dp + j);
-    *reinterpret_cast<uint2*>(qh_ivf + row * dp + j) = v;
-  }
-}
-
-// IVF phase A seed: exact rescoring of the R best lane maxima of the nearest
-// list (distinct real items) -> e_k = their k-th best exact (goodness, id),
-// a lower bound on the true k-th best s_k.  Every true top-k item x then has
-// screened(x) >= exact(x) - B >= e_k - B =: T (screened units, rounded down;
-// same error bound B_q as the flat certificate), and (e_k, id) is the
-// fallback threshold.  Fewer than k seeds: the query goes to the fallback.
-__global__ __launch_bounds__(256) void ivf_seed_kernel(const int* __restrict__ seed_pos, int R, int k,
-                                                       const int64_t* __restrict__ pos2id,
-                                                       const float* __restrict__ xq, const float* __restrict__ xb,
-                                                       int d, int l2, const double* __restrict__ qmeta,
-                                                       const float* __restrict__ stats, int dp,
-                                                       float* __restrict__ thr, double* __restrict__ lb_g,
-                                                       int64_t* __restrict__ lb_i, int* __restrict__ cand_cnt,
-                                                       int cap) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int q = blockIdx.x, tid = threadIdx.x;
-  const int P = pow2ceil(R);
-  double* g = reinterpret_cast<double*>(smem);
-  int64_t* id = reinterpret_cast<int64_t*>(g + P);
-  float* qs = reinterpret_cast<float*>(id + P);
-  __shared__ int s_valid;
-  if (tid == 0) s_valid = 0;
-  for (int i = tid; i < d; i += 256) qs[i] = xq[(int64_t)q * d + i];
-  __syncthreads();
-  for (int i = tid; i < P; i += 256) {
-    const int pos = i < R ? seed_pos[(int64_t)q * R + i] : -1;
-    if (pos >= 0) {
-      const int64_t item = pos2id[pos];
-      const double sc = exact_score(qs, xb + item * d, d, l2 != 0);
-      g[i] = l2 ? -sc : sc;
-      id[i] = item;
-      atomicAdd(&s_valid, 1);
-    } else {
-      g[i] = -INFINITY;
-      id[i] = INT64_MAX;
-    }
-  }
-  __syncthreads();
-  block_bitonic_sort(g, id, P);
-  if (tid != 0) return;
-  if (s_valid < k) {  // too few seeds for a bound: no collection, straight to the fallback
-    thr[q] = INFINITY;
-    lb_g[q] = -INFINITY;
-    lb_i[q] = -1;
-    cand_cnt[q] = cap + 1;
-    return;
-  }
-  const double ek = g[k - 1];
-  const double nqh = qmeta[4 * q + 0], nrq = qmeta[4 * q + 1], qn2 = qmeta[4 * q + 2];
-  const double Xh = stats[0], Rr = stats[1], NX = stats[2];
-  const double gam = (double)dp * 0x1p-22;
-  const double bip = gam * nqh * Xh + nqh * Rr + nrq * Xh + nrq * Rr;
-  const double B = l2 ? 2.0 * bip + 0x1p-21 * (NX + nqh * Xh) : bip;
-  double t = (l2 ? qn2 + ek : ek) - B;
-  t -= 1e-9 * (fabs(t) + fabs(ek) + qn2 + B);  // slack for the fp64 evaluation of the bound itself
-  float f = (float)t;
-  if ((double)f > t) f = nextafterf(f, -INFINITY);
-  thr[q] = f < -FLT_MAX ? -FLT_MAX : f;
-  lb_g[q] = ek;
-  lb_i[q] = id[k - 1];
-}
-
-// IVF phase B: exact rescoring of every collected candidate, top-k.  Queries
-// whose buffer overflowed go to the fallback with threshold (e_k, id).
-__global__ __launch_bounds__(256) void collect_rescore_kernel(
-    const int* __restrict__ cand_cnt, const int* __restrict__ cand_pos, int cap, const int64_t* __restrict__ pos2id,
-    const float* __restrict__ xq, const float* __restrict__ xb, int d, int k, int l2,
-    const double* __restrict__ lb_g, const int64_t* __restrict__ lb_i, float* __restrict__ D,
-    int64_t* __restrict__ I, double* __restrict__ S, int64_t id_offset, FbState fb) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int qi = blockIdx.x, tid = threadIdx.x;
-  const int c = cand_cnt[qi];
-  if (c > cap) {
-    if (tid == 0) fb.push(qi, lb_g[qi], lb_i[qi]);
-    return;
-  }
-  const int P = pow2ceil(c > 0 ? c : 1);
-  double* g = reinterpret_cast<double*>(smem);
-  int64_t* id = reinterpret_cast<int64_t*>(g + P);
-  float* qs = reinterpret_cast<float*>(id + P);
-  for (int i = tid; i < d; i += 256) qs[i] = xq[(int64_t)qi * d + i];
-  __syncthreads();
-  for (int i = tid; i < P; i += 256) {
-    if (i < c) {
-      const int64_t item = pos2id[cand_pos[(int64_t)qi * cap + i]];
-      const double sc = exact_score(qs, xb + item * d, d, l2 != 0);
-      g[i] = l2 ? -sc : sc;
-      id[i] = item;
-    } else {
-      g[i] = -INFINITY;
-      id[i] = INT64_MAX;
-    }
-  }
-  __syncthreads();
-  block_bitonic_sort(g, id, P);
-  for (int j = tid; j < k; j += 256) {
-    const int64_t o = (int64_t)qi * k + j;
-    const bool valid = j < c;
-    const double sc = valid ? (l2 ? -g[j] : g[j]) : (l2 ? DBL_MAX : -DBL_MAX);
-    D[o] = valid ? (float)sc : (l2 ? FLT_MAX : -FLT_MAX);
-    I[o] = valid ? id[j] + id_offset : -1;
-    if (S) S[o] = sc;
-  }
-}
-
 struct IvfPlan {
   int dp, qt, M, waves, wq, nqt;
   int qtA, wqA;             // phase A query tiles per wave / queries per work item
@@ -1445,12 +1463,11 @@ static IvfPlan make_ivf_plan(int64_t nq, int nprobe, int nlist, int64_t max_list
   else if (k <= 24) { p.M = 8; p.qt = 1; }
   else { p.M = 16; p.qt = 1; }
   if (p.dp == 256) p.qt = 1;
-  if (env_int("NRK_IVF_QT", 0) == 1) p.qt = 1;  // A/B: one query tile per wave (the deferred IVF screens)
   p.wq = p.waves * 32 * p.qt;
   // phase A (lane maxima over the nA nearest lists) runs one query tile per
   // wave: half the work-item padding of the grouped queries and a lighter
   // epilogue.  Phase B keeps p.qt (two tiles share each A fragment).
-  p.qtA = env_int("NRK_IVF_QTA", 1) == 1 ? 1 : p.qt;
+  p.qtA = 1;
   p.wqA = p.waves * 32 * p.qtA;
   p.nqt = (int)cdiv(nq, p.wq);
   p.nq_pad = (int64_t)p.nqt * p.wq;
@@ -1460,9 +1477,7 @@ static IvfPlan make_ivf_plan(int64_t nq, int nprobe, int nlist, int64_t max_list
   // streams per chunk and query; more streams -> tighter seeds); tau_select
   // takes <= 1024 values per query
   p.nA = nprobe < 2 ? nprobe : 2;
-  int64_t chA = env_int("NRK_IVF_CHUNK_A", 1024);
-  if (chA < 64) chA = 64;
-  chA = (int64_t)align_up((size_t)chA, 64);
+  int64_t chA = 1024;
   const int64_t cmax_a = 512 / p.nA;
   if (cdiv(ml, chA) > cmax_a) chA = (int64_t)align_up((size_t)cdiv(ml, cmax_a), 64);
   if (chA > ch_gib) chA = ch_gib;
@@ -1472,20 +1487,16 @@ static IvfPlan make_ivf_plan(int64_t nq, int nprobe, int nlist, int64_t max_list
   if (p.R > 2 * p.nA * p.cmaxA) p.R = 2 * p.nA * p.cmaxA;
   if (p.R < 1) p.R = 1;
   // phase B: chunk size only sets the work-item granularity
-  int64_t chB = env_int("NRK_IVF_CHUNK", 4096);
-  if (chB < 64) chB = 64;
-  chB = (int64_t)align_up((size_t)chB, 64);
+  int64_t chB = 4096;
   if (chB > ch_gib) chB = ch_gib;
   p.chB = (int)chB;
   p.cmaxB = (int)cdiv(ml, chB);
-  p.cap = env_int("NRK_IVF_CAP", 2048);
-  if (p.cap < k) p.cap = k;
-  if (p.cap > 8192) p.cap = 8192;
+  p.cap = k > 2048 ? k : 2048;
   const int64_t npairs = nq * nprobe;
   p.max_rows = npairs + (int64_t)nlist * (p.wq - 1);
   p.max_rows = (p.max_rows + p.wq - 1) / p.wq * p.wq;
   // persistent grids over the device work tables (upper bound on the items)
-  const int64_t gcap = env_int("NRK_IVF_GRID", 2048);
+  const int64_t gcap = 2048;
   p.ubA = (cdiv(nq * p.nA, (int64_t)p.wqA) + nlist) * p.cmaxA;
   p.ubB = (cdiv(npairs, (int64_t)p.wq) + nlist) * p.cmaxB;
   if (p.ubA > gcap) p.ubA = gcap;
@@ -1493,7 +1504,7 @@ static IvfPlan make_ivf_plan(int64_t nq, int nprobe, int nlist, int64_t max_list
   p.fb_slots = (int)(nq < 4096 ? nq : 4096);
   p.fb_cap = host_pow2ceil(2 * k + 64);
   if (p.fb_cap < 512) p.fb_cap = 512;
-  p.fb_cap = env_int("NRK_FB_CAP", p.fb_cap);
+  p.fb_cap = test_hook("NRK_FB_CAP", p.fb_cap);
   if (p.fb_cap < 1) p.fb_cap = 1;
   if (p.fb_cap > 8192) p.fb_cap = 8192;
   size_t off = 0;
@@ -1582,7 +1593,7 @@ extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe,
   char* w = static_cast<char*>(ws);
   int* fbc = reinterpret_cast<int*>(w + p.off_fbc);
   if (hipMemsetAsync(fbc, 0, 16, st) != hipSuccess) return fail(NRK_ELAUNCH, "ivf_search: memset failed");
-  if (n_fallback && hipMemsetAsync(n_fallback, 0, 4, st) != hipSuccess)
+  if (n_fallback && hipMemsetAsync(n_fallback, 0, 8, st) != hipSuccess)
     return fail(NRK_ELAUNCH, "ivf_search: memset failed");
   if (nq == 0) return NRK_OK;
   NRK_CHECK_ARG(xq && probe && D && I && list_off, "ivf_search: null pointer");
@@ -1621,7 +1632,7 @@ extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe,
   int64_t* fci = reinterpret_cast<int64_t*>(w + p.off_fci);
   int* ovl = reinterpret_cast<int*>(w + p.off_ovl);
   IvfFb ivf{pos2id, pos2list, list_off, probe, nprobe};
-  const bool force_fb = env_int("NRK_FORCE_FALLBACK", 0) != 0;
+  const bool force_fb = test_hook("NRK_FORCE_FALLBACK", 0) != 0;
 
   mark(0);
   hipLaunchKernelGGL(query_prepare_kernel, dim3((unsigned)cdiv(p.nq_pad, 4)), dim3(256), 0, st, xq, nq, p.nq_pad, d,
@@ -1693,7 +1704,8 @@ extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe,
   int rc = exact_launch(xq, nq, xb, n, d, k, l2, ovl, fbc + 1, 256, D, I, S, id_offset, st, ivf);
   if (rc != NRK_OK) return rc;
   mark(4);
-  if (n_fallback && hipMemcpyAsync(n_fallback, fbc, 4, hipMemcpyDeviceToDevice, st) != hipSuccess)
-    return fail(NRK_ELAUNCH, "ivf_search: copy of fallback count failed");
+  if (n_fallback && (hipMemcpyAsync(n_fallback, fbc, 4, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+                     hipMemcpyAsync(n_fallback + 1, fbc, 4, hipMemcpyDeviceToDevice, st) != hipSuccess))
+    return fail(NRK_ELAUNCH, "ivf_search: copy of fallback counts failed");
   return NRK_OK;
 }

@@ -131,9 +131,9 @@ struct NoLds {};
 // straight-line part of the epilogue (L2 correction, max tree, threshold
 // test) is scheduled between the MFMAs, only the rare list insertions follow
 // the chain.  Without it every chain's results are waited for and reduced
-// before the next chain issues (the MFMA-only ablation, EPI 2, is 30 % faster).
+// before the next chain issues (an MFMA-only ablation was 30 % faster).
 // TIL: items per tile (deferred IP main pass may use 128: half the barriers).
-template <int DP, int QT, int M, int WAVES, bool L2, int MODE, int EPI = 0, bool AFRAG_GROUP = true, bool DEFER = false,
+template <int DP, int QT, int M, int WAVES, bool L2, int MODE, bool AFRAG_GROUP = true, bool DEFER = false,
           int TIL = 64>
 __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
     const uint16_t* __restrict__ qh, const uint16_t* __restrict__ xbh, const float* __restrict__ xmeta,
@@ -149,8 +149,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
   constexpr int KS = DP / 16;
   constexpr int WQ = WAVES * 32 * QT;
   constexpr int BUF = TI * DP + 2 * TI;  // uint16 per buffer: rows + TI float norms
-  static_assert(!DEFER || ((MODE <= 1 || MODE == 3 || MODE == 4) && (EPI == 0 || EPI == 3)),
-                "deferred epilogue: flat modes, IVF collect / lane maxima (EPI 3: no epilogue)");
+  static_assert(!DEFER || MODE <= 1 || MODE == 3 || MODE == 4, "deferred epilogue: flat modes, IVF collect / lane maxima");
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BUF];
   __shared__ std::conditional_t<MODE == 3, CollectLds<WQ>, NoLds> cl;
 
@@ -286,11 +285,6 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
           __builtin_amdgcn_sched_group_barrier(0x100, KS, 0);
           __builtin_amdgcn_sched_group_barrier(0x008, KS * QT, 0);
         }
-        if constexpr (EPI == 2) {  // ablation: MFMA only
-  #pragma unroll
-          for (int t = 0; t < QT; ++t) asm volatile("" ::"v"(acc[t][0]), "v"(acc[t][5]), "v"(acc[t][15]));
-          continue;
-        }
         // Epilogue.  MASKED only for the (rare) partial last tile of a chunk: a
         // wave-uniform branch, so full tiles carry no per-score selects.
         auto epilogue = [&](auto masked_tag) {
@@ -345,7 +339,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
               }
               continue;
             }
-            if constexpr (MODE == 1 || EPI == 1) {  // pre-pass (or ablation): lane maximum only
+            if constexpr (MODE == 1) {  // pre-pass: lane maximum only
               ls[t][0] = fmax_ieee(ls[t][0], m);
               continue;
             }
@@ -506,14 +500,9 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
         af[s] = *reinterpret_cast<const bf16x8*>(narow + 8 * ((2 * s + h) ^ nsw));
       }
       float m4[QT][4], m[QT];
-      if constexpr (EPI == 3) {  // ablation: keep the chain alive, no epilogue
+      tree(pend, n16, m4, m);
   #pragma unroll
-        for (int t = 0; t < QT; ++t) asm volatile("" ::"v"(cur[t][0]), "v"(cur[t][5]), "v"(cur[t][15]));
-      } else {
-        tree(pend, n16, m4, m);
-      }
-  #pragma unroll
-      for (int t = 0; t < QT; ++t) m[t] = (EPI != 3 && pbase >= 0) ? m[t] : -INFINITY;  // drain is a no-op
+      for (int t = 0; t < QT; ++t) m[t] = pbase >= 0 ? m[t] : -INFINITY;  // nothing pending: drain is a no-op
       constexpr int VPM = L2 ? 4 : 2;
   #pragma unroll
       for (int s = 0; s < KS; ++s) {
@@ -521,7 +510,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
         __builtin_amdgcn_sched_group_barrier(0x002, VPM * QT, 0);
       }
-      if constexpr (EPI != 3) drain(pend, pbase, m4, m);
+      drain(pend, pbase, m4, m);
       if constexpr (par == 0) {
         baseA = i0 + 32 * st;
         nvA = nvalid - 32 * st;
@@ -577,7 +566,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
         tile_d(it, std::integral_constant<int, 0>{});
         if (it + 1 < ntiles) tile_d(it + 1, std::integral_constant<int, 1>{});
       }
-      if (EPI != 3 && baseB >= 0) {  // the last sub-tile's epilogue
+      if (baseB >= 0) {  // the last sub-tile's epilogue
         if (nvB < 32) mask_rows(accB, nvB);
         float m4[QT][4], m[QT];
         tree(accB, pnB, m4, m);
@@ -641,7 +630,48 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
 typedef void (*screen_fn)(const uint16_t*, const uint16_t*, const float*, int64_t, int64_t, int64_t, int, int, int,
                           float*, int*, float*, const float*, IvfScreen);
 
-// mode: 0 main pass, 1 threshold pre-pass, 2 IVF list scan, 3 IVF collect, 4 IVF lane maxima
+// The one kernel variant per (DP, QT, M, L2, MODE).  Flat modes (main pass and
+// pre-pass) defer each sub-tile's epilogue into the next MFMA chain, except
+// where the second accumulator set and the fragment prefetch would spill (DP =
+// 256, L2 with two query tiles, the DP = 128 two-tile pre-pass); the IP main
+// pass streams 128-item tiles (half the barriers, measured +9 %).  The IVF
+// modes read each sub-tile's A fragments as one group before the MFMA chain
+// (measured faster there).  DESIGN.md "K-GEMM-TOPK" has the ablations.
+template <int DP, int QT, int M, bool L2, int MODE>
+constexpr screen_fn screen_variant() {
+  constexpr bool defer = MODE <= 1 && DP < 256 && !(L2 && QT == 2) && !(DP == 128 && QT == 2 && MODE == 1);
+  if constexpr (defer)
+    return screen_kernel<DP, QT, M, 4, L2, MODE, false, true, (MODE == 0 && !L2) ? 128 : 64>;
+  else
+    return screen_kernel<DP, QT, M, 4, L2, MODE, (MODE >= 2)>;
+}
+
+// mode: 0 main pass, 1 threshold pre-pass, 2 IVF list scan, 3 IVF collect, 4 IVF lane maxima.
+// DP = 256 always runs one query tile per wave.
+template <int DP, bool L2>
+screen_fn screen_for(int qt, int M, int mode) {
+  constexpr int Q2 = DP == 256 ? 1 : 2;
+  const bool two = qt == 2;
+  switch (mode) {
+    case 1: return two ? screen_variant<DP, Q2, 1, L2, 1>() : screen_variant<DP, 1, 1, L2, 1>();
+    case 3: return two ? screen_variant<DP, Q2, 1, L2, 3>() : screen_variant<DP, 1, 1, L2, 3>();
+    case 4: return two ? screen_variant<DP, Q2, 1, L2, 4>() : screen_variant<DP, 1, 1, L2, 4>();
+    case 0:
+    case 2: {
+      if (mode == 0) {
+        if (M == 4) return two ? screen_variant<DP, Q2, 4, L2, 0>() : screen_variant<DP, 1, 4, L2, 0>();
+        if (M == 8) return screen_variant<DP, 1, 8, L2, 0>();
+        return screen_variant<DP, 1, 16, L2, 0>();
+      }
+      if (M == 4) return two ? screen_variant<DP, Q2, 4, L2, 2>() : screen_variant<DP, 1, 4, L2, 2>();
+      if (M == 8) return screen_variant<DP, 1, 8, L2, 2>();
+      return screen_variant<DP, 1, 16, L2, 2>();
+    }
+  }
+  return nullptr;
+}
+
+// one translation unit per padded dimension (screen_dp*.hip) instantiates these
 screen_fn pick_screen_dp32(int qt, int M, bool l2, int mode);
 screen_fn pick_screen_dp64(int qt, int M, bool l2, int mode);
 screen_fn pick_screen_dp128(int qt, int M, bool l2, int mode);
@@ -649,6 +679,11 @@ screen_fn pick_screen_dp256(int qt, int M, bool l2, int mode);
 // DP = 256, QT = 1, 8 waves (256 queries per workgroup and corpus pass):
 // the flat main pass with M = 16 (mode 0) and its pre-pass (mode 1)
 screen_fn pick_screen_dp256_w8(bool l2, int mode);
+
+#define NRK_SCREEN_DP(DP)                                                  \
+  screen_fn pick_screen_dp##DP(int qt, int M, bool l2, int mode) {         \
+    return l2 ? screen_for<DP, true>(qt, M, mode) : screen_for<DP, false>(qt, M, mode); \
+  }
 
 inline screen_fn pick_screen(int dp, int qt, int M, bool l2, int mode) {
   switch (dp) {

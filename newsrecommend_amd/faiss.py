@@ -44,7 +44,22 @@ def _default_device():
     return torch.device("cuda", torch.cuda.current_device())
 
 
-class IndexFlat:
+class _FallbackCounters:
+    """Diagnostics of the last search (include/nrk.h n_fallback), device views."""
+
+    @property
+    def last_fallback(self):
+        """int32[1]: queries the main path did not answer (flat: not covered by
+        the certificate, answered by the collect pass; IVF: collect overflow)."""
+        return None if self.fallback_counts is None else self.fallback_counts[0:1]
+
+    @property
+    def last_exact_scan(self):
+        """int32[1]: of those, queries answered by the fp64 corpus scan."""
+        return None if self.fallback_counts is None else self.fallback_counts[1:2]
+
+
+class IndexFlat(_FallbackCounters):
     """Exhaustive index (faiss.IndexFlat).  `metric` as faiss.MetricType."""
 
     def __init__(self, d: int, metric: int = METRIC_L2, device=None):
@@ -56,7 +71,9 @@ class IndexFlat:
         self.device = torch.device(device) if device is not None else _default_device()
         self.dp = _lib.load().nrk_padded_dim(self.d)
         self._ws = None
-        self.last_fallback = None  # device int32[1]: queries that needed the exact scan
+        # device int32[2] (include/nrk.h n_fallback): [0] queries the certificate
+        # did not cover, [1] of those, answered by the fp64 scan
+        self.fallback_counts = None
         self.reset()
 
     # -------------------------------------------------------------- storage
@@ -145,8 +162,8 @@ class IndexFlat:
         D = torch.empty((nq, k), dtype=torch.float32, device=self.device)
         I = torch.empty((nq, k), dtype=torch.int64, device=self.device)
         S = torch.empty((nq, k), dtype=torch.float64, device=self.device) if exact_scores else None
-        if self.last_fallback is None:
-            self.last_fallback = torch.zeros(1, dtype=torch.int32, device=self.device)
+        if self.fallback_counts is None:
+            self.fallback_counts = torch.zeros(2, dtype=torch.int32, device=self.device)
         with torch.cuda.device(self.device):
             sz = _lib.c_size(0)
             _lib.check(L.nrk_knn_flat_workspace(nq, self._n, self.d, k, sz), "knn_flat_workspace")
@@ -155,7 +172,7 @@ class IndexFlat:
             _lib.check(L.nrk_knn_flat(
                 _lib.ptr(xq), nq, _lib.ptr(self._xb[:n]) if n else None, _lib.ptr(self._xbh[:n]) if n else None,
                 _lib.ptr(self._meta[:n]) if n else None, _lib.ptr(self._stats), n, self.d, k, self.metric_type,
-                _lib.ptr(D), _lib.ptr(I), _lib.ptr(S), int(id_offset), _lib.ptr(self.last_fallback), _lib.ptr(ws),
+                _lib.ptr(D), _lib.ptr(I), _lib.ptr(S), int(id_offset), _lib.ptr(self.fallback_counts), _lib.ptr(ws),
                 ws.numel(), stage_events.ev if stage_events is not None else None, _lib.stream(self.device)),
                 "knn_flat")
         return (D, I, S) if exact_scores else (D, I)
@@ -324,7 +341,7 @@ def kmeans_assign(index: "IndexFlat", x: torch.Tensor):
 
 
 # --------------------------------------------------------------- IVF --
-class IndexIVFFlat:
+class IndexIVFFlat(_FallbackCounters):
     """faiss.IndexIVFFlat(quantizer, d, nlist, metric) (BASELINE configs[3]).
 
     train(x): faiss Clustering(d, nlist) with the quantizer as the assignment
@@ -354,7 +371,7 @@ class IndexIVFFlat:
         self.flat = IndexFlat(d, metric, device=self.device)  # id-order rows, bf16 copy, norms, stats
         self._assign = torch.empty(0, dtype=torch.int64, device=self.device)
         self._ws = None
-        self.last_fallback = None
+        self.fallback_counts = None
         self._lists_valid = True
         self._n_lists = 0
         self.list_off = torch.zeros(self.nlist + 1, dtype=torch.int64, device=self.device)
@@ -451,8 +468,8 @@ class IndexIVFFlat:
         D = torch.empty((nq, k), dtype=torch.float32, device=dev)
         I = torch.empty((nq, k), dtype=torch.int64, device=dev)
         S = torch.empty((nq, k), dtype=torch.float64, device=dev) if exact_scores else None
-        if self.last_fallback is None:
-            self.last_fallback = torch.zeros(1, dtype=torch.int32, device=dev)
+        if self.fallback_counts is None:
+            self.fallback_counts = torch.zeros(2, dtype=torch.int32, device=dev)
         n = self.ntotal
         f = self.flat
         with torch.cuda.device(dev):
@@ -465,7 +482,7 @@ class IndexIVFFlat:
                 _lib.ptr(self.xbh_ivf) if n else None, _lib.ptr(self.meta_ivf) if n else None, _lib.ptr(f._stats),
                 _lib.ptr(self.list_off), _lib.ptr(self.pos2id) if n else None,
                 _lib.ptr(self.pos2list) if n else None, self.nlist, n, self.max_list, self.d, k, self.metric_type,
-                _lib.ptr(D), _lib.ptr(I), _lib.ptr(S), int(id_offset), _lib.ptr(self.last_fallback), _lib.ptr(ws),
+                _lib.ptr(D), _lib.ptr(I), _lib.ptr(S), int(id_offset), _lib.ptr(self.fallback_counts), _lib.ptr(ws),
                 ws.numel(), stage_events.ev if stage_events is not None else None, _lib.stream(dev)), "ivf_search")
         return (D, I, S) if exact_scores else (D, I)
 

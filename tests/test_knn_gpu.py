@@ -32,8 +32,8 @@ def _check(xq, xb, k, metric, gpu, exact_below=None, monkeypatch=None):
 
 @pytest.mark.parametrize("metric", [ko.METRIC_IP, ko.METRIC_L2])
 def test_c1_shape(gpu, metric):
-    """configs[0]: 10k x 64, 1k queries, k=5 (screening path: NRK_EXACT_BELOW default 16384 -> exact path;
-    both paths are covered by the larger tests)."""
+    """configs[0]: 10k x 64, 1k queries, k=5 (below 16384 rows: the fp64 exact
+    path; the screened path is covered by the larger tests)."""
     xq, xb = _mixture(10_000, 1000, 64, seed=1)
     _check(xq, xb, 5, metric, gpu)
 
@@ -46,16 +46,29 @@ def test_screened_path(gpu, metric, d, k):
     assert idx.last_fallback is not None
 
 
-@pytest.mark.parametrize("defer", ["0", "1"])
 @pytest.mark.parametrize("metric", [ko.METRIC_IP, ko.METRIC_L2])
 @pytest.mark.parametrize("d,k", [(128, 5), (64, 10), (100, 32), (256, 5), (32, 1)])
-def test_screen_deferred_epilogue(gpu, monkeypatch, defer, metric, d, k):
-    """Both screen epilogues (reduced right after each MFMA chain; deferred into
-    the next chain, with the last sub-tile flushed after the loop) give the
-    oracle's exact results, including the short last tile of each chunk."""
-    monkeypatch.setenv("NRK_SCREEN_DEFER", defer)
+def test_screen_partial_chunk_tiles(gpu, metric, d, k):
+    """A corpus size whose chunks end in partial tiles (the deferred epilogue
+    masks the last sub-tile's rows after the loop) gives the oracle's results."""
     xq, xb = _mixture(70_003, 300, d, seed=d + k + 1)
     _check(xq, xb, k, metric, gpu)
+
+
+@pytest.mark.parametrize("metric", [ko.METRIC_IP, ko.METRIC_L2])
+def test_collect_pass_dense_neighbourhoods(gpu, metric):
+    """Few, dense clusters (8 centres, 400k rows): neighbours closer together
+    than the bf16 screening error bound, so the certificate leaves queries
+    uncovered; the collect pass (one more screen for those queries, every item
+    within the bound of the merge's exact k-th, exact rescoring) answers them
+    without the fp64 corpus scan, bit-exact vs the oracle."""
+    xq, xb = _mixture(400_000, 256, 128, seed=21, centers=8, sigma=0.2)
+    idx = _check(xq, xb, 10, metric, gpu)
+    nfb, nscan = int(idx.last_fallback.item()), int(idx.last_exact_scan.item())
+    print(f"uncertified {nfb}, fp64 scan {nscan}")
+    if metric == ko.METRIC_L2:
+        assert nfb > 0
+    assert nscan == 0
 
 
 def test_gaussian_unstructured(gpu):
@@ -166,12 +179,13 @@ def test_full_size_properties(gpu):
     assert int(idx.last_fallback.item()) <= 41  # certificate covers (nearly) every query
 
 
-@pytest.mark.parametrize("cap", [None, "6"])
-def test_forced_fallback_paths(gpu, monkeypatch, cap):
-    """Every query uncertified (NRK_FORCE_FALLBACK): the tiled fp64 fallback
-    (scan + select) must reproduce the oracle; with a tiny candidate cap the
-    overflow path (block-per-query exact kernel) must too."""
-    monkeypatch.setenv("NRK_FORCE_FALLBACK", "1")
+@pytest.mark.parametrize("force,cap", [("1", None), ("2", None), ("2", "6")])
+def test_forced_fallback_paths(gpu, monkeypatch, force, cap):
+    """Every query uncertified (NRK_FORCE_FALLBACK=1): the collect pass must
+    reproduce the oracle; with every collect buffer overflowed (=2) the tiled
+    fp64 fallback (scan + select) must; with a tiny candidate cap the overflow
+    path (block-per-query exact kernel) must too."""
+    monkeypatch.setenv("NRK_FORCE_FALLBACK", force)
     if cap:
         monkeypatch.setenv("NRK_FB_CAP", cap)
     xq, xb = _mixture(50_000, 200, 96, seed=11)
@@ -181,6 +195,7 @@ def test_forced_fallback_paths(gpu, monkeypatch, cap):
         for k in (1, 5, 40):
             idx = _check(xq, xb, k, metric, gpu)
             assert int(idx.last_fallback.item()) == 200
+            assert int(idx.last_exact_scan.item()) == (200 if force == "2" else 0)
 
 
 @pytest.mark.parametrize("metric", [ko.METRIC_IP, ko.METRIC_L2])
