@@ -944,8 +944,9 @@ __global__ __launch_bounds__(256) void collect_rescore_kernel(
 // Collect storage is indexed by slot s (the merge's fallback order; the first
 // fb.slots uncertified queries, which are also the ones with a stored e_k).
 // One block: turns the merge's fallback list into the one-list work table
-// (list_off, seg_off, work_off, slot_pair = s) and the per-slot thresholds,
-// saves the slot -> query map for the gather and collect_rescore, and empties
+// (list_off, seg_off, work_off, slot_pair = s), the per-slot thresholds and
+// the gathered bf16 query rows, saves the slot -> query map for
+// collect_rescore, and empties
 // the fallback list, which the overflowing queries refill.  Entries past the
 // storage (nq > 4096 only) stay in the fallback list, moved to its front,
 // with threshold -inf (they were pushed without one).
@@ -954,7 +955,7 @@ __global__ __launch_bounds__(1024) void flat_collect_plan_kernel(
     const float* __restrict__ stats, int dp, int l2, int cap, int force_overflow, int64_t* __restrict__ list_off,
     int* __restrict__ seg_off, int* __restrict__ work_off, int* __restrict__ slot_pair, float* __restrict__ thr,
     double* __restrict__ lb_g, int64_t* __restrict__ lb_i, int* __restrict__ cand_cnt, int* __restrict__ clist,
-    int* __restrict__ ccount) {
+    int* __restrict__ ccount, const uint16_t* __restrict__ qh, uint16_t* __restrict__ qc) {
   const int t = threadIdx.x, nt = blockDim.x;
   const int n = (int)min((int64_t)fb.count[0], nq);
   const int nc = n < fb.slots ? n : fb.slots;  // collected slots
@@ -979,6 +980,15 @@ __global__ __launch_bounds__(1024) void flat_collect_plan_kernel(
     ccount[0] = nc;
     ccount[1] = n;  // queries the certificate did not cover (reported as n_fallback[0])
   }
+  // the collected slots' bf16 query rows (padding rows zero): one wave per row
+  for (int row = t >> 6; row < rows; row += nt >> 6) {
+    const int64_t q = row < nc ? fb.list[row] : -1;
+    for (int j = (t & 63) * 4; j < dp; j += 256) {
+      uint2 v = make_uint2(0u, 0u);
+      if (q >= 0) v = *reinterpret_cast<const uint2*>(qh + q * dp + j);
+      *reinterpret_cast<uint2*>(qc + (int64_t)row * dp + j) = v;
+    }
+  }
   __syncthreads();  // every thread has read fb.count and the collected part of fb.list
   // the rest (s >= slots >= 1024 > nt): move to the front in rounds of nt;
   // each round reads above everything written so far
@@ -997,22 +1007,6 @@ __global__ __launch_bounds__(1024) void flat_collect_plan_kernel(
     __syncthreads();
   }
   if (t == 0) fb.count[0] = n - nc;
-}
-
-// collected slot rows of the bf16 queries: one wave per row (padding rows zeroed)
-__global__ void flat_collect_gather_kernel(const uint16_t* __restrict__ qh, int dp, const int* __restrict__ clist,
-                                           const int* __restrict__ ccount, int64_t max_rows, int wq,
-                                           uint16_t* __restrict__ qc) {
-  const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  const int nc = *ccount;
-  if (row >= max_rows || row >= (int64_t)(nc + wq - 1) / wq * wq) return;
-  const int64_t q = row < nc ? clist[row] : -1;
-  for (int j = lane * 4; j < dp; j += 256) {
-    uint2 v = make_uint2(0u, 0u);
-    if (q >= 0) v = *reinterpret_cast<const uint2*>(qh + q * dp + j);
-    *reinterpret_cast<uint2*>(qc + row * dp + j) = v;
-  }
 }
 
 // ================================================================== plan ==
@@ -1092,7 +1086,11 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
   // DP = 256 with M = 16 (k > 24, e.g. configs[4]'s 10M x 256, k = 200): 8-wave
   // workgroups, 256 queries per corpus pass; a chunk far larger than L2 is
   // then re-read by half as many query tiles
-  if (p.dp == 256 && p.M == 16) p.waves = 8;
+  // DP = 256 with M = 4 or 16: 8-wave workgroups (256 queries per corpus pass):
+  // half the LDS-DMA pieces per MFMA of the 4-wave form (10M x 256, k = 5:
+  // screen 17.4 -> 15.0 ms) and, at k = 200, a chunk far larger than L2
+  // re-read by half as many query tiles
+  if (p.dp == 256 && (p.M == 4 || p.M == 16)) p.waves = 8;
   p.R = k <= 8 ? 16 : 2 * k;
   p.tau = true;  // k = 200 at 10M x 256: -5% retrieve time
   if (p.dp == 256) p.qt = 1;
@@ -1137,7 +1135,16 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
   }
   // pre-pass: every tstride-th 64-item tile, chunks small enough that each
   // query gets >= 8R short lane streams (their maxima are distinct items)
-  p.tstride = 8;
+  // pre-pass stride: the pre-pass costs ~nb / stride per query, the main pass
+  // admits ~stride * R items above tau per query (list insertions); the best
+  // stride grows like sqrt(nb / R) (measured, IP: 1M x 128 k = 5 -> 8,
+  // 10M x 256 k = 5 -> 32 (total 17.0 -> 15.8 ms), 10M x 256 k = 200 -> 8)
+  {
+    const double want = 8.0 * sqrt((double)nb / 1e6 * 16.0 / p.R);
+    int st = 8;
+    while (st < 64 && st * 1.41421356 < want) st *= 2;
+    p.tstride = st;
+  }
   {
     const int TI = 64;  // must equal screen_kernel TI
     int64_t tiles = cdiv(nb, TI);
@@ -1190,7 +1197,7 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
   p.crows = cdiv(p.fb_slots, p.cwq) * p.cwq;
   {
     const int64_t items = (p.crows / p.cwq) * cdiv(nb, (int64_t)p.cch);
-    p.cgrid = (int)(items < 2048 ? items : 2048);
+    p.cgrid = (int)(items < 512 ? items : 512);  // two 4-wave blocks per CU fill the chip
   }
   p.off_clo = take(16);
   p.off_cseg = take(8);
@@ -1349,7 +1356,7 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
                      p.dp, qh, qmeta);
   NRK_CHECK_LAUNCH("query_prepare_kernel");
   if (p.tau) {
-    screen_fn pf = p.waves == 8 ? pick_screen_dp256_w8(l2 != 0, 1) : pick_screen(p.dp, p.qt, p.M, l2 != 0, 1);
+    screen_fn pf = p.waves == 8 ? pick_screen_dp256_w8(p.M, l2 != 0, 1) : pick_screen(p.dp, p.qt, p.M, l2 != 0, 1);
     if (!pf) return fail(NRK_EUNSUPPORTED, "knn_flat: no pre-pass kernel for dp=%d", p.dp);
     hipLaunchKernelGGL(pf, dim3(p.nqt * p.nch_pre), dim3(p.waves * 64), 0, st, qh, xb_bf16, xb_meta, nq, nb,
                        p.chunk_pre, p.nch_pre, p.nqt, p.tstride, nullptr, nullptr, pre, nullptr, IvfScreen{});
@@ -1359,7 +1366,7 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
     NRK_CHECK_LAUNCH("tau_select_kernel");
   }
 
-  screen_fn fn = p.waves == 8 ? pick_screen_dp256_w8(l2 != 0, 0) : pick_screen(p.dp, p.qt, p.M, l2 != 0, 0);
+  screen_fn fn = p.waves == 8 ? pick_screen_dp256_w8(p.M, l2 != 0, 0) : pick_screen(p.dp, p.qt, p.M, l2 != 0, 0);
   if (!fn) return fail(NRK_EUNSUPPORTED, "knn_flat: no screen kernel for dp=%d", p.dp);
   const int nblk = p.nqt * p.nch;
   mark(1);
@@ -1393,11 +1400,8 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
     int* ccount = reinterpret_cast<int*>(w + p.off_ccount);
     hipLaunchKernelGGL(flat_collect_plan_kernel, dim3(1), dim3(1024), 0, st, fb, nq, nb, p.cwq, p.cch, qmeta, stats,
                        p.dp, l2, p.ccap, fb.force >= 2 ? 1 : 0, clo, cseg, cwork, csp, cthr, clbg, clbi, ccnt, clist,
-                       ccount);
+                       ccount, qh, cqi);
     NRK_CHECK_LAUNCH("flat_collect_plan_kernel");
-    hipLaunchKernelGGL(flat_collect_gather_kernel, dim3((unsigned)cdiv(p.crows, 4)), dim3(256), 0, st, qh, p.dp, clist,
-                       ccount, p.crows, p.cwq, cqi);
-    NRK_CHECK_LAUNCH("flat_collect_gather_kernel");
     screen_fn fc = pick_screen(p.dp, 1, p.M, l2 != 0, 3);
     if (!fc) return fail(NRK_EUNSUPPORTED, "knn_flat: no collect kernel for dp=%d", p.dp);
     IvfScreen isc{cwork, clo, cseg, csp, 1, p.cch, (int)cdiv(nb, (int64_t)p.cch), cthr, ccnt, cpos, p.ccap, 1};

@@ -677,8 +677,10 @@ screen_fn pick_screen_dp64(int qt, int M, bool l2, int mode);
 screen_fn pick_screen_dp128(int qt, int M, bool l2, int mode);
 screen_fn pick_screen_dp256(int qt, int M, bool l2, int mode);
 // DP = 256, QT = 1, 8 waves (256 queries per workgroup and corpus pass):
-// the flat main pass with M = 16 (mode 0) and its pre-pass (mode 1)
-screen_fn pick_screen_dp256_w8(bool l2, int mode);
+// the flat main pass with M = 4 or 16 (mode 0) and its pre-pass (mode 1).
+// (Lane lists kept in LDS instead of registers for M = 16 measured slower at
+// k = 200: 18.8 -> 21.6 ms; each lane stream admits ~30 items above tau.)
+screen_fn pick_screen_dp256_w8(int M, bool l2, int mode);
 
 #define NRK_SCREEN_DP(DP)                                                  \
   screen_fn pick_screen_dp##DP(int qt, int M, bool l2, int mode) {         \

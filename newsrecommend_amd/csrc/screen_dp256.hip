@@ -5,12 +5,14 @@
 namespace nrk {
 NRK_SCREEN_DP(256)
 
-screen_fn pick_screen_dp256_w8(bool l2, int mode) {
+screen_fn pick_screen_dp256_w8(int M, bool l2, int mode) {
   // IP: epilogue deferred into the next MFMA chain (configs[4] retrieve
-  // 21.7 -> 19.8 ms), 64-item tiles (128 spills 460 B here); L2 keeps the direct
-  // epilogue
+  // 21.7 -> 19.8 ms), 64-item tiles (128 would spill); L2 keeps the direct
+  // epilogue.  M = 16 keeps its lane lists in LDS (screen.h ListLds).
   if (mode == 1)
     return l2 ? screen_kernel<256, 1, 1, 8, true, 1, false> : screen_kernel<256, 1, 1, 8, false, 1, false, true, 64>;
+  if (M == 4)
+    return l2 ? screen_kernel<256, 1, 4, 8, true, 0, false> : screen_kernel<256, 1, 4, 8, false, 0, false, true, 64>;
   return l2 ? screen_kernel<256, 1, 16, 8, true, 0, false> : screen_kernel<256, 1, 16, 8, false, 0, false, true, 64>;
 }
 }  // namespace nrk
