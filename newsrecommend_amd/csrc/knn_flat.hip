@@ -741,15 +741,74 @@ __global__ void ivf_count_kernel(const int64_t* __restrict__ probe, int64_t npai
   if (l >= 0 && l < nlist) atomicAdd(&cnt[l], 1);
 }
 
+// Contention-free grouping (nlist <= GROUP_LDS_LISTS): GROUP_BLOCKS blocks
+// each count their slice of the (query, probe) pairs per list in LDS and write
+// one histogram row; the plan kernel turns the rows into per-block offsets; the
+// placing blocks re-read their slice and rank inside the block with LDS
+// atomics.  (One global atomic per pair on a few hundred list counters cost
+// ~50 us per grouping at 131K pairs.)  The order of a list's queries inside its
+// segment is arbitrary: every consumer is order-independent.
+constexpr int GROUP_BLOCKS = 64;
+constexpr int GROUP_LDS_LISTS = 16384;
+
+__global__ __launch_bounds__(1024) void ivf_hist_kernel(const int64_t* __restrict__ probe, int64_t npairs, int nlist,
+                                                        int* __restrict__ H) {
+  extern __shared__ int hist[];
+  for (int l = threadIdx.x; l < nlist; l += blockDim.x) hist[l] = 0;
+  __syncthreads();
+  const int64_t per = cdiv(npairs, (int64_t)gridDim.x);
+  const int64_t i0 = (int64_t)blockIdx.x * per, i1 = i0 + per < npairs ? i0 + per : npairs;
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const int64_t l = probe[i];
+    if (l >= 0 && l < nlist) atomicAdd(&hist[l], 1);
+  }
+  __syncthreads();
+  for (int l = threadIdx.x; l < nlist; l += blockDim.x) H[(int64_t)blockIdx.x * nlist + l] = hist[l];
+}
+
+__global__ __launch_bounds__(1024) void ivf_place_kernel(const int64_t* __restrict__ probe, int64_t npairs, int nlist,
+                                                         const int* __restrict__ seg_off, const int* __restrict__ H,
+                                                         int* __restrict__ slot_pair) {
+  extern __shared__ int base[];
+  for (int l = threadIdx.x; l < nlist; l += blockDim.x) base[l] = seg_off[l] + H[(int64_t)blockIdx.x * nlist + l];
+  __syncthreads();
+  const int64_t per = cdiv(npairs, (int64_t)gridDim.x);
+  const int64_t i0 = (int64_t)blockIdx.x * per, i1 = i0 + per < npairs ? i0 + per : npairs;
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const int64_t l = probe[i];
+    if (l >= 0 && l < nlist) slot_pair[atomicAdd(&base[l], 1)] = (int)i;
+  }
+}
+
 // One block: per-list query segments (padded to wq rows) and work-item prefix.
-__global__ __launch_bounds__(1024) void ivf_plan_kernel(const int* __restrict__ cnt,
+// With H (the histogram rows of ivf_hist_kernel), the per-list counts are
+// first summed over the GB rows, which become exclusive per-block offsets.
+__global__ __launch_bounds__(1024) void ivf_plan_kernel(int* __restrict__ cnt,
                                                         const int64_t* __restrict__ list_off, int nlist, int wq,
                                                         int ch, int* __restrict__ seg_off, int* __restrict__ work_off,
-                                                        int* __restrict__ fill) {
+                                                        int* __restrict__ fill, int* __restrict__ H = nullptr,
+                                                        int GB = 0) {
   __shared__ int s_seg[1024], s_work[1024];
   const int t = threadIdx.x;
   const int per = (nlist + 1023) / 1024;
   const int lo = t * per < nlist ? t * per : nlist, hi = lo + per < nlist ? lo + per : nlist;
+  if (H) {
+    for (int l = lo; l < hi; ++l) {
+      int run = 0;
+      for (int b0 = 0; b0 < GB; b0 += 16) {  // 16 loads in flight
+        int v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = b0 + u < GB ? H[(int64_t)(b0 + u) * nlist + l] : 0;
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          if (b0 + u < GB) {
+            H[(int64_t)(b0 + u) * nlist + l] = run;
+            run += v[u];
+          }
+      }
+      cnt[l] = run;  // read back below by this same thread
+    }
+  }
   int ss = 0, sw = 0;
   for (int l = lo; l < hi; ++l) {
     const int rows = (cnt[l] + wq - 1) / wq * wq;
@@ -1453,7 +1512,7 @@ struct IvfPlan {
   int chB, cmaxB, cap;      // phase B: all probed lists, collect above e_k - B
   int fb_slots, fb_cap;
   int64_t nq_pad, max_rows, ubA, ubB;
-  size_t off_fbc, off_cnt, off_fill, off_seg, off_work, off_sp, off_qh, off_qmeta, off_qi, off_p0, off_ps, off_pi,
+  size_t off_fbc, off_cnt, off_fill, off_hist, off_seg, off_work, off_sp, off_qh, off_qmeta, off_qi, off_p0, off_ps, off_pi,
       off_pt, off_pa, off_tau, off_seed, off_lbg, off_lbi, off_thr, off_ccnt, off_cpos, off_fbl, off_fbt, off_fbi, off_fbn, off_fcg, off_fci,
       off_ovl, total;
 };
@@ -1520,6 +1579,7 @@ static IvfPlan make_ivf_plan(int64_t nq, int nprobe, int nlist, int64_t max_list
   p.off_fbc = take(16);
   p.off_cnt = take((size_t)nlist * 4);
   p.off_fill = take((size_t)nlist * 4);
+  p.off_hist = take((size_t)GROUP_BLOCKS * nlist * 4);
   p.off_seg = take((size_t)(nlist + 1) * 4);
   p.off_work = take((size_t)(nlist + 1) * 4);
   p.off_sp = take((size_t)p.max_rows * 4);
@@ -1550,18 +1610,32 @@ static IvfPlan make_ivf_plan(int64_t nq, int nprobe, int nlist, int64_t max_list
 // group (query, probe) pairs by list and gather the probing queries list-major
 static int ivf_group(const int64_t* probe, int64_t nq, int nprobe, int nlist, const int64_t* list_off, int wq, int ch,
                      int dp, int64_t max_rows, const uint16_t* qh, int* cnt, int* fill, int* seg, int* work, int* sp,
-                     uint16_t* qi, hipStream_t st) {
+                     uint16_t* qi, int* H, hipStream_t st) {
   const int64_t npairs = nq * nprobe;
-  if (hipMemsetAsync(cnt, 0, (size_t)nlist * 4, st) != hipSuccess ||
-      hipMemsetAsync(sp, 0xff, (size_t)max_rows * 4, st) != hipSuccess)
+  if (hipMemsetAsync(sp, 0xff, (size_t)max_rows * 4, st) != hipSuccess)
     return fail(NRK_ELAUNCH, "ivf_search: memset failed");
-  hipLaunchKernelGGL(ivf_count_kernel, dim3((unsigned)cdiv(npairs, 256)), dim3(256), 0, st, probe, npairs, nlist, cnt);
-  NRK_CHECK_LAUNCH("ivf_count_kernel");
-  hipLaunchKernelGGL(ivf_plan_kernel, dim3(1), dim3(1024), 0, st, cnt, list_off, nlist, wq, ch, seg, work, fill);
-  NRK_CHECK_LAUNCH("ivf_plan_kernel");
-  hipLaunchKernelGGL(ivf_scatter_kernel, dim3((unsigned)cdiv(npairs, 256)), dim3(256), 0, st, probe, npairs, nlist,
-                     seg, fill, sp);
-  NRK_CHECK_LAUNCH("ivf_scatter_kernel");
+  if (nlist <= GROUP_LDS_LISTS) {
+    const size_t lds = (size_t)nlist * 4;
+    hipLaunchKernelGGL(ivf_hist_kernel, dim3(GROUP_BLOCKS), dim3(1024), lds, st, probe, npairs, nlist, H);
+    NRK_CHECK_LAUNCH("ivf_hist_kernel");
+    hipLaunchKernelGGL(ivf_plan_kernel, dim3(1), dim3(1024), 0, st, cnt, list_off, nlist, wq, ch, seg, work, fill, H,
+                       GROUP_BLOCKS);
+    NRK_CHECK_LAUNCH("ivf_plan_kernel");
+    hipLaunchKernelGGL(ivf_place_kernel, dim3(GROUP_BLOCKS), dim3(1024), lds, st, probe, npairs, nlist, seg, H, sp);
+    NRK_CHECK_LAUNCH("ivf_place_kernel");
+  } else {
+    if (hipMemsetAsync(cnt, 0, (size_t)nlist * 4, st) != hipSuccess)
+      return fail(NRK_ELAUNCH, "ivf_search: memset failed");
+    hipLaunchKernelGGL(ivf_count_kernel, dim3((unsigned)cdiv(npairs, 256)), dim3(256), 0, st, probe, npairs, nlist,
+                       cnt);
+    NRK_CHECK_LAUNCH("ivf_count_kernel");
+    hipLaunchKernelGGL(ivf_plan_kernel, dim3(1), dim3(1024), 0, st, cnt, list_off, nlist, wq, ch, seg, work, fill,
+                       nullptr, 0);
+    NRK_CHECK_LAUNCH("ivf_plan_kernel");
+    hipLaunchKernelGGL(ivf_scatter_kernel, dim3((unsigned)cdiv(npairs, 256)), dim3(256), 0, st, probe, npairs, nlist,
+                       seg, fill, sp);
+    NRK_CHECK_LAUNCH("ivf_scatter_kernel");
+  }
   hipLaunchKernelGGL(ivf_gather_kernel, dim3((unsigned)cdiv(max_rows, 4)), dim3(256), 0, st, qh, dp, nprobe, sp, seg,
                      nlist, max_rows, qi);
   NRK_CHECK_LAUNCH("ivf_gather_kernel");
@@ -1608,6 +1682,7 @@ extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe,
   };
   int* cnt = reinterpret_cast<int*>(w + p.off_cnt);
   int* fill = reinterpret_cast<int*>(w + p.off_fill);
+  int* hist = reinterpret_cast<int*>(w + p.off_hist);
   int* seg = reinterpret_cast<int*>(w + p.off_seg);
   int* work = reinterpret_cast<int*>(w + p.off_work);
   int* sp = reinterpret_cast<int*>(w + p.off_sp);
@@ -1650,13 +1725,13 @@ extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe,
         hipMemsetAsync(ccnt, 0, (size_t)nq * 4, st) != hipSuccess)
       return fail(NRK_ELAUNCH, "ivf_search: copy/memset failed");
     int rc =
-        ivf_group(p0, nq, p.nA, nlist, list_off, p.wqA, p.chA, p.dp, p.max_rows, qh, cnt, fill, seg, work, sp, qi, st);
+        ivf_group(p0, nq, p.nA, nlist, list_off, p.wqA, p.chA, p.dp, p.max_rows, qh, cnt, fill, seg, work, sp, qi, hist, st);
     if (rc != NRK_OK) return rc;
     screen_fn fa = pick_screen(p.dp, p.qtA, p.M, l2 != 0, 4);
     if (!fa) return fail(NRK_EUNSUPPORTED, "ivf_search: no screen kernel for dp=%d", p.dp);
     IvfScreen isa{work, list_off, seg, sp, nlist, p.chA, p.cmaxA, nullptr, nullptr, nullptr, 0, p.nA};
-    hipLaunchKernelGGL(fa, dim3((unsigned)p.ubA), dim3(p.waves * 64), 0, st, qi, xbh_ivf, meta_ivf, nq, n, 0, 0, 0, 1,
-                       nullptr, pa, pt, nullptr, isa);
+    hipLaunchKernelGGL(fa, dim3((unsigned)p.ubA), dim3(p.waves * 64), 0, st, qi, xbh_ivf, meta_ivf, nq, n, 0, 0, 0,
+                       2, nullptr, pa, pt, nullptr, isa);  // every other tile: seeds from half the rows (measured +3 %)
     NRK_CHECK_LAUNCH("screen_kernel (ivf phase A)");
     hipLaunchKernelGGL(tau_select_kernel, dim3((unsigned)cdiv(nq, 4)), dim3(256), 0, st, pt, 2 * p.nA * p.cmaxA, p.R,
                        nq, tau, pa, seed);
@@ -1667,7 +1742,7 @@ extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe,
     NRK_CHECK_LAUNCH("ivf_thr_kernel");
     // ---- phase B grouping: every probed list
     rc = ivf_group(probe, nq, nprobe, nlist, list_off, p.wq, p.chB, p.dp, p.max_rows, qh, cnt, fill, seg, work, sp, qi,
-                   st);
+                   hist, st);
     if (rc != NRK_OK) return rc;
   } else if (hipMemsetAsync(ccnt, 0, (size_t)nq * 4, st) != hipSuccess) {  // empty index: all -1
     return fail(NRK_ELAUNCH, "ivf_search: memset");
