@@ -564,6 +564,65 @@ __global__ __launch_bounds__(256) void small_select_kernel(const double* __restr
   }
 }
 
+// k <= SW_K and nb <= 64 * VPL (the coarse quantizer: nlist centroids, k =
+// nprobe): one wave per query, VPL goodness values per lane in registers, k
+// rounds of wave argmax in the bitonic sort's order (goodness descending, id
+// ascending).  A block sort per query spends most of its time in barriers.
+constexpr int SW_K = 64;
+template <int VPL>
+__global__ __launch_bounds__(256) void small_select_wave_kernel(const double* __restrict__ G, int64_t ldg, int64_t q0,
+                                                                int64_t nc, int64_t nq, int64_t nb, int k, int l2,
+                                                                float* __restrict__ D, int64_t* __restrict__ I,
+                                                                double* __restrict__ S, int64_t id_offset) {
+  const int lane = threadIdx.x & 63;
+  const int64_t ql = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t qi = q0 + ql;
+  if (ql >= nc || qi >= nq) return;
+  const double* row = G + ql * ldg;
+  double v[VPL];
+#pragma unroll
+  for (int j = 0; j < VPL; ++j) {
+    const int64_t i = (int64_t)j * 64 + lane;
+    v[j] = i < nb ? row[i] : -INFINITY;
+  }
+  for (int r = 0; r < k; ++r) {
+    // the lane's best (an extracted entry reads -inf; it can only win once no
+    // real item is left, i.e. r >= nb): first item, then strictly greater, so
+    // the lowest index wins ties
+    double bv = -INFINITY;
+    int bj = VPL;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j)
+      if ((int64_t)j * 64 + lane < nb && (bj == VPL || v[j] > bv)) {
+        bv = v[j];
+        bj = j;
+      }
+    int bi = bj < VPL ? bj * 64 + lane : INT_MAX;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double ov = __shfl_xor(bv, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ov > bv || (ov == bv && oi < bi)) {
+        bv = ov;
+        bi = oi;
+      }
+    }
+    const bool valid = r < nb && bi != INT_MAX;
+    if (valid && lane == (bi & 63)) {
+#pragma unroll
+      for (int j = 0; j < VPL; ++j)
+        if (j == (bi >> 6)) v[j] = -INFINITY;
+    }
+    if (lane == 0) {
+      const int64_t o = qi * k + r;
+      const double sc = valid ? (l2 ? -bv : bv) : (l2 ? DBL_MAX : -DBL_MAX);
+      D[o] = valid ? (float)sc : (l2 ? FLT_MAX : -FLT_MAX);
+      I[o] = valid ? (int64_t)bi + id_offset : -1;
+      if (S) S[o] = sc;
+    }
+  }
+}
+
 // ========================================================= tiled fallback ==
 // Chip-wide fp64 scan for the fallback slots: 64-row fp32 tiles staged in LDS
 // (row stride d+1, so lane = row reads are bank-conflict free), each wave
@@ -1303,9 +1362,23 @@ static int small_launch(const FlatPlan& p, const float* xq, int64_t nq, const fl
         hipLaunchKernelGGL(small_scores_kernel<false>, grid, dim3(256), 0, st, xq, q0, nq, xb, nb, d, G, p.small_ld);
       NRK_CHECK_LAUNCH("small_scores_kernel");
     }
-    hipLaunchKernelGGL(small_select_kernel, dim3((unsigned)nc), dim3(256), smem, st, G, p.small_ld, q0, nq, nb, k, l2,
-                       p.small_P, D, I, S, id_offset);
-    NRK_CHECK_LAUNCH("small_select_kernel");
+    if (k <= SW_K && nb <= 1024) {
+      const dim3 g4((unsigned)cdiv(nc, (int64_t)4));
+      if (nb <= 256)
+        hipLaunchKernelGGL(small_select_wave_kernel<4>, g4, dim3(256), 0, st, G, p.small_ld, q0, nc, nq, nb, k, l2, D,
+                           I, S, id_offset);
+      else if (nb <= 512)
+        hipLaunchKernelGGL(small_select_wave_kernel<8>, g4, dim3(256), 0, st, G, p.small_ld, q0, nc, nq, nb, k, l2, D,
+                           I, S, id_offset);
+      else
+        hipLaunchKernelGGL(small_select_wave_kernel<16>, g4, dim3(256), 0, st, G, p.small_ld, q0, nc, nq, nb, k, l2, D,
+                           I, S, id_offset);
+      NRK_CHECK_LAUNCH("small_select_wave_kernel");
+    } else {
+      hipLaunchKernelGGL(small_select_kernel, dim3((unsigned)nc), dim3(256), smem, st, G, p.small_ld, q0, nq, nb, k,
+                         l2, p.small_P, D, I, S, id_offset);
+      NRK_CHECK_LAUNCH("small_select_kernel");
+    }
   }
   return NRK_OK;
 }
