@@ -134,7 +134,9 @@ def bench_flat(args, rank, world, dev):
         "fallback_queries": fallback[0], "exact_scan_queries": fallback[1],
         "roofline": {"bound": "mfma", "kernel": "screen_kernel (bf16 v_mfma_f32_32x32x16)",
                      "achieved": achieved, "peak": BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / BF16_DENSE_TFLOPS, "traffic": _pmc_traffic(args, world),
+                     "frac": achieved / BF16_DENSE_TFLOPS,
+                     "traffic": _pmc_traffic(f"nb={args.nb},d={args.d},nq={args.nq},k={args.k},metric={args.metric},"
+                                             f"gpus={world}"),
                      "algorithmic": f"2*nq*nb_local*d = {flops:.4g} flop per launch"},
     }
     if rank == 0:
@@ -188,14 +190,13 @@ def _cpu_flat(args, xq, xb_host, metric, nb=None, d=None, k=None):
                       f"blocks + running top-k, {cores} threads), {dt:.1f} s"}
 
 
-def _pmc_traffic(args, world):
-    """HBM bytes per screen launch from a committed rocprofv3 --pmc summary for
-    this exact workload (profiles/pmc_screen.json), else null."""
+def _pmc_traffic(key):
+    """HBM bytes per launch of the record's dominant kernel from a committed
+    rocprofv3 --pmc summary for this exact workload (profiles/pmc_screen.json,
+    FETCH_SIZE x2 + WRITE_SIZE from separate passes), else null."""
     p = os.path.join(ROOT, "profiles", "pmc_screen.json")
     try:
-        j = json.load(open(p))
-        key = f"nb={args.nb},d={args.d},nq={args.nq},k={args.k},metric={args.metric},gpus={world}"
-        return j.get(key, {}).get("hbm_bytes_per_launch")
+        return json.load(open(p)).get(key, {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None
 
@@ -254,7 +255,9 @@ def bench_ivf(args, rank, world, dev):
         "exact_scan_queries": int(index.local.last_exact_scan.item()),
         "roofline": {"bound": "mfma", "kernel": "screen_kernel MODE 3 (IVF collect, bf16 v_mfma_f32_32x32x16)",
                      "achieved": achieved, "peak": BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / BF16_DENSE_TFLOPS, "traffic": None,
+                     "frac": achieved / BF16_DENSE_TFLOPS,
+                     "traffic": _pmc_traffic(f"ivf:nb={args.ivf_nb},d={d},nq={nq},k={k},nlist={nlist},"
+                                             f"nprobe={nprobe},gpus={world}"),
                      "algorithmic": f"2*d*sum(probed local list sizes) = {flops:.4g} flop per launch"},
     }
     # recall@5 against the exact flat search over the whole corpus (our flat
@@ -366,9 +369,10 @@ def bench_n1(args, rank, world, dev, index, xb):
                       "merge_rescore": float(st[2]), "exact_fallback": float(st[3])},
         "fallback_queries": int(index.local.last_fallback.item()),
         "exact_scan_queries": int(index.local.last_exact_scan.item()),
-        "roofline": {"bound": "mfma", "kernel": "screen_kernel (bf16 v_mfma_f32_32x32x16, dp 256)",
+        "roofline": {"bound": "mfma", "kernel": "screen_kernel (bf16 v_mfma_f32_32x32x16, dp 256, 8 waves)",
                      "achieved": achieved, "peak": BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / BF16_DENSE_TFLOPS, "traffic": None,
+                     "frac": achieved / BF16_DENSE_TFLOPS,
+                     "traffic": _pmc_traffic(f"n1:nb={n},d={d},nq={nq},k={k},metric=ip,gpus={world}"),
                      "algorithmic": f"2*nq*nb_local*d = {flops:.4g} flop per launch"},
     }
     if rank == 0:
