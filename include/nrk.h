@@ -251,7 +251,10 @@ int nrk_din_head_train(const float* q, const float* pooled, int64_t ld_pooled, c
  * grads are scaled in place by the clip coefficient, exp_avg / exp_avg_sq /
  * params updated with torch's capturable-Adam formulas.  lr_dev (device f32,
  * optional) overrides lr when non-null, so ReduceLROnPlateau (DIN.py:246,254)
- * can change the rate of a captured step between graph replays. */
+ * can change the rate of a captured step between graph replays.  The
+ * workspace must be ZEROED once before the first call (n <= 131072 runs one
+ * launch whose completion ticket lives there and is left zero); calls sharing
+ * one workspace must be stream-ordered. */
 int nrk_clip_adam_workspace(int64_t n, size_t* ws_bytes);
 int nrk_clip_adam(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
                   float* step, float lr, const float* lr_dev, float beta1, float beta2, float eps, float weight_decay,

@@ -53,10 +53,11 @@ __device__ __forceinline__ float hx(const HeadArgs& a, int64_t r, int c) {
   return c < a.d ? a.q[r * a.d + c] : a.pooled[r * a.ld + (c - a.d)];
 }
 
-// counter-based dropout mask (splitmix64 of (seed, step, layer, row, col))
-__device__ __forceinline__ float keep_scale(const HeadArgs& a, int layer, int64_t r, int c) {
+// counter-based dropout mask (splitmix64 of (seed, step, layer, row, col));
+// keep_scale_s takes the step value read once per thread
+__device__ __forceinline__ float keep_scale_s(const HeadArgs& a, float stepv, int layer, int64_t r, int c) {
   if (a.p_drop <= 0.f) return 1.f;
-  uint64_t z = a.seed ^ ((uint64_t)(int64_t)(*a.step) * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)layer << 58) ^
+  uint64_t z = a.seed ^ ((uint64_t)(int64_t)stepv * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)layer << 58) ^
                ((uint64_t)r << 20) ^ (uint64_t)c;
   z += 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -64,6 +65,9 @@ __device__ __forceinline__ float keep_scale(const HeadArgs& a, int layer, int64_
   z ^= z >> 31;
   const float u = (float)(z >> 40) * (1.0f / 16777216.0f);
   return u >= a.p_drop ? 1.f / (1.f - a.p_drop) : 0.f;
+}
+__device__ __forceinline__ float keep_scale(const HeadArgs& a, int layer, int64_t r, int c) {
+  return keep_scale_s(a, *a.step, layer, r, c);
 }
 
 // Column sums over the blocks' partials, fixed order (deterministic): a
@@ -604,10 +608,14 @@ __global__ __launch_bounds__(256) void hf_stats0(HeadArgs a) {
 }
 
 // LDS (floats): mean/inv [D2] x 2 | h0 [32][D2+4] | W1 [32][D2+4] | red [4][32][32] | d1 [32][33]
+// NX = D2 / 32: float4 of the block's x rows per thread (issued before the
+// prologue's partial sums, so the two memory round trips overlap)
+template <int NX>
 __global__ __launch_bounds__(256) void hf_fwd1(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   __shared__ double pro_tmp[256], pro_sum[1024];
-  const int D2 = a.D2, hs = D2 + 4, t = threadIdx.x;
+  constexpr int D2 = NX * 32, hs = D2 + 4, q4 = D2 / 4;
+  const int t = threadIdx.x;
   float* mean = sm;
   float* inv = mean + D2;
   float* h0 = inv + D2;
@@ -615,39 +623,39 @@ __global__ __launch_bounds__(256) void hf_fwd1(HeadArgs a) {
   float* red = w1 + HF * hs;
   float* d1 = red + 4 * HR * HF;
   const int64_t r0 = (int64_t)blockIdx.x * HR;
+  float4 xv[NX];
+#pragma unroll
+  for (int u = 0; u < NX; ++u) {
+    const int e = t + u * 256;
+    xv[u] = hx4(a, r0 + e / q4, 4 * (e % q4));
+  }
   colsum_prologue(a.part0, a.nrg0, 2 * D2, 2 * D2, pro_tmp, pro_sum);
   bn_finalize(a, pro_sum, D2, mean, inv, a.stat0, a.p.bn0_rm, a.p.bn0_rv, a.p.bn0_nb, blockIdx.x == 0);
-  {  // W1 and the block's x rows, 8 float4 loads in flight per thread
-    const int n4 = HF * D2 / 4, q4 = D2 / 4;
-    for (int e0 = t; e0 < n4; e0 += 8 * 256) {
-      float4 wv[8], xv[8];
+  {  // W1 (L2-resident: every block reads it)
+    float4 wv[NX];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int e = e0 + u * 256;
-        if (e < n4) {
-          wv[u] = *reinterpret_cast<const float4*>(a.p.fc1_w + 4 * e);
-          xv[u] = hx4(a, r0 + e / q4, 4 * (e % q4));
-        }
-      }
+    for (int u = 0; u < NX; ++u) wv[u] = *reinterpret_cast<const float4*>(a.p.fc1_w + 4 * (t + u * 256));
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int e = e0 + u * 256;
-        if (e < n4) {
-          const int row = e / q4, c = 4 * (e % q4);
-          *reinterpret_cast<float4*>(w1 + row * hs + c) = wv[u];
-          xv[u].x = (xv[u].x - mean[c]) * inv[c] * a.p.bn0_w[c] + a.p.bn0_b[c];
-          xv[u].y = (xv[u].y - mean[c + 1]) * inv[c + 1] * a.p.bn0_w[c + 1] + a.p.bn0_b[c + 1];
-          xv[u].z = (xv[u].z - mean[c + 2]) * inv[c + 2] * a.p.bn0_w[c + 2] + a.p.bn0_b[c + 2];
-          xv[u].w = (xv[u].w - mean[c + 3]) * inv[c + 3] * a.p.bn0_w[c + 3] + a.p.bn0_b[c + 3];
-          *reinterpret_cast<float4*>(h0 + row * hs + c) = xv[u];
-        }
-      }
+    for (int u = 0; u < NX; ++u) {
+      const int e = t + u * 256;
+      *reinterpret_cast<float4*>(w1 + (e / q4) * hs + 4 * (e % q4)) = wv[u];
     }
+  }
+  __syncthreads();  // mean / inv published
+#pragma unroll
+  for (int u = 0; u < NX; ++u) {
+    const int e = t + u * 256, row = e / q4, c = 4 * (e % q4);
+    float4 x = xv[u];
+    x.x = (x.x - mean[c]) * inv[c] * a.p.bn0_w[c] + a.p.bn0_b[c];
+    x.y = (x.y - mean[c + 1]) * inv[c + 1] * a.p.bn0_w[c + 1] + a.p.bn0_b[c + 1];
+    x.z = (x.z - mean[c + 2]) * inv[c + 2] * a.p.bn0_w[c + 2] + a.p.bn0_b[c + 2];
+    x.w = (x.w - mean[c + 3]) * inv[c + 3] * a.p.bn0_w[c + 3] + a.p.bn0_b[c + 3];
+    *reinterpret_cast<float4*>(h0 + row * hs + c) = x;
   }
   __syncthreads();
   {  // a1 = h0 W1^T: lane half h covers k in [h D2/2, (h+1) D2/2), wave w a quarter of that
     const int lane = t & 63, w = t >> 6, i = lane & 31, h = lane >> 5;
-    const int kw = D2 / 8;
+    constexpr int kw = D2 / 8;
     const float* ar = h0 + i * hs + h * (D2 / 2) + w * kw;
     const float* br = w1 + i * hs + h * (D2 / 2) + w * kw;
     f32x16 acc;
@@ -684,10 +692,12 @@ __global__ __launch_bounds__(256) void hf_fwd1(HeadArgs a) {
 }
 
 // LDS (floats): m0/i0 [D2] x 2 | xhat0 [32][D2+4] | da1 [32][33] | m1/i1/sb1/sg1 [32] x 4
+template <int NX>
 __global__ __launch_bounds__(256) void hf_bwd1(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   __shared__ double pro_tmp[256], pro_sum[64];
-  const int D2 = a.D2, hs = D2 + 4, t = threadIdx.x;
+  constexpr int D2 = NX * 32, hs = D2 + 4;
+  const int t = threadIdx.x;
   float* m0 = sm;
   float* i0 = m0 + D2;
   float* xh = i0 + D2;
@@ -698,46 +708,41 @@ __global__ __launch_bounds__(256) void hf_bwd1(HeadArgs a) {
   float* sg1 = sb1 + HF;
   const int64_t r0 = (int64_t)blockIdx.x * HR;
   const int s4 = 2 * HF + a.F2 * HF + a.F2;
-  colsum_prologue(a.part4, a.nblk, s4, 2 * HF, pro_tmp, pro_sum);
+  constexpr int q4 = D2 / 4;
+  // every load of the block's rows first, then the prologue's partial sums
+  float4 xv[NX];
+#pragma unroll
+  for (int u = 0; u < NX; ++u) {
+    const int e = t + u * 256;
+    xv[u] = hx4(a, r0 + e / q4, 4 * (e % q4));
+  }
+  float a1v[HR * HF / 256], dhv[HR * HF / 256];
+#pragma unroll
+  for (int u = 0; u < HR * HF / 256; ++u) {
+    const int e = t + u * 256;
+    a1v[u] = a.a1[r0 * HF + e];
+    dhv[u] = a.dh1[r0 * HF + e];
+  }
   load_stat(a.stat0, D2, m0, i0);
   load_stat(a.stat1, HF, m1, i1);
+  colsum_prologue(a.part4, a.nblk, s4, 2 * HF, pro_tmp, pro_sum);
   if (t < HF) {
     sb1[t] = (float)pro_sum[t];
     sg1[t] = (float)pro_sum[HF + t];
   }
   __syncthreads();
-  {
-    const int q4 = D2 / 4, n4 = HR * q4;
-    for (int e0 = t; e0 < n4; e0 += 8 * 256) {
-      float4 xv[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int e = e0 + u * 256;
-        if (e < n4) xv[u] = hx4(a, r0 + e / q4, 4 * (e % q4));
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int e = e0 + u * 256;
-        if (e < n4) {
-          const int row = e / q4, c = 4 * (e % q4);
-          xv[u].x = (xv[u].x - m0[c]) * i0[c];
-          xv[u].y = (xv[u].y - m0[c + 1]) * i0[c + 1];
-          xv[u].z = (xv[u].z - m0[c + 2]) * i0[c + 2];
-          xv[u].w = (xv[u].w - m0[c + 3]) * i0[c + 3];
-          *reinterpret_cast<float4*>(xh + row * hs + c) = xv[u];
-        }
-      }
-    }
+  for (int u = 0; u < NX; ++u) {
+    const int e = t + u * 256, row = e / q4, c = 4 * (e % q4);
+    float4 x = xv[u];
+    x.x = (x.x - m0[c]) * i0[c];
+    x.y = (x.y - m0[c + 1]) * i0[c + 1];
+    x.z = (x.z - m0[c + 2]) * i0[c + 2];
+    x.w = (x.w - m0[c + 3]) * i0[c + 3];
+    *reinterpret_cast<float4*>(xh + row * hs + c) = x;
   }
   const float invB = 1.f / (float)a.B;
   {
-    float a1v[HR * HF / 256], dhv[HR * HF / 256];
-#pragma unroll
-    for (int u = 0; u < HR * HF / 256; ++u) {
-      const int e = t + u * 256;
-      a1v[u] = a.a1[r0 * HF + e];
-      dhv[u] = a.dh1[r0 * HF + e];
-    }
 #pragma unroll
     for (int u = 0; u < HR * HF / 256; ++u) {
       const int e = t + u * 256, r = e / HF, j = e % HF;
@@ -788,6 +793,11 @@ __global__ __launch_bounds__(1024) void hf_reduce(HeadArgs a) {
     __shared__ double Gt[32][4], St[32];
     const int ph = t >> 7, j = (t >> 2) & 31, cl = t & 3;
     const int c = 4 * blockIdx.x + cl;
+    float wv[HF];  // W1 column of this block's column t (t < 4), loaded with the partials
+    if (t < 4) {
+#pragma unroll
+      for (int jj = 0; jj < HF; ++jj) wv[jj] = a.p.fc1_w[(int64_t)jj * D2 + 4 * blockIdx.x + t];
+    }
     double acc = 0.0;
     for (int b0 = ph; b0 < nblk; b0 += 8 * 16) {
       float v[16];
@@ -835,9 +845,6 @@ __global__ __launch_bounds__(1024) void hf_reduce(HeadArgs a) {
     if (t < 4) {
       const int col = 4 * blockIdx.x + t;
       double sb = 0.0, sg = 0.0;
-      float wv[HF];
-#pragma unroll
-      for (int jj = 0; jj < HF; ++jj) wv[jj] = a.p.fc1_w[(int64_t)jj * D2 + col];
 #pragma unroll
       for (int jj = 0; jj < HF; ++jj) {
         sb += (double)wv[jj] * St[jj];
@@ -893,6 +900,300 @@ __global__ __launch_bounds__(1024) void hf_reduce(HeadArgs a) {
   }
 }
 
+// ---- the small layers of the fast head (F = 32, F/2 = 16, 32 rows per block).
+// Every global load of the block's rows and weights is issued before the
+// prologue's partial sums (one memory round trip instead of two), and the
+// column sums over the block's rows run as row-group partials combined in a
+// fixed order (no 32-step dependent LDS chains): the kernels are latency-bound.
+constexpr int HF2 = HF / 2;
+
+// BN1 (prologue sums) -> Linear(32, 16) -> ReLU -> Dropout; BN2 partial sums
+__global__ __launch_bounds__(256) void hf_fwd2(HeadArgs a) {
+  __shared__ __attribute__((aligned(16))) float h1[HR][HF + 4];
+  __shared__ __attribute__((aligned(16))) float w2[HF2][HF + 4];
+  __shared__ float d2[HR][HF2 + 1];
+  __shared__ float mean[HF], inv[HF], b2s[HF2];
+  __shared__ double red[2][16][HF2];
+  __shared__ double pro_tmp[256], pro_sum[2 * HF];
+  const int t = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * HR;
+  const float stepv = *a.step;
+  const float4 av = reinterpret_cast<const float4*>(a.a1 + r0 * HF)[t];  // row t/8, cols 4(t%8)..
+  float4 wv = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (t < HF2 * HF / 4) wv = reinterpret_cast<const float4*>(a.p.fc2_w)[t];
+  const float gw = t < HF ? a.p.bn1_w[t] : 0.f, gb = t < HF ? a.p.bn1_b[t] : 0.f;
+  if (t < HF2) b2s[t] = a.p.fc2_b[t];
+  colsum_prologue(a.part1, a.nblk, 2 * HF, 2 * HF, pro_tmp, pro_sum);
+  bn_finalize(a, pro_sum, HF, mean, inv, a.stat1, a.p.bn1_rm, a.p.bn1_rv, a.p.bn1_nb, blockIdx.x == 0);
+  __shared__ float gws[HF], gbs[HF];
+  if (t < HF) {
+    gws[t] = gw;
+    gbs[t] = gb;
+  }
+  __syncthreads();
+  {
+    const int r = t >> 3, j0 = (t & 7) * 4;
+    const float x[4] = {av.x, av.y, av.z, av.w};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = j0 + u;
+      const float d1 = fmaxf(x[u], 0.f) * keep_scale_s(a, stepv, 1, r0 + r, j);
+      h1[r][j] = (d1 - mean[j]) * inv[j] * gws[j] + gbs[j];
+    }
+    if (t < HF2 * HF / 4) *reinterpret_cast<float4*>(&w2[t >> 3][(t & 7) * 4]) = wv;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {  // a2 = h1 W2^T + b2: 512 outputs
+    const int o = t + 256 * u, r = o >> 4, k = o & 15;
+    float4 hv[HF / 4], wq[HF / 4];
+#pragma unroll
+    for (int i = 0; i < HF / 4; ++i) {
+      hv[i] = *reinterpret_cast<const float4*>(&h1[r][4 * i]);
+      wq[i] = *reinterpret_cast<const float4*>(&w2[k][4 * i]);
+    }
+    float c0 = b2s[k], c1 = 0.f, c2 = 0.f, c3 = 0.f;
+#pragma unroll
+    for (int i = 0; i < HF / 4; ++i) {
+      c0 = fmaf(hv[i].x, wq[i].x, c0);
+      c1 = fmaf(hv[i].y, wq[i].y, c1);
+      c2 = fmaf(hv[i].z, wq[i].z, c2);
+      c3 = fmaf(hv[i].w, wq[i].w, c3);
+    }
+    const float acc = (c0 + c1) + (c2 + c3);
+    a.a2[(r0 + r) * HF2 + k] = acc;
+    d2[r][k] = fmaxf(acc, 0.f) * keep_scale_s(a, stepv, 2, r0 + r, k);
+  }
+  __syncthreads();
+  {  // BN2 partial sums: 16 columns x 16 groups of 2 rows
+    const int k = t & 15, g = t >> 4;
+    const double v0 = d2[2 * g][k], v1 = d2[2 * g + 1][k];
+    red[0][g][k] = v0 + v1;
+    red[1][g][k] = v0 * v0 + v1 * v1;
+  }
+  __syncthreads();
+  if (t < 2 * HF2) {
+    const int which = t >> 4, k = t & 15;
+    double s = 0.0;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) s += red[which][g][k];
+    a.part2[(int64_t)blockIdx.x * 2 * HF2 + which * HF2 + k] = s;
+  }
+}
+
+// BN2 (prologue sums) -> Linear(16, 1) -> BCEWithLogits (mean); dlogit;
+// dh2 = dlogit w3; BN2-backward and fc3 partial sums, loss partial
+__global__ __launch_bounds__(256) void hf_fwd3(HeadArgs a) {
+  __shared__ float h2[HR][HF2 + 1], xh[HR][HF2 + 1];
+  __shared__ float mean[HF2], inv[HF2], w3[HF2], gw2[HF2], gb2[HF2], dl[HR], lo[HR];
+  __shared__ double red[3][16][HF2];
+  __shared__ double pro_tmp[256], pro_sum[2 * HF2];
+  const int t = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * HR;
+  const float stepv = *a.step;
+  float4 av = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (t < HR * HF2 / 4) av = reinterpret_cast<const float4*>(a.a2 + r0 * HF2)[t];  // row t/4, cols 4(t%4)..
+  const float yv = t < HR ? a.y[r0 + t] : 0.f;
+  const float b3 = a.p.fc3_b[0];
+  if (t < HF2) {
+    w3[t] = a.p.fc3_w[t];
+    gw2[t] = a.p.bn2_w[t];
+    gb2[t] = a.p.bn2_b[t];
+  }
+  colsum_prologue(a.part2, a.nblk, 2 * HF2, 2 * HF2, pro_tmp, pro_sum);
+  bn_finalize(a, pro_sum, HF2, mean, inv, a.stat2, a.p.bn2_rm, a.p.bn2_rv, a.p.bn2_nb, blockIdx.x == 0);
+  __syncthreads();
+  if (t < HR * HF2 / 4) {
+    const int r = t >> 2, k0 = (t & 3) * 4;
+    const float x4[4] = {av.x, av.y, av.z, av.w};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = k0 + u;
+      const float d2 = fmaxf(x4[u], 0.f) * keep_scale_s(a, stepv, 2, r0 + r, k);
+      const float x = (d2 - mean[k]) * inv[k];
+      xh[r][k] = x;
+      h2[r][k] = x * gw2[k] + gb2[k];
+    }
+  }
+  __syncthreads();
+  if (t < HR) {
+    float z = b3;
+#pragma unroll
+    for (int k = 0; k < HF2; ++k) z = fmaf(h2[t][k], w3[k], z);
+    a.logits[r0 + t] = z;
+    lo[t] = fmaxf(z, 0.f) - z * yv + log1pf(expf(-fabsf(z)));
+    dl[t] = (1.f / (1.f + expf(-z)) - yv) / (float)a.B;
+  }
+  __syncthreads();
+  if (t < HR * HF2 / 4) {
+    const int r = t >> 2, k0 = (t & 3) * 4;
+    reinterpret_cast<float4*>(a.dh2 + r0 * HF2)[t] =
+        make_float4(dl[r] * w3[k0], dl[r] * w3[k0 + 1], dl[r] * w3[k0 + 2], dl[r] * w3[k0 + 3]);
+  }
+  {  // partials: 16 columns x 16 groups of 2 rows
+    const int k = t & 15, g = t >> 4;
+    double sb = 0.0, sg = 0.0, sw = 0.0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = 2 * g + i;
+      const double gg = (double)dl[r] * w3[k];
+      sb += gg;
+      sg += gg * xh[r][k];
+      sw += (double)dl[r] * h2[r][k];
+    }
+    red[0][g][k] = sb;
+    red[1][g][k] = sg;
+    red[2][g][k] = sw;
+  }
+  __syncthreads();
+  double* pp = a.part3 + (int64_t)blockIdx.x * (3 * HF2 + 2);
+  if (t < 3 * HF2) {
+    const int which = t >> 4, k = t & 15;
+    double s = 0.0;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) s += red[which][g][k];
+    pp[which * HF2 + k] = s;
+  } else if (t >= 64 && t < 128) {  // one wave: sum dlogit and the loss over the rows
+    const int l = t - 64;
+    const double s = wave_sum(l < HR ? (double)dl[l] : 0.0);
+    const double ls = wave_sum(l < HR ? (double)lo[l] : 0.0);
+    if (l == 0) {
+      pp[3 * HF2] = s;
+      pp[3 * HF2 + 1] = ls;
+    }
+  }
+}
+
+// BN2 backward (prologue sums) -> Dropout/ReLU backward -> Linear(32, 16)
+// backward (dW2, db2, dh1 = da2 W2); BN1-backward partial sums
+__global__ __launch_bounds__(256) void hf_bwd2(HeadArgs a) {
+  __shared__ __attribute__((aligned(16))) float h1[HR][HF + 4];
+  __shared__ __attribute__((aligned(16))) float xh1[HR][HF + 4];
+  __shared__ float da2[HR][HF2 + 1];
+  __shared__ float w2[HF2][HF + 1];
+  __shared__ float m1[HF], i1[HF], g1[HF], b1[HF], m2[HF2], i2[HF2], g2[HF2], sb2[HF2], sg2[HF2];
+  __shared__ double red[2][8][HF];
+  __shared__ double pro_tmp[256], pro_sum[2 * HF2];
+  const int t = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * HR;
+  const float stepv = *a.step;
+  // every load of the block first
+  const float4 a1v = reinterpret_cast<const float4*>(a.a1 + r0 * HF)[t];  // row t/8, cols 4(t%8)..
+  float4 a2v = make_float4(0.f, 0.f, 0.f, 0.f), dhv = a2v, wv = a2v;
+  if (t < HR * HF2 / 4) {
+    a2v = reinterpret_cast<const float4*>(a.a2 + r0 * HF2)[t];  // row t/4, cols 4(t%4)..
+    dhv = reinterpret_cast<const float4*>(a.dh2 + r0 * HF2)[t];
+    wv = reinterpret_cast<const float4*>(a.p.fc2_w)[t];  // row t/8 of W2 (16 x 32)
+  }
+  if (t < HF) {
+    m1[t] = a.stat1[t];
+    i1[t] = a.stat1[HF + t];
+    g1[t] = a.p.bn1_w[t];
+    b1[t] = a.p.bn1_b[t];
+  } else if (t >= 64 && t < 64 + HF2) {
+    const int k = t - 64;
+    m2[k] = a.stat2[k];
+    i2[k] = a.stat2[HF2 + k];
+    g2[k] = a.p.bn2_w[k];
+  }
+  colsum_prologue(a.part3, a.nblk, 3 * HF2 + 2, 2 * HF2, pro_tmp, pro_sum);
+  if (t < HF2) {
+    sb2[t] = (float)pro_sum[t];
+    sg2[t] = (float)pro_sum[HF2 + t];
+  }
+  __syncthreads();
+  const float invB = 1.f / (float)a.B;
+  {
+    const int r = t >> 3, j0 = (t & 7) * 4;
+    const float x4[4] = {a1v.x, a1v.y, a1v.z, a1v.w};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = j0 + u;
+      const float d1 = fmaxf(x4[u], 0.f) * keep_scale_s(a, stepv, 1, r0 + r, j);
+      const float x = (d1 - m1[j]) * i1[j];
+      xh1[r][j] = x;
+      h1[r][j] = x * g1[j] + b1[j];
+    }
+  }
+  if (t < HR * HF2 / 4) {
+    const int r = t >> 2, k0 = (t & 3) * 4;
+    const float a4[4] = {a2v.x, a2v.y, a2v.z, a2v.w}, d4[4] = {dhv.x, dhv.y, dhv.z, dhv.w};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = k0 + u;
+      const float ks = keep_scale_s(a, stepv, 2, r0 + r, k);
+      const float xhat = (fmaxf(a4[u], 0.f) * ks - m2[k]) * i2[k];
+      const float dd2 = i2[k] * g2[k] * (d4[u] - sb2[k] * invB - xhat * sg2[k] * invB);
+      da2[r][k] = a4[u] > 0.f ? dd2 * ks : 0.f;
+    }
+    const int wr = t >> 3, wc = (t & 7) * 4;
+    w2[wr][wc] = wv.x;
+    w2[wr][wc + 1] = wv.y;
+    w2[wr][wc + 2] = wv.z;
+    w2[wr][wc + 3] = wv.w;
+  }
+  __syncthreads();
+  double* pp = a.part4 + (int64_t)blockIdx.x * (2 * HF + HF2 * HF + HF2);
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {  // dW2[k][j] = sum_r da2[r][k] h1[r][j] (fp64, rows in order)
+    const int o = t + 256 * u, k = o >> 5, j = o & 31;
+    double s = 0.0;
+#pragma unroll 8
+    for (int r = 0; r < HR; ++r) s += (double)da2[r][k] * h1[r][j];
+    pp[2 * HF + o] = s;
+  }
+  if (t < HF2) {
+    double s = 0.0;
+#pragma unroll 8
+    for (int r = 0; r < HR; ++r) s += da2[r][t];
+    pp[2 * HF + HF2 * HF + t] = s;
+  }
+  float dh[4];
+  {  // dh1 = da2 W2: row t/8, columns 4(t%8)..
+    const int r = t >> 3, j0 = (t & 7) * 4;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f;
+#pragma unroll
+      for (int k = 0; k < HF2; k += 4) {
+        c0 = fmaf(da2[r][k], w2[k][j0 + u], c0);
+        c1 = fmaf(da2[r][k + 1], w2[k + 1][j0 + u], c1);
+        c2 = fmaf(da2[r][k + 2], w2[k + 2][j0 + u], c2);
+        c3 = fmaf(da2[r][k + 3], w2[k + 3][j0 + u], c3);
+      }
+      dh[u] = (c0 + c1) + (c2 + c3);
+    }
+    reinterpret_cast<float4*>(a.dh1 + r0 * HF)[t] = make_float4(dh[0], dh[1], dh[2], dh[3]);
+  }
+  __syncthreads();  // h1 is re-used below as the dh1 image
+  {
+    const int r = t >> 3, j0 = (t & 7) * 4;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) h1[r][j0 + u] = dh[u];
+  }
+  __syncthreads();
+  {  // BN1-backward partials: 32 columns x 8 groups of 4 rows
+    const int j = t & 31, g = t >> 5;
+    double sb = 0.0, sg = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = 4 * g + i;
+      sb += h1[r][j];
+      sg += (double)h1[r][j] * xh1[r][j];
+    }
+    red[0][g][j] = sb;
+    red[1][g][j] = sg;
+  }
+  __syncthreads();
+  if (t < 2 * HF) {
+    const int which = t >> 5, j = t & 31;
+    double s = 0.0;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) s += red[which][g][j];
+    pp[which * HF + j] = s;
+  }
+}
+
 // dpooled = BN0 backward of dh0's pooled half, dh0 = da1 W1 on MFMA
 // (wave w: 32-column tiles w, w+4, ... of the pooled half).
 __global__ __launch_bounds__(256) void hf_bwd0(HeadArgs a) {
@@ -909,18 +1210,20 @@ __global__ __launch_bounds__(256) void hf_bwd0(HeadArgs a) {
     f32x16 acc;
 #pragma unroll
     for (int g = 0; g < 16; ++g) acc[g] = 0.f;
-    float wv[HF / 2];
+    float wv[HF / 2], pv[16];  // every global load before the MFMA chain
 #pragma unroll
     for (int kk = 0; kk < HF / 2; ++kk) wv[kk] = a.p.fc1_w[(int64_t)(2 * kk + h) * D2 + c];
 #pragma unroll
-    for (int kk = 0; kk < HF / 2; ++kk)
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(da[i][2 * kk + h], wv[kk], acc, 0, 0, 0);
+    for (int g = 0; g < 16; ++g) pv[g] = a.pooled[(r0 + hacc_row(g, h)) * ld + (c - d)];
     const float m = a.stat0[c], iv = a.stat0[D2 + c], gw = a.p.bn0_w[c];
     const float sb = (float)a.sum5[c] * invB, sg = (float)a.sum5[D2 + c] * invB;
 #pragma unroll
+    for (int kk = 0; kk < HF / 2; ++kk)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(da[i][2 * kk + h], wv[kk], acc, 0, 0, 0);
+#pragma unroll
     for (int g = 0; g < 16; ++g) {
       const int64_t r = r0 + hacc_row(g, h);
-      const float xhat = (a.pooled[r * ld + (c - d)] - m) * iv;
+      const float xhat = (pv[g] - m) * iv;
       a.dpooled[r * ld + (c - d)] = iv * gw * (acc[g] - sb - xhat * sg);
     }
   }
@@ -985,6 +1288,88 @@ __global__ __launch_bounds__(256) void clip_adam_kernel(float* __restrict__ p, f
     v[i] = vi;
     const float denom = sqrtf(vi) / bc2_sqrt + eps;
     p[i] = p[i] - step_size * (mi / denom);
+  }
+}
+
+// clip_grad_norm_ + Adam in ONE launch: every 1024-thread block sums the
+// squares of ALL n gradients itself (fixed order, fp64: identical in every
+// block, n is ~42K for the DIN model) and updates its own 1024 parameters;
+// the block that finishes last advances Adam's step count (every block read
+// it before its ticket).  Two launches (partials, then update) cost ~9 us.
+__global__ __launch_bounds__(1024) void clip_adam_fused_kernel(float* __restrict__ p, float* __restrict__ g,
+                                                              float* __restrict__ m, float* __restrict__ v,
+                                                              int64_t n, float* __restrict__ step,
+                                                              unsigned int* __restrict__ ticket, float lr,
+                                                              const float* __restrict__ lr_dev, float beta1,
+                                                              float beta2, float eps, float wd, float max_norm) {
+  __shared__ double red[1024];
+  const int t = threadIdx.x;
+  const int64_t i = (int64_t)blockIdx.x * 1024 + t;
+  // this thread's element first (its loads overlap the norm's)
+  float gi = 0.f, pi = 0.f, mi = 0.f, vi = 0.f;
+  if (i < n) {
+    gi = g[i];
+    pi = p[i];
+    mi = m[i];
+    vi = v[i];
+  }
+  const float tstep = *step + 1.f;
+  if (lr_dev) lr = *lr_dev;  // device-resident lr: a scheduler updates it between graph replays
+  // the norm: float4 loads, 12 in flight per thread (the DIN model's ~42K
+  // gradients: one round), four fp64 chains, then a fixed butterfly per wave
+  // and the 16 wave sums in order
+  const int64_t n4 = n >> 2;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  for (int64_t j0 = t; j0 < n4; j0 += 12 * 1024) {
+    float4 x[12];
+#pragma unroll
+    for (int u = 0; u < 12; ++u) {
+      const int64_t j = j0 + (int64_t)u * 1024;
+      x[u] = j < n4 ? reinterpret_cast<const float4*>(g)[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < 12; ++u) {
+      s0 += (double)x[u].x * x[u].x;
+      s1 += (double)x[u].y * x[u].y;
+      s2 += (double)x[u].z * x[u].z;
+      s3 += (double)x[u].w * x[u].w;
+    }
+  }
+  if (t < (int)(n & 3)) {
+    const float x = g[4 * n4 + t];
+    s0 += (double)x * x;
+  }
+  const double ws = wave_sum((s0 + s1) + (s2 + s3));
+  if ((t & 63) == 0) red[t >> 6] = ws;
+  __syncthreads();
+  if (t == 0) {
+    double tot = 0.0;
+    for (int w = 0; w < 16; ++w) tot += red[w];
+    red[16] = tot;
+  }
+  __syncthreads();
+  const float norm = (float)sqrt(red[16]);
+  const float c = max_norm / (norm + 1e-6f);
+  const float coef = c < 1.f ? c : 1.f;
+  const float bc1 = 1.f - powf(beta1, tstep), bc2 = 1.f - powf(beta2, tstep);
+  const float step_size = lr / bc1, bc2_sqrt = sqrtf(bc2);
+  if (i < n) {
+    gi *= coef;
+    g[i] = gi;  // clip_grad_norm_ scales the stored gradients
+    gi = gi + wd * pi;
+    mi = mi + (gi - mi) * (1.f - beta1);  // torch: exp_avg.lerp_(grad, 1 - beta1)
+    vi = vi * beta2 + (1.f - beta2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    p[i] = pi - step_size * (mi / denom);
+  }
+  if (t == 0) {
+    // every block read *step before its ticket; the last one advances it
+    if (atomicAdd(ticket, 1u) == gridDim.x - 1) {
+      *step = tstep;
+      *ticket = 0u;
+    }
   }
 }
 
@@ -1090,19 +1475,34 @@ extern "C" int nrk_din_head_train(const float* q, const float* pooled, int64_t l
   const char* ef = getenv("NRK_DIN_HEAD_FAST");
   a.fast = F == HF && d % 32 == 0 && !(ef && atoi(ef) == 0);
   a.nrg0 = nblk < 8 ? nblk : 8;
-  const size_t lds2_ = ((size_t)HR * F + F2 * F + 2 * F + HR * F2) * 4;
-  const size_t lds3_ = ((size_t)2 * HR * F2 + 2 * F2 + 2 * HR) * 4;
-  const size_t lds4_ = ((size_t)3 * HR * F + HR * F2 + 2 * F + 4 * F2 + F2 * F) * 4;
   if (a.fast) {
     const size_t lf1 = ((size_t)2 * D2 + (size_t)(HR + HF) * (D2 + 4) + 4 * HR * HF + HR * (HF + 1)) * 4;
     const size_t lb1 = ((size_t)2 * D2 + (size_t)HR * (D2 + 4) + HR * (HF + 1) + 4 * HF) * 4;
     const int s3_ = 3 * F2 + 2, s4_ = 2 * F + F2 * F + F2;
     hipLaunchKernelGGL(hf_stats0, dim3((unsigned)(D2 / 32 * a.nrg0)), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(hf_fwd1, dim3(nblk), dim3(256), lf1, st, a);
-    hipLaunchKernelGGL(head_fwd2, dim3(nblk), dim3(256), lds2_, st, a);
-    hipLaunchKernelGGL(head_fwd3, dim3(nblk), dim3(256), lds3_, st, a);
-    hipLaunchKernelGGL(head_bwd2, dim3(nblk), dim3(256), lds4_, st, a);
-    hipLaunchKernelGGL(hf_bwd1, dim3(nblk), dim3(256), lb1, st, a);
+    switch (D2) {  // the fast path needs d % 32 == 0, 2d <= 512
+      case 64: hipLaunchKernelGGL(hf_fwd1<2>, dim3(nblk), dim3(256), lf1, st, a); break;
+      case 128: hipLaunchKernelGGL(hf_fwd1<4>, dim3(nblk), dim3(256), lf1, st, a); break;
+      case 192: hipLaunchKernelGGL(hf_fwd1<6>, dim3(nblk), dim3(256), lf1, st, a); break;
+      case 256: hipLaunchKernelGGL(hf_fwd1<8>, dim3(nblk), dim3(256), lf1, st, a); break;
+      case 320: hipLaunchKernelGGL(hf_fwd1<10>, dim3(nblk), dim3(256), lf1, st, a); break;
+      case 384: hipLaunchKernelGGL(hf_fwd1<12>, dim3(nblk), dim3(256), lf1, st, a); break;
+      case 448: hipLaunchKernelGGL(hf_fwd1<14>, dim3(nblk), dim3(256), lf1, st, a); break;
+      default: hipLaunchKernelGGL(hf_fwd1<16>, dim3(nblk), dim3(256), lf1, st, a); break;
+    }
+    hipLaunchKernelGGL(hf_fwd2, dim3(nblk), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(hf_fwd3, dim3(nblk), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(hf_bwd2, dim3(nblk), dim3(256), 0, st, a);
+    switch (D2) {
+      case 64: hipLaunchKernelGGL(hf_bwd1<2>, dim3(nblk), dim3(256), lb1, st, a); break;
+      case 128: hipLaunchKernelGGL(hf_bwd1<4>, dim3(nblk), dim3(256), lb1, st, a); break;
+      case 192: hipLaunchKernelGGL(hf_bwd1<6>, dim3(nblk), dim3(256), lb1, st, a); break;
+      case 256: hipLaunchKernelGGL(hf_bwd1<8>, dim3(nblk), dim3(256), lb1, st, a); break;
+      case 320: hipLaunchKernelGGL(hf_bwd1<10>, dim3(nblk), dim3(256), lb1, st, a); break;
+      case 384: hipLaunchKernelGGL(hf_bwd1<12>, dim3(nblk), dim3(256), lb1, st, a); break;
+      case 448: hipLaunchKernelGGL(hf_bwd1<14>, dim3(nblk), dim3(256), lb1, st, a); break;
+      default: hipLaunchKernelGGL(hf_bwd1<16>, dim3(nblk), dim3(256), lb1, st, a); break;
+    }
     hipLaunchKernelGGL(hf_reduce, dim3((unsigned)(D2 / 4 + cdiv(s3_ + s4_, 64))), dim3(1024), 0, st, a);
     hipLaunchKernelGGL(hf_bwd0, dim3(nblk), dim3(256), 0, st, a);
     NRK_CHECK_LAUNCH("din_head_train (fast)");
@@ -1146,9 +1546,11 @@ extern "C" int nrk_din_head_train(const float* q, const float* pooled, int64_t l
   return NRK_OK;
 }
 
+// workspace: 256 fp64 partials (two-launch form) | the fused form's ticket;
+// zero-initialise it once (the kernel leaves it zero)
 extern "C" int nrk_clip_adam_workspace(int64_t n, size_t* ws_bytes) {
   NRK_CHECK_ARG(ws_bytes && n >= 0, "clip_adam_workspace: bad arguments");
-  *ws_bytes = 256 * 8;
+  *ws_bytes = 256 * 8 + 256;
   return NRK_OK;
 }
 
@@ -1156,8 +1558,16 @@ extern "C" int nrk_clip_adam(float* params, float* grads, float* exp_avg, float*
                              float lr, const float* lr_dev, float beta1, float beta2, float eps, float weight_decay, float max_norm,
                              void* ws, size_t ws_bytes, void* stream) {
   NRK_CHECK_ARG(n > 0 && params && grads && exp_avg && exp_avg_sq && step && ws, "clip_adam: bad arguments");
-  if (ws_bytes < 256 * 8) return fail(NRK_EWORKSPACE, "clip_adam: workspace %zu < 2048", ws_bytes);
+  if (ws_bytes < 256 * 8 + 256) return fail(NRK_EWORKSPACE, "clip_adam: workspace %zu < 2304", ws_bytes);
   hipStream_t st = (hipStream_t)stream;
+  if (n <= ((int64_t)1 << 17)) {  // small models (DIN: ~42K): one launch
+    unsigned int* ticket = reinterpret_cast<unsigned int*>(static_cast<char*>(ws) + 256 * 8);
+    hipLaunchKernelGGL(clip_adam_fused_kernel, dim3((unsigned)cdiv(n, (int64_t)1024)), dim3(1024), 0, st, params,
+                       grads, exp_avg, exp_avg_sq, n, step, ticket, lr, lr_dev, beta1, beta2, eps, weight_decay,
+                       max_norm);
+    NRK_CHECK_LAUNCH("clip_adam_fused_kernel");
+    return NRK_OK;
+  }
   int nb = (int)cdiv(n, 256);
   if (nb > 256) nb = 256;
   int ns = (int)cdiv(n, 256 * 8);  // sumsq: 8 loads in flight per thread, few partials

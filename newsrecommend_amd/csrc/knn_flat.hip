@@ -1228,9 +1228,6 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
   if (k <= 8) { p.M = 4; p.qt = 2; }
   else if (k <= 24) { p.M = 8; p.qt = 1; }
   else { p.M = 16; p.qt = 1; }
-  // DP = 256 with M = 16 (k > 24, e.g. configs[4]'s 10M x 256, k = 200): 8-wave
-  // workgroups, 256 queries per corpus pass; a chunk far larger than L2 is
-  // then re-read by half as many query tiles
   // DP = 256 with M = 4 or 16: 8-wave workgroups (256 queries per corpus pass):
   // half the LDS-DMA pieces per MFMA of the 4-wave form (10M x 256, k = 5:
   // screen 17.4 -> 15.0 ms) and, at k = 200, a chunk far larger than L2

@@ -475,7 +475,7 @@ class FusedTrainStep:
         _lib.check(L_.nrk_din_attn_bwd_workspace(B, Dk, A, sz), "din_attn_bwd_workspace")
         self.ws_attn = torch.empty(max(sz.value, 1), dtype=torch.uint8, device=dev)
         _lib.check(L_.nrk_clip_adam_workspace(n, sz), "clip_adam_workspace")
-        self.ws_opt = torch.empty(max(sz.value, 1), dtype=torch.uint8, device=dev)
+        self.ws_opt = torch.zeros(max(sz.value, 1), dtype=torch.uint8, device=dev)  # holds a ticket: zeroed once
         self.n = n
         # fast path (bf16 table, emb_dim 64/128): one batch-assembly kernel
         # (rows -> ids, labels, f32 query, U = q W1q^T + b1, bf16 W1k) and an
