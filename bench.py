@@ -5,20 +5,23 @@
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 Headline (BASELINE.json `metric`, configs[1]): exact flat retrieval, 1M x 128
-items, batches of nq = 4096 queries, k = 5, inner product.  One STEP = one
-search of one 4096-query batch (inputs resident in HBM).  At N > 1 the corpus
-is row-sharded over the ranks (fixed 1M corpus: strong scaling); each rank
-searches its shard and the per-shard exact top-k lists are merged after ONE
-RCCL all_gather (newsrecommend_amd.dist).  value = queries answered / max-
-over-ranks wall time of the K timed steps.
+items, batches of nq = 4096 queries per GPU, k = 5, inner product.  One STEP =
+one search of one batch (inputs resident in HBM).  At N > 1 the corpus is
+row-sharded over the ranks (north_star: per-shard exact top-k lists merged
+after ONE RCCL all_gather, newsrecommend_amd.dist) and the global batch is
+N x 4096 queries, every rank searching all of them against its shard: the
+per-GPU work is that of one GPU at N = 1 (weak scaling).  value = queries
+answered / max-over-ranks wall time of the K timed steps.
 
 Secondary record `ivf` (configs[3] shape): IVF-Flat nlist=300, nprobe=32 over
 10M x 128 items (L2), rows split over the ranks, exact top-k per rank merged
-after one all_gather; recall@5 against the exact flat search.
+after one all_gather; recall@5 against the exact flat search; N x 4096
+queries per step.  `n1_retrieval_10m_256_k5` (north_star's target): flat IP
+k = 5 over 10M x 256, corpus sharded the same way, N x 4096 queries.
 
 Secondary record `e2e` (configs[4] shape): flat top-200 over 10M x 256 items
-(corpus sharded) -> ground truth appended -> DIN re-rank of this rank's users
-(users sharded) -> NDCG@5; value = users/s end to end.
+(corpus sharded) for N x 4096 users -> ground truth appended -> DIN re-rank of
+this rank's 4096 users (users sharded) -> NDCG@5; value = users/s end to end.
 
 Secondary record `din` (configs[2]): DIN training, bf16 table of 2M items,
 5M synthetic click rows, L = 50, d = 128, A = 128, F = 32; one step = fwd +
@@ -53,15 +56,26 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# Rehearsal of the N > 1 code paths on a one-GPU box (never the measured
+# configuration): NRK_BENCH_BACKEND=gloo with NRK_BENCH_ONE_DEVICE=1 runs every
+# rank on cuda:0 and carries the collectives over gloo host copies.
+BACKEND = os.environ.get("NRK_BENCH_BACKEND", "nccl")
+
+
 def setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if os.environ.get("NRK_BENCH_ONE_DEVICE") == "1":
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if BACKEND == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(BACKEND)
     return rank, world, torch.device("cuda", local)
 
 
@@ -74,7 +88,7 @@ def barrier(world):
 def max_over_ranks(x: float, world: int, dev) -> float:
     if world == 1:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    t = torch.tensor([x], dtype=torch.float64, device=dev if BACKEND == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -92,7 +106,8 @@ def bench_flat(args, rank, world, dev):
 
     metric = 0 if args.metric == "ip" else 1
     xb = clustered_corpus(args.nb, args.d, seed=1234, device=dev)
-    xq = clustered_corpus(args.nq, args.d, seed=4321, device=dev)
+    nq = args.nq * world  # global batch: args.nq queries per GPU
+    xq = clustered_corpus(nq, args.d, seed=4321, device=dev)
     index = ShardedIndexFlat(args.d, metric, device=dev)
     index.add_full(xb)
     keep_full = rank == 0
@@ -113,7 +128,7 @@ def bench_flat(args, rank, world, dev):
             pass
     barrier(world)
     el = max_over_ranks(time.perf_counter() - t0, world, dev)
-    qps = args.nq * args.steps / el
+    qps = nq * args.steps / el
 
     # per-stage device times (rank-local), averaged over the timed steps
     if world > 1:  # one extra instrumented local search per step-count for the stage split
@@ -123,7 +138,7 @@ def bench_flat(args, rank, world, dev):
     st = np.array([e.elapsed_ms() for e in evs])
     stage_ms = st.mean(0)
     screen_ms = float(stage_ms[1])
-    flops = 2.0 * args.nq * nb_local * args.d
+    flops = 2.0 * nq * nb_local * args.d
     achieved = flops / (screen_ms * 1e-3) / 1e12
     fallback = index.local.fallback_counts.tolist()
 
@@ -149,7 +164,7 @@ def bench_flat(args, rank, world, dev):
 def _recall(args, xq, xb_host, D, I, metric):
     from oracle import knn_oracle as ko
 
-    sample = np.arange(0, args.nq, max(1, args.nq // 64))
+    sample = np.arange(0, xq.shape[0], max(1, xq.shape[0] // 64))
     q = xq.cpu().numpy()[sample]
     _, Io, _ = ko.exact_search(q, xb_host, args.k, metric)
     Ig = I.cpu().numpy()[sample]
@@ -211,7 +226,8 @@ def bench_ivf(args, rank, world, dev):
     from newsrecommend_amd.data import clustered_corpus
     from newsrecommend_amd.dist import ShardedIndexIVFFlat
 
-    d, k, nq, nlist, nprobe = args.d, args.k, args.nq, args.ivf_nlist, args.ivf_nprobe
+    d, k, nlist, nprobe = args.d, args.k, args.ivf_nlist, args.ivf_nprobe
+    nq = args.nq * world  # global batch: args.nq queries per GPU (weak scaling)
     xb = clustered_corpus(args.ivf_nb, d, seed=1234, device=dev)
     xq = clustered_corpus(nq, d, seed=4321, device=dev)
     barrier(world)
@@ -343,7 +359,8 @@ def bench_n1(args, rank, world, dev, index, xb):
     from newsrecommend_amd import _lib
     from newsrecommend_amd.data import clustered_corpus
 
-    n, d, nq, k = xb.shape[0], xb.shape[1], args.nq, 5
+    n, d, k = xb.shape[0], xb.shape[1], 5
+    nq = args.nq * world  # global batch: args.nq queries per GPU (weak scaling)
     xq = clustered_corpus(nq, d, seed=4321, device=dev)
     for _ in range(args.warmup):
         index.search_device(xq, k)
@@ -403,7 +420,8 @@ def bench_e2e(args, rank, world, dev):
     from newsrecommend_amd.dist import ShardedIndexFlat, shard_range
     from newsrecommend_amd.pipeline import ndcg_at_k, rerank
 
-    n, d, U, L, kr = args.e2e_nb, 256, args.e2e_users, 50, args.e2e_k
+    n, d, L, kr = args.e2e_nb, 256, 50, args.e2e_k
+    U = args.e2e_users * world  # global batch of users: e2e_users per GPU (weak scaling)
     xb = clustered_corpus(n, d, seed=1234, device=dev)
     index = ShardedIndexFlat(d, 0, device=dev)
     index.add_full(xb)
@@ -505,9 +523,10 @@ def bench_din(args, rank, world, dev):
     if fused:
         from newsrecommend_amd.din import FusedTrainStep
 
-        def allreduce(G):
-            dist.all_reduce(G)
-            G.div_(world)
+        from newsrecommend_amd.dist import all_reduce_mean_
+
+        def allreduce(G):  # RCCL on the flat gradient buffer (gloo: a host copy)
+            all_reduce_mean_(G)
 
         trainer = FusedTrainStep(model, table, hist, tgt, lab, B, lr=1.62e-3, weight_decay=8.96e-5, clip=1.0,
                                  graph=graphed, grad_hook=allreduce if world > 1 else None)
@@ -521,9 +540,9 @@ def bench_din(args, rank, world, dev):
         opt.zero_grad(set_to_none=True)
         loss.backward()
         if world > 1:
-            flat = torch.cat([p.grad.reshape(-1) for p in model.parameters()])
-            dist.all_reduce(flat)
-            flat /= world
+            from newsrecommend_amd.dist import all_reduce_mean_
+
+            flat = all_reduce_mean_(torch.cat([p.grad.reshape(-1) for p in model.parameters()]))
             o = 0
             for p in model.parameters():
                 n = p.numel()
@@ -673,13 +692,14 @@ def main():
 
     rank, world, dev = setup(args)
     rec = {"metric": METRIC, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-           "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "bf16",
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
            "data": "synthetic"}
     if args.workload in ("flat", "all"):
         r = bench_flat(args, rank, world, dev)
         rec.update({k: r[k] for k in ("value", "unit", "ms_per_step")})
-        rec["config"] = {"workload": f"configs[1]: flat kNN {args.nb}x{args.d}, batch={args.nq} queries, k={args.k}, "
-                                     f"{args.metric.upper()}", "nb": args.nb, "d": args.d, "nq": args.nq, "k": args.k,
+        rec["config"] = {"workload": f"configs[1]: flat kNN {args.nb}x{args.d}, batch={args.nq} queries per GPU, "
+                                     f"k={args.k}, {args.metric.upper()}", "nb": args.nb, "d": args.d, "nq": args.nq,
+                         "global_batch": args.nq * world, "k": args.k,
                          "metric": args.metric, "screen": "bf16 MFMA, fp32 accumulate", "rescore": "f64 exact",
                          "parallelism": f"corpus-shard{world} + RCCL all_gather merge" if world > 1 else "single GPU"}
         for k in ("roofline", "stages_ms", "fallback_queries", "recall_at_5", "exact_match", "cpu_baseline"):
