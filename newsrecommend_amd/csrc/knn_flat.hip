@@ -1242,8 +1242,27 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
   // k > 24 (M = 16): twice the lane streams, so that dense neighbourhoods do
   // not overflow a lane's list (10M x 256, k = 200: 2 uncertified queries per
   // 4096 -> 0, and the 4.5 ms fp64 fallback scan with them)
+  // pre-pass stride: the pre-pass costs ~nb / stride per query, the main pass
+  // admits ~stride * R items above tau per query (list insertions); the best
+  // stride grows like sqrt(nb / R): the power of two >= 8 sqrt(nb/1M * 16/R),
+  // in [2, 64].  Measured (IP, per GPU): 1M x 128 k = 5 -> 8; 10M x 256 k = 5
+  // -> 32 (total 17.0 -> 15.8 ms vs 8); 10M x 256 k = 200 -> 8 (4: +0.8 ms,
+  // 16: +1.3 ms); the 8-GPU shards: 1.25M x 256 k = 200, 32768 queries -> 2
+  // (52.6 -> 37.0 ms vs 8), 125K x 128 k = 5, 32768 queries -> 4 (-7 %)
+  {
+    const double want = 8.0 * sqrt((double)nb / 1e6 * 16.0 / p.R);
+    int st = 2;
+    while (st < 64 && st < want) st *= 2;
+    p.tstride = st;
+  }
   int target = p.M >= 16 ? 2048 : 1024;
   int64_t nch = target / (p.nqt > 0 ? p.nqt : 1);
+  // ... but at least enough chunks (2 lane streams each) that the ~stride * R
+  // items above tau spread to <= M per stream: with many query tiles (a
+  // corpus shard searched by N x 4096 queries) the workgroup target alone
+  // left 16 streams per query and ~1/6 of the queries uncertified at k = 200
+  const int64_t min_streams = cdiv((int64_t)p.tstride * p.R, (int64_t)2 * p.M);
+  if (nch < min_streams) nch = min_streams;
   if (nch < 1) nch = 1;
   int64_t max_by_u = 2048 / (2 * p.M);
   if (nch > max_by_u) nch = max_by_u;
@@ -1276,17 +1295,9 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
     return p;
   }
   // pre-pass: every tstride-th 64-item tile, chunks small enough that each
-  // query gets >= 8R short lane streams (their maxima are distinct items)
-  // pre-pass stride: the pre-pass costs ~nb / stride per query, the main pass
-  // admits ~stride * R items above tau per query (list insertions); the best
-  // stride grows like sqrt(nb / R) (measured, IP: 1M x 128 k = 5 -> 8,
-  // 10M x 256 k = 5 -> 32 (total 17.0 -> 15.8 ms), 10M x 256 k = 200 -> 8)
-  {
-    const double want = 8.0 * sqrt((double)nb / 1e6 * 16.0 / p.R);
-    int st = 8;
-    while (st < 64 && st * 1.41421356 < want) st *= 2;
-    p.tstride = st;
-  }
+  // query gets >= 8R short lane streams (their maxima are distinct items), but
+  // >= 8 visited tiles per workgroup (a small shard searched by many query
+  // tiles otherwise launched thousands of 2-tile workgroups)
   {
     const int TI = 64;  // must equal screen_kernel TI
     int64_t tiles = cdiv(nb, TI);
@@ -1294,7 +1305,7 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
     const int64_t min_pre = cdiv(nb * (int64_t)p.dp * 2, (int64_t)1 << 30);
     if (want < min_pre) want = min_pre;
     if (want > 512) want = 512;
-    int64_t maxc = cdiv(tiles, p.tstride);
+    int64_t maxc = cdiv(tiles, (int64_t)p.tstride * 8);
     if (want > maxc) want = maxc;
     if (want < 1) want = 1;
     p.chunk_pre = cdiv(cdiv(tiles, want), p.tstride) * p.tstride * TI;
