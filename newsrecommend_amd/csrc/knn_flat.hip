@@ -1648,7 +1648,12 @@ static IvfPlan make_ivf_plan(int64_t nq, int nprobe, int nlist, int64_t max_list
   // streams per chunk and query; more streams -> tighter seeds); tau_select
   // takes <= 1024 values per query
   p.nA = nprobe < 2 ? nprobe : 2;
-  int64_t chA = 1024;
+  // chunks scale with the lists (max_list / 128, in [64, 1024] rows): a
+  // corpus shard's short lists (the 8-GPU configs[3]: ~4K rows) otherwise
+  // gave ~20 lane maxima per query, weak seeds, a low collect threshold and
+  // ~3 % of the queries overflowing into the fp64 scan
+  int64_t chA = (int64_t)align_up((size_t)(ml / 128 > 64 ? ml / 128 : 64), 64);
+  if (chA > 1024) chA = 1024;
   const int64_t cmax_a = 512 / p.nA;
   if (cdiv(ml, chA) > cmax_a) chA = (int64_t)align_up((size_t)cdiv(ml, cmax_a), 64);
   if (chA > ch_gib) chA = ch_gib;
