@@ -52,6 +52,12 @@ def main():
         res[f"flat{metric}_I_equal"] = bool(torch.equal(I, I1))
         res[f"flat{metric}_D_equal"] = bool(torch.equal(D, D1))
         res[f"flat{metric}_local_rows"] = sh.local.ntotal
+        # the all_to_all form (configs[4]'s user-sharded re-rank): this rank's query slice only
+        from newsrecommend_amd.dist import shard_range
+
+        Do, Io = sh.search_device_own(q, 10)
+        qlo, qhi = shard_range(q.shape[0], rank, world)
+        res[f"flat{metric}_own_equal"] = bool(torch.equal(Io, I1[qlo:qhi]) and torch.equal(Do, D1[qlo:qhi]))
     # ---- IVF: replicated deterministic k-means, row-split lists == single IVF
     xq, xb = _mixture(60_000, 257, 32, seed=6)
     sh = ShardedIndexIVFFlat(32, 24, nf.METRIC_L2, device=dev)

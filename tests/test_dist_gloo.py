@@ -90,3 +90,43 @@ def test_two_rank_sharded_ivf(tmp_path):
     mp.spawn(_ivf_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     for r in range(world):
         assert np.load(tmp_path / f"ivf_ok_{r}.npy").all()
+
+
+def _scatter_worker(rank, world, port, out_dir):
+    """The all_to_all exchange of the user-sharded e2e (ShardedIndexFlat.
+    search_device_own): rank r receives every shard's lists for its own query
+    slice only, and their merge equals the single-index result of that slice."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from newsrecommend_amd.dist import scatter_results, shard_range
+        from oracle import knn_oracle as ko
+
+        rng = np.random.default_rng(9)
+        xb = rng.standard_normal((1999, 24)).astype(np.float32)
+        xq = rng.standard_normal((37, 24)).astype(np.float32)  # odd: unequal query slices
+        xb[1500] = xb[4]
+        xq[0] = xb[4]  # a cross-shard tie in each query slice
+        xq[20] = xb[4]
+        k = 7
+        oks = []
+        for metric in (ko.METRIC_IP, ko.METRIC_L2):
+            lo, hi = shard_range(xb.shape[0], rank, world)
+            _, I, S = ko.exact_search(xq, xb[lo:hi], k, metric, id_offset=lo)
+            S_own, I_own = scatter_results(torch.from_numpy(S), torch.from_numpy(I))
+            qlo, qhi = shard_range(xq.shape[0], rank, world)
+            assert S_own.shape == (world, qhi - qlo, k)
+            _, Im, Sm = ko.merge(S_own.numpy(), I_own.numpy(), k, metric)
+            _, Ig, Sg = ko.exact_search(xq[qlo:qhi], xb, k, metric)
+            oks.append(np.array_equal(Im, Ig) and np.array_equal(Sm, Sg))
+        np.save(os.path.join(out_dir, f"scatter_ok_{rank}.npy"), np.array(oks))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_scatter_exchange(tmp_path):
+    world = 2
+    mp.spawn(_scatter_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        assert np.load(tmp_path / f"scatter_ok_{r}.npy").all()

@@ -38,6 +38,7 @@ def test_world2_sharded_search_and_dp_hook(gpu, tmp_path):
         assert x["world"] == 2
         for m in (0, 1):
             assert x[f"flat{m}_I_equal"] and x[f"flat{m}_D_equal"], (m, x)
+            assert x[f"flat{m}_own_equal"], (m, x)
         assert x["ivf_centroids_equal"] and x["ivf_I_equal"] and x["ivf_D_equal"], x
         assert x["dp_grad_rel_err"] < 1e-6, x
         assert x["dp_replica_param_diff"] == 0.0, x
