@@ -854,7 +854,7 @@ __global__ __launch_bounds__(256, 1) void din_bwd_deep_kernel(
     const uint16_t* __restrict__ table, const int32_t* __restrict__ ids, int64_t n_table, const float* __restrict__ U,
     const uint16_t* __restrict__ W1k, const float* __restrict__ w2, int B, int L, int A,
     const float* __restrict__ dpooled, const float* __restrict__ alpha, float* __restrict__ slabs,
-    const float* __restrict__ q, int dq, int dbg) {
+    const float* __restrict__ q, int dq) {
   constexpr int CPR = D / 8, KS = D / 16, NCT = D / 32, NC = LP / 32;
   constexpr int NPW = LP * CPR / 256;  // key-image DMA pieces per wave
   constexpr int N_IDS = LP > 64 ? 2 : 1;
@@ -896,7 +896,6 @@ __global__ __launch_bounds__(256, 1) void din_bwd_deep_kernel(
   };
   // key rows + small pieces of sample b (its ids in ring entry e) into slot sl
   auto issue_data = [&](int64_t b, int sl, int e) {
-    if (dbg & 16) b = B;  // timing only: every key row from the zero rows
     float* sp = slot0 + sl * SLOT_F;
     uint16_t* img = reinterpret_cast<uint16_t*>(sp + 4 * 128);
 #pragma unroll
@@ -934,14 +933,9 @@ __global__ __launch_bounds__(256, 1) void din_bwd_deep_kernel(
   int sl = 0, e = P % RING;  // e: ring entry holding the ids of sample b + P grid
   for (; b < B; b += grid) {
     // this wave's DMA group of sample b landed; all waves' after the barrier; slot of b - grid is free
-    if (dbg & 32) {  // timing only: no DMA waits (results are garbage)
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      issue_ids(b + (P + X) * grid, e + X < RING ? e + X : e + X - RING);
-    } else {
-      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"((P - 1) * N_D) : "memory");
-      issue_ids(b + (P + X) * grid, e + X < RING ? e + X : e + X - RING);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(X * N_D) : "memory");  // ids of b + P grid landed
-    }
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"((P - 1) * N_D) : "memory");
+    issue_ids(b + (P + X) * grid, e + X < RING ? e + X : e + X - RING);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(X * N_D) : "memory");  // ids of b + P grid landed
     issue_data(b + P * grid, sl + P < NSLOT ? sl + P : sl + P - NSLOT, e);
     e = e + 1 < RING ? e + 1 : 0;
 
@@ -951,7 +945,7 @@ __global__ __launch_bounds__(256, 1) void din_bwd_deep_kernel(
     const float* sU = sp + 256;
     const float* sq = sp + 384;
     const unsigned char* img = reinterpret_cast<const unsigned char*>(sp + 512);
-    if (!(dbg & 1)) {  // dalpha[row] = dpooled . K[row], split over the waves: wave w owns rows [w R, (w+1) R)
+    {  // dalpha[row] = dpooled . K[row], split over the waves: wave w owns rows [w R, (w+1) R)
       constexpr int R = LP / 4, LPR = 64 / R, CH = CPR / LPR;
       const int row = w * R + lane / LPR, part = lane % LPR;
       float acc = 0.f;
@@ -975,7 +969,7 @@ __global__ __launch_bounds__(256, 1) void din_bwd_deep_kernel(
       if (part == 0) dabuf[row] = acc;
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (w < nsl && !(dbg & 2)) {
+    if (w < nsl) {
       const float un = sU[32 * w + r];
       float qcur[NCT];
 #pragma unroll
@@ -1040,7 +1034,6 @@ __global__ __launch_bounds__(256, 1) void din_bwd_deep_kernel(
           }
           const int grp = lane >> 4, i16 = lane & 15;
           const int rowq = 32 * c + 16 * s + 4 * h + (i16 >> 2);
-          if (dbg & 4) continue;
 #pragma unroll
           for (int cc = 0; cc < NCT; ++cc) {
             const int col = 32 * cc + 16 * (grp & 1) + 4 * (i16 & 3);
@@ -1064,7 +1057,7 @@ __global__ __launch_bounds__(256, 1) void din_bwd_deep_kernel(
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup exits
   float* slab = slabs + (size_t)blockIdx.x * slab_floats(A, D);
-  if (w < nsl && !(dbg & 8)) {
+  if (w < nsl) {
     float* sqs = slab + slab_q_off(A, D);
 #pragma unroll
     for (int c = 0; c < NCT; ++c)
@@ -1094,7 +1087,7 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8_kernel(
     const uint16_t* __restrict__ table, const int32_t* __restrict__ ids, int64_t n_table, const float* __restrict__ U,
     const uint16_t* __restrict__ W1k, const float* __restrict__ w2, int B, int L, int A,
     const float* __restrict__ dpooled, const float* __restrict__ alpha, float* __restrict__ slabs,
-    const float* __restrict__ q, int dq, float* __restrict__ dUp, float* __restrict__ dummy, int dbg) {
+    const float* __restrict__ q, int dq, float* __restrict__ dUp, float* __restrict__ dummy) {
   constexpr int CPR = D / 8, KS = D / 16, NCT = D / 32, NC = LP / 32;
   constexpr int NPW = LP * CPR / 512;  // key-image DMA pieces per wave
   constexpr int N_IDS = LP > 64 ? 2 : 1;
@@ -1147,7 +1140,6 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8_kernel(
   };
   // key rows + small pieces of sample b (its ids in ring entry e) into slot sl
   auto issue_data = [&](int64_t b, int sl, int e) {
-    if (dbg & 16) b = B;  // timing only: every key row from the zero rows
     float* sp = slot0 + sl * SLOT_F;
     uint16_t* img = reinterpret_cast<uint16_t*>(sp + 4 * 128);
 #pragma unroll
@@ -1198,7 +1190,7 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8_kernel(
     const float* sU = sp + 256;
     
     const unsigned char* img = reinterpret_cast<const unsigned char*>(sp + 512);
-    if (!(dbg & 1)) {  // dalpha[row] = dpooled . K[row], split over the waves: wave w owns rows [w R, (w+1) R)
+    {  // dalpha[row] = dpooled . K[row], split over the waves: wave w owns rows [w R, (w+1) R)
       constexpr int R = LP / 8, LPR = 64 / R, CH = CPR / LPR;
       const int row = w * R + lane / LPR, part = lane % LPR;
       float acc = 0.f;
@@ -1223,7 +1215,7 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8_kernel(
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     float du = 0.f;
-    if (us < nsl && rg < NC && !(dbg & 2)) {
+    if (us < nsl && rg < NC) {
       const float un = sU[32 * us + r];
       float da[NC];
 #pragma unroll
@@ -1285,7 +1277,6 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8_kernel(
           }
           const int grp = lane >> 4, i16 = lane & 15;
           const int rowq = 32 * c + 16 * s + 4 * h + (i16 >> 2);
-          if (dbg & 4) continue;
 #pragma unroll
           for (int cc = 0; cc < NCT; ++cc) {
             const int col = 32 * cc + 16 * (grp & 1) + 4 * (i16 & 3);
@@ -1336,7 +1327,7 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8_kernel(
     if (rg == 1 && us == 0 && lane == 0) xs[256] = tb2;
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     float* slab = slabs + (size_t)blockIdx.x * slab_floats(A, D);
-    if (rg == 0 && act && !(dbg & 8)) {
+    if (rg == 0 && act) {
       float* sqs = slab + slab_q_off(A, D);
 #pragma unroll
       for (int c = 0; c < NCT; ++c)
@@ -1621,8 +1612,7 @@ int din_grid(int B, bool bwd) {
   // forward: many small workgroups; backward: one workgroup per CU (its
   // registers allow one wave per SIMD) so the per-workgroup gradient slabs
   // stay few
-  const char* e = getenv(bwd ? "NRK_DIN_BWD_WGS" : "NRK_DIN_WGS");
-  int cap = e && *e ? atoi(e) : (bwd ? 256 : 1024);
+  const int cap = bwd ? 256 : 1024;
   return B < cap ? B : cap;
 }
 
@@ -1677,33 +1667,22 @@ extern "C" int nrk_din_attn_fwd(const void* keys, const int32_t* hist_ids, int64
   const bool bf = dtype == NRK_DTYPE_BF16;
   const size_t smem = fwd_smem(bf, d, L);
   NRK_CHECK_ARG(smem <= 160 * 1024, "din_fwd: L=%d d=%d needs %zu B LDS", L, d, smem);
-  const char* ew = getenv("NRK_DIN_WAVE_FWD");
-  const bool wave_ok = bf && hist_ids && (d == 64 || d == 128) && (ew == nullptr || atoi(ew) != 0);
+  const bool wave_ok = bf && hist_ids && (d == 64 || d == 128);
   if (wave_ok) {
     const int Lp = (L + 31) & ~31;
     const size_t AP = (size_t)((A + 63) & ~63);
     const size_t slot = AP * 4 + (size_t)Lp * d * 2;
-    const char* enb = getenv("NRK_DIN_FWD_NBUF");
-    // single-buffered slots (two workgroups per CU) measured faster than
-    // double-buffered ones (one per CU): 41 vs 51 us at B=4096, L=50, d=128
-    const bool dbl = AP * 4 + 4 * 2 * slot <= 150 * 1024 && enb && atoi(enb) == 2;
-    const size_t wsm = AP * 4 + 4 * (dbl ? 2 : 1) * slot;
+    // single-buffered slots, two workgroups per CU: measured faster than
+    // double-buffered ones at one per CU (41 vs 51 us at B=4096, L=50, d=128)
+    const size_t wsm = AP * 4 + 4 * slot;
     int grid = (int)cdiv(B, 4);
-    const char* ecap = getenv("NRK_DIN_FWD_WGS");
-    const int cap = ecap && *ecap ? atoi(ecap) : dbl ? 256 : 512;
-    if (grid > cap) grid = cap;
+    if (grid > 512) grid = 512;
     const uint16_t* tb = static_cast<const uint16_t*>(keys);
     const uint16_t* wk = static_cast<const uint16_t*>(W1k);
     hipStream_t st = (hipStream_t)stream;
 #define NRK_FWD_WAVE(DD, NN)                                                                                        \
-  do {                                                                                                              \
-    if (dbl)                                                                                                        \
-      hipLaunchKernelGGL((din_fwd_wave_kernel<DD, NN, 2>), dim3(grid), dim3(256), wsm, st, tb, hist_ids, n_table, U, wk, \
-                         w2, B, L, pooled, alpha);                                                                  \
-    else                                                                                                            \
-      hipLaunchKernelGGL((din_fwd_wave_kernel<DD, NN, 1>), dim3(grid), dim3(256), wsm, st, tb, hist_ids, n_table, U, wk, \
-                         w2, B, L, pooled, alpha);                                                                  \
-  } while (0)
+  hipLaunchKernelGGL((din_fwd_wave_kernel<DD, NN, 1>), dim3(grid), dim3(256), wsm, st, tb, hist_ids, n_table, U, wk, \
+                     w2, B, L, pooled, alpha)
     const int na = A / 32;
     if (d == 128) {
       if (na == 1) NRK_FWD_WAVE(128, 1); else if (na == 2) NRK_FWD_WAVE(128, 2);
@@ -1765,8 +1744,7 @@ extern "C" int nrk_din_attn_bwd(const void* keys, const int32_t* hist_ids, int64
   const size_t smem = bwd_smem(bf, d, L);
   NRK_CHECK_ARG(smem <= 160 * 1024, "din_bwd: L=%d d=%d needs %zu B LDS", L, d, smem);
   float* slabs = static_cast<float*>(ws);
-  const char* ep = getenv("NRK_DIN_PIPE_BWD");
-  const bool pipe_ok = bf && hist_ids && (d == 64 || d == 128) && (ep == nullptr || atoi(ep) != 0);
+  const bool pipe_ok = bf && hist_ids && (d == 64 || d == 128);
   if (pipe_ok) {
     const int Lp = (L + 31) & ~31;
     const size_t psm = (size_t)(2 * (d + 128 + Lp * d / 2) + 4 * 128) * 4;
@@ -1862,15 +1840,10 @@ extern "C" int nrk_din_attn_bwd_params(const void* table, const int32_t* hist_id
   float* slabs = static_cast<float*>(ws);
   const uint16_t* tb = static_cast<const uint16_t*>(table);
   const uint16_t* wk = static_cast<const uint16_t*>(W1k);
-  const char* ed = getenv("NRK_DIN_BWD_DEEP");
-  if (dU == nullptr && !(ed && atoi(ed) == 0)) {
-    const char* edb = getenv("NRK_DIN_BWD_DBG");  // timing experiments only: skip parts of the math
-    const int dbg = edb ? atoi(edb) : 0;
+  if (dU == nullptr) {  // the fused train step: deep-prefetch kernels, dW1q formed here too
     const int LPk = Lp <= 32 ? 32 : Lp <= 64 ? 64 : 128;
-    const char* ens = getenv("NRK_DIN_BWD_SLOTS");
-    const int nslot = ens && atoi(ens) == 3 ? 3 : 4;
-    const char* e8 = getenv("NRK_DIN_BWD_8W");
-    const bool w8 = !(e8 && atoi(e8) == 0) && LPk * d >= 4096;  // >= 8 key-image pieces: one per wave
+    const int nslot = 4;
+    const bool w8 = LPk * d >= 4096;  // >= 8 key-image pieces: one per wave
     size_t dsm = (size_t)(nslot * (4 * 128 + LPk * d / 2) + 4 * 4 * 128 + 5 * 128) * 4;
     if (w8) {
       dsm = (size_t)(nslot * (4 * 128 + LPk * d / 2) + 8 * 4 * 128 + 9 * 128) * 4;
@@ -1882,13 +1855,10 @@ extern "C" int nrk_din_attn_bwd_params(const void* table, const int32_t* hist_id
   do {                                                                                                              \
     if (w8)                                                                                                         \
       hipLaunchKernelGGL((din_bwd_deep8_kernel<DD, LL, 3>), dim3(grid), dim3(512), dsm, st, tb, hist_ids, n_table, U, \
-                         wk, w2, B, L, A, dpooled, alpha, slabs, q, d, dUp, dmy, dbg);                                \
-    else if (nslot == 3)                                                                                            \
-      hipLaunchKernelGGL((din_bwd_deep_kernel<DD, LL, 3>), dim3(grid), dim3(256), dsm, st, tb, hist_ids, n_table, U, wk, \
-                         w2, B, L, A, dpooled, alpha, slabs, q, d, dbg);                                              \
+                         wk, w2, B, L, A, dpooled, alpha, slabs, q, d, dUp, dmy);                                     \
     else                                                                                                            \
       hipLaunchKernelGGL((din_bwd_deep_kernel<DD, LL, 4>), dim3(grid), dim3(256), dsm, st, tb, hist_ids, n_table, U, wk, \
-                         w2, B, L, A, dpooled, alpha, slabs, q, d, dbg);                                              \
+                         w2, B, L, A, dpooled, alpha, slabs, q, d);                                                   \
   } while (0)
     if (d == 128) {
       if (LPk == 32) NRK_BWD_DEEP(128, 32); else if (LPk == 64) NRK_BWD_DEEP(128, 64); else NRK_BWD_DEEP(128, 128);

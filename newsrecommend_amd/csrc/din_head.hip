@@ -1472,8 +1472,7 @@ extern "C" int nrk_din_head_train(const float* q, const float* pooled, int64_t l
   a.dpooled = dpooled;
   hipStream_t st = (hipStream_t)stream;
   const int D2 = 2 * d, F2 = F / 2;
-  const char* ef = getenv("NRK_DIN_HEAD_FAST");
-  a.fast = F == HF && d % 32 == 0 && !(ef && atoi(ef) == 0);
+  a.fast = F == HF && d % 32 == 0;
   a.nrg0 = nblk < 8 ? nblk : 8;
   if (a.fast) {
     const size_t lf1 = ((size_t)2 * D2 + (size_t)(HR + HF) * (D2 + 4) + 4 * HR * HF + HR * (HF + 1)) * 4;

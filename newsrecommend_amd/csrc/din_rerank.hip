@@ -45,7 +45,7 @@ __global__ __launch_bounds__(256, 1) void din_rerank_kernel(const uint16_t* __re
                                                             const float* __restrict__ Uc, int C,
                                                             const uint16_t* __restrict__ W1k,
                                                             const float* __restrict__ w2, int A,
-                                                            float* __restrict__ pooled, int dbg) {
+                                                            float* __restrict__ pooled) {
   constexpr int CPR = D / 8, KS = D / 16, NDT = D / 32;
   constexpr int PS = 129;  // P row stride (floats): lane = row reads its own row conflict-free
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -138,7 +138,7 @@ __global__ __launch_bounds__(256, 1) void din_rerank_kernel(const uint16_t* __re
       for (int g4 = 0; g4 < 4; ++g4) {
         const int cb = 16 * w + 4 * g4;
         float sc[4] = {0.f, 0.f, 0.f, 0.f};
-        if (!(dbg & 1) && cb < nc) {
+        if (cb < nc) {
           const float* u0 = Us + cb * 128;
 #pragma unroll
           for (int n = 0; n < 128; n += 4) {  // units >= A contribute w2 = 0
@@ -158,14 +158,10 @@ __global__ __launch_bounds__(256, 1) void din_rerank_kernel(const uint16_t* __re
           const int cl = cb + i;
           float al = 0.f;
           if (cl < nc) {
-            if (dbg & 1) {
-              al = rowok ? 1.f / L : 0.f;
-            } else {
-              const float sv = rowok ? sc[i] : -INFINITY;
-              const float m = wave_max(sv);
-              const float ex = rowok ? expf(sv - m) : 0.f;
-              al = ex / wave_sum(ex);
-            }
+            const float sv = rowok ? sc[i] : -INFINITY;
+            const float m = wave_max(sv);
+            const float ex = rowok ? expf(sv - m) : 0.f;
+            al = ex / wave_sum(ex);
           }
           const bf16x2_t hl = {(__bf16)al, (__bf16)0.f};
           const uint16_t hb = (uint16_t)(__builtin_bit_cast(uint32_t, hl) & 0xFFFF);
@@ -177,7 +173,7 @@ __global__ __launch_bounds__(256, 1) void din_rerank_kernel(const uint16_t* __re
       }
       __syncthreads();
       // 4. pooled = alpha K (hi and lo passes); wave w: dim tiles w, w + 4, ...
-      for (int cg = 0; cg < ((dbg & 2) ? 0 : nc); cg += 32) {
+      for (int cg = 0; cg < nc; cg += 32) {
         for (int dt = w; dt < NDT; dt += 4) {
           f32x16 acc;
 #pragma unroll
@@ -238,20 +234,18 @@ extern "C" int nrk_din_rerank_attn(const void* table, int64_t n_table, int32_t d
   const size_t smem = (size_t)rr::LP * d * 2 + ((size_t)rr::LP * 129 + rr::CCH * 128 + 128) * 4 + 2 * (size_t)rr::CCH * rr::LP * 2;
   NRK_CHECK_ARG(smem <= 160 * 1024, "din_rerank: %zu B LDS", smem);
   const int grid = nU < 256 ? nU : 256;
-  const char* edb = getenv("NRK_RR_DBG");  // timing experiments only: 1 skip scores, 2 skip the pool
-  const int dbg = edb ? atoi(edb) : 0;
   hipStream_t st = (hipStream_t)stream;
   const uint16_t* tb = static_cast<const uint16_t*>(table);
   const uint16_t* wk = static_cast<const uint16_t*>(W1k_bf16);
   if (d == 256)
     hipLaunchKernelGGL(rr::din_rerank_kernel<256>, dim3(grid), dim3(256), smem, st, tb, n_table, hist, nU, L, Uc, C, wk,
-                       w2, A, pooled, dbg);
+                       w2, A, pooled);
   else if (d == 128)
     hipLaunchKernelGGL(rr::din_rerank_kernel<128>, dim3(grid), dim3(256), smem, st, tb, n_table, hist, nU, L, Uc, C, wk,
-                       w2, A, pooled, dbg);
+                       w2, A, pooled);
   else
     hipLaunchKernelGGL(rr::din_rerank_kernel<64>, dim3(grid), dim3(256), smem, st, tb, n_table, hist, nU, L, Uc, C, wk,
-                       w2, A, pooled, dbg);
+                       w2, A, pooled);
   NRK_CHECK_LAUNCH("din_rerank_kernel");
   return NRK_OK;
 }
