@@ -166,13 +166,34 @@ int nrk_din_batch(const int64_t* idx, int32_t B, const int32_t* hist_all, const 
 
 /* DIN attention for re-ranking (DIN.py:166-173: every candidate of a user
  * attends over the same history): pooled [nU*C][d] f32 for candidates whose
- * query rows give Uc [nU*C][A] f32 (= q W1[:, :d]^T + b1, caller GEMM), users'
- * history ids hist [nU][L] int32 (-1 = zero row), table [N][d] bf16, W1k
- * [A][d] bf16 = W1[:, d:], w2 [A].  P = K W1k^T is formed once per user.
- * d in {64, 128, 256}, L <= 64. */
+ * query rows give Uc [nU*C][ldu] f32 (first A columns = q W1[:, :d]^T + b1,
+ * e.g. from nrk_din_item_proj), users' history ids hist [nU][L] int32 (-1 or
+ * >= n_table = zero row, DIN.py:108 padding), table [N][d] bf16, W1k [A][d]
+ * bf16 = W1[:, d:], w2 [A].  P = K W1k^T is formed once per user; padding
+ * slots share one logit.  d in {64, 128, 256}, L <= 64, A in {32,64,96,128}. */
 int nrk_din_rerank_attn(const void* table, int64_t n_table, int32_t dtype, const int32_t* hist,
-                        int32_t nU, int32_t L, const float* Uc, int32_t C, int32_t d,
+                        int32_t nU, int32_t L, const float* Uc, int32_t ldu, int32_t C, int32_t d,
                         const void* W1k_bf16, const float* w2, int32_t A, float* pooled, void* stream);
+
+/* Query-side projections of re-rank candidates, gathered from the item table:
+ * out [n][NO] f32 = table[ids[i]] W^T + bias (ids outside [0, n_table): zero
+ * row).  W [NO][d] f32 enters as W_hi = bf16(W), W_lo = bf16(W - W_hi)
+ * ([NO][d] bf16 each).  Replaces the q gather + torch.addmm of the attention
+ * query half (DIN.py:96-104) and of the head's first layer (DIN.py:200-204).
+ * d in {64, 128, 256}, NO in 128..256 step 32 (pad W with zero rows). */
+int nrk_din_item_proj(const void* table, int64_t n_table, int32_t dtype, const int32_t* ids, int64_t n,
+                      int32_t d, const void* W_hi, const void* W_lo, const float* bias, int32_t NO,
+                      float* out, void* stream);
+
+/* Eval-mode DIN head on re-rank candidates (DIN.py:200-204, BatchNorms folded
+ * into the Linears by the caller): logit[i] = h3 . relu(H2 relu(Q1[i] +
+ * H1p pooled[i] + c1) + c2) + c3, -inf where cand[i] < 0.  pooled [n][d] f32
+ * (nrk_din_rerank_attn), Q1 [n][ldq] f32 (query half, no bias), H1p [F][d] as
+ * bf16 hi + lo, c1 [F], H2 [F/2][F], c2 [F/2], h3 [F/2].  F = 32. */
+int nrk_din_rerank_head(const float* pooled, int64_t n, int32_t d, const float* Q1, int32_t ldq,
+                        const int32_t* cand, const void* H1p_hi, const void* H1p_lo, const float* c1,
+                        int32_t F, const float* H2, const float* c2, const float* h3, float c3,
+                        float* logit, void* stream);
 
 /* ------------------------------------------------------ inverted lists --
  * faiss Clustering / IndexIVFFlat building blocks (Retrieval.py:11-23).

@@ -59,8 +59,11 @@ SIGNATURES = {
                                                c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_size, c_p]),
     "nrk_din_batch": (ctypes.c_int, [c_p, c_i32, c_p, c_p, c_p, c_i64, c_i32, c_p, c_i64, c_i32, c_i32, c_p, c_p,
                                      c_i32, c_p, c_p, c_p, c_p, c_p, c_p]),
-    "nrk_din_rerank_attn": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_i32, c_i32, c_p, c_i32, c_i32, c_p, c_p, c_i32,
-                                           c_p, c_p]),
+    "nrk_din_rerank_attn": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_i32, c_i32, c_p, c_i32, c_i32, c_i32, c_p, c_p,
+                                           c_i32, c_p, c_p]),
+    "nrk_din_item_proj": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_i64, c_i32, c_p, c_p, c_p, c_i32, c_p, c_p]),
+    "nrk_din_rerank_head": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_i32, c_p, c_p, c_p, c_p, c_i32, c_p, c_p, c_p,
+                                           c_f32, c_p, c_p]),
     "nrk_gather_rows": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_i64, c_i32, c_p, c_p]),
 }
 

@@ -75,37 +75,82 @@ def _fold_eval_head(fc):
     return out
 
 
+def _split_bf16(w: torch.Tensor):
+    """f32 weights -> (hi, lo) bf16 with hi + lo = w to 16 mantissa bits."""
+    hi = w.to(torch.bfloat16)
+    return hi.contiguous(), (w - hi.float()).to(torch.bfloat16).contiguous()
+
+
 def _rerank_shared(model, table, hist_rows, cand_rows, batch_samples):
-    """Shared-history path: U = q W1q^T + b1 for all candidates (one GEMM),
-    nrk_din_rerank_attn (P = K W1k^T once per user), the eval-mode head with
-    its BatchNorms folded into the Linears (no [q, pooled] concatenation: the
-    first layer is two GEMMs accumulating into one output)."""
+    """Shared-history path, three HIP kernels per batch of users:
+      nrk_din_item_proj    [U | Q1] = q [W1q ; H1q]^T + [b1 ; 0] gathered from
+                           the bf16 table (the attention query half and the
+                           head's first-layer query half in one pass),
+      nrk_din_rerank_attn  P = K W1k^T once per user, per-candidate scores,
+                           softmax over the L slots, pooled = alpha K,
+      nrk_din_rerank_head  the eval-mode head (BatchNorms folded into the
+                           Linears) -> logits, -inf on padded candidates.
+    Heads the fused kernel does not cover (F != 32, BatchNorm without running
+    statistics) run as torch ops on the gathered rows."""
     from . import _lib
     from .din import gather_rows
 
     U, C = cand_rows.shape
     L = hist_rows.shape[1]
     d = table.shape[1]
+    dev = table.device
     W1, b1 = model.attn.attn[0].weight, model.attn.attn[0].bias
     A = W1.shape[0]
     W1k = W1[:, d:].to(torch.bfloat16).contiguous()
     w2 = model.attn.attn[2].weight.reshape(-1).contiguous()
     head = _fold_eval_head(model.fc)
-    if head is not None:
+    fused = head is not None and head[0][0].shape[0] == 32
+    if fused:
         (H1, c1), (H2, c2), (H3, c3) = head
-        H1q, H1p = H1[:, :d].t(), H1[:, d:].t()
-    out = torch.empty((U, C), dtype=torch.float32, device=table.device)
+        F = H1.shape[0]
+        Wcat = torch.cat([W1[:, :d], H1[:, :d]], 0)
+        bcat = torch.cat([b1, torch.zeros(F, device=dev)]).contiguous()
+    else:
+        Wcat, bcat = W1[:, :d], b1.contiguous()
+        if head is not None:
+            (H1, c1), (H2, c2), (H3, c3) = head
+            H1q, H1p = H1[:, :d].t(), H1[:, d:].t()
+    NO = max(128, -(-Wcat.shape[0] // 32) * 32)  # nrk_din_item_proj: 128..256 outputs, zero rows pad
+    Wpad = torch.zeros((NO, d), device=dev)
+    Wpad[:Wcat.shape[0]] = Wcat
+    bpad = torch.zeros(NO, device=dev)
+    bpad[:bcat.shape[0]] = bcat
+    W_hi, W_lo = _split_bf16(Wpad)
+    if fused:
+        Hp_hi, Hp_lo = _split_bf16(H1[:, d:].contiguous())
+        H2c, c2c, h3c = H2.contiguous(), c2.contiguous(), H3.reshape(-1).contiguous()
+        c3v = float(c3.reshape(-1)[0])
+    lib = _lib.load()
+    st = _lib.stream(dev)
+    out = torch.empty((U, C), dtype=torch.float32, device=dev)
     ub = max(1, batch_samples // max(C, 1))
     for lo in range(0, U, ub):
         hi = min(U, lo + ub)
+        n = (hi - lo) * C
         cr = cand_rows[lo:hi].reshape(-1).to(torch.int32).contiguous()
-        q = gather_rows(table, cr)
-        Uc = torch.addmm(b1, q, W1[:, :d].t())
-        pooled = torch.empty_like(q)
+        proj = torch.empty((n, NO), dtype=torch.float32, device=dev)
+        _lib.check(lib.nrk_din_item_proj(_lib.ptr(table), table.shape[0], _lib.NRK_DTYPE_BF16, _lib.ptr(cr), n, d,
+                                         _lib.ptr(W_hi), _lib.ptr(W_lo), _lib.ptr(bpad), NO, _lib.ptr(proj), st),
+                   "din_item_proj")
+        pooled = torch.empty((n, d), dtype=torch.float32, device=dev)
         hr = hist_rows[lo:hi].to(torch.int32).contiguous()
-        _lib.check(_lib.load().nrk_din_rerank_attn(
-            _lib.ptr(table), table.shape[0], _lib.NRK_DTYPE_BF16, _lib.ptr(hr), hi - lo, L, _lib.ptr(Uc), C, d,
-            _lib.ptr(W1k), _lib.ptr(w2), A, _lib.ptr(pooled), _lib.stream(table.device)), "din_rerank_attn")
+        _lib.check(lib.nrk_din_rerank_attn(
+            _lib.ptr(table), table.shape[0], _lib.NRK_DTYPE_BF16, _lib.ptr(hr), hi - lo, L, _lib.ptr(proj), NO, C, d,
+            _lib.ptr(W1k), _lib.ptr(w2), A, _lib.ptr(pooled), st), "din_rerank_attn")
+        if fused:
+            lg = torch.empty(n, dtype=torch.float32, device=dev)
+            _lib.check(lib.nrk_din_rerank_head(
+                _lib.ptr(pooled), n, d, _lib.ptr(proj) + 4 * A, NO, _lib.ptr(cr), _lib.ptr(Hp_hi), _lib.ptr(Hp_lo),
+                _lib.ptr(c1), F, _lib.ptr(H2c), _lib.ptr(c2c), _lib.ptr(h3c), c3v, _lib.ptr(lg), st),
+                "din_rerank_head")
+            out[lo:hi] = lg.view(hi - lo, C)
+            continue
+        q = gather_rows(table, cr)
         if head is None:
             lg = model.fc(torch.cat([q, pooled], dim=1)).view(hi - lo, C)
         else:
@@ -117,7 +162,7 @@ def _rerank_shared(model, table, hist_rows, cand_rows, batch_samples):
 
 @torch.no_grad()
 def rerank(model, table: torch.Tensor, hist_rows: torch.Tensor, cand_rows: torch.Tensor,
-           batch_samples: int = 1 << 18, shared: bool = True) -> torch.Tensor:
+           batch_samples: int = 1 << 20, shared: bool = True) -> torch.Tensor:
     """DIN logits (U, C) for candidate rows (U, C) (-1 = padding -> -inf) of
     users with history rows (U, L) (-1 = padding), all rows of `table` on the
     device.  Eval-mode BatchNorm is row-independent, so one forward over many

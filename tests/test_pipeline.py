@@ -150,3 +150,72 @@ def test_rerank_shared_history_matches_per_candidate(d, L, C):
     assert torch.equal(fin, torch.isfinite(a))
     err = (a[fin] - b[fin]).abs().max().item()
     assert err < 2e-3 * max(1.0, b[fin].abs().max().item()), err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d,NO,n", [(256, 160, 1000), (128, 128, 77), (64, 256, 33)])
+def test_item_proj_matches_fp64(d, NO, n):
+    """nrk_din_item_proj (gathered bf16 rows x W^T + bias, W as bf16 hi + lo)
+    vs fp64 on the same rows; invalid ids give the bias."""
+    from newsrecommend_amd import _lib
+    from newsrecommend_amd.pipeline import _split_bf16
+
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(7)
+    N = 3000
+    table = torch.randn((N, d), generator=g, device=dev).to(torch.bfloat16)
+    ids = torch.randint(0, N, (n,), generator=g, device=dev, dtype=torch.int32)
+    ids[::7] = -1
+    ids[3::11] = N + 5
+    W = torch.randn((NO, d), generator=g, device=dev) * 0.1
+    b = torch.randn(NO, generator=g, device=dev)
+    hi, lo = _split_bf16(W)
+    out = torch.empty((n, NO), device=dev)
+    _lib.check(_lib.load().nrk_din_item_proj(_lib.ptr(table), N, _lib.NRK_DTYPE_BF16, _lib.ptr(ids), n, d,
+                                             _lib.ptr(hi), _lib.ptr(lo), _lib.ptr(b), NO, _lib.ptr(out),
+                                             _lib.stream(dev)), "item_proj")
+    ok = (ids >= 0) & (ids < N)
+    q = torch.where(ok[:, None], table[ids.clamp(0, N - 1).long()].double(), 0.0)
+    ref = q @ W.double().t() + b.double()
+    bound = (q.abs() @ W.double().abs().t()).max().item() * 2.0 ** -15 + 1e-6
+    err = (out.double() - ref).abs().max().item()
+    assert err <= bound, (err, bound)
+    assert torch.equal(out[~ok], b.expand(int((~ok).sum()), NO))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d", [256, 64])
+def test_rerank_head_matches_fp64(d):
+    """nrk_din_rerank_head (pooled H1p on MFMA with hi/lo splits, two small
+    layers per lane) vs the fp64 composition; -inf on padded candidates."""
+    from newsrecommend_amd import _lib
+    from newsrecommend_amd.pipeline import _split_bf16
+
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(9)
+    n, F, ldq = 301, 32, 160
+    pooled = torch.randn((n, d), generator=g, device=dev)
+    Q = torch.randn((n, ldq), generator=g, device=dev)
+    cand = torch.randint(0, 100, (n,), generator=g, device=dev, dtype=torch.int32)
+    cand[::9] = -1
+    H1p = torch.randn((F, d), generator=g, device=dev) * 0.1
+    c1 = torch.randn(F, generator=g, device=dev) * 0.1
+    H2 = torch.randn((F // 2, F), generator=g, device=dev) * 0.3
+    c2 = torch.randn(F // 2, generator=g, device=dev) * 0.1
+    h3 = torch.randn(F // 2, generator=g, device=dev) * 0.3
+    c3 = 0.25
+    hi, lo = _split_bf16(H1p)
+    lg = torch.empty(n, device=dev)
+    off = 128  # Q1 = columns 128..159 of each Q row
+    _lib.check(_lib.load().nrk_din_rerank_head(_lib.ptr(pooled), n, d, _lib.ptr(Q) + 4 * off, ldq, _lib.ptr(cand),
+                                               _lib.ptr(hi), _lib.ptr(lo), _lib.ptr(c1), F, _lib.ptr(H2),
+                                               _lib.ptr(c2), _lib.ptr(h3), c3, _lib.ptr(lg), _lib.stream(dev)),
+               "rerank_head")
+    p64 = pooled.double()
+    h1 = (Q[:, off:off + F].double() + p64 @ H1p.double().t() + c1.double()).relu()
+    h2 = (h1 @ H2.double().t() + c2.double()).relu()
+    ref = h2 @ h3.double() + c3
+    valid = cand >= 0
+    assert torch.isneginf(lg[~valid]).all()
+    err = (lg[valid].double() - ref[valid]).abs().max().item()
+    assert err < 1e-4 * max(1.0, ref.abs().max().item()), err
