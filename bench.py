@@ -502,6 +502,9 @@ def bench_e2e(args, rank, world, dev):
 
 
 # ------------------------------------------------------------------ DIN --
+DIN_STEPS_PER_GRAPH = 8  # fused steps per HIP-graph launch (one index copy + one launch per 8 steps)
+
+
 def bench_din(args, rank, world, dev):
     from newsrecommend_amd.data import synthetic_click_rows
     from newsrecommend_amd.din import DIN, KernelTimer
@@ -529,7 +532,22 @@ def bench_din(args, rank, world, dev):
             all_reduce_mean_(G)
 
         trainer = FusedTrainStep(model, table, hist, tgt, lab, B, lr=1.62e-3, weight_decay=8.96e-5, clip=1.0,
-                                 graph=graphed, grad_hook=allreduce if world > 1 else None)
+                                 graph=graphed, grad_hook=allreduce if world > 1 else None,
+                                 steps_per_graph=DIN_STEPS_PER_GRAPH if graphed else 1)
+
+    def run(s0, n):
+        """steps s0 .. s0 + n - 1: K-step graph launches where K consecutive batches are contiguous in perm"""
+        s, loss = s0, None
+        while s < s0 + n:
+            K = trainer.K if fused else 1
+            if K > 1 and s + K <= s0 + n and s % nbatch + K <= nbatch:
+                b = s % nbatch
+                loss = trainer.step_many(perm[b * B:(b + K) * B].view(K, B))[-1]
+                s += K
+            else:
+                loss = step(s)
+                s += 1
+        return loss
 
     def step(s):
         idx = perm[(s % nbatch) * B:(s % nbatch + 1) * B]
@@ -553,12 +571,10 @@ def bench_din(args, rank, world, dev):
         return loss
 
     model.train()
-    for s in range(args.warmup):
-        step(s)
+    run(0, args.warmup)
     barrier(world)
     t0 = time.perf_counter()
-    for s in range(args.steps):
-        loss = step(args.warmup + s)
+    loss = run(args.warmup, args.steps)
     barrier(world)
     el = max_over_ranks(time.perf_counter() - t0, world, dev)
     # attention kernel times: a few extra steps of the same path, outside the
@@ -587,7 +603,7 @@ def bench_din(args, rank, world, dev):
         "config": {"workload": "configs[2]: DIN train bf16, 5M synthetic click rows, seq_len=50, emb_dim=128",
                    "rows": rows, "items": n_items, "batch": B, "attn_units": A, "fc_units": F,
                    "parallelism": f"dp{world}",
-                   "step": ("fused head/optimizer kernels, one hip graph" if graphed else
+                   "step": (f"fused head/optimizer kernels, one hip graph per {DIN_STEPS_PER_GRAPH} steps" if graphed else
                             "fused head/optimizer kernels + RCCL grad all_reduce") if fused else "eager torch"},
         "final_loss": float(loss.reshape(-1)[0].item()),
         "kernels_ms": {"attn_fwd": fwd_ms, "attn_bwd (deep8 + dwq + reduce)" if fused else "attn_bwd+reduce": bwd_ms},

@@ -16,15 +16,15 @@
 // rows to the front and scores nv rows plus ONE padding row that enters the
 // softmax denominator npad = L - nv times.
 //
-// One workgroup (4 waves) per user; lane = candidate (64 per wave, 256 per
+// One workgroup (8 waves) per user; lane = candidate (64 per wave, 256 per
 // chunk), so the softmax is a per-lane loop, not a cross-lane reduction:
 //   1. valid mask by ballot, compacted history rows -> LDS image [64][D] bf16
 //      (XOR-swizzled, zero rows past nv),
 //   2. P = K W1k^T on bf16 MFMA (wave w: units 32w..32w+31) -> LDS, row-major,
-//   3. each lane holds its candidate's U row in registers; per history row the
-//      P row is a broadcast LDS read and w2 a scalar (SGPR) operand: packed
-//      add, max, packed fma — 2 VALU per (candidate, row, unit); logits -> the
-//      lane's LDS row S[c][.],
+//   3. each lane holds its candidate's U slice in registers; per history row
+//      the P row and w2 are broadcast LDS reads: packed add, max, packed fma —
+//      2 VALU per (candidate, row, unit); logits -> the lane's LDS row S[c][.];
+//      two waves per 64-candidate group split the rows (8 waves, 2 per SIMD),
 //   4. per-lane softmax over S[c][0..nr), alpha split hi + lo bf16, stored as
 //      one dword per row in place,
 //   5. pooled (64 cand x D) per wave = alpha K on bf16 MFMA (hi and lo passes,

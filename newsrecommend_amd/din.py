@@ -400,7 +400,7 @@ class FusedTrainStep:
 
     def __init__(self, model: "DIN", table, hist_ids, target_ids, labels, batch_size, lr=1.62e-3,
                  betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, clip=1.0, seed=1234, graph=True,
-                 grad_hook=None):
+                 grad_hook=None, steps_per_graph=1):
         dev = table.device
         _lib.require_device(table, hist_ids, target_ids, labels, what="FusedTrainStep")
         self.model, self.table = model, table
@@ -461,11 +461,14 @@ class FusedTrainStep:
             fc[9].weight.grad, fc[9].bias.grad)])
         B, d, A, Dk = self.B, self.d, self.A, self.Dk
         L_ = _lib.load()
-        self.idx = torch.zeros(B, dtype=torch.long, device=dev)
+        # batch rows and losses of the K steps one graph replays (step(): K = 1 slot)
+        self.K = max(1, int(steps_per_graph))
+        self.idx_ring = torch.zeros((self.K, B), dtype=torch.long, device=dev)
+        self.loss_ring = torch.zeros((self.K, 1), dtype=torch.float32, device=dev)
+        self.idx, self.loss = self.idx_ring[0], self.loss_ring[0]
         self.pooled = torch.empty((B, Dk), dtype=torch.float32, device=dev)
         self.alpha = torch.empty((B, hist_ids.shape[1]), dtype=torch.float32, device=dev)
         self.logits = torch.empty(B, dtype=torch.float32, device=dev)
-        self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
         self.dpooled = torch.empty((B, Dk), dtype=torch.float32, device=dev)
         self.dU = torch.empty((B, A), dtype=torch.float32, device=dev)
         self.dW1k = torch.empty((A, Dk), dtype=torch.float32, device=dev)
@@ -489,7 +492,7 @@ class FusedTrainStep:
             self.y_b = torch.empty(B, dtype=torch.float32, device=dev)
             self.U_b = torch.empty((B, A), dtype=torch.float32, device=dev)
             self.W1k_b = torch.empty((A, d), dtype=torch.bfloat16, device=dev)
-        self.graph = None
+        self.graph = self.graph_k = None
         if graph:
             snap = [t.detach().clone() for t in (self.P, self.M, self.V, self.step_t)]
             bufs = {k: v.detach().clone() for k, v in model.named_buffers()}
@@ -501,23 +504,29 @@ class FusedTrainStep:
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph):
                 self._body()
+            if self.K > 1:  # K consecutive steps in one graph: one index copy and one launch per K steps
+                self.graph_k = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.graph_k):
+                    for k in range(self.K):
+                        self._body(k)
             with torch.no_grad():  # capture ran real steps: restore the model and optimizer state
                 for t, s in zip((self.P, self.M, self.V, self.step_t), snap):
                     t.copy_(s)
                 for k, v in model.named_buffers():
                     v.copy_(bufs[k])
 
-    def _body(self):
+    def _body(self, k=0):
+        idx, loss = self.idx_ring[k], self.loss_ring[k]
         if self.fast:
-            return self._body_fast()
+            return self._body_fast(idx, loss)
         L_ = _lib.load()
         m = self.model
         dev = self.table.device
         st = _lib.stream(dev)
         B, d, A, Dk = self.B, self.d, self.A, self.Dk
-        hist = self.hist_all.index_select(0, self.idx)
-        tgt = self.tgt_all.index_select(0, self.idx)
-        y = self.lab_all.index_select(0, self.idx).reshape(-1)
+        hist = self.hist_all.index_select(0, idx)
+        tgt = self.tgt_all.index_select(0, idx)
+        y = self.lab_all.index_select(0, idx).reshape(-1)
         q = gather_rows(self.table, tgt)
         W1, b1 = m.attn.attn[0].weight, m.attn.attn[0].bias
         w2 = m.attn.attn[2].weight.reshape(-1)
@@ -532,7 +541,7 @@ class FusedTrainStep:
         _lib.check(L_.nrk_din_head_train(
             _lib.ptr(q), _lib.ptr(self.pooled), Dk, _lib.ptr(y), B, d, self.F, self.bn_momentum, self.bn_eps, self.p_drop,
             self.seed,
-            _lib.ptr(self.step_t), ctypes.byref(self.hp), _lib.ptr(self.logits), _lib.ptr(self.loss),
+            _lib.ptr(self.step_t), ctypes.byref(self.hp), _lib.ptr(self.logits), _lib.ptr(loss),
             _lib.ptr(self.dpooled), _lib.ptr(self.ws_head), self.ws_head.numel(), st), "din_head_train")
         gW2, gb2 = m.attn.attn[2].weight.grad, m.attn.attn[2].bias.grad
         _lib.check(L_.nrk_din_attn_bwd(
@@ -552,7 +561,7 @@ class FusedTrainStep:
             _lib.ptr(self.ws_opt),
             self.ws_opt.numel(), st), "clip_adam")
 
-    def _body_fast(self):
+    def _body_fast(self, idx, loss):
         L_ = _lib.load()
         m = self.model
         st = _lib.stream(self.table.device)
@@ -563,7 +572,7 @@ class FusedTrainStep:
         W1, b1 = m.attn.attn[0].weight, m.attn.attn[0].bias
         w2 = m.attn.attn[2].weight
         _lib.check(L_.nrk_din_batch(
-            _lib.ptr(self.idx), B, _lib.ptr(self.hist_all), _lib.ptr(self.tgt_all), _lib.ptr(self.lab_all),
+            _lib.ptr(idx), B, _lib.ptr(self.hist_all), _lib.ptr(self.tgt_all), _lib.ptr(self.lab_all),
             self.hist_all.shape[0], L, _lib.ptr(self.table), N, dt, d, _lib.ptr(W1), _lib.ptr(b1), A,
             _lib.ptr(self.hist_b), _lib.ptr(self.q_b), _lib.ptr(self.y_b), _lib.ptr(self.U_b), _lib.ptr(self.W1k_b),
             st), "din_batch")
@@ -575,7 +584,7 @@ class FusedTrainStep:
         _lib.check(L_.nrk_din_head_train(
             _lib.ptr(self.q_b), _lib.ptr(self.pooled), d, _lib.ptr(self.y_b), B, d, self.F, self.bn_momentum,
             self.bn_eps, self.p_drop,
-            self.seed, _lib.ptr(self.step_t), ctypes.byref(self.hp), _lib.ptr(self.logits), _lib.ptr(self.loss),
+            self.seed, _lib.ptr(self.step_t), ctypes.byref(self.hp), _lib.ptr(self.logits), _lib.ptr(loss),
             _lib.ptr(self.dpooled), _lib.ptr(self.ws_head), self.ws_head.numel(), st), "din_head_train")
         t0 = KernelTimer.mark("bwd")
         _lib.check(L_.nrk_din_attn_bwd_params(
@@ -615,6 +624,24 @@ class FusedTrainStep:
         else:
             self._body()
         return self.loss
+
+    def step_many(self, batch_indices: torch.Tensor):
+        """K = steps_per_graph consecutive training steps, batch k on rows
+        `batch_indices[k]` ((K, B) device int64), as ONE graph launch; returns
+        the K device losses (K, 1).  Same result as K calls of step()."""
+        if batch_indices.shape != (self.K, self.B):
+            raise ValueError(f"step_many: expected batch indices of shape {(self.K, self.B)}, "
+                             f"got {tuple(batch_indices.shape)}")
+        self._sync_lr()
+        self.idx_ring.copy_(batch_indices, non_blocking=True)
+        if self.graph_k is not None:
+            self.graph_k.replay()
+        elif self.graph is not None and self.K == 1:
+            self.graph.replay()
+        else:
+            for k in range(self.K):
+                self._body(k)
+        return self.loss_ring
 
 
 def fit(model, table, hist_ids, target_ids, labels, eval_loader, epochs=10, batch_size=64, lr=1.62e-3,

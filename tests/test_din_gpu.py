@@ -308,6 +308,27 @@ def test_fused_head_with_dropout_matches_torch_with_same_masks(gpu):
             (n, (pa.grad - ref).abs().max().item())
 
 
+def test_fused_step_many_equals_single_steps(gpu):
+    """FusedTrainStep.step_many (K steps captured in one HIP graph, dropout on)
+    == K step() calls: losses, parameters, Adam moments and BN buffers
+    bit-identical (the same kernels in the same order)."""
+    from newsrecommend_amd.din import FusedTrainStep
+
+    dev, table, hist, tgt, lab, ma, mb = _setup_fused(0.36, d=128, L=50)
+    K, B = 4, 512
+    ta = FusedTrainStep(ma, table, hist, tgt, lab, B, lr=1e-3, weight_decay=1e-4, steps_per_graph=K)
+    tb = FusedTrainStep(mb, table, hist, tgt, lab, B, lr=1e-3, weight_decay=1e-4)
+    perm = torch.randperm(hist.shape[0], device=dev)
+    for r in range(2):
+        la = ta.step_many(perm[r * K * B:(r + 1) * K * B].view(K, B)).clone()
+        lb = torch.stack([tb.step(perm[(r * K + k) * B:(r * K + k + 1) * B]).clone() for k in range(K)])
+        assert torch.equal(la, lb), (r, la.flatten(), lb.flatten())
+    for t_a, t_b in ((ta.P, tb.P), (ta.M, tb.M), (ta.V, tb.V), (ta.step_t, tb.step_t)):
+        assert torch.equal(t_a, t_b)
+    for (n, x), (_, y) in zip(ma.named_buffers(), mb.named_buffers()):
+        assert torch.equal(x, y), n
+
+
 @pytest.mark.parametrize("d,A,L", [(64, 64, 20), (128, 128, 50), (128, 96, 7)])
 def test_din_batch_kernel(gpu, d, A, L):
     """nrk_din_batch (batch assembly + U = q W1q^T + b1 on split-bf16 MFMA)
