@@ -169,6 +169,10 @@ __global__ __launch_bounds__(256) void tau_select_kernel(const float* __restrict
 }
 
 // ========================================================= merge/rescore ==
+// fp64 score in the oracle's serial order (bit-identical).  One lane per
+// candidate row: scalar loads measured faster than float4 ones here (k = 5
+// merge 0.086 vs 0.103 ms); many candidates go through the LDS-staged loop of
+// merge_rescore_kernel instead.
 __device__ __forceinline__ double exact_score(const float* __restrict__ qs, const float* __restrict__ x,
                                               int d, bool l2) {
   double acc = 0.0;
@@ -223,7 +227,10 @@ struct IvfFb {
 };
 
 // One 256-thread workgroup per query.  Dynamic LDS: P doubles + P int64 (the
-// union), P2 doubles + P2 int64 (rescored), d floats (query), reductions.
+// union; later the rescoring's row stage, at least 256 x (RS_CW + 4) floats),
+// P2 doubles + P2 int64 (rescored), d floats (query), reductions.
+constexpr int RS_CW = 32;       // columns per rescoring stage (one 128-B line of each candidate row)
+constexpr int RS_MIN_KP = 128;  // staged rescoring from this many candidates (k = 5: lane-per-row loads)
 __global__ __launch_bounds__(256) void merge_rescore_kernel(
     const float* __restrict__ part_s, const int* __restrict__ part_i, const float* __restrict__ part_t,
     int nch, int M, int KP, int k, int dp, const float* __restrict__ xq, const float* __restrict__ xb,
@@ -236,7 +243,8 @@ __global__ __launch_bounds__(256) void merge_rescore_kernel(
   double* g = reinterpret_cast<double*>(smem);
   int64_t* id = reinterpret_cast<int64_t*>(g + P);
   const int P2 = pow2ceil(KP);
-  double* g2 = reinterpret_cast<double*>(id + P);
+  const int UB = KP < RS_MIN_KP || 16 * P > 256 * (RS_CW + 4) * 4 ? 16 * P : 256 * (RS_CW + 4) * 4;  // union / stage
+  double* g2 = reinterpret_cast<double*>(smem + UB);
   int64_t* id2 = reinterpret_cast<int64_t*>(g2 + P2);
   float* qs = reinterpret_cast<float*>(id2 + P2);
   __shared__ float red[256];
@@ -302,15 +310,58 @@ __global__ __launch_bounds__(256) void merge_rescore_kernel(
   if (tau_q) theta = fmax(theta, (double)tau_q[qi]);  // items below the bound were never kept
 
   // exact rescoring of the top kp screened candidates
-  for (int i = tid; i < P2; i += 256) {
-    if (i < kp) {
-      const int64_t item = id[i];
-      const double s = exact_score(qs, xb + item * d, d, l2 != 0);
-      g2[i] = l2 ? -s : s;
-      id2[i] = item;
-    } else {
-      g2[i] = -INFINITY;
-      id2[i] = INT64_MAX;
+  if ((d & 3) == 0 && KP >= RS_MIN_KP) {
+    // lane = candidate row, fp64 in the oracle's serial order, rows staged
+    // through LDS RS_CW columns at a time by coalesced loads (8 lanes per
+    // 128-B row piece); the union's LDS is the stage (its ids moved to id2)
+    for (int i = tid; i < P2; i += 256) id2[i] = i < kp ? id[i] : INT64_MAX;
+    __syncthreads();
+    float* stg = reinterpret_cast<float*>(smem);  // [256][RS_CW + 4]
+    for (int r0 = 0; r0 < kp; r0 += 256) {
+      const int nr = kp - r0 < 256 ? kp - r0 : 256;
+      double acc = 0.0;
+      for (int c0 = 0; c0 < d; c0 += RS_CW) {
+        const int cw = d - c0 < RS_CW ? d - c0 : RS_CW;
+#pragma unroll
+        for (int t = 0; t < RS_CW / 4; ++t) {
+          const int e = tid + 256 * t, row = e / (RS_CW / 4), c4 = e % (RS_CW / 4);
+          if (row < nr && 4 * c4 < cw)
+            *reinterpret_cast<float4*>(stg + row * (RS_CW + 4) + 4 * c4) =
+                *reinterpret_cast<const float4*>(xb + id2[r0 + row] * d + c0 + 4 * c4);
+        }
+        __syncthreads();
+        if (tid < nr) {
+          const float* xr = stg + tid * (RS_CW + 4);
+          for (int j = 0; j < cw; j += 4) {
+            const float4 v = *reinterpret_cast<const float4*>(xr + j);
+            const float xv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              if (l2) {
+                const double t = (double)qs[c0 + j + u] - (double)xv[u];
+                acc = fma(t, t, acc);
+              } else {
+                acc = fma((double)qs[c0 + j + u], (double)xv[u], acc);
+              }
+            }
+          }
+        }
+        __syncthreads();
+      }
+      if (tid < nr) g2[r0 + tid] = l2 ? -acc : acc;
+    }
+    for (int i = kp + tid; i < P2; i += 256) g2[i] = -INFINITY;
+  } else {
+    for (int i = tid; i < P2; i += 256) {
+      if (i < kp) {
+        const int64_t item = id[i];
+        const double s = exact_score(qs, xb + item * d, d, l2 != 0);
+        g2[i] = l2 ? -s : s;
+        id2[i] = item;
+      } else {
+        g2[i] = -INFINITY;
+        id2[i] = INT64_MAX;
+      }
     }
   }
   __syncthreads();
@@ -1544,7 +1595,9 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
   mark(2);
   {
     const int P = host_pow2ceil(p.U), P2 = host_pow2ceil(p.KP);
-    const size_t smem = (size_t)P * 16 + (size_t)P2 * 16 + (size_t)d * 4;
+    const size_t ub = p.KP < RS_MIN_KP || (size_t)P * 16 > (size_t)256 * (RS_CW + 4) * 4 ? (size_t)P * 16
+                                                                                            : (size_t)256 * (RS_CW + 4) * 4;
+    const size_t smem = ub + (size_t)P2 * 16 + (size_t)d * 4;
     if (smem > 150 * 1024) return fail(NRK_EUNSUPPORTED, "knn_flat: merge needs %zu B LDS", smem);
     hipLaunchKernelGGL(merge_rescore_kernel, dim3((unsigned)nq), dim3(256), smem, st, ps, pi, pt, p.nch, p.M, p.KP, k,
                        p.dp, xq, xb, nb, d, l2, qmeta, stats, p.tau ? tau : nullptr, D, I, S, id_offset, fb, nullptr);
