@@ -226,6 +226,100 @@ struct IvfFb {
   int nprobe;
 };
 
+// Top-kp selection for merge_rescore_kernel (256 threads, EPT union entries
+// per thread in registers): the kp best by (score desc, id asc) -> ids[0, kp)
+// (unordered; ids[kp, P2) = INT64_MAX), by a bisection on the order-preserving
+// keys of the float scores (32 block counts) instead of a bitonic sort of the
+// union; ties at the cut are taken by ascending id.  Returns the best score
+// left out (the old sorted g[kp]).  g / id (the union's LDS) are scratch.
+__device__ __forceinline__ uint32_t score_key(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key_score(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k ^ 0x80000000u) : ~k);
+}
+template <int EPT>
+__device__ float select_top(const double* rg, const int64_t* ri, const bool* rv, int kp, double* g, int64_t* id,
+                            int64_t* ids, int P2) {
+  __shared__ int cnt[2][4], csum[4];
+  __shared__ uint32_t kmax[4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  uint32_t key[EPT];
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) key[e] = rv[e] ? score_key((float)rg[e]) : 0u;  // valid keys are >= 1
+  auto block_count = [&](uint32_t c, bool strict, int buf) {
+    int n = 0;
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) n += __popcll(__ballot(strict ? key[e] > c : key[e] >= c));
+    if (lane == 0) cnt[buf][w] = n;
+    __syncthreads();
+    return cnt[buf][0] + cnt[buf][1] + cnt[buf][2] + cnt[buf][3];
+  };
+  uint32_t T = 0;  // the kp-th largest key
+  for (int bit = 31; bit >= 0; --bit) {
+    const uint32_t c = T | (1u << bit);
+    if (block_count(c, false, bit & 1) >= kp) T = c;
+  }
+  const int ngt = block_count(T, true, 1);  // (buffer 1: last written two barriers ago)
+  const int nge = block_count(T, false, 0);
+  const int r = kp - ngt;  // ties at T to take (>= 1)
+  // the id cut among the ties: all of them, or the r smallest ids
+  int64_t idcut = INT64_MAX;
+  if (nge - ngt > r) {
+    __shared__ int nt;
+    if (tid == 0) nt = 0;
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < EPT; ++e)
+      if (key[e] == T) {
+        const int o = atomicAdd(&nt, 1);
+        g[o] = 0.0;
+        id[o] = ri[e];
+      }
+    __syncthreads();
+    const int n2 = nt, P = pow2ceil(n2);
+    for (int i = n2 + tid; i < P; i += 256) {
+      g[i] = 0.0;
+      id[i] = INT64_MAX;
+    }
+    __syncthreads();
+    block_bitonic_sort(g, id, P);  // equal scores: ascending id
+    idcut = id[r - 1];
+    __syncthreads();
+  }
+  // compaction of the selected entries into ids[0, kp); the best key left out
+  int ns = 0;
+  uint32_t kout = 0;
+  bool sel[EPT];
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    sel[e] = key[e] > T || (key[e] == T && ri[e] <= idcut);
+    ns += sel[e] ? 1 : 0;
+    if (!sel[e] && rv[e]) kout = max(kout, key[e]);
+  }
+  int incl = ns;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) kout = max(kout, (uint32_t)__shfl_xor((int)kout, o, 64));
+  if (lane == 63) csum[w] = incl;
+  if (lane == 0) kmax[w] = kout;
+  __syncthreads();
+  int off = incl - ns;
+  for (int j = 0; j < w; ++j) off += csum[j];
+#pragma unroll
+  for (int e = 0; e < EPT; ++e)
+    if (sel[e]) ids[off++] = ri[e];
+  for (int i = kp + tid; i < P2; i += 256) ids[i] = INT64_MAX;
+  const uint32_t km = max(max(kmax[0], kmax[1]), max(kmax[2], kmax[3]));
+  __syncthreads();
+  return km ? key_score(km) : -INFINITY;
+}
+
 // One 256-thread workgroup per query.  Dynamic LDS: P doubles + P int64 (the
 // union; later the rescoring's row stage, at least 256 x (RS_CW + 4) floats),
 // P2 doubles + P2 int64 (rescored), d floats (query), reductions.
@@ -293,28 +387,39 @@ __global__ __launch_bounds__(256) void merge_rescore_kernel(
       id[off] = ri[e];
       ++off;
     }
+  // staged rescoring (many candidates): the top kp are SELECTED, not sorted
+  // (the exact scores are sorted afterwards anyway)
+  const bool staged = (d & 3) == 0 && KP >= RS_MIN_KP;
   const int PS = pow2ceil(V > 1 ? V : 1);
-  for (int i = V + tid; i < PS; i += 256) {
-    g[i] = -INFINITY;
-    id[i] = INT64_MAX;
-  }
+  if (!staged)
+    for (int i = V + tid; i < PS; i += 256) {
+      g[i] = -INFINITY;
+      id[i] = INT64_MAX;
+    }
   for (int o = 128; o > 0; o >>= 1) {  // (its first barrier also publishes the compaction)
     __syncthreads();
     if (tid < o) red[tid] = fmaxf(red[tid], red[tid + o]);
   }
   __syncthreads();
   const float theta_lanes = red[0];
-  block_bitonic_sort(g, id, PS);
   const int kp = KP < V ? KP : V;
-  double theta = fmax((double)theta_lanes, kp < V ? g[kp] : -INFINITY);
+  double theta = theta_lanes;
+  if (!staged) {
+    block_bitonic_sort(g, id, PS);
+    theta = fmax(theta, kp < V ? g[kp] : -INFINITY);
+  } else if (kp < V) {
+    theta = fmax(theta, (double)select_top<EPT>(rg, ri, rv, kp, g, id, id2, P2));
+  }
   if (tau_q) theta = fmax(theta, (double)tau_q[qi]);  // items below the bound were never kept
 
   // exact rescoring of the top kp screened candidates
-  if ((d & 3) == 0 && KP >= RS_MIN_KP) {
+  if (staged) {
     // lane = candidate row, fp64 in the oracle's serial order, rows staged
     // through LDS RS_CW columns at a time by coalesced loads (8 lanes per
     // 128-B row piece); the union's LDS is the stage (its ids moved to id2)
-    for (int i = tid; i < P2; i += 256) id2[i] = i < kp ? id[i] : INT64_MAX;
+    if (kp == V) {
+      for (int i = tid; i < P2; i += 256) id2[i] = i < kp ? id[i] : INT64_MAX;
+    }
     __syncthreads();
     float* stg = reinterpret_cast<float*>(smem);  // [256][RS_CW + 4]
     for (int r0 = 0; r0 < kp; r0 += 256) {
