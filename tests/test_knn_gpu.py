@@ -94,6 +94,20 @@ def test_duplicates_and_ties_take_lower_id(gpu):
     assert I[0].tolist() == [3, 5, 17000, 20001]
 
 
+@pytest.mark.parametrize("metric", [ko.METRIC_IP, ko.METRIC_L2])
+def test_k200_tied_block_at_the_selection_cut(gpu, metric):
+    """k = 200 (the merge SELECTS its 400 rescoring candidates by score keys):
+    900 exact copies of one row spread over the corpus tie at the cut, so the
+    tie rule (ascending id) decides which copies are rescored; results equal
+    the oracle's."""
+    xq, xb = _mixture(60_001, 64, 64, seed=11)
+    rng = np.random.default_rng(5)
+    dup = np.sort(rng.choice(np.arange(1, 60_001), 900, replace=False))
+    xb[dup] = xb[0]
+    xq[:8] = xb[0] * np.float32(1.5)
+    _check(xq, xb, 200, metric, gpu)
+
+
 def test_k_exceeds_ntotal_and_empty(gpu):
     from newsrecommend_amd import faiss as nf
 
