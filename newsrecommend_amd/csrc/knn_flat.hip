@@ -325,6 +325,7 @@ __device__ float select_top(const double* rg, const int64_t* ri, const bool* rv,
 // P2 doubles + P2 int64 (rescored), d floats (query), reductions.
 constexpr int RS_CW = 32;       // columns per rescoring stage (one 128-B line of each candidate row)
 constexpr int RS_MIN_KP = 128;  // staged rescoring from this many candidates (k = 5: lane-per-row loads)
+constexpr int SEL_MIN_KP = 0;   // top-KP by selection (else bitonic sort of the union) from this KP
 __global__ __launch_bounds__(256) void merge_rescore_kernel(
     const float* __restrict__ part_s, const int* __restrict__ part_i, const float* __restrict__ part_t,
     int nch, int M, int KP, int k, int dp, const float* __restrict__ xq, const float* __restrict__ xb,
@@ -390,8 +391,9 @@ __global__ __launch_bounds__(256) void merge_rescore_kernel(
   // staged rescoring (many candidates): the top kp are SELECTED, not sorted
   // (the exact scores are sorted afterwards anyway)
   const bool staged = (d & 3) == 0 && KP >= RS_MIN_KP;
+  const bool selected = staged || KP >= SEL_MIN_KP;
   const int PS = pow2ceil(V > 1 ? V : 1);
-  if (!staged)
+  if (!selected)
     for (int i = V + tid; i < PS; i += 256) {
       g[i] = -INFINITY;
       id[i] = INT64_MAX;
@@ -404,11 +406,14 @@ __global__ __launch_bounds__(256) void merge_rescore_kernel(
   const float theta_lanes = red[0];
   const int kp = KP < V ? KP : V;
   double theta = theta_lanes;
-  if (!staged) {
+  if (!selected) {
     block_bitonic_sort(g, id, PS);
     theta = fmax(theta, kp < V ? g[kp] : -INFINITY);
   } else if (kp < V) {
     theta = fmax(theta, (double)select_top<EPT>(rg, ri, rv, kp, g, id, id2, P2));
+  } else {
+    for (int i = tid; i < P2; i += 256) id2[i] = i < kp ? id[i] : INT64_MAX;
+    __syncthreads();
   }
   if (tau_q) theta = fmax(theta, (double)tau_q[qi]);  // items below the bound were never kept
 
@@ -417,10 +422,6 @@ __global__ __launch_bounds__(256) void merge_rescore_kernel(
     // lane = candidate row, fp64 in the oracle's serial order, rows staged
     // through LDS RS_CW columns at a time by coalesced loads (8 lanes per
     // 128-B row piece); the union's LDS is the stage (its ids moved to id2)
-    if (kp == V) {
-      for (int i = tid; i < P2; i += 256) id2[i] = i < kp ? id[i] : INT64_MAX;
-    }
-    __syncthreads();
     float* stg = reinterpret_cast<float*>(smem);  // [256][RS_CW + 4]
     for (int r0 = 0; r0 < kp; r0 += 256) {
       const int nr = kp - r0 < 256 ? kp - r0 : 256;
@@ -459,7 +460,7 @@ __global__ __launch_bounds__(256) void merge_rescore_kernel(
   } else {
     for (int i = tid; i < P2; i += 256) {
       if (i < kp) {
-        const int64_t item = id[i];
+        const int64_t item = selected ? id2[i] : id[i];
         const double s = exact_score(qs, xb + item * d, d, l2 != 0);
         g2[i] = l2 ? -s : s;
         id2[i] = item;
