@@ -286,11 +286,12 @@ __global__ __launch_bounds__(256, 2) void din_fwd_wave_kernel(const uint16_t* __
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int r = lane & 31, h = lane >> 5;
-  const int Lp = (L + 31) & ~31, nct = Lp >> 5;
-  // LDS: w2 [AP] (shared) | per wave, NBUF slots of {U row [AP] f32, key image [Lp][D] bf16}
+  const int Lp = (L + 31) & ~31;
+  // LDS: w2 [AP] (shared) | per wave, NBUF slots of {U row [AP] f32, key image [Lp][D] bf16} | ids [4][128]
   const int slot_f = AP + Lp * D / 2;  // floats per slot
   float* w2s = reinterpret_cast<float*>(smem);
   float* wbase = w2s + AP + (size_t)wv * NBUF * slot_f;
+  int32_t* idtab = reinterpret_cast<int32_t*>(w2s + AP + 4 * (size_t)NBUF * slot_f) + wv * 128;  // [128] per wave
   typedef __attribute__((address_space(3))) void* lds_ptr;
   for (int i = threadIdx.x; i < A; i += 256) w2s[i] = w2[i];
   __syncthreads();
@@ -303,22 +304,33 @@ __global__ __launch_bounds__(256, 2) void din_fwd_wave_kernel(const uint16_t* __
       wf[t][s] = *reinterpret_cast<const bf16x8*>(W1k + (int64_t)(32 * t + r) * D + 16 * s + 8 * h);
 
   const int nw = gridDim.x * 4;
-  auto load_ids = [&](int b, int32_t& i0, int32_t& i1) {
+  // ids of sample b's slots (lane, 64 + lane) and the wave-uniform masks of
+  // its valid slots (padding slots hold zero keys and share one logit)
+  auto load_ids = [&](int b, int32_t& i0, int32_t& i1, uint64_t& v0, uint64_t& v1) {
     i0 = (b < B && lane < L) ? ids[(int64_t)b * L + lane] : -1;
     i1 = (b < B && lane + 64 < L) ? ids[(int64_t)b * L + lane + 64] : -1;
+    v0 = __ballot(i0 >= 0 && i0 < n_table);
+    v1 = __ballot(i1 >= 0 && i1 < n_table);
   };
-  // gather sample b's key rows + U row into slot `sl` (asynchronous LDS-DMA)
-  auto issue = [&](int b, int sl, int32_t i0, int32_t i1) {
+  // gather sample b's key rows, valid slots first (compacted row j <- the
+  // (j+1)-th valid slot), zero rows after, + U row into slot `sl` (LDS-DMA);
+  // only the 32-row tiles holding the valid rows and the padding row
+  auto issue = [&](int b, int sl, int32_t i0, int32_t i1, uint64_t v0, uint64_t v1) {
     float* us = wbase + sl * slot_f;
     uint16_t* img = reinterpret_cast<uint16_t*>(us + AP);
-    const int npieces = Lp * CPR / 64;
+    const int n0 = __popcll(v0), nv = n0 + __popcll(v1);
+    const int ntile = (nv + (nv < L ? 1 : 0) + 31) >> 5;
+    const int npieces = 32 * ntile * CPR / 64;
+    {  // compacted id table of this wave (LDS operations of one wave complete in order)
+      const uint64_t below = (1ull << lane) - 1;
+      if ((v0 >> lane) & 1) idtab[__popcll(v0 & below)] = i0;
+      if ((v1 >> lane) & 1) idtab[n0 + __popcll(v1 & below)] = i1;
+    }
     for (int u = 0; u < npieces; ++u) {
       const int p = u * 64 + lane;
       const int row = p / CPR, pc = p % CPR;
       const int cc = pc ^ kswz<CPR>(row);
-      const int ida = __shfl(i0, row & 63, 64), idb = __shfl(i1, row & 63, 64);  // both: source lanes differ
-      const int idr = row < 64 ? ida : idb;
-      const uint16_t* src = (row < L && idr >= 0 && idr < n_table) ? table + (int64_t)idr * D + cc * 8 : zero_row(b, row) + cc * 8;
+      const uint16_t* src = row < nv ? table + (int64_t)idtab[row] * D + cc * 8 : zero_row(b, row) + cc * 8;
       __builtin_amdgcn_global_load_lds(src, (lds_ptr)(img + u * 64 * 8), 16, 0, 0);
     }
 #pragma unroll
@@ -330,16 +342,24 @@ __global__ __launch_bounds__(256, 2) void din_fwd_wave_kernel(const uint16_t* __
 
   int b = blockIdx.x * 4 + wv;
   int32_t c0, c1, n0 = -1, n1 = -1;
-  load_ids(b, c0, c1);
-  if (b < B) issue(b, 0, c0, c1);
-  if (NBUF == 2) load_ids(b + nw, n0, n1);
+  uint64_t cv0, cv1, nv0 = 0, nv1 = 0;
+  load_ids(b, c0, c1, cv0, cv1);
+  if (b < B) issue(b, 0, c0, c1, cv0, cv1);
+  if (NBUF == 2) load_ids(b + nw, n0, n1, nv0, nv1);
   int sl = 0;
   for (; b < B; b += nw) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this sample's rows (and the next ids) landed
     const int bn = b + nw;
+    // this sample: compacted valid rows [0, nv), the padding row nv (zero
+    // key, npad = L - nv slots) when nv < L, nct tiles of 32 rows
+    const uint64_t sv0 = cv0, sv1 = cv1;
+    const int sn0 = __popcll(sv0), nv = sn0 + __popcll(sv1), npad = L - nv, nr = nv + (npad > 0 ? 1 : 0);
+    const int nct = (nr + 31) >> 5;
     if constexpr (NBUF == 2) {
-      if (bn < B) issue(bn, sl ^ 1, n0, n1);
-      load_ids(bn + nw, n0, n1);
+      if (bn < B) issue(bn, sl ^ 1, n0, n1, nv0, nv1);
+      cv0 = nv0;
+      cv1 = nv1;
+      load_ids(bn + nw, n0, n1, nv0, nv1);
     }
     const float* us = wbase + sl * slot_f;
     const uint16_t* img = reinterpret_cast<const uint16_t*>(us + AP);
@@ -377,31 +397,47 @@ __global__ __launch_bounds__(256, 2) void din_fwd_wave_kernel(const uint16_t* __
           }
         }
         part += __shfl_xor(part, 32, 64);
-        sc[c] = (row < L) ? part : -INFINITY;
+        sc[c] = (row < nr) ? part : -INFINITY;
       }
     }
-    // ---- softmax over the L rows (padding rows of the history included)
+    // ---- softmax over the L slots (DIN.py:108, padding included): rows < nv
+    // once each, the padding row nv for its npad slots
     float m = fmaxf(fmaxf(sc[0], sc[1]), fmaxf(sc[2], sc[3]));
     m = wave_max(m);
     float e[4], sum = 0.f;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      e[c] = c < nct && 32 * c + r < L ? expf(sc[c] - m) : 0.f;
-      sum += h == 0 ? e[c] : 0.f;
+      const int row = 32 * c + r;
+      e[c] = c < nct && row < nr ? expf(sc[c] - m) : 0.f;
+      sum += h == 0 ? (row < nv ? e[c] : (float)npad * e[c]) : 0.f;
     }
     sum = wave_sum(sum);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      e[c] = e[c] / sum;
-      if (h == 0 && c < nct && 32 * c + r < L) alpha[(int64_t)b * L + 32 * c + r] = e[c];
+    for (int c = 0; c < 4; ++c) e[c] = e[c] / sum;
+    {  // alpha in slot order: a valid slot's compacted row, or the padding row
+      auto erow = [&](int row) {
+        float v = 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float t = __shfl(e[c], row & 31, 64);
+          if ((row >> 5) == c) v = t;
+        }
+        return v;
+      };
+      const uint64_t below = (1ull << lane) - 1;
+      const bool ok0 = (sv0 >> lane) & 1, ok1 = (sv1 >> lane) & 1;
+      const float a0 = erow(ok0 ? __popcll(sv0 & below) : nv);
+      const float a1 = erow(ok1 ? sn0 + __popcll(sv1 & below) : nv);
+      if (lane < L) alpha[(int64_t)b * L + lane] = a0;
+      if (64 + lane < L) alpha[(int64_t)b * L + 64 + lane] = a1;
     }
-    // ---- pooled = sum_rows alpha[row] K[row][:]
-    // rows in groups of 8 up to round_up(L, 8) <= Lp: rows >= L are zero rows
-    // with alpha 0, so the 8 LDS reads of a group issue back to back
+    // ---- pooled = sum_rows alpha[row] K[row][:] over the valid rows
+    // rows in groups of 8 up to round_up(nv, 8) <= 32 nct: rows >= nv are zero
+    // rows, so the 8 LDS reads of a group issue back to back
     float acc2[DPL];
 #pragma unroll
     for (int j = 0; j < DPL; ++j) acc2[j] = 0.f;
-    const int L8 = (L + 7) & ~7;
+    const int L8 = (nv + 7) & ~7;
     for (int row0 = 0; row0 < L8; row0 += 8) {
       const int c = row0 >> 5;
       const float ec = c == 0 ? e[0] : c == 1 ? e[1] : c == 2 ? e[2] : e[3];
@@ -436,8 +472,8 @@ __global__ __launch_bounds__(256, 2) void din_fwd_wave_kernel(const uint16_t* __
     if constexpr (NBUF == 2) {
       sl ^= 1;
     } else {
-      load_ids(bn, c0, c1);
-      if (bn < B) issue(bn, 0, c0, c1);
+      load_ids(bn, c0, c1, cv0, cv1);
+      if (bn < B) issue(bn, 0, c0, c1, cv0, cv1);
     }
   }
 }
@@ -1674,7 +1710,7 @@ extern "C" int nrk_din_attn_fwd(const void* keys, const int32_t* hist_ids, int64
     const size_t slot = AP * 4 + (size_t)Lp * d * 2;
     // single-buffered slots, two workgroups per CU: measured faster than
     // double-buffered ones at one per CU (41 vs 51 us at B=4096, L=50, d=128)
-    const size_t wsm = AP * 4 + 4 * slot;
+    const size_t wsm = AP * 4 + 4 * slot + 4 * 128 * 4;  // + the waves' compacted id tables
     int grid = (int)cdiv(B, 4);
     if (grid > 512) grid = 512;
     const uint16_t* tb = static_cast<const uint16_t*>(keys);

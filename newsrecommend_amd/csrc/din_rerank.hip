@@ -62,20 +62,6 @@ constexpr size_t smem_bytes() {
   return (size_t)LP * D * 2 + (size_t)LP * A * 4 + (size_t)CPB * SST * 4 + A * 4;
 }
 
-// Position of the (j+1)-th set bit of m (j < popcount(m)).
-__device__ __forceinline__ int nth_set_bit(uint64_t m, int j) {
-  int pos = 0;
-#pragma unroll
-  for (int half = 32; half > 0; half >>= 1) {
-    const int c = __popcll((m >> pos) & ((1ull << half) - 1));
-    if (j >= c) {
-      j -= c;
-      pos += half;
-    }
-  }
-  return pos;
-}
-
 // History of user u: slot ids (lane = slot), the wave-uniform valid mask, and
 // this thread's share of the compacted image rows (row (tid + NT k) / CPR,
 // 16 B column chunk (tid + NT k) % CPR), loads issued, zeros past nv.

@@ -79,6 +79,21 @@ __device__ inline float wave_max(float v) {
   return v;
 }
 
+// Position of the (j+1)-th set bit of m (j < popcount(m)): history slot of
+// compacted row j (the DIN kernels score valid rows first, padding once).
+__device__ __forceinline__ int nth_set_bit(uint64_t m, int j) {
+  int pos = 0;
+#pragma unroll
+  for (int half = 32; half > 0; half >>= 1) {
+    const int c = __popcll((m >> pos) & ((1ull << half) - 1));
+    if (j >= c) {
+      j -= c;
+      pos += half;
+    }
+  }
+  return pos;
+}
+
 // --------------------------------------------------- ordering (k-NN) --
 // "goodness" g: larger is better.  IP: g = score; L2: g = -distance.
 // Ties on g break toward the lower id.
