@@ -22,7 +22,8 @@
 //      (XOR-swizzled, zero rows past nv),
 //   2. P = K W1k^T on bf16 MFMA (wave w: units 32w..32w+31) -> LDS, row-major,
 //   3. each lane holds its candidate's U slice in registers; per history row
-//      the P row and w2 are broadcast LDS reads: packed add, max, packed fma —
+//      the P row is a broadcast LDS read and w2 sits in SGPRs (scalar loads of
+//      the pass's 64 units): packed add, max, packed fma —
 //      2 VALU per (candidate, row, unit); logits -> the lane's LDS row S[c][.];
 //      two waves per 64-candidate group split the rows (8 waves, 2 per SIMD),
 //   4. per-lane softmax over S[c][0..nr), alpha split hi + lo bf16, stored as
@@ -59,7 +60,7 @@ typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
 
 template <int D, int A>
 constexpr size_t smem_bytes() {
-  return (size_t)LP * D * 2 + (size_t)LP * A * 4 + (size_t)CPB * SST * 4 + A * 4;
+  return (size_t)LP * D * 2 + (size_t)LP * A * 4 + (size_t)CPB * SST * 4;
 }
 
 // History of user u: slot ids (lane = slot), the wave-uniform valid mask, and
@@ -100,11 +101,9 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(const uint16_t* __res
   unsigned char* img = smem;                                          // [LP][D] bf16
   float* Ps = reinterpret_cast<float*>(smem + LP * D * 2);            // [LP][A]
   float* S = Ps + LP * A;                                             // [CPB][SST]
-  float* w2s = S + CPB * SST;                                         // [A]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, r = lane & 31;
   const int cw = w & 3, hw = w >> 2;  // candidate group (64 lanes) and its share (row pairs / dim tiles)
   float* Sl = S + (64 * cw + lane) * SST;  // this lane's candidate row; [64 + hw] partial max, [66 + hw] partial sum
-  for (int i = tid; i < A; i += NT) w2s[i] = w2[i];
 
   HistRows<D> cur, nxt;
   if (blockIdx.x < nU) cur.load(table, n_table, hist, blockIdx.x, L, tid);
@@ -168,7 +167,7 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(const uint16_t* __res
           for (int j = 0; j < UH / 4; ++j) {
             const float4 q0 = *reinterpret_cast<const float4*>(p0 + 4 * j);
             const float4 q1 = *reinterpret_cast<const float4*>(p0 + A + 4 * j);
-            const float4 wv = *reinterpret_cast<const float4*>(w2s + n0 + 4 * j);
+            const float4 wv = *reinterpret_cast<const float4*>(w2 + n0 + 4 * j);  // uniform: scalar loads
             const f2 wa = {wv.x, wv.y}, wb = {wv.z, wv.w};
             const f2 z = {0.f, 0.f};
             a00 = __builtin_elementwise_fma(wa, __builtin_elementwise_max(ua[2 * j] + f2{q0.x, q0.y}, z), a00);
