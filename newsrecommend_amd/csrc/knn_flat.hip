@@ -68,8 +68,12 @@ __global__ void flat_prepare_kernel(const float* __restrict__ xb, int64_t nb, in
 
 // qmeta[4*q] = {||q^|| (up), ||q - q^|| (up), ||q||^2, 0}
 __global__ void query_prepare_kernel(const float* __restrict__ xq, int64_t nq, int64_t nq_pad, int d,
-                                     int dp, uint16_t* __restrict__ qh, double* __restrict__ qmeta) {
+                                     int dp, uint16_t* __restrict__ qh, double* __restrict__ qmeta,
+                                     int* __restrict__ zero4 = nullptr, int* __restrict__ zero2 = nullptr) {
   const int lane = threadIdx.x & 63;
+  // the search's fallback counters (instead of two memset launches)
+  if (blockIdx.x == 0 && threadIdx.x < 4 && zero4) zero4[threadIdx.x] = 0;
+  if (blockIdx.x == 0 && threadIdx.x < 2 && zero2) zero2[threadIdx.x] = 0;
   const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (row >= nq_pad) return;
   double sq2 = 0.0, sh2 = 0.0, sr2 = 0.0;
@@ -510,7 +514,15 @@ __global__ __launch_bounds__(256) void merge_rescore_kernel(
 __global__ __launch_bounds__(256) void exact_topk_kernel(
     const float* __restrict__ xq, int64_t nq, const float* __restrict__ xb, int64_t nb, int d, int k,
     int l2, const int* __restrict__ qlist, const int* __restrict__ qcount, float* __restrict__ D,
-    int64_t* __restrict__ I, double* __restrict__ S, int64_t id_offset, IvfFb iv) {
+    int64_t* __restrict__ I, double* __restrict__ S, int64_t id_offset, IvfFb iv,
+    int* __restrict__ cnt_out = nullptr, const int* __restrict__ cnt_a = nullptr,
+    const int* __restrict__ cnt_b = nullptr) {
+  // the search's fallback counts (final: written by earlier launches) -> the
+  // caller's n_fallback (instead of two copy launches)
+  if (cnt_out && blockIdx.x == 0 && threadIdx.x == 0) {
+    cnt_out[0] = *cnt_a;
+    cnt_out[1] = *cnt_b;
+  }
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int P = pow2ceil(k + 256);
   double* g = reinterpret_cast<double*>(smem);
@@ -1581,14 +1593,15 @@ static int small_launch(const FlatPlan& p, const float* xq, int64_t nq, const fl
 
 static int exact_launch(const float* xq, int64_t nq, const float* xb, int64_t nb, int d, int k, int l2,
                         const int* qlist, const int* qcount, int64_t max_work, float* D, int64_t* I,
-                        double* S, int64_t id_offset, hipStream_t st, IvfFb iv = IvfFb{}) {
+                        double* S, int64_t id_offset, hipStream_t st, IvfFb iv = IvfFb{},
+                        int* cnt_out = nullptr, const int* cnt_a = nullptr, const int* cnt_b = nullptr) {
   const int P = host_pow2ceil(k + 256);
   const size_t smem = (size_t)P * 16 + (size_t)d * 4;
   if (smem > 160 * 1024) return fail(NRK_EUNSUPPORTED, "exact search: k=%d d=%d needs %zu B of LDS", k, d, smem);
   int grid = (int)(max_work < 2048 ? max_work : 2048);
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(exact_topk_kernel, dim3(grid), dim3(256), smem, st, xq, nq, xb, nb, d, k, l2, qlist, qcount,
-                     D, I, S, id_offset, iv);
+                     D, I, S, id_offset, iv, cnt_out, cnt_a, cnt_b);
   NRK_CHECK_LAUNCH("exact_topk_kernel");
   return NRK_OK;
 }
@@ -1640,9 +1653,14 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
   NRK_CHECK_ARG(ws != nullptr, "knn_flat: null workspace");
   char* w = static_cast<char*>(ws);
   int* fbc = reinterpret_cast<int*>(w + p.off_fbc);
-  if (hipMemsetAsync(fbc, 0, 16, st) != hipSuccess) return fail(NRK_ELAUNCH, "knn_flat: memset failed");
-  if (n_fallback && hipMemsetAsync(n_fallback, 0, 8, st) != hipSuccess)
-    return fail(NRK_ELAUNCH, "knn_flat: memset failed");
+  // the screened path zeroes its counters in query_prepare_kernel and publishes
+  // them from exact_topk_kernel; the other paths use memsets
+  const bool fused_counts = nq > 0 && !p.small && !p.exact_only;
+  if (!fused_counts) {
+    if (hipMemsetAsync(fbc, 0, 16, st) != hipSuccess) return fail(NRK_ELAUNCH, "knn_flat: memset failed");
+    if (n_fallback && hipMemsetAsync(n_fallback, 0, 8, st) != hipSuccess)
+      return fail(NRK_ELAUNCH, "knn_flat: memset failed");
+  }
   if (nq == 0) return NRK_OK;
   NRK_CHECK_ARG(xq && D && I && (xb || nb == 0), "knn_flat: null pointer");
   const int l2 = metric == NRK_METRIC_L2;
@@ -1681,7 +1699,7 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
 
   mark(0);
   hipLaunchKernelGGL(query_prepare_kernel, dim3((unsigned)cdiv(p.nq_pad, 4)), dim3(256), 0, st, xq, nq, p.nq_pad, d,
-                     p.dp, qh, qmeta);
+                     p.dp, qh, qmeta, fbc, n_fallback);
   NRK_CHECK_LAUNCH("query_prepare_kernel");
   if (p.tau) {
     screen_fn pf = p.waves == 8 ? pick_screen_dp256_w8(p.M, l2 != 0, 1) : pick_screen(p.dp, p.qt, p.M, l2 != 0, 1);
@@ -1753,12 +1771,10 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
                        p.fb_cap, k, l2, D, I, S, id_offset, ovl);
     NRK_CHECK_LAUNCH("fallback_select_kernel");
   }
-  int rc = exact_launch(xq, nq, xb, nb, d, k, l2, ovl, fbc + 1, 256, D, I, S, id_offset, st);
+  int rc = exact_launch(xq, nq, xb, nb, d, k, l2, ovl, fbc + 1, 256, D, I, S, id_offset, st, IvfFb{}, n_fallback,
+                        reinterpret_cast<const int*>(w + p.off_ccount + 4), fbc);
   if (rc != NRK_OK) return rc;
   mark(4);
-  if (n_fallback && (hipMemcpyAsync(n_fallback, w + p.off_ccount + 4, 4, hipMemcpyDeviceToDevice, st) != hipSuccess ||
-                     hipMemcpyAsync(n_fallback + 1, fbc, 4, hipMemcpyDeviceToDevice, st) != hipSuccess))
-    return fail(NRK_ELAUNCH, "knn_flat: copy of fallback counts failed");
   return NRK_OK;
 }
 
