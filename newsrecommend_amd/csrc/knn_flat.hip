@@ -243,6 +243,64 @@ __device__ __forceinline__ uint32_t score_key(float f) {
 __device__ __forceinline__ float key_score(uint32_t k) {
   return __uint_as_float((k & 0x80000000u) ? (k ^ 0x80000000u) : ~k);
 }
+// The same selection for a union of at most 64 NK entries (U <= 1024): the
+// keys and ids go to LDS, then wave 0 alone runs the bisection with wave
+// ballots over NK keys per lane (no block barrier per round); ties at the cut
+// are taken in slot order (deterministic; any choice keeps the certificate,
+// which bounds every left-out item by the best left-out score, returned).
+template <int NK, int EPT>
+__device__ float select_top_wave(const double* rg, const int64_t* ri, const bool* rv, int U, int kp,
+                                 uint32_t* kbuf, int64_t* ibuf, int64_t* ids, int P2) {
+  __shared__ float s_out;
+  const int tid = threadIdx.x, lane = tid & 63;
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    const int i = tid + 256 * e;
+    if (i < U) {
+      kbuf[i] = rv[e] ? score_key((float)rg[e]) : 0u;  // valid keys are >= 1
+      ibuf[i] = ri[e];
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {
+    uint32_t kk[NK];
+#pragma unroll
+    for (int j = 0; j < NK; ++j) kk[j] = lane + 64 * j < U ? kbuf[lane + 64 * j] : 0u;
+    uint32_t T = 0;  // the kp-th largest key
+    for (int bit = 31; bit >= 0; --bit) {
+      const uint32_t c = T | (1u << bit);
+      int n = 0;
+#pragma unroll
+      for (int j = 0; j < NK; ++j) n += __popcll(__ballot(kk[j] >= c));
+      if (n >= kp) T = c;
+    }
+    int ngt = 0;
+#pragma unroll
+    for (int j = 0; j < NK; ++j) ngt += __popcll(__ballot(kk[j] > T));
+    int ties = kp - ngt, off = 0;  // ties at T still to take; output offset
+    const uint64_t below = (1ull << lane) - 1;
+    uint32_t kout = 0;
+#pragma unroll
+    for (int j = 0; j < NK; ++j) {
+      const uint64_t eq = __ballot(kk[j] == T);
+      const int rank = __popcll(eq & below);  // ties before this slot in this group
+      const bool sel = kk[j] > T || (kk[j] == T && rank < ties);
+      const uint64_t sm = __ballot(sel);
+      if (sel) ids[off + __popcll(sm & below)] = ibuf[lane + 64 * j];
+      if (!sel && kk[j] > kout) kout = kk[j];
+      off += __popcll(sm);
+      const int te = __popcll(eq);
+      ties -= te < ties ? te : ties;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) kout = max(kout, (uint32_t)__shfl_xor((int)kout, o, 64));
+    if (lane == 0) s_out = kout ? key_score(kout) : -INFINITY;
+  }
+  for (int i = kp + tid; i < P2; i += 256) ids[i] = INT64_MAX;
+  __syncthreads();
+  return s_out;
+}
+
 template <int EPT>
 __device__ float select_top(const double* rg, const int64_t* ri, const bool* rv, int kp, double* g, int64_t* id,
                             int64_t* ids, int P2) {
@@ -330,6 +388,14 @@ __device__ float select_top(const double* rg, const int64_t* ri, const bool* rv,
 constexpr int RS_CW = 32;       // columns per rescoring stage (one 128-B line of each candidate row)
 constexpr int RS_MIN_KP = 128;  // staged rescoring from this many candidates (k = 5: lane-per-row loads)
 constexpr int SEL_MIN_KP = 0;   // top-KP by selection (else bitonic sort of the union) from this KP
+// bytes of the merge's union region: the union (P doubles + P ids), the
+// rescoring stage, or the small selection's 256 keys + 256 ids
+__host__ __device__ inline int merge_union_bytes(int P, int KP) {
+  int ub = 16 * P;
+  if (KP >= RS_MIN_KP && ub < 256 * (RS_CW + 4) * 4) ub = 256 * (RS_CW + 4) * 4;
+  if (ub < 12 * P + 16) ub = 12 * P + 16;  // the wave selection: P keys + P ids (P >= U)
+  return ub;
+}
 __global__ __launch_bounds__(256) void merge_rescore_kernel(
     const float* __restrict__ part_s, const int* __restrict__ part_i, const float* __restrict__ part_t,
     int nch, int M, int KP, int k, int dp, const float* __restrict__ xq, const float* __restrict__ xb,
@@ -342,7 +408,7 @@ __global__ __launch_bounds__(256) void merge_rescore_kernel(
   double* g = reinterpret_cast<double*>(smem);
   int64_t* id = reinterpret_cast<int64_t*>(g + P);
   const int P2 = pow2ceil(KP);
-  const int UB = KP < RS_MIN_KP || 16 * P > 256 * (RS_CW + 4) * 4 ? 16 * P : 256 * (RS_CW + 4) * 4;  // union / stage
+  const int UB = merge_union_bytes(P, KP);  // union / stage / small selection
   double* g2 = reinterpret_cast<double*>(smem + UB);
   int64_t* id2 = reinterpret_cast<int64_t*>(g2 + P2);
   float* qs = reinterpret_cast<float*>(id2 + P2);
@@ -414,7 +480,13 @@ __global__ __launch_bounds__(256) void merge_rescore_kernel(
     block_bitonic_sort(g, id, PS);
     theta = fmax(theta, kp < V ? g[kp] : -INFINITY);
   } else if (kp < V) {
-    theta = fmax(theta, (double)select_top<EPT>(rg, ri, rv, kp, g, id, id2, P2));
+    uint32_t* kb = reinterpret_cast<uint32_t*>(smem);
+    int64_t* ib = reinterpret_cast<int64_t*>(smem + 4 * P);
+    const float left = U <= 256 ? select_top_wave<4, EPT>(rg, ri, rv, U, kp, kb, ib, id2, P2)
+                       : U <= 512 ? select_top_wave<8, EPT>(rg, ri, rv, U, kp, kb, ib, id2, P2)
+                       : U <= 1024 ? select_top_wave<16, EPT>(rg, ri, rv, U, kp, kb, ib, id2, P2)
+                                   : select_top<EPT>(rg, ri, rv, kp, g, id, id2, P2);
+    theta = fmax(theta, (double)left);
   } else {
     for (int i = tid; i < P2; i += 256) id2[i] = i < kp ? id[i] : INT64_MAX;
     __syncthreads();
@@ -1723,8 +1795,7 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
   mark(2);
   {
     const int P = host_pow2ceil(p.U), P2 = host_pow2ceil(p.KP);
-    const size_t ub = p.KP < RS_MIN_KP || (size_t)P * 16 > (size_t)256 * (RS_CW + 4) * 4 ? (size_t)P * 16
-                                                                                            : (size_t)256 * (RS_CW + 4) * 4;
+    const size_t ub = (size_t)merge_union_bytes(P, p.KP);
     const size_t smem = ub + (size_t)P2 * 16 + (size_t)d * 4;
     if (smem > 150 * 1024) return fail(NRK_EUNSUPPORTED, "knn_flat: merge needs %zu B LDS", smem);
     hipLaunchKernelGGL(merge_rescore_kernel, dim3((unsigned)nq), dim3(256), smem, st, ps, pi, pt, p.nch, p.M, p.KP, k,
