@@ -1474,7 +1474,14 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
   // screen 17.4 -> 15.0 ms) and, at k = 200, a chunk far larger than L2
   // re-read by half as many query tiles
   if (p.dp == 256 && (p.M == 4 || p.M == 16)) p.waves = 8;
-  p.R = k <= 8 ? 16 : 2 * k;
+  // R: tau bounds the R-th best screened score from the pre-pass's lane maxima
+  // (every stride-th tile), so it sits near global rank ~stride * R; the main
+  // pass then admits ~stride * R items per query (list insertions, the VALU
+  // cost of the k = 200 screen).  k > 8: R = k / 4 and stride * R >= 4k (below
+  // that a few queries per thousand are uncertified: 1M x 128 k = 100 at 2k:
+  // 36 of 4096).  Measured at 10M x 256 k = 200 (stride 16): screen 19.05 ms at
+  // R = 2k -> 16.83; 1.25M x 256, 32768 queries: total 38.4 -> 29.2 ms.
+  p.R = k <= 8 ? 16 : (k / 4 > 16 ? k / 4 : 16);
   p.tau = true;  // k = 200 at 10M x 256: -5% retrieve time
   if (p.dp == 256) p.qt = 1;
   p.wq = p.waves * 32 * p.qt;
@@ -1486,14 +1493,15 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
   // pre-pass stride: the pre-pass costs ~nb / stride per query, the main pass
   // admits ~stride * R items above tau per query (list insertions); the best
   // stride grows like sqrt(nb / R): the power of two >= 8 sqrt(nb/1M * 16/R),
-  // in [2, 64].  Measured (IP, per GPU): 1M x 128 k = 5 -> 8; 10M x 256 k = 5
-  // -> 32 (total 17.0 -> 15.8 ms vs 8); 10M x 256 k = 200 -> 8 (4: +0.8 ms,
-  // 16: +1.3 ms); the 8-GPU shards: 1.25M x 256 k = 200, 32768 queries -> 2
-  // (52.6 -> 37.0 ms vs 8), 125K x 128 k = 5, 32768 queries -> 4 (-7 %)
+  // in [2, 64] (and stride * R >= 4k, above).  Measured (IP, per GPU): 1M x 128
+  // k = 5 -> 8; 10M x 256 k = 5 -> 32 (total 17.0 -> 15.8 ms vs 8); 125K x 128
+  // k = 5, 32768 queries -> 4 (-7 %)
   {
     const double want = 8.0 * sqrt((double)nb / 1e6 * 16.0 / p.R);
     int st = 2;
     while (st < 64 && st < want) st *= 2;
+    if (k > 8)
+      while (st < 64 && (int64_t)st * p.R < 4 * (int64_t)k) st *= 2;
     p.tstride = st;
   }
   int target = p.M >= 16 ? 2048 : 1024;

@@ -26,6 +26,7 @@ grid = [[(v.split("=")[0], x) for x in v.split("=")[1].split(",")] for v in a.va
 combos = list(itertools.product(*grid))
 ref = None
 res = {c: [] for c in combos}
+fbs = {c: 0 for c in combos}
 for r in range(a.rounds):
     for c in combos:
         for k, v in c:
@@ -40,8 +41,10 @@ for r in range(a.rounds):
             ref = I.clone()
         ok = "" if ref is None else ("ok" if torch.equal(I, ref) else "DIFF")
         fb = int(idx.last_fallback.item())
+        fbs[c] = max(fbs[c], fb)
         print(f"round {r} {c}: stages ms {np.round(st, 4).tolist()} fallback={fb} {ok}", flush=True)
 for c in combos:
     m = np.median(np.array(res[c]), 0)
     flops = 2.0 * a.nq * a.nb * a.d
-    print(f"{c}: screen {m[1]:.4f} ms = {flops / m[1] / 1e9:.1f} TFLOP/s; merge {m[2]:.4f}; total {m.sum():.4f}")
+    print(f"{c}: screen {m[1]:.4f} ms = {flops / m[1] / 1e9:.1f} TFLOP/s; merge {m[2]:.4f}; total {m.sum():.4f}; "
+          f"stages {np.round(m, 4).tolist()}; fallback {fbs[c]}; id checksum {int(ref.sum())}")
