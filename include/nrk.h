@@ -287,6 +287,35 @@ int nrk_clip_adam(float* params, float* grads, float* exp_avg, float* exp_avg_sq
 int nrk_gather_rows(const void* table, int64_t n_table, int32_t dtype, const int32_t* ids,
                     int64_t n, int32_t d, float* out, void* stream);
 
+/* ------------------------------------------------------------------------- *
+ * Typed click logs (HOST memory, no stream): the training-row builders.
+ * A click log is CSR: user u's clicks are click_rows[click_off[u] ..
+ * click_off[u+1]) (oldest -> newest), as row indices into the article list the
+ * reference draws negatives from (list(article_emb.keys()) order).
+ * rng_state [625] is Python's random.getstate()[1] (624 Mersenne Twister words
+ * + position), read and written back advanced: the negatives are the ones
+ * `random.choice` draws in the reference loop, so the rows are identical.
+ * A user whose clicks cover every item returns NRK_EINVAL (the reference's
+ * rejection loop would not terminate). */
+
+/* Replaces TrainDataset.__init__ (DIN.py:66-76): per user with >= 2 clicks and
+ * click i >= 1, a positive row (target clicks[i], label 1) then a negative row
+ * (label 0), both with history clicks[:i][-max_history:].
+ *   n_samples must be 2 * sum(max(len_u - 1, 0));
+ *   user_idx, target_rows int32 [n_samples], labels f32 [n_samples];
+ *   hist_rows int32 [n_samples][max_history] (-1 padded) or NULL. */
+int nrk_train_samples(const int64_t* click_off, int64_t n_users, const int32_t* click_rows,
+                      int64_t n_items, int32_t max_history, uint32_t* rng_state, int64_t n_samples,
+                      int32_t* user_idx, int32_t* target_rows, float* labels, int32_t* hist_rows);
+
+/* Replaces ArticleTripletDataset.__init__ (embedding_generate.py:25-39): per
+ * user with >= 2 clicks and every pair i < j, (anchor clicks[i], positive
+ * clicks[j], a random never-clicked negative).
+ *   n_triplets must be sum(len_u * (len_u - 1) / 2) over users with >= 2 clicks;
+ *   triplets int32 [n_triplets][3]. */
+int nrk_triplet_samples(const int64_t* click_off, int64_t n_users, const int32_t* click_rows,
+                        int64_t n_items, uint32_t* rng_state, int64_t n_triplets, int32_t* triplets);
+
 #ifdef __cplusplus
 }
 #endif

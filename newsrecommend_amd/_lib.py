@@ -65,6 +65,8 @@ SIGNATURES = {
     "nrk_din_rerank_head": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_i32, c_p, c_p, c_p, c_p, c_i32, c_p, c_p, c_p,
                                            c_f32, c_p, c_p]),
     "nrk_gather_rows": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_i64, c_i32, c_p, c_p]),
+    "nrk_train_samples": (ctypes.c_int, [c_p, c_i64, c_p, c_i64, c_i32, c_p, c_i64, c_p, c_p, c_p, c_p]),
+    "nrk_triplet_samples": (ctypes.c_int, [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p]),
 }
 
 _lib = None

@@ -54,6 +54,92 @@ class ArticleTable:
         return np.where(a < 0, -1, self._sorted_rows[pos]).astype(np.int32)
 
 
+class ClickLog:
+    """Typed click log in place of the reference's
+    {uid: [article ids]} dicts (DIN.py:17-18, embedding_generate.py:21-22):
+    users int64 (U,) in dict order, CSR offsets int64 (U+1,), clicks int64
+    (nnz,) article ids oldest -> newest.  `save`/`load` use a plain .npz
+    (no pickles)."""
+
+    def __init__(self, users, offsets, clicks):
+        self.users = np.ascontiguousarray(users, dtype=np.int64)
+        self.offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+        self.clicks = np.ascontiguousarray(clicks, dtype=np.int64)
+        if self.offsets.shape != (len(self.users) + 1,) or self.offsets[0] != 0 or \
+                self.offsets[-1] != len(self.clicks) or np.any(np.diff(self.offsets) < 0):
+            raise ValueError("ClickLog: offsets must be a non-decreasing (U+1,) CSR index over the clicks")
+
+    @classmethod
+    def from_dict(cls, user_clicks: dict) -> "ClickLog":
+        users = np.fromiter(user_clicks.keys(), dtype=np.int64, count=len(user_clicks))
+        lens = np.fromiter((len(v) for v in user_clicks.values()), dtype=np.int64, count=len(user_clicks))
+        off = np.zeros(len(users) + 1, np.int64)
+        np.cumsum(lens, out=off[1:])
+        clicks = np.fromiter((int(a) for v in user_clicks.values() for a in v), dtype=np.int64, count=int(off[-1]))
+        return cls(users, off, clicks)
+
+    def to_dict(self) -> dict:
+        return {int(u): self.clicks[self.offsets[i]:self.offsets[i + 1]].tolist() for i, u in enumerate(self.users)}
+
+    def __len__(self):
+        return len(self.users)
+
+    def save(self, path: str) -> None:
+        np.savez(path, users=self.users, offsets=self.offsets, clicks=self.clicks)
+
+    @classmethod
+    def load(cls, path: str) -> "ClickLog":
+        z = np.load(path)
+        return cls(z["users"], z["offsets"], z["clicks"])
+
+
+def _rng_words(rng):
+    st = rng.getstate()
+    if st[0] != 3 or len(st[1]) != 625:
+        raise ValueError("expected a CPython Mersenne Twister state (version 3, 625 words)")
+    return st, np.array(st[1], dtype=np.uint32)
+
+
+def _rng_restore(rng, st, words):
+    rng.setstate((st[0], tuple(int(w) for w in words), st[2]))
+
+
+class TrainRows:
+    """Typed TrainDataset rows: uid int64 (n,), hist int32 (n, L) table rows
+    (-1 padded), target int32 (n,) table rows, label f32 (n, 1).  The id-based
+    DIN path (FusedTrainStep / nrk_din_batch) consumes these directly."""
+
+    def __init__(self, uid, hist, target, label):
+        self.uid, self.hist, self.target, self.label = uid, hist, target, label
+
+    def __len__(self):
+        return len(self.target)
+
+
+def train_rows(max_history: int, log: ClickLog, table: "ArticleTable", rng=random) -> TrainRows:
+    """TrainDataset.__init__ (DIN.py:66-76) over a typed click log, built by
+    libnrk's host builder (nrk_train_samples): the same rows as the Python loop
+    and the same `random` draws, `rng` left advanced exactly as the loop would
+    leave it.  Negatives index `table`'s row order (= list(article_emb.keys()))."""
+    from . import _lib
+
+    rows = table.rows(log.clicks)
+    lens = np.diff(log.offsets)
+    n = int(2 * np.maximum(lens - 1, 0).sum())
+    L = int(max_history)
+    uidx = np.empty(n, np.int32)
+    tgt = np.empty(n, np.int32)
+    lab = np.empty(n, np.float32)
+    hist = np.empty((n, L), np.int32)
+    st, words = _rng_words(rng)
+    rc = _lib.load().nrk_train_samples(log.offsets.ctypes.data, len(log), rows.ctypes.data, len(table.ids), L,
+                                       words.ctypes.data, n, uidx.ctypes.data, tgt.ctypes.data, lab.ctypes.data,
+                                       hist.ctypes.data)
+    _rng_restore(rng, st, words)
+    _lib.check(rc, "train_rows")
+    return TrainRows(log.users[uidx], hist, tgt, lab.reshape(n, 1))
+
+
 class TrainDataset(Dataset):
     """DIN.py:66-92.  For each user (dict order) and click i >= 1: history =
     clicks[:i][-max_history:], one positive (target clicks[i], label 1) and one

@@ -126,6 +126,28 @@ class ArticleTripletDataset(torch.utils.data.Dataset):
                     trip.append((clicked_articles[i], clicked_articles[j], neg))
         self.triplets = np.asarray(trip, dtype=np.int64).reshape(-1, 3)
 
+    @classmethod
+    def from_click_log(cls, log, all_article_ids, rng=random) -> "ArticleTripletDataset":
+        """The same triplets (and `random` draws) from a typed data.ClickLog,
+        built by libnrk's host builder (nrk_triplet_samples) instead of the
+        per-pair Python loop."""
+        from . import _lib
+        from .data import ArticleTable, _rng_restore, _rng_words
+
+        ids = np.asarray(list(all_article_ids), dtype=np.int64)
+        rows = ArticleTable(ids, np.zeros((len(ids), 0), np.float32)).rows(log.clicks)
+        lens = np.diff(log.offsets)
+        n = int((lens * (lens - 1) // 2)[lens >= 2].sum())
+        out = np.empty((n, 3), np.int32)
+        st, words = _rng_words(rng)
+        rc = _lib.load().nrk_triplet_samples(log.offsets.ctypes.data, len(log), rows.ctypes.data, len(ids),
+                                             words.ctypes.data, n, out.ctypes.data)
+        _rng_restore(rng, st, words)
+        _lib.check(rc, "ArticleTripletDataset.from_click_log")
+        self = cls.__new__(cls)
+        self.triplets = ids[out]
+        return self
+
     def __len__(self):
         return len(self.triplets)
 
