@@ -21,7 +21,12 @@ the producer side of the retrieval path.
                           numeric (N, d+1) table (ids in the last column)
   ArticleTripletDataset / train_triplet   embedding_generate.py:25-49,67-107
                           (TripletMarginLoss(margin=1, p=2), Adam with L2
-                          weight decay), features gathered on the device
+                          weight decay), features gathered on the device;
+                          .from_click_log builds the triplets natively
+  fit_triplet             main() (embedding_generate.py:67-107): shuffled
+                          train/eval loaders, per-epoch losses, best-eval-loss
+                          checkpoint; pinned to the reference's own main() run
+                          (tests/golden/embedding_train.npz)
 """
 from __future__ import annotations
 
@@ -180,3 +185,63 @@ def train_triplet(model, triplets: np.ndarray, id_to_row: dict, features: torch.
         running += loss.detach() * r.shape[0]
         nb += 1
     return (running / max(nb, 1)).item()
+
+
+def _triplet_rows(triplets, ids: np.ndarray, device) -> torch.Tensor:
+    from .data import ArticleTable
+
+    rows = ArticleTable(ids, np.zeros((len(ids), 0), np.float32)).rows(np.asarray(triplets, np.int64))
+    return torch.from_numpy(rows.astype(np.int64)).to(device)
+
+
+def fit_triplet(model, train_triplets, test_triplets, article_ids, features: torch.Tensor, epochs: int = 3,
+                batch_size: int = 64, lr: float = LR, weight_decay: float = WEIGHT_DECAY, margin: float = MARGIN,
+                save_path: str | None = None):
+    """embedding_generate.py:67-107 (main()) over id triplets, features
+    (N, 253) resident on the device in `article_ids` order.
+
+    Same loop as the reference: shuffled DataLoaders over the train and test
+    triplets (same sampler, so the same torch RNG draws and batch order),
+    TripletMarginLoss(margin, p=2), Adam(lr, weight_decay); per epoch
+    train_loss = Σ loss·rows / number of batches (running_loss /
+    len(trainDataloader), :92) and the same for the eval pass (:103); the
+    state_dict with the lowest eval loss is kept (:105-107) and saved to
+    `save_path` if given.  The rows are gathered from `features` on the device
+    by index batches instead of per-item dict lookups (:45-49).
+    Returns (history [(train_loss, eval_loss)], best_state_dict)."""
+    dev = features.device
+    ids = np.asarray(article_ids, np.int64)
+    tr_rows = _triplet_rows(train_triplets, ids, dev).reshape(-1, 3)
+    te_rows = _triplet_rows(test_triplets, ids, dev).reshape(-1, 3)
+    loader = lambda n: torch.utils.data.DataLoader(range(n), batch_size=batch_size, shuffle=True)  # noqa: E731
+    tr_loader, te_loader = loader(len(tr_rows)), loader(len(te_rows))
+    crit = nn.TripletMarginLoss(margin=margin, p=2)
+    opt = torch.optim.Adam(model.parameters(), lr=lr, weight_decay=weight_decay)
+    best_loss, best_sd, history = float("inf"), None, []
+    for _ in range(epochs):
+        model.train()
+        running = 0.0
+        for idx in tr_loader:
+            r = tr_rows[idx.to(dev)]
+            opt.zero_grad()
+            a, p, n = (model(features[r[:, c]]) for c in range(3))
+            loss = crit(a, p, n)
+            loss.backward()
+            opt.step()
+            running += loss.item() * r.shape[0]
+        train_loss = running / len(tr_loader)
+        running = 0.0
+        model.eval()
+        with torch.no_grad():
+            for idx in te_loader:
+                r = te_rows[idx.to(dev)]
+                a, p, n = (model(features[r[:, c]]) for c in range(3))
+                running += crit(a, p, n).item() * r.shape[0]
+        eval_loss = running / len(te_loader)
+        history.append((train_loss, eval_loss))
+        if eval_loss < best_loss:
+            best_loss = eval_loss
+            best_sd = {k: v.detach().clone() for k, v in model.state_dict().items()}
+            if save_path is not None:
+                torch.save(model.state_dict(), save_path)
+    return history, best_sd

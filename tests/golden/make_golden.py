@@ -331,8 +331,73 @@ def embedding_fixture(name, seed, n_articles=48):
                             emb=emb, table_loadable=np.bool_(table_loadable), **_sd(m))
 
 
+def embedding_train_fixture(name, seed, n_articles=120, n_train=16, n_test=9, max_clicks=8):
+    """The reference's triplet training main() (embedding_generate.py:67-107),
+    run as written (3 epochs, batch 64, shuffled loaders, dropout 0.13, Adam
+    with weight decay, best-eval-loss checkpoint) on a small synthetic world.
+    Every TripletMarginLoss value main() computes is recorded by handing the
+    module a loss subclass that logs (value, batch rows, train/eval)."""
+    with tempfile.TemporaryDirectory() as wd:
+        rng = np.random.default_rng(seed)
+        aids = rng.choice(np.arange(10, 10 * n_articles + 10), size=n_articles, replace=False)
+        feats = rng.standard_normal((n_articles, 253)).astype(np.float32)
+        a2f = {int(a): feats[i] for i, a in enumerate(aids)}
+
+        def clicks(n_users, base):
+            return {base + u: [int(x) for x in rng.choice(aids, size=int(rng.integers(1, max_clicks + 1)),
+                                                          replace=False)] for u in range(n_users)}
+
+        trc, tec = clicks(n_train, 100), clicks(n_test, 900)
+        _write_news(wd, {0: np.zeros(4, np.float32)}, trc, tec, {}, {"article_embedding_dict.npy": a2f})
+        ref = _import_ref("embedding_generate", wd)
+        log = []
+
+        class RecordingLoss(torch.nn.TripletMarginLoss):
+            def forward(self, a, p, n):
+                out = super().forward(a, p, n)
+                log.append((float(out.detach()), a.shape[0], torch.is_grad_enabled()))
+                return out
+
+        class NNProxy:  # the module's `nn` with TripletMarginLoss swapped for the recorder
+            TripletMarginLoss = RecordingLoss
+
+            def __getattr__(self, k):
+                return getattr(torch.nn, k)
+
+        ref.nn = NNProxy()
+        ref.tqdm = lambda it, desc=None: it
+        random.seed(seed)
+        torch.manual_seed(seed)
+        cwd = os.getcwd()
+        os.chdir(wd)
+        try:
+            ref.main()
+            best = torch.load(os.path.join("news", "best_eg_model.pth"), weights_only=True)  # written by main() above
+        finally:
+            os.chdir(cwd)
+        random.seed(seed)  # the triplets main() built (the datasets are its first `random` consumers)
+        tr = np.asarray(ref.ArticleTripletDataset(True).triplets, np.int64)
+        te = np.asarray(ref.ArticleTripletDataset(False).triplets, np.int64)
+        np.savez_compressed(
+            os.path.join(OUT, f"{name}.npz"), seed=np.int64(seed), aids=aids.astype(np.int64), feats=feats,
+            train_users=np.array(list(trc.keys()), np.int64),
+            train_click_len=np.array([len(v) for v in trc.values()], np.int64),
+            train_clicks=np.concatenate([np.asarray(v, np.int64) for v in trc.values()]),
+            test_users=np.array(list(tec.keys()), np.int64),
+            test_click_len=np.array([len(v) for v in tec.values()], np.int64),
+            test_clicks=np.concatenate([np.asarray(v, np.int64) for v in tec.values()]),
+            train_triplets=tr, test_triplets=te,
+            loss_values=np.array([v for v, _, _ in log], np.float64),
+            loss_rows=np.array([b for _, b, _ in log], np.int64),
+            loss_train=np.array([g for _, _, g in log], np.bool_),
+            **{f"best::{k}": v.numpy() for k, v in best.items()})
+
+
 def main():
     torch.set_num_threads(4)
+    if sys.argv[1:] == ["embedding_train"]:  # regenerate only the triplet-training fixture
+        embedding_train_fixture("embedding_train", seed=18)
+        return
     din_forward_fixture("din_fwd_c1", d=64, A=32, F=32, B=64, L=20, n_items=300, seed=11)
     din_forward_fixture("din_fwd_c3", d=128, A=128, F=32, B=96, L=50, n_items=600, seed=12)
     din_train_fixture("din_train_c1", d=64, A=32, F=32, B=48, L=20, n_items=300, seed=13)
@@ -340,6 +405,7 @@ def main():
     din_dataset_fixture("din_dataset", seed=15)
     embedding_fixture("embedding_infer", seed=16)
     din_rerank_fixture("din_rerank_c5", seed=17)
+    embedding_train_fixture("embedding_train", seed=18)
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))

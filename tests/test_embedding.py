@@ -75,3 +75,90 @@ def test_embed_gpu_and_triplet_step(gpu):
     l0 = train_triplet(mt, trip, id_to_row, feats, opt, batch_size=8)
     l1 = train_triplet(mt, trip, id_to_row, feats, opt, batch_size=8)
     assert np.isfinite(l0) and l1 < l0
+
+
+def _fixture_logs(z):
+    from newsrecommend_amd.data import ClickLog
+
+    def log(prefix):
+        lens = z[f"{prefix}_click_len"]
+        off = np.concatenate([[0], np.cumsum(lens)])
+        return ClickLog(z[f"{prefix}_users"], off, z[f"{prefix}_clicks"])
+
+    return log("train"), log("test")
+
+
+def _epoch_losses(z):
+    """per-epoch (train, eval) as main() computes them (embedding_generate.py:90-103)"""
+    v, rows, tr = z["loss_values"], z["loss_rows"], z["loss_train"]
+    out, i = [], 0
+    while i < len(v):
+        j = i
+        while j < len(v) and tr[j]:
+            j += 1
+        k = j
+        while k < len(v) and not tr[k]:
+            k += 1
+        out.append((float(np.sum(v[i:j] * rows[i:j])) / (j - i), float(np.sum(v[j:k] * rows[j:k])) / (k - j)))
+        i = k
+    return out
+
+
+def test_fit_triplet_matches_reference_main(tmp_path):
+    """The reference's main() (embedding_generate.py:67-107) run as written on
+    a synthetic world (tests/golden/embedding_train.npz): triplets from the
+    typed click logs under the same `random` seed, then fit_triplet on the CPU
+    under the same torch seed: the same batches, dropout masks and Adam
+    steps, so every epoch's train/eval loss and the best-eval-loss checkpoint
+    match the reference's."""
+    from newsrecommend_amd.embedding import ArticleEmbeddingModel, ArticleTripletDataset, fit_triplet
+
+    z = np.load(os.path.join(GOLDEN, "embedding_train.npz"))
+    seed = int(z["seed"])
+    tr_log, te_log = _fixture_logs(z)
+    rng = random.Random(seed)
+    tr = ArticleTripletDataset.from_click_log(tr_log, z["aids"], rng).triplets
+    te = ArticleTripletDataset.from_click_log(te_log, z["aids"], rng).triplets
+    np.testing.assert_array_equal(tr, z["train_triplets"])
+    np.testing.assert_array_equal(te, z["test_triplets"])
+    torch.manual_seed(seed)
+    m = ArticleEmbeddingModel()
+    path = str(tmp_path / "best_eg_model.pth")
+    nt = torch.get_num_threads()
+    torch.set_num_threads(4)  # as make_golden.py: CPU sgemm blocking follows the thread count
+    try:
+        hist, best = fit_triplet(m, tr, te, z["aids"], torch.from_numpy(z["feats"]), save_path=path)
+    finally:
+        torch.set_num_threads(nt)
+    np.testing.assert_allclose(np.array(hist), np.array(_epoch_losses(z)), rtol=1e-6, atol=0)
+    saved = torch.load(path, weights_only=True)
+    for k, v in best.items():
+        np.testing.assert_allclose(v.numpy(), z[f"best::{k}"], rtol=0, atol=1e-6, err_msg=k)
+        np.testing.assert_array_equal(saved[k].numpy(), v.numpy())
+
+
+@pytest.mark.gpu
+def test_fit_triplet_on_device(gpu):
+    """The reference's best checkpoint (embedding_train.npz) evaluated on the
+    device reproduces main()'s best eval loss: Σ per-triplet losses / number
+    of batches does not depend on the shuffled batch order.  Then fit_triplet
+    runs with the features resident on the GPU (dropout masks come from the
+    device RNG, so that trajectory is checked for finiteness and the
+    best-checkpoint rule only)."""
+    from newsrecommend_amd.embedding import ArticleEmbeddingModel, _triplet_rows, fit_triplet
+
+    z = np.load(os.path.join(GOLDEN, "embedding_train.npz"))
+    feats = torch.from_numpy(z["feats"]).to(gpu)
+    m = ArticleEmbeddingModel().to(gpu)
+    m.load_state_dict({k[6:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("best::")})
+    m.eval()
+    r = _triplet_rows(z["test_triplets"], z["aids"], gpu)
+    with torch.no_grad():
+        per = torch.nn.TripletMarginLoss(margin=1.0, p=2, reduction="none")(*(m(feats[r[:, c]]) for c in range(3)))
+    n_batches = -(-len(r) // 64)
+    best_eval = min(e for _, e in _epoch_losses(z))
+    np.testing.assert_allclose(per.double().sum().item() / n_batches, best_eval, rtol=1e-5)
+    hist, best = fit_triplet(m, z["train_triplets"], z["test_triplets"], z["aids"], feats, epochs=2)
+    assert np.all(np.isfinite(np.array(hist)))
+    ev = [e for _, e in hist]
+    assert best is not None and len(hist) == 2 and min(ev) <= ev[-1]
