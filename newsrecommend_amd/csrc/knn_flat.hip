@@ -1481,7 +1481,11 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
   // that a few queries per thousand are uncertified: 1M x 128 k = 100 at 2k:
   // 36 of 4096).  Measured at 10M x 256 k = 200 (stride 16): screen 19.05 ms at
   // R = 2k -> 16.83; 1.25M x 256, 32768 queries: total 38.4 -> 29.2 ms.
-  p.R = k <= 8 ? 16 : (k / 4 > 16 ? k / 4 : 16);
+  // k <= 8: R = max(8, k + 3) (was 16; with the stride rule below it halves the
+  // pre-pass and leaves stride * R, the admitted items, unchanged: 1M x 128
+  // k = 5 total 1.055 -> 1.001 ms, L2 1.41 -> 1.27 ms, 10M x 256 16.66 -> 16.41
+  // ms, 125K x 128 x 32768 queries 1.78 -> 1.64 ms; same results).
+  p.R = k <= 8 ? (k + 3 > 8 ? k + 3 : 8) : (k / 4 > 16 ? k / 4 : 16);
   p.tau = true;  // k = 200 at 10M x 256: -5% retrieve time
   if (p.dp == 256) p.qt = 1;
   p.wq = p.waves * 32 * p.qt;
@@ -1493,9 +1497,10 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
   // pre-pass stride: the pre-pass costs ~nb / stride per query, the main pass
   // admits ~stride * R items above tau per query (list insertions); the best
   // stride grows like sqrt(nb / R): the power of two >= 8 sqrt(nb/1M * 16/R),
-  // in [2, 64] (and stride * R >= 4k, above).  Measured (IP, per GPU): 1M x 128
-  // k = 5 -> 8; 10M x 256 k = 5 -> 32 (total 17.0 -> 15.8 ms vs 8); 125K x 128
-  // k = 5, 32768 queries -> 4 (-7 %)
+  // in [2, 64] (and stride * R >= 4k, above).  Measured at R = 16 (IP, per
+  // GPU): 1M x 128 k = 5 -> 8; 10M x 256 k = 5 -> 32 (total 17.0 -> 15.8 ms vs
+  // 8); 125K x 128 k = 5, 32768 queries -> 4 (-7 %).  At R = 8 the same rule
+  // gives 16, 64 and 8 (1M x 128: stride 16 1.001 ms, 32 1.026 ms)
   {
     const double want = 8.0 * sqrt((double)nb / 1e6 * 16.0 / p.R);
     int st = 2;
