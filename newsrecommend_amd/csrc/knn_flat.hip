@@ -119,6 +119,10 @@ __device__ __forceinline__ int lanes_below(unsigned long long mask) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
+// VPL: values per lane (nvals <= 64 * VPL); the flat pre-pass writes 8R = 64
+// values per query for k <= 8, so VPL = 1 there (16x fewer ballots per
+// bisection round than the VPL = 16 form)
+template <int VPL>
 __global__ __launch_bounds__(256) void tau_select_kernel(const float* __restrict__ premax, int nvals, int R,
                                                          int64_t nq, float* __restrict__ tau,
                                                          const int* __restrict__ ids_in = nullptr,
@@ -128,7 +132,6 @@ __global__ __launch_bounds__(256) void tau_select_kernel(const float* __restrict
   if (q >= nq) return;
   if (ids_out)
     for (int i = lane; i < R; i += 64) ids_out[q * R + i] = -1;
-  constexpr int VPL = 16;  // nvals <= 64 * VPL
   uint32_t key[VPL];       // 0: not finite (-inf, NaN: never selected)
   int nfin = 0;
 #pragma unroll
@@ -1800,8 +1803,9 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
     hipLaunchKernelGGL(pf, dim3(p.nqt * p.nch_pre), dim3(p.waves * 64), 0, st, qh, xb_bf16, xb_meta, nq, nb,
                        p.chunk_pre, p.nch_pre, p.nqt, p.tstride, nullptr, nullptr, pre, nullptr, IvfScreen{});
     NRK_CHECK_LAUNCH("screen_kernel (pre-pass)");
-    hipLaunchKernelGGL(tau_select_kernel, dim3((unsigned)cdiv(nq, 4)), dim3(256), 0, st, pre, 2 * p.nch_pre, p.R, nq,
-                       tau);
+    const int nv = 2 * p.nch_pre;
+    auto tsel = nv <= 64 ? tau_select_kernel<1> : nv <= 256 ? tau_select_kernel<4> : tau_select_kernel<16>;
+    hipLaunchKernelGGL(tsel, dim3((unsigned)cdiv(nq, 4)), dim3(256), 0, st, pre, nv, p.R, nq, tau, nullptr, nullptr);
     NRK_CHECK_LAUNCH("tau_select_kernel");
   }
 
@@ -2117,8 +2121,9 @@ extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe,
     hipLaunchKernelGGL(fa, dim3((unsigned)p.ubA), dim3(p.waves * 64), 0, st, qi, xbh_ivf, meta_ivf, nq, n, 0, 0, 0,
                        2, nullptr, pa, pt, nullptr, isa);  // every other tile: seeds from half the rows (measured +3 %)
     NRK_CHECK_LAUNCH("screen_kernel (ivf phase A)");
-    hipLaunchKernelGGL(tau_select_kernel, dim3((unsigned)cdiv(nq, 4)), dim3(256), 0, st, pt, 2 * p.nA * p.cmaxA, p.R,
-                       nq, tau, pa, seed);
+    const int nva = 2 * p.nA * p.cmaxA;
+    auto tsel = nva <= 64 ? tau_select_kernel<1> : nva <= 256 ? tau_select_kernel<4> : tau_select_kernel<16>;
+    hipLaunchKernelGGL(tsel, dim3((unsigned)cdiv(nq, 4)), dim3(256), 0, st, pt, nva, p.R, nq, tau, pa, seed);
     NRK_CHECK_LAUNCH("tau_select_kernel (ivf)");
     hipLaunchKernelGGL(ivf_seed_kernel, dim3((unsigned)nq), dim3(256), (size_t)host_pow2ceil(p.R) * 16 + (size_t)d * 4,
                        st, seed, p.R, k, pos2id, xq, xb, d, l2, qmeta, stats, p.dp, thr, lbg, lbi, ccnt, p.cap);
