@@ -570,11 +570,18 @@ def bench_din(args, rank, world, dev):
         opt.step()
         return loss
 
+    # a training epoch is thousands of steps: time at least 20 K-step graph
+    # launches (160 steps, ~30 ms) so the fixed launch/sync cost of a 20-step
+    # window does not masquerade as per-step time; warmup rounded to K so the
+    # timed steps are whole K-step launches
+    K = trainer.K if fused else 1
+    n_steps = max(args.steps, 20 * K)
+    n_warm = -(-max(args.warmup, 1) // K) * K
     model.train()
-    run(0, args.warmup)
+    run(0, n_warm)
     barrier(world)
     t0 = time.perf_counter()
-    loss = run(args.warmup, args.steps)
+    loss = run(n_warm, n_steps)
     barrier(world)
     el = max_over_ranks(time.perf_counter() - t0, world, dev)
     # attention kernel times: a few extra steps of the same path, outside the
@@ -588,18 +595,19 @@ def bench_din(args, rank, world, dev):
                 lg = model.forward_ids(table, tgt[perm[:B]], hist[perm[:B]])
                 crit(lg, lab[perm[:B]]).backward()
         torch.cuda.synchronize()
-    sps = B * args.steps * world / el
+    sps = B * n_steps * world / el
     fwd_ms, bwd_ms = kt.mean_ms("fwd", skip=1), kt.mean_ms("bwd", skip=1)
     # algorithmic bytes per sample: history ids + bf16 key rows, the U row and
     # outputs (fwd: pooled, alpha); bwd adds dpooled, alpha, q and the dU row
     fwd_bytes = B * (4 * L + L * d * 2 + 4 * A + 4 * d + 4 * L)
     bwd_bytes = B * (4 * L + L * d * 2 + 4 * A + 4 * d + 4 * L + 4 * d + 2 * 4 * A)
     STEP_BYTES = L * d * 2 + d * 2 + 4 * (L + 1) + 4
-    step_gbs = STEP_BYTES * B * args.steps / el / 1e9  # per GPU
+    step_gbs = STEP_BYTES * B * n_steps / el / 1e9  # per GPU
     fwd_gbs = fwd_bytes / (fwd_ms * 1e-3) / 1e9
     bwd_gbs = bwd_bytes / (bwd_ms * 1e-3) / 1e9
     out = {
-        "metric": "DIN train samples/s", "value": sps, "unit": "samples/s", "ms_per_step": el / args.steps * 1e3,
+        "metric": "DIN train samples/s", "value": sps, "unit": "samples/s", "ms_per_step": el / n_steps * 1e3,
+        "steps": n_steps, "warmup": n_warm,
         "config": {"workload": "configs[2]: DIN train bf16, 5M synthetic click rows, seq_len=50, emb_dim=128",
                    "rows": rows, "items": n_items, "batch": B, "attn_units": A, "fc_units": F,
                    "parallelism": f"dp{world}",
