@@ -788,15 +788,20 @@ __global__ __launch_bounds__(1024) void hf_reduce(HeadArgs a) {
   const int D2 = a.D2, F2 = a.F2, t = threadIdx.x, nblk = a.nblk;
   const int nA = D2 / 4;
   if ((int)blockIdx.x < nA) {
+    // XCD-aware column groups: blocks b, b+8, ... run on one XCD (round-robin
+    // dispatch), so give them adjacent 4-column groups: each XCD's L2 then
+    // fetches whole 128-B lines of the partial rows once, instead of all 8 XCDs
+    // fetching every line for their 16-B pieces
+    const int cgp = nA % 8 == 0 ? ((int)blockIdx.x % 8) * (nA / 8) + (int)blockIdx.x / 8 : (int)blockIdx.x;
     __shared__ double red[8][32][4];
     __shared__ double sred[8][32];
     __shared__ double Gt[32][4], St[32];
     const int ph = t >> 7, j = (t >> 2) & 31, cl = t & 3;
-    const int c = 4 * blockIdx.x + cl;
+    const int c = 4 * cgp + cl;
     float wv[HF];  // W1 column of this block's column t (t < 4), loaded with the partials
     if (t < 4) {
 #pragma unroll
-      for (int jj = 0; jj < HF; ++jj) wv[jj] = a.p.fc1_w[(int64_t)jj * D2 + 4 * blockIdx.x + t];
+      for (int jj = 0; jj < HF; ++jj) wv[jj] = a.p.fc1_w[(int64_t)jj * D2 + 4 * cgp + t];
     }
     double acc = 0.0;
     for (int b0 = ph; b0 < nblk; b0 += 8 * 16) {
@@ -839,11 +844,11 @@ __global__ __launch_bounds__(1024) void hf_reduce(HeadArgs a) {
     }
     __syncthreads();
     if (t < 128) {
-      const int jj = t >> 2, cc = t & 3, col = 4 * blockIdx.x + cc;
+      const int jj = t >> 2, cc = t & 3, col = 4 * cgp + cc;
       a.p.g_fc1_w[(int64_t)jj * D2 + col] = (float)(a.p.bn0_w[col] * Gt[jj][cc] + a.p.bn0_b[col] * St[jj]);
     }
     if (t < 4) {
-      const int col = 4 * blockIdx.x + t;
+      const int col = 4 * cgp + t;
       double sb = 0.0, sg = 0.0;
 #pragma unroll
       for (int jj = 0; jj < HF; ++jj) {
@@ -855,7 +860,7 @@ __global__ __launch_bounds__(1024) void hf_reduce(HeadArgs a) {
       a.sum5[col] = sb;
       a.sum5[D2 + col] = sg;
     }
-    if (blockIdx.x == 0 && t < HF) a.p.g_fc1_b[t] = (float)St[t];
+    if (cgp == 0 && t < HF) a.p.g_fc1_b[t] = (float)St[t];
     return;
   }
   // small layers: column q of the concatenation [part3 (3F2+2) | part4 (2F + F2 F + F2)]
