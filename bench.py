@@ -605,6 +605,7 @@ def bench_din(args, rank, world, dev):
     step_gbs = STEP_BYTES * B * n_steps / el / 1e9  # per GPU
     fwd_gbs = fwd_bytes / (fwd_ms * 1e-3) / 1e9
     bwd_gbs = bwd_bytes / (bwd_ms * 1e-3) / 1e9
+    din_key = f"B={B},L={L},d={d},A={A},gpus={world}"  # profiles/pmc_screen.json (tools/din_pmc.sh)
     out = {
         "metric": "DIN train samples/s", "value": sps, "unit": "samples/s", "ms_per_step": el / n_steps * 1e3,
         "steps": n_steps, "warmup": n_warm,
@@ -620,10 +621,10 @@ def bench_din(args, rank, world, dev):
                           "algorithmic": f"{STEP_BYTES} B/sample (SURVEY.md 8d: L*d*2 + d*2 + 4*(L+1) + 4) x "
                                          f"samples/s over the whole step"},
         "roofline_fwd": {"bound": "hbm", "achieved": fwd_gbs, "peak": HBM_GBS, "unit": "GB/s",
-                         "frac": fwd_gbs / HBM_GBS, "traffic": None,
+                         "frac": fwd_gbs / HBM_GBS, "traffic": _pmc_traffic(f"din_fwd:{din_key}") if fused else None,
                          "algorithmic": f"{fwd_bytes // B} B/sample x {B} samples"},
         "roofline_bwd": {"bound": "hbm", "achieved": bwd_gbs, "peak": HBM_GBS, "unit": "GB/s",
-                         "frac": bwd_gbs / HBM_GBS, "traffic": None,
+                         "frac": bwd_gbs / HBM_GBS, "traffic": _pmc_traffic(f"din_bwd:{din_key}") if fused else None,
                          "algorithmic": f"{bwd_bytes // B} B/sample x {B} samples"},
     }
     if fused and world == 1 and args.din_sweep:
