@@ -482,8 +482,14 @@ __global__ __launch_bounds__(256, 2) void din_fwd_wave_kernel(const uint16_t* __
 // Workgroup slab layout (floats): dW1k [A][D], then dw2 [A], then db2 [1].
 // The pipelined backward with the query (nrk_din_attn_bwd_params) appends
 // dW1q [A][D] and db1 [A] at slab_q_off.
-__host__ __device__ __forceinline__ size_t slab_q_off(int A, int D) { return (size_t)A * D + A + 4; }
-__host__ __device__ __forceinline__ size_t slab_floats(int A, int D) { return 2 * ((size_t)A * D + A + 4); }
+__host__ __device__ __forceinline__ size_t slab_q_off(int A, int D) { return ((size_t)A * D + A + 4 + 31) / 32 * 32; }
+// slab stride rounded up to 32 floats: every slab starts on a 128-B line, so the
+// parameter reduction's 64-float output windows read 2 whole lines per slab (an
+// unaligned stride made it 3, the boundary line shared with a block on another
+// XCD: 26.5 MB fetched per launch for 16.9 MB of slabs at B = 4096)
+__host__ __device__ __forceinline__ size_t slab_floats(int A, int D) {
+  return (slab_q_off(A, D) + (size_t)A * D + A + 4 + 31) / 32 * 32;
+}
 
 template <bool BF16, int D>
 __global__ __launch_bounds__(256) void din_bwd_kernel(
