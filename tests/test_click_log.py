@@ -113,3 +113,34 @@ def test_click_log_roundtrip(tmp_path):
     assert back.to_dict() == clicks
     with pytest.raises(ValueError):
         ClickLog(log.users, log.offsets[:-1], log.clicks)
+
+
+def test_row_builder_c_abi_rejects_bad_input():
+    """The host builders through the raw C-ABI (include/nrk.h): wrong sample
+    counts, non-monotone offsets, out-of-range rows and a bad Mersenne Twister
+    position are NRK_EINVAL (-1) with a message in nrk_last_error()."""
+    from newsrecommend_amd import _lib
+
+    L = _lib.load()
+    off = np.array([0, 3, 5], np.int64)
+    rows = np.array([0, 1, 2, 3, 4], np.int32)
+    st = np.array(random.Random(1).getstate()[1], np.uint32)
+    n = 2 * (2 + 1)
+    u, t, lab = np.empty(n, np.int32), np.empty(n, np.int32), np.empty(n, np.float32)
+
+    def call(off_, rows_, n_items, st_, n_):
+        return L.nrk_train_samples(off_.ctypes.data, len(off_) - 1, rows_.ctypes.data, n_items, 4, st_.ctypes.data,
+                                   n_, u.ctypes.data, t.ctypes.data, lab.ctypes.data, None)
+
+    assert call(off, rows, 10, st.copy(), n) == 0
+    assert call(off, rows, 10, st.copy(), n + 2) == -1 and b"yields" in L.nrk_last_error()
+    assert call(np.array([0, 3, 2], np.int64), rows, 10, st.copy(), n) == -1
+    assert call(off, rows, 4, st.copy(), n) == -1 and b"outside" in L.nrk_last_error()
+    bad = st.copy()
+    bad[624] = 1000
+    assert call(off, rows, 10, bad, n) == -1 and b"position" in L.nrk_last_error()
+    trip = np.empty((4, 3), np.int32)
+    assert L.nrk_triplet_samples(off.ctypes.data, 2, rows.ctypes.data, 10, st.copy().ctypes.data, 4,
+                                 trip.ctypes.data) == 0
+    assert L.nrk_triplet_samples(off.ctypes.data, 2, rows.ctypes.data, 10, st.copy().ctypes.data, 5,
+                                 trip.ctypes.data) == -1
