@@ -219,3 +219,31 @@ def test_rerank_head_matches_fp64(d):
     assert torch.isneginf(lg[~valid]).all()
     err = (lg[valid].double() - ref[valid]).abs().max().item()
     assert err < 1e-4 * max(1.0, ref.abs().max().item()), err
+
+
+def test_top_and_ndcg_equal_stable_sort_and_segment_ndcg():
+    """CPU: the e2e ranking tail (key top-k + row-sum NDCG) equals a stable
+    descending sort and din.ndcg_from_logits's segment formulation, with exact
+    ties, -inf padding, +/-0 logits and users without a positive."""
+    import torch
+
+    from newsrecommend_amd.din import ndcg_from_logits
+    from newsrecommend_amd.pipeline import _top_and_ndcg
+
+    g = torch.Generator().manual_seed(3)
+    U, C = 300, 37
+    logits = torch.randn((U, C), generator=g)
+    logits[:, 5] = logits[:, 2]
+    logits[:10, :4] = 0.0
+    logits[:10, 4] = -0.0
+    logits[::3, -1] = float("-inf")
+    cand = torch.randint(0, 1 << 20, (U, C), generator=g, dtype=torch.int32)
+    labels = torch.zeros((U, C), dtype=torch.bool)
+    labels[torch.arange(U), torch.randint(0, C, (U,), generator=g)] = True
+    labels[::5] = False
+    top, nd = _top_and_ndcg(logits, cand, labels, 5)
+    order = torch.sort(logits, dim=1, descending=True, stable=True).indices[:, :5]
+    assert torch.equal(top, torch.gather(cand, 1, order))
+    seg = torch.arange(U).repeat_interleave(C)
+    ref = ndcg_from_logits(logits.reshape(-1), labels.reshape(-1).float(), seg, U, 5)
+    assert torch.equal(nd, ref)
