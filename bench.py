@@ -501,6 +501,74 @@ def bench_e2e(args, rank, world, dev):
     return out
 
 
+# ------------------------------------------------------------- embedding --
+FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense fp32 MFMA (no TF32 on gfx950)
+
+
+def bench_embed(args, rank, world, dev):
+    """The corpus producer (embedding_generate.py:109-131):
+    ArticleEmbeddingModel in eval mode over N x 253 article features ->
+    N x 256 embeddings (fp32, as the reference), inputs resident in HBM.
+    Sizes: the reference's 364,047 articles and configs[4]'s 10M corpus, each
+    shard of N / world rows on its rank (replicas: no collective).  Roofline:
+    fp32 MFMA, 2 (253 * 512 + 512 * 256) flop per row; the dominant kernel is
+    the first GEMM, timed by rocprof (profiles/)."""
+    from newsrecommend_amd.embedding import ArticleEmbeddingModel
+
+    torch.manual_seed(5)
+    model = ArticleEmbeddingModel().to(dev).eval()
+    with torch.no_grad():  # non-trivial BN statistics (folded into fc.4 by embed())
+        bn = model.fc[3]
+        bn.running_mean.uniform_(-0.2, 0.2)
+        bn.running_var.uniform_(0.5, 1.5)
+    flop_row = 2.0 * (253 * 512 + 512 * 256)
+    out = {"metric": "article embeddings/s (corpus producer, fp32)", "unit": "rows/s",
+           "roofline_note": f"fp32 MFMA peak {FP32_MFMA_TFLOPS} TF; {flop_row:.0f} flop per row"}
+    for name, n_total in (("reference_364047", 364_047), ("corpus_10m", args.e2e_nb)):
+        n = -(-n_total // world)
+        g = torch.Generator(device=dev).manual_seed(9 + rank)
+        x = torch.randn((n, 253), generator=g, device=dev)
+        for _ in range(2):
+            model.embed(x)
+        barrier(world)
+        reps = 5 if n < 1_000_000 else 3
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            y = model.embed(x)
+        barrier(world)
+        el = max_over_ranks(time.perf_counter() - t0, world, dev) / reps
+        rec = {"value": n * world / el, "ms_per_pass": el * 1e3, "rows_per_gpu": n,
+               "achieved_tflops": flop_row * n / el / 1e12,
+               "frac_fp32_mfma": flop_row * n / el / 1e12 / FP32_MFMA_TFLOPS}
+        if rank == 0 and name == "reference_364047":
+            # parity on a row sample: the reference's eval forward (fc as nn.Sequential, BN unfolded), fp32
+            with torch.no_grad():
+                ref = model(x[:4096])
+            rec["max_abs_vs_module_forward"] = float((y[:4096] - ref).abs().max())
+        out[name] = rec
+        del x, y
+        torch.cuda.empty_cache()
+    out["value"] = out["corpus_10m"]["value"]
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cores = cpu_cores()
+        torch.set_num_threads(cores)
+        mc = ArticleEmbeddingModel().eval()
+        mc.load_state_dict({k: v.cpu() for k, v in model.state_dict().items()})
+        xc = torch.randn((65536, 253))
+
+        def run(n):
+            with torch.no_grad():
+                for lo in range(0, n, 8192):
+                    mc(xc[lo % 65536:lo % 65536 + 8192])
+
+        n, dt = _timed_sample(run, 10**8, 8192, args.cpu_seconds / 2, align=8192)
+        out["cpu_baseline"] = {"value": n / dt, "unit": "rows/s", "cores": cores, "kind": "port",
+                               "sample": f"{n} rows in batches of 8192 through the reference's eval-mode module "
+                                         f"(PyTorch-CPU fp32, {cores} threads; the reference itself runs batch-1 "
+                                         f"forwards, embedding_generate.py:118-121), {dt:.1f} s"}
+    return out
+
+
 # ------------------------------------------------------------------ DIN --
 DIN_STEPS_PER_GRAPH = 8  # fused steps per HIP-graph launch (one index copy + one launch per 8 steps)
 
@@ -691,7 +759,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["flat", "din", "ivf", "e2e", "all"], default="all")
+    ap.add_argument("--workload", choices=["flat", "din", "ivf", "e2e", "embed", "all"], default="all")
     ap.add_argument("--nb", type=int, default=1_000_000)
     ap.add_argument("--d", type=int, default=128)
     ap.add_argument("--nq", type=int, default=4096)
@@ -745,6 +813,13 @@ def main():
             rec.update({"metric": r["metric"], "value": r["value"], "unit": r["unit"], "ms_per_step": r["ms_per_step"],
                         "config": r["config"]})
         rec["e2e"] = r
+    if args.workload in ("embed", "all"):
+        r = bench_embed(args, rank, world, dev)
+        if args.workload == "embed":
+            rec.update({"metric": r["metric"], "value": r["value"], "unit": r["unit"],
+                        "ms_per_step": r["corpus_10m"]["ms_per_pass"]})
+        rec["embed"] = r
+        torch.cuda.empty_cache()
     if args.workload in ("din", "all"):
         r = bench_din(args, rank, world, dev)
         if args.workload == "din":

@@ -63,7 +63,13 @@ int nrk_padded_dim(int32_t d);
 int nrk_flat_prepare(const float* xb, int64_t nb, int32_t d, uint16_t* xb_bf16,
                      float* xb_meta, float* stats, void* stream);
 
-/* Workspace bytes needed by nrk_knn_flat for this problem. */
+/* Workspace bytes needed by nrk_knn_flat for this problem.  For the screened
+ * path it is about nq * (2 * 4 * U + 2 * dp + 64) bytes (U = per-query
+ * candidate union, <= 2048: 32..256 at k <= 8) plus s * (16 * fb_cap + 4 * 2048
+ * + 2 * dp + 32) bytes for s = min(nq, 16384) fallback / collect slots
+ * (fb_cap = max(512, pow2ceil(2k + 64))): ~60 MB at nq = 4096, k = 5 and at most
+ * ~256 MB + nq * 16 KB at k = 200.  Uncertified queries beyond the 16384
+ * slots are answered by the block-per-query fp64 scan. */
 int nrk_knn_flat_workspace(int64_t nq, int64_t nb, int32_t d, int32_t k, size_t* ws_bytes);
 
 /* Exact top-k: bf16 MFMA screening with per-chunk candidate lists, fp64

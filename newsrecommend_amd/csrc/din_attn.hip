@@ -321,10 +321,14 @@ __global__ __launch_bounds__(256, 2) void din_fwd_wave_kernel(const uint16_t* __
     const int n0 = __popcll(v0), nv = n0 + __popcll(v1);
     const int ntile = (nv + (nv < L ? 1 : 0) + 31) >> 5;
     const int npieces = 32 * ntile * CPR / 64;
-    {  // compacted id table of this wave (LDS operations of one wave complete in order)
+    {  // compacted id table of this wave, written by some lanes, read by others below
       const uint64_t below = (1ull << lane) - 1;
       if ((v0 >> lane) & 1) idtab[__popcll(v0 & below)] = i0;
       if ((v1 >> lane) & 1) idtab[n0 + __popcll(v1 & below)] = i1;
+      // explicit fence: the LDS stores have completed (lgkmcnt 0) and the
+      // compiler may not move the reads across (wave barrier + memory clobber)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
     }
     for (int u = 0; u < npieces; ++u) {
       const int p = u * 64 + lane;

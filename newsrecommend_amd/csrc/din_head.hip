@@ -1359,8 +1359,7 @@ __global__ __launch_bounds__(1024) void clip_adam_fused_kernel(float* __restrict
   const float bc1 = 1.f - powf(beta1, tstep), bc2 = 1.f - powf(beta2, tstep);
   const float step_size = lr / bc1, bc2_sqrt = sqrtf(bc2);
   if (i < n) {
-    gi *= coef;
-    g[i] = gi;  // clip_grad_norm_ scales the stored gradients
+    gi *= coef;  // the clipped gradient (stored back by the last block, below)
     gi = gi + wd * pi;
     mi = mi + (gi - mi) * (1.f - beta1);  // torch: exp_avg.lerp_(grad, 1 - beta1)
     vi = vi * beta2 + (1.f - beta2) * gi * gi;
@@ -1369,12 +1368,34 @@ __global__ __launch_bounds__(1024) void clip_adam_fused_kernel(float* __restrict
     const float denom = sqrtf(vi) / bc2_sqrt + eps;
     p[i] = pi - step_size * (mi / denom);
   }
+  // clip_grad_norm_ scales the stored gradients.  No block may do that for its
+  // own slice: every block reads ALL of g for the norm, and a block that runs
+  // late would read gradients another block had already scaled.  Each block's
+  // reads of g are complete here (they fed the norm before the barrier above);
+  // the block that draws the last ticket scales g in place, after all of them,
+  // and advances Adam's step count (every block read *step before its ticket).
+  __shared__ bool s_last;
   if (t == 0) {
-    // every block read *step before its ticket; the last one advances it
-    if (atomicAdd(ticket, 1u) == gridDim.x - 1) {
-      *step = tstep;
-      *ticket = 0u;
+    __threadfence();
+    s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  if (coef < 1.f) {
+    for (int64_t j = t; j < n4; j += 1024) {
+      float4 x = reinterpret_cast<float4*>(g)[j];
+      x.x *= coef;
+      x.y *= coef;
+      x.z *= coef;
+      x.w *= coef;
+      reinterpret_cast<float4*>(g)[j] = x;
     }
+    if (t < (int)(n & 3)) g[4 * n4 + t] *= coef;
+  }
+  if (t == 0) {
+    *step = tstep;
+    *ticket = 0u;
   }
 }
 

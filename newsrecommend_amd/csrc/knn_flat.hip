@@ -901,6 +901,7 @@ __global__ __launch_bounds__(256) void small_select_wave_kernel(const double* __
 // with exact_score, and keeps the items at least as good as the slot's
 // threshold.  Cost = slots x nb x d fp64 FMA, spread over every CU.
 constexpr int FB_TR = 64;
+constexpr int FB_SLOTS_MAX = 16384;  // fallback / collect slots per search (uncertified queries beyond them: exact_topk)
 
 __global__ __launch_bounds__(256) void fallback_scan_kernel(const float* __restrict__ xq,
                                                             const float* __restrict__ xb, int64_t nb, int d,
@@ -1586,11 +1587,14 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
   p.off_fbl = take((size_t)nq * 4);
   // fallback storage: candidates at least as good as the merge's k-th; the cap
   // leaves room for 2k + 64 (ties and near-ties), overflow goes to exact_topk.
-  // A slot for every query (up to 64 K): a corpus shard searched by N x 4096
-  // queries (weak scaling) leaves more than 4096 of them uncertified at L2, and
-  // the queries beyond the slots took the block-per-query exact scan (2.3 s
-  // for 574 queries over a 2.5M-row shard at world 4)
-  p.fb_slots = (int)(nq < 65536 ? nq : 65536);
+  // A slot for every query up to FB_SLOTS_MAX (16 K): a corpus shard searched
+  // by N x 4096 queries (weak scaling) leaves more than 4096 of them uncertified
+  // at L2, and the queries beyond the slots took the block-per-query exact scan
+  // (2.3 s for 574 queries over a 2.5M-row shard at world 4).  Each slot holds
+  // fb_cap x 16 B of fallback candidates and ccap x 4 B of collect positions
+  // (16 KB at k <= 224), so the cap bounds this part of the workspace at 256 MB
+  // (it was 1 GB at 64 K slots, almost all of it idle)
+  p.fb_slots = (int)(nq < FB_SLOTS_MAX ? nq : FB_SLOTS_MAX);
   p.fb_cap = host_pow2ceil(2 * k + 64);
   if (p.fb_cap < 512) p.fb_cap = 512;
   p.fb_cap = test_hook("NRK_FB_CAP", p.fb_cap);
@@ -1952,7 +1956,7 @@ static IvfPlan make_ivf_plan(int64_t nq, int nprobe, int nlist, int64_t max_list
   p.ubB = (cdiv(npairs, (int64_t)p.wq) + nlist) * p.cmaxB;
   if (p.ubA > gcap) p.ubA = gcap;
   if (p.ubB > gcap) p.ubB = gcap;
-  p.fb_slots = (int)(nq < 65536 ? nq : 65536);  // as the flat plan
+  p.fb_slots = (int)(nq < FB_SLOTS_MAX ? nq : FB_SLOTS_MAX);  // as the flat plan
   p.fb_cap = host_pow2ceil(2 * k + 64);
   if (p.fb_cap < 512) p.fb_cap = 512;
   p.fb_cap = test_hook("NRK_FB_CAP", p.fb_cap);

@@ -20,6 +20,7 @@ restatement, for CPU checks).
 from __future__ import annotations
 
 import ctypes
+import warnings
 
 import torch
 import torch.nn as nn
@@ -485,6 +486,14 @@ class FusedTrainStep:
         # attention backward that also forms dW1q / db1 and writes every
         # attention gradient in place: no torch ops left inside the step
         self.fast = (table.dtype == torch.bfloat16 and d in (64, 128) and Dk == d and hist_ids.shape[1] <= 128)
+        why = [w for w, bad in (("table is not bf16", table.dtype != torch.bfloat16),
+                                (f"emb_dim {d} not in (64, 128)", d not in (64, 128)),
+                                (f"history length {hist_ids.shape[1]} > 128", hist_ids.shape[1] > 128)) if bad]
+        # which path the step runs (the generic one has torch ops around the kernels)
+        self.path = "fast" if self.fast else "generic: " + ", ".join(why)
+        if not self.fast:
+            warnings.warn(f"FusedTrainStep: {self.path} -> the generic step (torch GEMMs and gathers around the "
+                          f"attention kernels), not the single-kernel-chain fast path", stacklevel=2)
         if self.fast:
             L = hist_ids.shape[1]
             self.hist_b = torch.empty((B, L), dtype=torch.int32, device=dev)
@@ -625,6 +634,39 @@ class FusedTrainStep:
             self._body()
         return self.loss
 
+    def step_rows(self, batch_index: torch.Tensor):
+        """One training step on ANY number of rows (> 1; the fused kernels need
+        the fixed batch): fit()'s last partial batch, which the reference's
+        DataLoader(shuffle=True) keeps (DIN.py:241).  Forward and backward run
+        through the model's autograd path (the HIP attention kernels, a torch
+        head), the gradients land in the step's flat buffer, then the same
+        grad_hook and clip_grad_norm_ + Adam kernel as step() (shared moments,
+        step count and lr).  Returns the device loss (1,).  With dropout > 0 the
+        masks come from torch's generator, not the fused head's hash."""
+        n = int(batch_index.numel())
+        if n == self.B:
+            return self.step(batch_index)
+        self._sync_lr()
+        m = self.model
+        m.train()
+        idx = batch_index.reshape(-1).to(torch.long)
+        params = list(m.parameters())
+        with torch.enable_grad():
+            logits = m.forward_ids(self.table, self.tgt_all[idx], self.hist_all[idx])
+            loss = nn.functional.binary_cross_entropy_with_logits(logits.reshape(-1), self.lab_all[idx])
+            grads = torch.autograd.grad(loss, params)
+        with torch.no_grad():
+            for p, g in zip(params, grads):
+                p.grad.copy_(g)
+        if self.grad_hook is not None:
+            self.grad_hook(self.G)
+        L_ = _lib.load()
+        _lib.check(L_.nrk_clip_adam(
+            _lib.ptr(self.P), _lib.ptr(self.G), _lib.ptr(self.M), _lib.ptr(self.V), self.n, _lib.ptr(self.step_t),
+            self._lr_host, _lib.ptr(self.lr_t), self.betas[0], self.betas[1], self.eps, self.wd, self.clip,
+            _lib.ptr(self.ws_opt), self.ws_opt.numel(), _lib.stream(self.table.device)), "clip_adam")
+        return loss.detach().reshape(1)
+
     def step_many(self, batch_indices: torch.Tensor):
         """K = steps_per_graph consecutive training steps, batch k on rows
         `batch_indices[k]` ((K, B) device int64), as ONE graph launch; returns
@@ -648,9 +690,10 @@ def fit(model, table, hist_ids, target_ids, labels, eval_loader, epochs=10, batc
         weight_decay=8.96e-5, clip=1.0, k=5, checkpoint=None, scheduler=None, seed=42, graph=True, log=None):
     """DIN.py:225-257 (main()) on the fused train step: per epoch, shuffle the
     rows (DataLoader(shuffle=True) -> torch.randperm from a generator seeded
-    with `seed`), train on every FULL batch (the fused step has a fixed batch;
-    the reference's last partial batch of n % batch_size rows is dropped),
-    report the mean of the per-batch losses (DIN.py:153), evaluate
+    with `seed`), train on every full batch with the fused step and on the last
+    partial batch of n % batch_size rows with FusedTrainStep.step_rows (as the
+    reference's DataLoader keeps it), report the mean of the per-batch losses
+    (DIN.py:153), evaluate
     (DIN.py:155-193), step the scheduler — by default
     ReduceLROnPlateau(mode='min', factor=0.5, patience=1) on the validation
     loss (DIN.py:246,254), any other LR scheduler with step() — and save the
@@ -666,7 +709,7 @@ def fit(model, table, hist_ids, target_ids, labels, eval_loader, epochs=10, batc
     crit = nn.BCEWithLogitsLoss()
     gen = torch.Generator(device=dev).manual_seed(seed)
     n, B = trainer.hist_all.shape[0], trainer.B
-    nb = n // B
+    nb, tail = divmod(n, B)
     best, history = 0.0, []
     for epoch in range(epochs):
         lr_epoch = trainer.lr
@@ -675,7 +718,9 @@ def fit(model, table, hist_ids, target_ids, labels, eval_loader, epochs=10, batc
         total = torch.zeros((), dtype=torch.float64, device=dev)
         for b in range(nb):
             total += trainer.step(perm[b * B:(b + 1) * B])[0]
-        train_loss = (total / max(nb, 1)).item()
+        if tail:
+            total += trainer.step_rows(perm[nb * B:])[0]
+        train_loss = (total / max(nb + (1 if tail else 0), 1)).item()
         val_loss, ndcg = evaluate(model, eval_loader, crit, dev, k)
         if plateau:
             sched.step(val_loss)

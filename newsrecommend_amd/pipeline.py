@@ -21,9 +21,12 @@ stage is a batch over users, with ids instead of embeddings:
 """
 from __future__ import annotations
 
+import warnings
+
 import numpy as np
 import torch
 
+RERANK_SHARED_MAX_L = 64  # nrk_din_rerank_attn holds the history image of one user in LDS
 
 
 def cluster_candidates(centroid_index, cluster_lists, profiles: np.ndarray, uids) -> dict:
@@ -171,9 +174,18 @@ def rerank(model, table: torch.Tensor, hist_rows: torch.Tensor, cand_rows: torch
     model.eval()
     U, C = cand_rows.shape
     L = hist_rows.shape[1]
-    if (shared and table.dtype == torch.bfloat16 and table.shape[1] in (64, 128, 256) and L <= 64
-            and model.attn.attn[0].weight.shape[1] == 2 * table.shape[1]):
+    why = [w for w, bad in (("shared=False", not shared), ("table is not bf16", table.dtype != torch.bfloat16),
+                            (f"emb_dim {table.shape[1]} not in (64, 128, 256)", table.shape[1] not in (64, 128, 256)),
+                            (f"history length {L} > {RERANK_SHARED_MAX_L}", L > RERANK_SHARED_MAX_L),
+                            ("model emb_dim != table width", model.attn.attn[0].weight.shape[1] != 2 * table.shape[1]))
+           if bad]
+    # which path ran, for callers and benchmarks (the per-candidate one costs C x the attention work)
+    rerank.path = "shared" if not why else "per-candidate: " + ", ".join(why)
+    if not why:
         return _rerank_shared(model, table, hist_rows, cand_rows, batch_samples)
+    if shared:
+        warnings.warn(f"rerank: {rerank.path} -> per-candidate DIN forward (C x the attention work of the shared "
+                      f"path)", stacklevel=2)
     out = torch.empty((U, C), dtype=torch.float32, device=table.device)
     ub = max(1, batch_samples // max(C, 1))
     for lo in range(0, U, ub):
@@ -185,12 +197,78 @@ def rerank(model, table: torch.Tensor, hist_rows: torch.Tensor, cand_rows: torch
     return out
 
 
+rerank.path = None
+
+
+@torch.no_grad()
+def rerank_clusters(model, table: torch.Tensor, hist_rows: torch.Tensor, user_cluster: torch.Tensor,
+                    cluster_off: torch.Tensor, cluster_rows: torch.Tensor, last_rows: torch.Tensor | None = None,
+                    k: int = 5, batch_samples: int = 1 << 22):
+    """Retrieval.py:28-34 -> DIN.py:155-193 as the reference runs it: every
+    user's candidates are the WHOLE cluster its profile is nearest to
+    (cluster_candidates), so all users of cluster c share one ragged list,
+    rows cluster_rows[cluster_off[c]:cluster_off[c+1]] (corpus row order).
+    Users are grouped by cluster and each group is re-ranked as a padding-free
+    (n_users_c, C_c) batch (rerank, the shared-history kernels).
+
+    last_rows (U,) -- the row of each user's last click -- gives
+    EvalDataset's labels (one-hot at the FIRST candidate equal to it, none when
+    absent; DIN.py:27-31), the per-user BCE (DIN.py:176-177) and NDCG@k
+    (DIN.py:181-189, ndcg_at_k's tie rule).  Returns a dict: `logits` list of
+    (n_users_c, C_c) per cluster, `users` list of the user indices of each
+    group, and with last_rows `loss` (U,) f64 and `ndcg` (U,) f64."""
+    dev = table.device
+    U = hist_rows.shape[0]
+    uc = user_cluster.to(dev).long()
+    off = cluster_off.to(dev).long()
+    rows = cluster_rows.to(dev).to(torch.int32)
+    order = torch.sort(uc, stable=True).indices
+    bounds = torch.searchsorted(uc[order], torch.arange(off.numel(), device=dev))
+    bh = bounds.cpu().tolist()  # one small host read: the group boundaries
+    oh = off.cpu().tolist()
+    out = {"logits": [], "users": []}
+    if last_rows is not None:
+        loss = torch.zeros(U, dtype=torch.float64, device=dev)
+        ndcg = torch.zeros(U, dtype=torch.float64, device=dev)
+        last = last_rows.to(dev).to(torch.int32)
+    for c in range(off.numel() - 1):
+        lo, hi = bh[c], bh[c + 1]
+        if hi <= lo or oh[c + 1] <= oh[c]:
+            continue
+        us = order[lo:hi]
+        cand = rows[oh[c]:oh[c + 1]]
+        C = cand.numel()
+        lg = rerank(model, table, hist_rows[us], cand[None, :].expand(hi - lo, C), batch_samples=batch_samples)
+        out["logits"].append(lg)
+        out["users"].append(us)
+        if last_rows is not None:
+            hit = cand[None, :] == last[us][:, None]
+            first = torch.where(hit.any(1), hit.to(torch.int8).argmax(1), torch.full_like(us, -1))
+            lab = torch.zeros((hi - lo, C), dtype=torch.bool, device=dev)
+            has = first >= 0
+            lab[has.nonzero().squeeze(1), first[has]] = True
+            per = torch.nn.functional.binary_cross_entropy_with_logits(lg, lab.float(), reduction="none")
+            loss[us] = per.double().mean(1)
+            ndcg[us] = ndcg_at_k(lg, lab, k)
+    if last_rows is not None:
+        out["loss"], out["ndcg"] = loss, ndcg
+    return out
+
+
 def ndcg_at_k(logits: torch.Tensor, labels: torch.Tensor, k: int) -> torch.Tensor:
     """Per-user NDCG@k with one relevant item (DIN.py:181-189); padded
     candidates carry -inf logits and label 0.  Same rule as
     din.ndcg_from_logits (rank of the FIRST positive = 1 + #{p_j > p_pos} +
     #{j before pos with p_j == p_pos}) on the rectangular (U, C) batch, as
-    row sums instead of segment scatters."""
+    row sums instead of segment scatters.
+
+    Ties are a deliberate deviation: the reference ranks with
+    np.argsort(-probs) (DIN.py:183), whose default sort is not stable, so the
+    rank of a positive tied with other candidates (f32 sigmoid saturates to 1.0
+    above logit ~17) depends on numpy's sort implementation and version.  Here
+    tied candidates keep column order (a stable descending sort), the same rule
+    as _top_and_ndcg's top-k.  Without ties the two agree exactly (pinned by
+    the din_dataset / din_rerank_c5 fixtures); tie cases are parity unpinned."""
     U, C = logits.shape
     col = torch.arange(C, device=logits.device, dtype=torch.int64)
     probs = torch.sigmoid(logits)

@@ -298,6 +298,82 @@ def din_rerank_fixture(name, seed, d=256, L=50, n_users=24, n_cand=201, n_items=
         )
 
 
+def din_rerank_cluster_fixture(name, seed, d=256, L=64, n_users=12, sizes=(403, 1187, 4410)):
+    """The candidate geometry the reference actually scores: Retrieval.py:28-34
+    hands each user the WHOLE nearest cluster (400-4,974 ragged candidates per
+    user, readme.md:20), scored by the reference's own EvalDataset + evaluate()
+    (DIN.py:21-57,155-193) at main()'s max_history L = 64 (DIN.py:237) and the
+    256-d corpus (embedding_generate.py:14).  Items are split into clusters
+    (member lists in corpus row order, as `ids[assign == i]` keeps them); user
+    u gets cluster u % len(sizes); for 3 of every 4 users the last click is a
+    member of that cluster (labelled), otherwise every label is 0.  The table
+    is bf16-representable (stored as bf16 bits) so the same numbers feed the
+    reference's fp32 forward and the bf16-table GPU path."""
+    with tempfile.TemporaryDirectory() as wd:
+        rng = np.random.default_rng(seed)
+        n_items = int(sum(sizes))
+        ids = rng.choice(np.arange(1000, 1000 + 10 * n_items), size=n_items, replace=False)
+        table = torch.from_numpy(rng.standard_normal((n_items, d)).astype(np.float32) * 0.5).to(torch.bfloat16)
+        table_bits = table.view(torch.int16).numpy().view(np.uint16).copy()
+        table = table.float().numpy()
+        emb = {int(a): table[i] for i, a in enumerate(ids)}
+        assign = np.repeat(np.arange(len(sizes)), sizes)
+        rng.shuffle(assign)
+        members = [np.nonzero(assign == c)[0] for c in range(len(sizes))]  # corpus row order
+        test_clicks, test_recs, user_cluster = {}, {}, []
+        for u in range(n_users):
+            c = u % len(sizes)
+            n = int(rng.integers(2, L + 12))  # 1..L+10 history clicks: short, full and truncated
+            rows = [int(x) for x in rng.choice(n_items, size=n, replace=False)]
+            if u % 4 != 3:
+                last = int(rng.choice(members[c]))
+                rows = [r for r in rows if r != last][: n - 1] + [last]
+            else:
+                rows = [r for r in rows if assign[r] != c] or [int(np.nonzero(assign != c)[0][0])] * 2
+            test_clicks[9000 + u] = [int(ids[r]) for r in rows]
+            test_recs[9000 + u] = ids[members[c]].astype(np.int64)
+            user_cluster.append(c)
+        _write_news(wd, emb, {1: [int(ids[0]), int(ids[1])]}, test_clicks, test_recs)
+        ref = _import_ref("DIN", wd)
+        torch.manual_seed(seed)
+        model = ref.DIN(d, 128, 32, 0.36)
+        _random_bn_stats(model, torch.Generator().manual_seed(seed + 1))
+        ev = ref.EvalDataset(L)
+        loader = torch.utils.data.DataLoader(ev, batch_size=8, shuffle=False, num_workers=0,
+                                             collate_fn=ref.custom_collate_fn)
+        ev_loss, ev_ndcg = ref.evaluate(model, loader, torch.nn.BCEWithLogitsLoss(), torch.device("cpu"), 5)
+        per_logits, per_ndcg = [], []
+        model.eval()
+        with torch.no_grad():
+            for b in loader:
+                for i in range(len(b["uid"])):
+                    c = b["cand_embs"][i]
+                    lg = model(c, b["history_emb"][i].unsqueeze(0).expand(c.size(0), -1, -1)).view(-1)
+                    per_logits.append(lg.numpy())
+                    probs = torch.sigmoid(lg).numpy()
+                    labs = b["labels"][i].numpy()
+                    nd = 0.0
+                    for rank, idx in enumerate(np.argsort(-probs)[:5], start=1):  # DIN.py:183-188
+                        if labs[idx] == 1:
+                            nd = 1 / np.log2(rank + 1)
+                            break
+                    per_ndcg.append(nd)
+        assert abs(float(np.mean(per_ndcg)) - ev_ndcg) < 1e-12
+        row_of = {int(a): i for i, a in enumerate(ids)}
+        np.savez_compressed(
+            os.path.join(OUT, f"{name}.npz"),
+            d=d, L=L, A=128, F=32, item_ids=ids.astype(np.int64), table_bf16=table_bits,
+            cluster_sizes=np.asarray(sizes, np.int64), cluster_rows=np.concatenate(members).astype(np.int32),
+            user_cluster=np.asarray([user_cluster[s["uid"] - 9000] for s in ev.data], np.int64),
+            ev_uid=np.array([s["uid"] for s in ev.data], np.int64),
+            ev_hist_rows=_pad_hist([[row_of[int(a)] for a in s["history"]] for s in ev.data], L).astype(np.int32),
+            ev_cand_len=np.array([len(s["candidates"]) for s in ev.data], np.int64),
+            ev_lab=np.concatenate([np.asarray(s["labels"], np.int8) for s in ev.data]),
+            ev_loss=np.float64(ev_loss), ev_ndcg=np.float64(ev_ndcg),
+            ev_logits=np.concatenate(per_logits), ev_ndcg_user=np.array(per_ndcg, np.float64), **_sd(model),
+        )
+
+
 def embedding_fixture(name, seed, n_articles=48):
     """ArticleEmbeddingModel + inference() (embedding_generate.py:51-65,109-131)."""
     with tempfile.TemporaryDirectory() as wd:
@@ -398,6 +474,9 @@ def main():
     if sys.argv[1:] == ["embedding_train"]:  # regenerate only the triplet-training fixture
         embedding_train_fixture("embedding_train", seed=18)
         return
+    if sys.argv[1:] == ["din_rerank_cluster"]:  # regenerate only the whole-cluster re-rank fixture
+        din_rerank_cluster_fixture("din_rerank_cluster", seed=19)
+        return
     din_forward_fixture("din_fwd_c1", d=64, A=32, F=32, B=64, L=20, n_items=300, seed=11)
     din_forward_fixture("din_fwd_c3", d=128, A=128, F=32, B=96, L=50, n_items=600, seed=12)
     din_train_fixture("din_train_c1", d=64, A=32, F=32, B=48, L=20, n_items=300, seed=13)
@@ -406,6 +485,7 @@ def main():
     embedding_fixture("embedding_infer", seed=16)
     din_rerank_fixture("din_rerank_c5", seed=17)
     embedding_train_fixture("embedding_train", seed=18)
+    din_rerank_cluster_fixture("din_rerank_cluster", seed=19)
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))

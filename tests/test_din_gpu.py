@@ -422,21 +422,20 @@ def _eval_batches(table32, n_users, L, C, seed, dev):
 def test_fit_epoch_driver_matches_eager_main_loop(gpu, tmp_path, sched):
     """din.fit (DIN.py:225-257 on the fused step, lr read from a device scalar)
     vs the reference's main() loop run eagerly with torch.optim.Adam and the
-    same scheduler, batch order (drop_last) and evaluate().
+    same scheduler, batch order and evaluate(); the last partial batch (12
+    rows) is trained on by both, as the reference's DataLoader keeps it.
 
     Checked exactly: the lr of every epoch equals what a torch scheduler fed
     fit's own validation losses produces (StepLR(gamma 0.5) forces a change
     every epoch), and the best-NDCG checkpoint (weights_only=True) reproduces
-    the best epoch's NDCG.  Checked loosely: per-epoch train / val losses vs
-    the eager loop, 2e-2 abs.  The two runs use different bf16 attention
-    kernels; over 51 Adam steps at lr 5e-3 on B = 64 their parameters drift
-    apart by ~3e-2 (BN running statistics ~2e-2) while both train (one-step
-    numerics are pinned tightly in test_fused_train_step_matches_eager and
-    tests/test_din_bf16_oracle.py)."""
+    the best epoch's NDCG.  Per-epoch train / val losses vs the eager loop:
+    1e-3 abs (the two runs use different bf16 attention kernels and head
+    reductions, so rounding differs; one-step numerics are pinned tightly in
+    test_fused_train_step_matches_eager and tests/test_din_bf16_oracle.py)."""
     from newsrecommend_amd.din import DIN, evaluate, fit
 
     dev, table, hist, tgt, lab, ma, mb = _setup_fused(0.0, d=64, L=20)
-    rows = 1100  # 17 full batches of 64, 12 rows dropped
+    rows = 1100  # 17 full batches of 64 + a partial batch of 12
     hist, tgt, lab = hist[:rows], tgt[:rows], lab[:rows]
     ev = _eval_batches(table.float(), 20, 20, 30, seed=8, dev=dev)
     factory = None if sched == "plateau" else (lambda o: torch.optim.lr_scheduler.StepLR(o, 1, gamma=0.5))
@@ -463,7 +462,7 @@ def test_fit_epoch_driver_matches_eager_main_loop(gpu, tmp_path, sched):
         mb.train()
         perm = torch.randperm(rows, generator=gen, device=dev)
         losses = []
-        for b in range(rows // 64):
+        for b in range(-(-rows // 64)):
             idx = perm[b * 64:(b + 1) * 64]
             opt.zero_grad()
             loss = crit(mb.forward_ids(table, tgt[idx], hist[idx]), lab[idx])
@@ -474,10 +473,53 @@ def test_fit_epoch_driver_matches_eager_main_loop(gpu, tmp_path, sched):
         vl, nd = evaluate(mb, ev, crit, dev, 5)
         sch.step(vl) if factory is None else sch.step()
         h = hist_f[e]
-        assert abs(h["train_loss"] - float(np.mean(losses))) < 2e-2, (e, h, np.mean(losses))
-        assert abs(h["val_loss"] - vl) < 2e-2, (e, h, vl)
+        print(f"epoch {e}: train {h['train_loss']:.6f} vs {float(np.mean(losses)):.6f}, "
+              f"val {h['val_loss']:.6f} vs {vl:.6f}")
+        assert abs(h["train_loss"] - float(np.mean(losses))) < 1e-3, (e, h, np.mean(losses))
+        assert abs(h["val_loss"] - vl) < 1e-3, (e, h, vl)
     assert max(h["ndcg"] for h in hist_f) > 0
     m2 = DIN(64, 64, 32, 0.0)
     m2.load_state_dict(torch.load(ck, weights_only=True))  # the reference's checkpoint format
     _, nd_ck = evaluate(m2.to(dev), ev, crit, dev, 5)
     assert nd_ck == pytest.approx(max(h["ndcg"] for h in hist_f), abs=1e-12)
+
+
+@pytest.mark.parametrize("n", [100_003, 200_000])
+def test_clip_adam_clipping_many_blocks_matches_torch(gpu, n):
+    """nrk_clip_adam with the norm far above max_norm (clipping active) over
+    many 1024-element blocks (100_003: the one-launch form, 98 blocks; 200_000:
+    the two-launch form) == torch clip_grad_norm_ + Adam applied to the
+    UNCLIPPED gradients: the stored (clipped) gradients and the parameters of
+    three steps.  Every block must see the same norm (the one-launch form reads
+    all of g in every block and stores the clipped values only after the last
+    block has read them)."""
+    from newsrecommend_amd import _lib
+
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(5)
+    P = torch.randn(n, generator=g, device=dev)
+    M = torch.zeros(n, device=dev)
+    V = torch.zeros(n, device=dev)
+    step = torch.zeros(1, device=dev)
+    lr_t = torch.full((1,), 1e-2, device=dev)
+    sz = _lib.c_size(0)
+    L = _lib.load()
+    _lib.check(L.nrk_clip_adam_workspace(n, sz), "clip_adam_workspace")
+    ws = torch.zeros(sz.value, dtype=torch.uint8, device=dev)
+    ref = torch.nn.Parameter(P.clone())
+    opt = torch.optim.Adam([ref], lr=1e-2, weight_decay=1e-3)
+    for s in range(3):
+        G = torch.randn(n, generator=g, device=dev) * (50.0 + 10 * s)  # norm ~ 1.6e4 >> max_norm 1
+        ref.grad = G.clone()
+        _lib.check(L.nrk_clip_adam(_lib.ptr(P), _lib.ptr(G), _lib.ptr(M), _lib.ptr(V), n, _lib.ptr(step), 1e-2,
+                                   _lib.ptr(lr_t), 0.9, 0.999, 1e-8, 1e-3, 1.0, _lib.ptr(ws), ws.numel(),
+                                   _lib.stream(dev)), "clip_adam")
+        norm = torch.nn.utils.clip_grad_norm_([ref], 1.0)
+        assert norm.item() > 1e3
+        opt.step()
+        torch.cuda.synchronize()
+        assert (G.norm() - 1.0).abs().item() < 1e-5, (s, G.norm().item())
+        assert torch.allclose(G, ref.grad, rtol=1e-5, atol=1e-9), (s, (G - ref.grad).abs().max().item())
+        assert torch.allclose(P, ref.detach(), rtol=1e-5, atol=1e-6), (s, (P - ref.detach()).abs().max().item())
+    assert step.item() == 3.0
+    assert int(ws[2048:2052].view(torch.int32).item()) == 0  # the ticket is left at zero

@@ -43,3 +43,22 @@ def test_world2_sharded_search_and_dp_hook(gpu, tmp_path):
         assert x["dp_grad_rel_err"] < 1e-6, x
         assert x["dp_replica_param_diff"] == 0.0, x
     assert res[0]["flat0_local_rows"] + res[1]["flat0_local_rows"] == 50_001
+
+
+def test_rccl_branch_world1(gpu, tmp_path):
+    """The RCCL (`nccl` backend) branches of newsrecommend_amd.dist on device
+    buffers, at world 1 on the one-GPU box (RCCL refuses two ranks on one
+    card): all_gather_results, scatter_results and all_reduce_mean_ equal the
+    gloo branches bit for bit, and the gradient all_reduce captured inside the
+    FusedTrainStep graph leaves the steps bit-identical to un-hooked ones."""
+    out = tmp_path / "rccl.json"
+    env = dict(os.environ, PYTHONPATH=ROOT, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0",
+               WORLD_SIZE="1", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "rccl_world1_worker.py"), str(out)], env=env,
+                       capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    x = json.load(open(out))
+    assert x["backend"] == "nccl" and x["gloo_backend"] == "gloo", x
+    for key in ("all_gather_device", "all_gather_equal", "scatter_equal", "merge_equal", "all_reduce_equal",
+                "dp_graph_equal", "dp_graph_loss_equal"):
+        assert x[key], (key, x)

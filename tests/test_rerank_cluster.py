@@ -1,0 +1,153 @@
+"""The candidate geometry the reference actually scores (Retrieval.py:28-34:
+each user re-ranks the WHOLE nearest cluster, 400-4,974 ragged candidates,
+readme.md:20) through the shared-history re-rank, against
+
+  * the reference's own EvalDataset + evaluate() (fixture din_rerank_cluster,
+    made by tests/golden/make_golden.py from DIN.py: d 256, L 64 = main()'s
+    max_history, clusters of 403 / 1187 / 4410 candidates),
+  * the float64 oracle fed the kernels' inputs ("emulated", W1k in bf16) on a
+    candidate sample of every user.
+
+Tolerances as tests/test_din_bf16_oracle.py: logits 2e-2 abs vs the
+reference, 1e-3 vs the emulated oracle; NDCG@5 per user equal wherever the
+positive's reference logit is more than 2x the tolerance away from every
+other candidate's (rank well defined); mean BCE within 1e-2 of evaluate()'s.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from tests.conftest import GOLDEN
+from tests.test_din_bf16_oracle import _params_f64, _rank_ambiguous, _rerank_oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _fixture(dev):
+    from newsrecommend_amd.din import DIN
+
+    z = np.load(os.path.join(GOLDEN, "din_rerank_cluster.npz"))
+    d, L = int(z["d"]), int(z["L"])
+    table = torch.from_numpy(z["table_bf16"].view(np.int16)).view(torch.bfloat16).to(dev)
+    model = DIN(d, int(z["A"]), int(z["F"]), 0.36)
+    model.load_state_dict({k[4:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("sd::")})
+    model = model.to(dev).eval()
+    sizes = z["cluster_sizes"]
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    return z, table, model, off, L
+
+
+def test_rerank_whole_cluster_vs_reference_evaluate(gpu):
+    from newsrecommend_amd.pipeline import ndcg_at_k, rerank
+
+    dev = torch.device("cuda")
+    z, table, model, off, L = _fixture(dev)
+    rows = z["cluster_rows"]
+    uc = z["user_cluster"]
+    cl = z["ev_cand_len"]
+    U, Cmax = len(uc), int(cl.max())
+    assert Cmax == max(z["cluster_sizes"]) and min(cl) == min(z["cluster_sizes"])
+    cand = np.full((U, Cmax), -1, np.int32)  # ragged whole-cluster lists padded to the longest
+    for u in range(U):
+        cand[u, :cl[u]] = rows[off[uc[u]]:off[uc[u] + 1]]
+    hist = torch.from_numpy(z["ev_hist_rows"]).to(dev)
+    assert hist.shape[1] == L == 64
+    logits = rerank(model, table, hist, torch.from_numpy(cand).to(dev))
+    assert rerank.path == "shared", rerank.path
+    lg = logits.cpu().numpy()
+    lab_flat, ref_flat = z["ev_lab"], z["ev_logits"]
+    seg = np.concatenate([[0], np.cumsum(cl)])
+    labels = np.zeros((U, Cmax), bool)
+    worst, losses = 0.0, []
+    for u in range(U):
+        got, ref = lg[u, :cl[u]], ref_flat[seg[u]:seg[u + 1]]
+        assert np.isneginf(lg[u, cl[u]:]).all()
+        worst = max(worst, float(np.abs(got - ref).max()))
+        labels[u, :cl[u]] = lab_flat[seg[u]:seg[u + 1]] == 1
+        y = labels[u, :cl[u]].astype(np.float64)
+        x = got.astype(np.float64)
+        losses.append(np.mean(np.maximum(x, 0) - x * y + np.log1p(np.exp(-np.abs(x)))))
+    print(f"whole-cluster re-rank: logits max abs err vs evaluate() {worst:.3g}, "
+          f"mean BCE {np.mean(losses):.6f} vs {float(z['ev_loss']):.6f}")
+    assert worst < 2e-2, worst
+    assert abs(float(np.mean(losses)) - float(z["ev_loss"])) < 1e-2
+    nd = ndcg_at_k(logits, torch.from_numpy(labels).to(dev), 5).cpu().numpy()
+    for u in range(U):
+        ref = ref_flat[seg[u]:seg[u + 1]]
+        lab_u = lab_flat[seg[u]:seg[u + 1]].astype(np.int64)
+        assert nd[u] == z["ev_ndcg_user"][u] or _rank_ambiguous(ref, lab_u, 2e-2), (u, nd[u], z["ev_ndcg_user"][u])
+
+
+def test_rerank_whole_cluster_vs_oracle_and_grouped(gpu):
+    """The same users through pipeline.rerank_clusters (users grouped by
+    cluster, no padding): logits bit-identical to the padded batch, 1e-3 of
+    the emulated fp64 oracle on every 37th candidate, per-user BCE and NDCG
+    equal to the padded path's."""
+    from newsrecommend_amd.pipeline import ndcg_at_k, rerank, rerank_clusters
+
+    dev = torch.device("cuda")
+    z, table, model, off, L = _fixture(dev)
+    rows_np, uc, cl = z["cluster_rows"], z["user_cluster"], z["ev_cand_len"]
+    hist = torch.from_numpy(z["ev_hist_rows"]).to(dev)
+    U, Cmax = len(uc), int(cl.max())
+    cand = np.full((U, Cmax), -1, np.int32)
+    for u in range(U):
+        cand[u, :cl[u]] = rows_np[off[uc[u]]:off[uc[u] + 1]]
+    padded = rerank(model, table, hist, torch.from_numpy(cand).to(dev)).cpu().numpy()
+    # the last click's row: labels are one-hot at its first occurrence in the cluster
+    seg = np.concatenate([[0], np.cumsum(cl)])
+    last = np.full(U, -1, np.int32)
+    for u in range(U):
+        pos = np.flatnonzero(z["ev_lab"][seg[u]:seg[u + 1]] == 1)
+        if pos.size:
+            last[u] = cand[u, pos[0]]
+    res = rerank_clusters(model, table, hist, torch.from_numpy(uc).to(dev), torch.from_numpy(off).to(dev),
+                          torch.from_numpy(rows_np).to(dev), torch.from_numpy(last).to(dev), k=5)
+    T = table.float().cpu().numpy().astype(np.float64)
+    p_emu = _params_f64(model, True)
+    worst = 0.0
+    for lg, us in zip(res["logits"], res["users"]):
+        lg, us = lg.cpu().numpy(), us.cpu().numpy()
+        for i, u in enumerate(us):
+            assert np.array_equal(lg[i], padded[u, :cl[u]]), u  # grouping changes nothing
+            sub = np.arange(0, cl[u], 37)
+            emu = _rerank_oracle(p_emu, T, z["ev_hist_rows"][u], cand[u, sub])
+            worst = max(worst, float(np.abs(lg[i, sub] - emu).max()))
+    print(f"whole-cluster re-rank vs emulated oracle: {worst:.3g}")
+    assert worst < 1e-3, worst
+    labels = np.zeros((U, Cmax), bool)
+    for u in range(U):
+        labels[u, :cl[u]] = z["ev_lab"][seg[u]:seg[u + 1]] == 1
+    nd_pad = ndcg_at_k(torch.from_numpy(padded).to(dev), torch.from_numpy(labels).to(dev), 5).cpu().numpy()
+    np.testing.assert_array_equal(res["ndcg"].cpu().numpy(), nd_pad)
+    loss = res["loss"].cpu().numpy()
+    for u in range(U):
+        x, y = padded[u, :cl[u]].astype(np.float64), labels[u, :cl[u]].astype(np.float64)
+        assert abs(loss[u] - np.mean(np.maximum(x, 0) - x * y + np.log1p(np.exp(-np.abs(x))))) < 1e-6
+
+
+def test_cluster_candidates_batched(gpu):
+    """pipeline.cluster_candidates (Retrieval.py:28-34 as ONE search) == the
+    nearest centroid by exact squared L2 per profile, and the lists are the
+    clusters' member arrays."""
+    from newsrecommend_amd import faiss as nf
+    from newsrecommend_amd.pipeline import cluster_candidates
+
+    rng = np.random.default_rng(3)
+    cent = rng.standard_normal((300, 256)).astype(np.float32)
+    prof = (cent[rng.integers(0, 300, 2000)] + 0.3 * rng.standard_normal((2000, 256))).astype(np.float32)
+    lists = {c: np.arange(c * 10, c * 10 + 3 + c % 7) for c in range(300)}
+    index = nf.IndexFlatL2(256)
+    index.add(cent)
+    uids = list(range(7000, 9000))
+    got = cluster_candidates(index, lists, prof, uids)
+    d2 = ((prof.astype(np.float64)[:, None, :] - cent.astype(np.float64)[None]) ** 2).sum(-1)
+    near = d2.argmin(1)
+    assert list(got.keys()) == uids
+    for i, u in enumerate(uids):
+        np.testing.assert_array_equal(got[u], lists[int(near[i])])
+    got_fn = cluster_candidates(index, lambda c: lists[c], prof[:10], uids[:10])
+    for i, u in enumerate(uids[:10]):
+        np.testing.assert_array_equal(got_fn[u], lists[int(near[i])])
