@@ -501,6 +501,81 @@ def bench_e2e(args, rank, world, dev):
     return out
 
 
+def bench_retrieval_flow(args, rank, world, dev):
+    """Retrieval.py:1-36 -> finialize_retrieval.py -> DIN.py:155-193 at the
+    reference's own sizes: 364,047 x 256 article embeddings (synthetic mixture),
+    faiss Clustering(256, 300) with niter 80 and an IndexHNSWFlat(256, 32)
+    assignment index, index.search(xb, 1) -> cluster lists, 50,000 user
+    profiles -> nearest centroid (one IndexFlatL2 search) -> the WHOLE cluster
+    as candidates (ground truth appended when missing) -> DIN(256, 128, 32)
+    re-rank with max_history 64 -> per-user BCE + NDCG@5.  Users are split
+    over the ranks (replicas).  value = users/s of the candidate + re-rank +
+    NDCG stage (the reference's evaluate() loop); build_s = k-means + assignment."""
+    from newsrecommend_amd import faiss as nf
+    from newsrecommend_amd.data import clustered_corpus, zipf_ids
+    from newsrecommend_amd.din import DIN
+    from newsrecommend_amd.dist import shard_range
+    from newsrecommend_amd.pipeline import rerank_clusters
+
+    n, d, nlist, L = 364_047, 256, 300, 64
+    U = args.flow_users
+    xb = clustered_corpus(n, d, seed=1234, device=dev)
+    table = xb.to(torch.bfloat16)
+    barrier(world)
+    t0 = time.perf_counter()
+    clustering = nf.Clustering(d, nlist)
+    clustering.niter = 80
+    index = nf.IndexHNSWFlat(d, 32, device=dev)
+    clustering.train(xb, index)
+    centroids = clustering.centroids.reshape(nlist, d)
+    _, assign = index.search_device(xb, 1)  # Retrieval.py:21
+    assign = assign[:, 0]
+    cluster_rows = torch.sort(assign, stable=True).indices.to(torch.int32)  # corpus row order inside a cluster
+    cluster_off = torch.zeros(nlist + 1, dtype=torch.int64, device=dev)
+    cluster_off[1:] = torch.cumsum(torch.bincount(assign, minlength=nlist), 0)
+    centroid_index = nf.IndexFlatL2(d, device=dev)
+    centroid_index.add(centroids)
+    torch.cuda.synchronize()
+    build_s = time.perf_counter() - t0
+    g = torch.Generator(device=dev).manual_seed(21)
+    hist = zipf_ids(U * L, n, generator=g, device=dev).view(U, L)
+    lens = torch.randint(1, L + 1, (U,), generator=g, device=dev)
+    hist = torch.where(torch.arange(L, device=dev)[None] < lens[:, None], hist, torch.full_like(hist, -1))
+    valid = (hist >= 0).unsqueeze(-1)
+    profiles = (xb[hist.clamp_min(0).long()] * valid).sum(1) / valid.sum(1)  # mean of the clicked embeddings
+    last = zipf_ids(U, n, generator=g, device=dev)
+    lo, hi = shard_range(U, rank, world)
+    torch.manual_seed(42)
+    model = DIN(d, 128, 32, 0.36).to(dev).eval()
+
+    def stage():
+        _, I = centroid_index.search_device(profiles[lo:hi], 1)  # Retrieval.py:28-34 as one search
+        return rerank_clusters(model, table, hist[lo:hi], I[:, 0], cluster_off, cluster_rows, last[lo:hi], k=5,
+                               batch_samples=1 << 21, append_missing=True)
+
+    res = stage()  # warm-up
+    barrier(world)
+    t0 = time.perf_counter()
+    res = stage()
+    barrier(world)
+    el = max_over_ranks(time.perf_counter() - t0, world, dev)
+    sizes = torch.diff(cluster_off)
+    _, Iu = centroid_index.search_device(profiles[lo:hi], 1)
+    cand_per_user = sizes[Iu[:, 0]].double()
+    out = {"metric": "Retrieval.py -> evaluate() users/s (whole-cluster candidates)", "value": U / el,
+           "unit": "users/s", "ms": el * 1e3, "build_s": build_s,
+           "config": f"{n}x{d} corpus, Clustering(k={nlist}, niter=80) + IndexHNSWFlat(M=32) assignment, {U} users, "
+                     f"whole nearest cluster + GT appended, DIN(256, 128, 32), L={L}, bf16 table",
+           "cluster_size_min_mean_max": [int(sizes.min()), float(sizes.double().mean()), int(sizes.max())],
+           "candidates_per_user_mean": float(cand_per_user.mean()),
+           "rerank_samples_per_s": float(cand_per_user.sum()) * world / el,
+           "rerank_path": __import__("newsrecommend_amd.pipeline", fromlist=["rerank"]).rerank.path,
+           "ndcg_at_5_mean_rank0": float(res["ndcg"].mean()), "loss_mean_rank0": float(res["loss"].mean())}
+    del xb, table, index, centroid_index
+    torch.cuda.empty_cache()
+    return out
+
+
 # ------------------------------------------------------------- embedding --
 FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense fp32 MFMA (no TF32 on gfx950)
 
@@ -697,18 +772,43 @@ def bench_din(args, rank, world, dev):
     }
     if fused and world == 1 and args.din_sweep:
         out["batch_sweep"] = {str(bs): _din_rate(table, hist, tgt, lab, d, A, F, bs, dev) for bs in (16384, 65536)}
+    if fused and world == 1 and args.din_d256:
+        out["d256"] = _din_d256(args, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = _cpu_din(args, n_items, L, d, A, F)
     return out
 
 
-def _din_rate(table, hist, tgt, lab, d, A, F, B, dev, steps=10):
+def _din_d256(args, dev):
+    """The reference's own training shape (DIN.py:16 EMBED_DIM = 256 from the
+    corpus of embedding_generate.py:14; main(): A 128, F 32, max_history 64,
+    DIN.py:233-237) on the fused step: its batch 64 (DIN.py:236) and the
+    bench's 4096, bf16 table of --din-items rows, synthetic click rows."""
+    from newsrecommend_amd.data import synthetic_click_rows
+
+    d, L, A, F = 256, 64, 128, 32
+    g = torch.Generator(device=dev).manual_seed(2)
+    table = (torch.randn((args.din_items, d), generator=g, device=dev) * 0.5).to(torch.bfloat16)
+    hist, tgt, lab = synthetic_click_rows(1_000_000, args.din_items, L, seed=8, device=dev)
+    out = {"config": f"d={d}, A={A}, F={F}, L={L}, dropout 0.36, bf16 table {args.din_items}x{d}"}
+    for B in (64, 4096):
+        path = []
+        rate = _din_rate(table, hist, tgt, lab, d, A, F, B, dev, steps=200 if B == 64 else 40, path=path)
+        out[f"B={B}"] = {"samples_per_s": rate, "us_per_step": B / rate * 1e6, "path": path[0]}
+    del table, hist, tgt, lab
+    torch.cuda.empty_cache()
+    return out
+
+
+def _din_rate(table, hist, tgt, lab, d, A, F, B, dev, steps=10, path=None):
     """samples/s of the graphed fused train step at batch B (fresh model)."""
     from newsrecommend_amd.din import DIN, FusedTrainStep
 
     torch.manual_seed(43)
     m = DIN(d, A, F, 0.36).to(dev)
     tr = FusedTrainStep(m, table, hist, tgt, lab, B, lr=1.62e-3, weight_decay=8.96e-5, clip=1.0)
+    if path is not None:
+        path.append(tr.path)
     perm = torch.randperm(hist.shape[0], device=dev)
     nb = hist.shape[0] // B
     for s in range(3):
@@ -759,7 +859,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["flat", "din", "ivf", "e2e", "embed", "all"], default="all")
+    ap.add_argument("--workload", choices=["flat", "din", "ivf", "e2e", "flow", "embed", "all"], default="all")
     ap.add_argument("--nb", type=int, default=1_000_000)
     ap.add_argument("--d", type=int, default=128)
     ap.add_argument("--nq", type=int, default=4096)
@@ -772,12 +872,14 @@ def main():
     ap.add_argument("--e2e-nb", type=int, default=10_000_000)
     ap.add_argument("--e2e-users", type=int, default=4096)
     ap.add_argument("--e2e-k", type=int, default=200)
+    ap.add_argument("--flow-users", type=int, default=50_000, help="users of the Retrieval.py -> evaluate() record")
     ap.add_argument("--din-rows", type=int, default=5_000_000)
     ap.add_argument("--din-items", type=int, default=2_000_000)
     ap.add_argument("--din-batch", type=int, default=4096)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--din-eager", action="store_true", help="no HIP-graph capture of the DIN train step")
     ap.add_argument("--din-sweep", type=int, default=1, help="also report the fused step at B=16384, 65536")
+    ap.add_argument("--din-d256", type=int, default=1, help="also report the fused step at d=256, L=64 (B=64, 4096)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-n1", action="store_true", help="skip the north_star 10M x 256 k=5 retrieval record")
     ap.add_argument("--no-flat-l2", action="store_true", help="skip the IndexFlatL2 10M x 128 record")
@@ -806,6 +908,12 @@ def main():
             if "cpu_baseline" in r:
                 rec["cpu_baseline"] = r["cpu_baseline"]
         rec["ivf"] = r
+        torch.cuda.empty_cache()
+    if args.workload in ("e2e", "flow", "all"):
+        r = bench_retrieval_flow(args, rank, world, dev)
+        if args.workload == "flow":
+            rec.update({"metric": r["metric"], "value": r["value"], "unit": r["unit"], "ms_per_step": r["ms"]})
+        rec["retrieval_py_flow"] = r
         torch.cuda.empty_cache()
     if args.workload in ("e2e", "all"):
         r = bench_e2e(args, rank, world, dev)

@@ -42,6 +42,8 @@ extern "C" {
 #define NRK_DTYPE_F32 0
 #define NRK_DTYPE_BF16 1
 
+struct nrk_din_head_params_s; /* typedef'd as nrk_din_head_params below */
+
 const char* nrk_last_error(void);
 int nrk_version(void);
 
@@ -157,6 +159,19 @@ int nrk_din_attn_bwd_params(const void* table, const int32_t* hist_ids, int64_t 
                             float* gW1, float* gb1, float* gw2, float* gb2, float* dU,
                             void* ws, size_t ws_bytes, void* stream);
 
+/* The same backward, forming dpooled itself from the train-mode head's state
+ * instead of reading it (the fused train step: one launch fewer, no dpooled
+ * round trip): dpooled = BN0-backward of da1 W1[:, d:] for the pooled columns,
+ * from the forward's pooled [B][d] f32, the head's parameters (fc.0 weight,
+ * fc.1 weight) and the workspace nrk_din_head_train left with dpooled == NULL
+ * (F = 32).  d in {64, 128}, L <= 64, L * d >= 4096 (the 8-wave backward). */
+int nrk_din_attn_bwd_params_head(const void* table, const int32_t* hist_ids, int64_t n_table, int32_t dtype,
+                                 const float* q, const float* U, const void* W1k, const float* w2,
+                                 int32_t B, int32_t L, int32_t d, int32_t A, const float* pooled, const float* alpha,
+                                 int32_t F, const struct nrk_din_head_params_s* hp, const void* head_ws,
+                                 size_t head_ws_bytes, float* gW1, float* gb1, float* gw2, float* gb2,
+                                 void* ws, size_t ws_bytes, void* stream);
+
 /* One train batch from a device-resident click log (replaces TrainDataset.
  * __getitem__'s CPU gather, DIN.py:81-92, and the query GEMM of DIN.py:105-106):
  *   idx [B] int64 rows of the log; hist_all [n_rows][L] int32, tgt_all [n_rows]
@@ -164,7 +179,7 @@ int nrk_din_attn_bwd_params(const void* table, const int32_t* hist_ids, int64_t 
  * Out: hist [B][L] int32, q [B][d] f32 (= table[target], id < 0 -> zeros),
  *   y [B] f32, U [B][A] f32 = q W1[:, :d]^T + b1 (products exact in f32),
  *   W1k_bf16 [A][d] = bf16(W1[:, d:]).  Rows outside [0, n_rows) give an
- *   empty history, a zero query and label 0.  d in {64, 128}. */
+ *   empty history, a zero query and label 0.  d in {64, 128, 256}. */
 int nrk_din_batch(const int64_t* idx, int32_t B, const int32_t* hist_all, const int32_t* tgt_all,
                   const float* lab_all, int64_t n_rows, int32_t L, const void* table, int64_t n_table,
                   int32_t dtype, int32_t d, const float* W1, const float* b1, int32_t A, int32_t* hist,
@@ -257,9 +272,10 @@ int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe, int32_t np
  * gradients are WRITTEN (not accumulated).  Dropout masks are a counter-based
  * hash of (seed, *step, layer, row, col).  Outputs: logits [B], loss [1]
  * (mean BCE), dpooled [B][ld] (the gradient w.r.t. pooled, the attention
- * backward's input; columns d..ld-1 zeroed).  B must be a multiple of 32,
+ * backward's input; columns d..ld-1 zeroed; may be NULL with F = 32, then
+ * nrk_din_attn_bwd_params_head forms it).  B must be a multiple of 32,
  * 2d <= 512, F even <= 64. */
-typedef struct {
+typedef struct nrk_din_head_params_s {
   const float *bn0_w, *bn0_b, *fc1_w, *fc1_b, *bn1_w, *bn1_b, *fc2_w, *fc2_b, *bn2_w, *bn2_b, *fc3_w, *fc3_b;
   float *bn0_rm, *bn0_rv, *bn1_rm, *bn1_rv, *bn2_rm, *bn2_rv;
   int64_t *bn0_nb, *bn1_nb, *bn2_nb;
@@ -267,6 +283,11 @@ typedef struct {
       *g_fc3_w, *g_fc3_b;
 } nrk_din_head_params;
 int nrk_din_head_workspace(int32_t B, int32_t d, int32_t F, size_t* ws_bytes);
+/* Views into a head workspace after nrk_din_head_train (F = 32 path): BN0's
+ * {mean [2d], invstd [2d]}, its backward sums {sum dh0 [2d], sum dh0 xhat0
+ * [2d]} (f64) and da1 [B][F] (the gradient at fc.1's output). */
+int nrk_din_head_ws_views(int32_t B, int32_t d, int32_t F, const void* ws, size_t ws_bytes,
+                          const float** stat0, const double** sum5, const float** da1);
 int nrk_din_head_train(const float* q, const float* pooled, int64_t ld_pooled, const float* labels,
                        int32_t B, int32_t d, int32_t F, float momentum, float eps, float p_drop,
                        uint64_t seed, const float* step, const nrk_din_head_params* params,

@@ -57,6 +57,10 @@ SIGNATURES = {
                                         c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_size, c_p]),
     "nrk_din_attn_bwd_params": (ctypes.c_int, [c_p, c_p, c_i64, c_i32, c_p, c_p, c_p, c_p, c_i32, c_i32, c_i32, c_i32,
                                                c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_size, c_p]),
+    "nrk_din_attn_bwd_params_head": (ctypes.c_int, [c_p, c_p, c_i64, c_i32, c_p, c_p, c_p, c_p, c_i32, c_i32, c_i32,
+                                                    c_i32, c_p, c_p, c_i32, c_p, c_p, c_size, c_p, c_p, c_p, c_p, c_p,
+                                                    c_size, c_p]),
+    "nrk_din_head_ws_views": (ctypes.c_int, [c_i32, c_i32, c_i32, c_p, c_size, c_p, c_p, c_p]),
     "nrk_din_batch": (ctypes.c_int, [c_p, c_i32, c_p, c_p, c_p, c_i64, c_i32, c_p, c_i64, c_i32, c_i32, c_p, c_p,
                                      c_i32, c_p, c_p, c_p, c_p, c_p, c_p]),
     "nrk_din_rerank_attn": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_i32, c_i32, c_p, c_i32, c_i32, c_i32, c_p, c_p,

@@ -364,6 +364,11 @@ __global__ __launch_bounds__(256, 2) void din_fwd_wave_kernel(const uint16_t* __
       cv0 = nv0;
       cv1 = nv1;
       load_ids(bn + nw, n0, n1, nv0, nv1);
+    } else {
+      // the next sample's ids: loads issued now, consumed (ballots) after this
+      // sample's math, so their latency hides behind it
+      n0 = (bn < B && lane < L) ? ids[(int64_t)bn * L + lane] : -1;
+      n1 = (bn < B && lane + 64 < L) ? ids[(int64_t)bn * L + lane + 64] : -1;
     }
     const float* us = wbase + sl * slot_f;
     const uint16_t* img = reinterpret_cast<const uint16_t*>(us + AP);
@@ -476,9 +481,217 @@ __global__ __launch_bounds__(256, 2) void din_fwd_wave_kernel(const uint16_t* __
     if constexpr (NBUF == 2) {
       sl ^= 1;
     } else {
-      load_ids(bn, c0, c1, cv0, cv1);
+      c0 = n0;
+      c1 = n1;
+      cv0 = __ballot(c0 >= 0 && c0 < n_table);
+      cv1 = __ballot(c1 >= 0 && c1 < n_table);
       if (bn < B) issue(bn, 0, c0, c1, cv0, cv1);
     }
+  }
+}
+
+// Forward at D = 256 (the reference's own training width, DIN.py:16 with the
+// 256-d corpus of embedding_generate.py:14): the W1k fragments of all A = 128
+// units would take 256 VGPRs, so a PAIR of waves shares one sample: wave half
+// hu keeps the unit tiles t = hu, hu + 2, ... (the d = 128 kernel's register
+// budget), both gather half of the key rows into the pair's LDS image, the
+// partial scores of the two halves meet in LDS (summed in a fixed order, so
+// both waves hold identical scores), both run the softmax, and each pools its
+// half of the 256 columns.  Four waves = two samples per workgroup, two
+// workgroups per CU (LDS).  Same math and padding-row compaction as
+// din_fwd_wave_kernel.
+template <int D, int NA>
+__global__ __launch_bounds__(256, 2) void din_fwd_pair_kernel(const uint16_t* __restrict__ table,
+                                                               const int32_t* __restrict__ ids, int64_t n_table,
+                                                               const float* __restrict__ U,
+                                                               const uint16_t* __restrict__ W1k,
+                                                               const float* __restrict__ w2, int B, int L,
+                                                               float* __restrict__ pooled,
+                                                               float* __restrict__ alpha) {
+  constexpr int CPR = D / 8, KS = D / 16, A = 32 * NA;
+  constexpr int NAH = (NA + 1) / 2;   // unit tiles per wave half
+  constexpr int DH = D / 2, DPL = DH / 64;  // pooled columns per wave half / per lane
+  static_assert(DPL == 2, "pair kernel: D = 256");
+  constexpr int AP = (A + 63) & ~63;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int pr = wv >> 1, hu = wv & 1;
+  const int r = lane & 31, h = lane >> 5;
+  const int Lp = (L + 31) & ~31;
+  // LDS: w2 [AP] | per pair {U row [AP] f32, key image [Lp][D] bf16} | per wave idtab [128] | per pair xch [2][128]
+  const int slot_f = AP + Lp * D / 2;
+  float* w2s = reinterpret_cast<float*>(smem);
+  float* us = w2s + AP + (size_t)pr * slot_f;
+  int32_t* idtab = reinterpret_cast<int32_t*>(w2s + AP + 2 * (size_t)slot_f) + wv * 128;
+  float* xch = reinterpret_cast<float*>(w2s + AP + 2 * (size_t)slot_f + 4 * 128) + pr * 256;
+  typedef __attribute__((address_space(3))) void* lds_ptr;
+  for (int i = threadIdx.x; i < A; i += 256) w2s[i] = w2[i];
+  __syncthreads();
+
+  bf16x8 wf[NAH][KS];
+#pragma unroll
+  for (int i = 0; i < NAH; ++i) {
+    const int t = hu + 2 * i < NA ? hu + 2 * i : 0;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+      wf[i][s] = *reinterpret_cast<const bf16x8*>(W1k + (int64_t)(32 * t + r) * D + 16 * s + 8 * h);
+  }
+
+  const int nw = gridDim.x * 2;  // samples in flight over the grid (one per pair)
+  auto load_ids = [&](int b, int32_t& i0, int32_t& i1, uint64_t& v0, uint64_t& v1) {
+    i0 = (b < B && lane < L) ? ids[(int64_t)b * L + lane] : -1;
+    i1 = (b < B && lane + 64 < L) ? ids[(int64_t)b * L + lane + 64] : -1;
+    v0 = __ballot(i0 >= 0 && i0 < n_table);
+    v1 = __ballot(i1 >= 0 && i1 < n_table);
+  };
+  // this wave's half of sample b's key pieces (compacted valid rows, then the
+  // padding row), and the U row (wave half 0)
+  auto issue = [&](int b, int32_t i0, int32_t i1, uint64_t v0, uint64_t v1) {
+    uint16_t* img = reinterpret_cast<uint16_t*>(us + AP);
+    const int n0 = __popcll(v0), nv = n0 + __popcll(v1);
+    const int ntile = (nv + (nv < L ? 1 : 0) + 31) >> 5;
+    const int npieces = 32 * ntile * CPR / 64;
+    {
+      const uint64_t below = (1ull << lane) - 1;
+      if ((v0 >> lane) & 1) idtab[__popcll(v0 & below)] = i0;
+      if ((v1 >> lane) & 1) idtab[n0 + __popcll(v1 & below)] = i1;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+    }
+    for (int u = hu; u < npieces; u += 2) {
+      const int p = u * 64 + lane;
+      const int row = p / CPR, pc = p % CPR;
+      const int cc = pc ^ kswz<CPR>(row);
+      const uint16_t* src = row < nv ? table + (int64_t)idtab[row] * D + cc * 8 : zero_row(b, row) + cc * 8;
+      __builtin_amdgcn_global_load_lds(src, (lds_ptr)(img + u * 64 * 8), 16, 0, 0);
+    }
+    if (hu == 0) {
+#pragma unroll
+      for (int u = 0; u < AP / 64; ++u) {
+        const int i = u * 64 + lane;
+        __builtin_amdgcn_global_load_lds(U + (int64_t)b * A + (i < A ? i : 0), (lds_ptr)(us + u * 64), 4, 0, 0);
+      }
+    }
+  };
+
+  // trip count uniform over the workgroup (barriers): pair 0's samples lead
+  const int b0 = blockIdx.x * 2;
+  int b = b0 + pr;
+  int32_t c0, c1;
+  uint64_t cv0, cv1;
+  load_ids(b, c0, c1, cv0, cv1);
+  if (b < B) issue(b, c0, c1, cv0, cv1);
+  for (int bl = b0; bl < B; bl += nw, b += nw) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // both halves of every pair's image (and U row) landed
+    const bool act = b < B;
+    const uint64_t sv0 = cv0, sv1 = cv1;
+    const int sn0 = __popcll(sv0), nv = sn0 + __popcll(sv1), npad = L - nv, nr = nv + (npad > 0 ? 1 : 0);
+    const int nct = act ? (nr + 31) >> 5 : 0;
+    const uint16_t* img = reinterpret_cast<const uint16_t*>(us + AP);
+    // ---- partial scores over this half's units
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (c < nct) {
+        const int row = 32 * c + r;
+        // k-outer: one key fragment live at a time, the half's unit tiles side by side
+        f32x16 acc[NAH];
+#pragma unroll
+        for (int i = 0; i < NAH; ++i) {
+          const int t = hu + 2 * i < NA ? hu + 2 * i : 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float4 uv = *reinterpret_cast<const float4*>(us + 32 * t + 8 * j + 4 * h);
+            acc[i][4 * j] = uv.x; acc[i][4 * j + 1] = uv.y; acc[i][4 * j + 2] = uv.z; acc[i][4 * j + 3] = uv.w;
+          }
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < KS; ++s2) {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(img + row * D + 8 * ((2 * s2 + h) ^ kswz<CPR>(row)));
+#pragma unroll
+          for (int i = 0; i < NAH; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[i][s2], kf, acc[i], 0, 0, 0);
+        }
+        float part = 0.f;
+#pragma unroll
+        for (int i = 0; i < NAH; ++i) {
+          const int t = hu + 2 * i;
+          if (t >= NA) continue;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float4 wv4 = *reinterpret_cast<const float4*>(w2s + 32 * t + 8 * j + 4 * h);
+            part = fmaf(wv4.x, fmaxf(acc[i][4 * j], 0.f), part);
+            part = fmaf(wv4.y, fmaxf(acc[i][4 * j + 1], 0.f), part);
+            part = fmaf(wv4.z, fmaxf(acc[i][4 * j + 2], 0.f), part);
+            part = fmaf(wv4.w, fmaxf(acc[i][4 * j + 3], 0.f), part);
+          }
+        }
+        part += __shfl_xor(part, 32, 64);
+        if (h == 0) xch[hu * 128 + row] = part;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();  // both halves' partial scores
+    float sc[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int row = 32 * c + r;
+      sc[c] = (c < nct && row < nr) ? xch[row] + xch[128 + row] : -INFINITY;
+    }
+    float m = fmaxf(fmaxf(sc[0], sc[1]), fmaxf(sc[2], sc[3]));
+    m = wave_max(m);
+    float e[4], sum = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int row = 32 * c + r;
+      e[c] = c < nct && row < nr ? expf(sc[c] - m) : 0.f;
+      sum += h == 0 ? (row < nv ? e[c] : (float)npad * e[c]) : 0.f;
+    }
+    sum = wave_sum(sum);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) e[c] = e[c] / sum;
+    if (act && hu == 0) {
+      auto erow = [&](int row) {
+        float v = 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float t = __shfl(e[c], row & 31, 64);
+          if ((row >> 5) == c) v = t;
+        }
+        return v;
+      };
+      const uint64_t below = (1ull << lane) - 1;
+      const bool ok0 = (sv0 >> lane) & 1, ok1 = (sv1 >> lane) & 1;
+      const float a0 = erow(ok0 ? __popcll(sv0 & below) : nv);
+      const float a1 = erow(ok1 ? sn0 + __popcll(sv1 & below) : nv);
+      if (lane < L) alpha[(int64_t)b * L + lane] = a0;
+      if (64 + lane < L) alpha[(int64_t)b * L + 64 + lane] = a1;
+    }
+    if (act) {  // ---- pooled, this half's DH columns
+      float acc2[DPL];
+#pragma unroll
+      for (int j = 0; j < DPL; ++j) acc2[j] = 0.f;
+      const int L8 = (nv + 7) & ~7;
+      for (int row0 = 0; row0 < L8; row0 += 8) {
+        const int c = row0 >> 5;
+        const float ec = c == 0 ? e[0] : c == 1 ? e[1] : c == 2 ? e[2] : e[3];
+        uint32_t u[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          u[i] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const unsigned char*>(img) +
+                                                    KImg<true, D>::off(row0 + i, DH * hu + 2 * lane));
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float al = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ec), (row0 + i) & 31));
+          acc2[0] = fmaf(al, __uint_as_float(u[i] << 16), acc2[0]);
+          acc2[1] = fmaf(al, __uint_as_float(u[i] & 0xFFFF0000u), acc2[1]);
+        }
+      }
+      *reinterpret_cast<float2*>(pooled + (int64_t)b * D + DH * hu + 2 * lane) = make_float2(acc2[0], acc2[1]);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();  // every read of the pair's image and exchange is done: refill
+    load_ids(b + nw, c0, c1, cv0, cv1);
+    if (b + nw < B) issue(b + nw, c0, c1, cv0, cv1);
   }
 }
 
@@ -895,6 +1108,20 @@ __device__ __forceinline__ void glds4_asm(const void* gsrc, uint32_t lds_dst) {
                : "memory");
 }
 
+// Where the fused train step's attention backward finds dpooled's inputs when
+// it forms dpooled itself (FDP): the head's state after nrk_din_head_train
+// (nrk_din_head_ws_views) and the forward's pooled rows.  stat0 / sum5 / bn0w /
+// w1 are indexed over the head's 2d input columns (the pooled half from d).
+struct DpSrc {
+  const float* pooled;  // [B][D]
+  const float* da1;     // [B][32]
+  const float* w1;      // fc.1 weight [32][2D]
+  const float* stat0;   // {mean [2D], invstd [2D]}
+  const double* sum5;   // {sum dh0 [2D], sum dh0 xhat0 [2D]}
+  const float* bn0w;    // fc.0 weight [2D]
+  float invB;
+};
+
 template <int D, int LP, int NSLOT>
 __global__ __launch_bounds__(256, 1) void din_bwd_deep_kernel(
     const uint16_t* __restrict__ table, const int32_t* __restrict__ ids, int64_t n_table, const float* __restrict__ U,
@@ -1128,18 +1355,21 @@ __global__ __launch_bounds__(256, 1) void din_bwd_deep_kernel(
 // units (us = w & 3) and split the sample's 32-row history tiles (rg = w >> 2
 // takes tiles rg, rg + 2, ...); each accumulates its rows' share of every
 // gradient, and the pairs are combined in a fixed order after the loop.
-template <int D, int LP, int NSLOT>
+template <int D, int LP, int NSLOT, bool FQ, bool FDP>
 __global__ __launch_bounds__(512, 1) void din_bwd_deep8_kernel(
     const uint16_t* __restrict__ table, const int32_t* __restrict__ ids, int64_t n_table, const float* __restrict__ U,
     const uint16_t* __restrict__ W1k, const float* __restrict__ w2, int B, int L, int A,
     const float* __restrict__ dpooled, const float* __restrict__ alpha, float* __restrict__ slabs,
-    const float* __restrict__ q, int dq, float* __restrict__ dUp, float* __restrict__ dummy) {
+    const float* __restrict__ q, int dq, float* __restrict__ dUp, float* __restrict__ dummy, DpSrc dps) {
   constexpr int CPR = D / 8, KS = D / 16, NCT = D / 32, NC = LP / 32;
   constexpr int NPW = LP * CPR / 512;  // key-image DMA pieces per wave
   constexpr int N_IDS = LP > 64 ? 2 : 1;
-  constexpr int N_D = 1 + NPW + 1 + N_IDS;  // per wave and iteration: the dU store, keys, one small piece, ids
+  // per wave and iteration: [the dU store,] keys, one small piece, ids.  FQ: dW1q is folded in here
+  // (the samples' dU and q rows staged in LDS, one f32 MFMA pass after the loop; the host uses FQ
+  // only when a workgroup has <= 16 samples: a flush inside the loop spilled 56 VGPRs), no dU stores
+  constexpr int N_D = (FQ ? 0 : 1) + NPW + 1 + N_IDS;
   constexpr int P = NSLOT - 1;          // data groups in flight ahead of the sample computed
-  constexpr int X = 3, RING = X + 1;    // ids are fetched X iterations before their data group
+  constexpr int X = P > 3 ? P : 3, RING = X + 1;  // ids are fetched X iterations before their data group
   static_assert(NPW >= 0 && P >= 2 && P <= X && X * N_D < 64, "vmcnt range");
   // slot (floats): dpooled [128] | alpha [128] | U [128] | q [128] | key image [LP][D] bf16
   constexpr int SLOT_F = 4 * 128 + LP * D / 2;
@@ -1152,6 +1382,26 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8_kernel(
   int32_t* idring = reinterpret_cast<int32_t*>(slot0 + NSLOT * SLOT_F) + w * RING * 128;  // [RING][128] per wave
   float* dsbuf = reinterpret_cast<float*>(reinterpret_cast<int32_t*>(slot0 + NSLOT * SLOT_F) + 8 * RING * 128) + w * 128;
   float* dabuf = reinterpret_cast<float*>(reinterpret_cast<int32_t*>(slot0 + NSLOT * SLOT_F) + 8 * RING * 128) + 8 * 128;
+  float* dul = dabuf + 128;                       // FQ: [16][2 row groups][128] dU rows of the samples
+  float* ql = dul + (FQ ? 16 * 2 * 128 : 0);      // FQ: [16][128] their query rows
+  // FDP: dpooled formed here from the head's state (BN0 backward of da1 W1[:, d:]), no
+  // separate launch: W1p [32][D] (fc.1 weight, pooled half), per pooled column {mean,
+  // invstd, gamma, sum dh0 / B, sum dh0 xhat0 / B}, and this sample's dpooled [D]
+  float* w1p = ql + (FQ ? 16 * 128 : 0);
+  float* colc = w1p + (FDP ? 32 * D : 0);
+  float* dpl = colc + 5 * D;
+  static_assert(!FDP || LP <= 64, "FDP: the da1 row takes the second alpha piece");
+  if constexpr (FDP) {
+    for (int i = tid; i < 32 * D; i += 512) w1p[i] = dps.w1[(size_t)(i / D) * 2 * D + D + i % D];
+    for (int c = tid; c < D; c += 512) {
+      colc[c] = dps.stat0[D + c];
+      colc[D + c] = dps.stat0[3 * D + c];
+      colc[2 * D + c] = dps.bn0w[D + c];
+      colc[3 * D + c] = (float)dps.sum5[D + c] * dps.invB;
+      colc[4 * D + c] = (float)dps.sum5[3 * D + c] * dps.invB;
+    }
+    // ordered before the first use by the loop's barriers
+  }
 
   WFrag<true, D> wf;
   const int wu = us < nsl ? us : 0;
@@ -1173,9 +1423,36 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8_kernel(
   int64_t b_keep = -1;
   float* const dmy = dummy + (size_t)blockIdx.x * 512 + tid;
   auto store_du = [&]() {
-    float* dst = (b_keep >= 0 && us < nsl && h == 0) ? dUp + ((size_t)rg * B + b_keep) * A + 32 * us + r : dmy;
-    asm volatile("global_store_dword %0, %1, off" ::"v"(dst), "v"(du_keep) : "memory");
+    if constexpr (!FQ) {
+      float* dst = (b_keep >= 0 && us < nsl && h == 0) ? dUp + ((size_t)rg * B + b_keep) * A + 32 * us + r : dmy;
+      asm volatile("global_store_dword %0, %1, off" ::"v"(dst), "v"(du_keep) : "memory");
+    }
   };
+  // FQ: dW1q partial of the staged samples [0, ns) into this workgroup's slab:
+  // wave (us, rg) owns tiles n = 32 us.., k = 32 (rg + 2 j)..
+  float* const sqs_slab = slabs + (size_t)blockIdx.x * slab_floats(A, D) + slab_q_off(A, D);
+  auto flush_q = [&](int ns) {
+    if (us < nsl) {
+#pragma unroll
+      for (int j = 0; j < (NCT + 1) / 2; ++j) {
+        const int tk = rg + 2 * j;
+        if (tk >= NCT) continue;
+        f32x16 acc;
+#pragma unroll
+        for (int g = 0; g < 16; ++g) acc[g] = 0.f;
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) {
+          const int sm = 2 * kk + h;
+          const float av = sm < ns ? dul[sm * 256 + 32 * us + r] + dul[sm * 256 + 128 + 32 * us + r] : 0.f;
+          const float bv = sm < ns ? ql[sm * 128 + 32 * tk + r] : 0.f;
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int g = 0; g < 16; ++g) sqs_slab[(size_t)(32 * us + acc_row(g, h)) * D + 32 * tk + r] = acc[g];
+      }
+    }
+  };
+  int it = 0;  // samples of this workgroup so far
 
   // ids of sample b (all LP rows; clamped) into ring entry e of this wave
   auto issue_ids = [&](int64_t b, int e) {
@@ -1201,11 +1478,18 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8_kernel(
     }
     const int64_t bc = b < B ? b : 0;
     {  // small piece w of [dp0, dp1, al0, al1, u0, u1, q0, q1]
+       // (FDP: pooled instead of dpooled, and the da1 row [32] in the al1 piece)
       const int pc = w, kind = pc >> 1, part = pc & 1;
       const int i = part * 64 + lane;
-      const float* base = kind == 0 ? dpooled + bc * D : kind == 1 ? alpha + bc * L : kind == 2 ? U + bc * A : q + bc * dq;
-      const int lim = kind == 0 ? D : kind == 1 ? L : kind == 2 ? A : dq;
-      glds4_asm(base + (i < lim ? i : 0), lds_u32(sp + kind * 128 + part * 64));
+      const float* base = kind == 0 ? (FDP ? dps.pooled : dpooled) + bc * D : kind == 1 ? alpha + bc * L
+                          : kind == 2 ? U + bc * A : q + bc * dq;
+      int lim = kind == 0 ? D : kind == 1 ? L : kind == 2 ? A : dq;
+      if (FDP && pc == 3) {
+        base = dps.da1 + bc * 32;
+        lim = 32;
+      }
+      const int ii = FDP && pc == 3 ? lane : i;
+      glds4_asm(base + (ii < lim ? ii : 0), lds_u32(sp + kind * 128 + part * 64));
     }
   };
 
@@ -1231,11 +1515,28 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8_kernel(
     e = e + 1 < RING ? e + 1 : 0;
 
     const float* sp = slot0 + sl * SLOT_F;
-    const float* sdp = sp;
+    const float* sdp = FDP ? dpl : sp;
     const float* sal = sp + 128;
     const float* sU = sp + 256;
-    
     const unsigned char* img = reinterpret_cast<const unsigned char*>(sp + 512);
+    if constexpr (FDP) {  // dpooled[c] = iv g (sum_j da1[j] W1p[j][c] - sb - xhat sg), xhat = (pooled - m) iv
+      if (tid < D) {
+        const float* da1s = sp + 192;
+        float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f;
+#pragma unroll
+        for (int j = 0; j < 32; j += 4) {
+          c0 = fmaf(da1s[j], w1p[j * D + tid], c0);
+          c1 = fmaf(da1s[j + 1], w1p[(j + 1) * D + tid], c1);
+          c2 = fmaf(da1s[j + 2], w1p[(j + 2) * D + tid], c2);
+          c3 = fmaf(da1s[j + 3], w1p[(j + 3) * D + tid], c3);
+        }
+        const float acc = (c0 + c1) + (c2 + c3);
+        const float m = colc[tid], iv = colc[D + tid], gw = colc[2 * D + tid];
+        const float xhat = (sp[tid] - m) * iv;
+        dpl[tid] = iv * gw * (acc - colc[3 * D + tid] - xhat * colc[4 * D + tid]);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
     {  // dalpha[row] = dpooled . K[row], split over the waves: wave w owns rows [w R, (w+1) R)
       constexpr int R = LP / 8, LPR = 64 / R, CH = CPR / LPR;
       const int row = w * R + lane / LPR, part = lane % LPR;
@@ -1338,12 +1639,24 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8_kernel(
       du += __shfl_xor(du, 32, 64);
       db1_acc += du;
     }
+    if constexpr (FQ) {  // stage this sample's dU rows (both row groups) and query row
+      if (h == 0 && us < nsl && it < 16) dul[it * 256 + rg * 128 + 32 * us + r] = du;
+      if (lane < 16 && it < 16) ql[it * 128 + 16 * w + lane] = sp[384 + 16 * w + lane];
+    }
+    ++it;
     du_keep = du;
     b_keep = b;
     sl = sl == NSLOT - 1 ? 0 : sl + 1;
   }
   store_du();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup exits
+  if constexpr (FQ) {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (it > 0) flush_q(it);
+    else if (us < nsl) {  // no sample: a zero dW1q partial
+      for (int i = lane; i < 32 * D; i += 64) sqs_slab[(size_t)(32 * us) * D + i] = 0.f;
+    }
+  }
   // combine the row-group pairs (rg 1 into rg 0, fixed order) through LDS
   float* xch = slot0;  // [4 unit slices][32][D] f32, reused for dW1k then dW1q
   const bool act = us < nsl;
@@ -1385,6 +1698,275 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8_kernel(
       }
     }
     if (rg == 0 && us == 0 && lane == 0) slab[(size_t)A * D + A] = tb2 + xs[256];
+  }
+}
+
+// D = 256 variant of the 8-wave backward (the reference's training width):
+// waves w and w + 4 own the same 32 units (us = w & 3) and split the 256
+// COLUMNS (ch = w >> 2 takes [128 ch, 128 ch + 128)) instead of the rows, so
+// each keeps the d = 128 register budget (W1k fragments of its half, dW1k
+// accumulators of its half).  z needs the full 256-term reduction: each wave
+// forms its half's partial z of both row tiles on MFMA, the partials meet in
+// LDS (summed ch 0 + ch 1 in that order by both waves, so both hold the same
+// z), then both form dz and accumulate dW1k for their columns; the ch = 0 wave
+// also accumulates dw2, db1 and the sample's dU row (its partner stores zeros
+// in the second dU half the dW1q kernel adds).  Small pieces per sample:
+// dpooled [256] (4 pieces), alpha [LP <= 64] (1), U [128] (2), one unused.
+template <int D, int LP, int NSLOT>
+__global__ __launch_bounds__(512, 1) void din_bwd_deep8c_kernel(
+    const uint16_t* __restrict__ table, const int32_t* __restrict__ ids, int64_t n_table, const float* __restrict__ U,
+    const uint16_t* __restrict__ W1k, const float* __restrict__ w2, int B, int L, int A,
+    const float* __restrict__ dpooled, const float* __restrict__ alpha, float* __restrict__ slabs,
+    float* __restrict__ dUp, float* __restrict__ dummy) {
+  static_assert(D == 256 && LP <= 64, "deep8c: D = 256, LP <= 64");
+  constexpr int DH = D / 2;
+  constexpr int CPR = D / 8, KSH = DH / 16, NCTH = DH / 32, NC = LP / 32;
+  constexpr int NPW = LP * CPR / 512;  // key-image DMA pieces per wave
+  constexpr int N_D = 1 + NPW + 1 + 1;  // per wave and iteration: the dU store, keys, one small piece, ids
+  constexpr int P = NSLOT - 1;
+  constexpr int X = P > 3 ? P : 3, RING = X + 1;
+  static_assert(NPW >= 1 && P >= 2 && P <= X && X * N_D < 64, "vmcnt range");
+  // slot (floats): dpooled [256] | alpha [128] | U [128] | key image [LP][D] bf16
+  constexpr int SLOT_F = 4 * 128 + LP * D / 2;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int us = w & 3, ch = w >> 2;
+  const int nsl = A >> 5;
+  float* slot0 = reinterpret_cast<float*>(smem);
+  int32_t* idring = reinterpret_cast<int32_t*>(slot0 + NSLOT * SLOT_F) + w * RING * 64;  // [RING][64] per wave
+  float* dsbuf = reinterpret_cast<float*>(reinterpret_cast<int32_t*>(slot0 + NSLOT * SLOT_F) + 8 * RING * 64) + w * 64;
+  float* dabuf = reinterpret_cast<float*>(reinterpret_cast<int32_t*>(slot0 + NSLOT * SLOT_F) + 8 * RING * 64) + 8 * 64;
+  float* xz = dabuf + 64;  // [4 unit slices][2 halves][1024] partial z of one row tile, lane-major
+  float* xzw = xz + (size_t)(us * 2 + ch) * 1024;
+  const float* xz0 = xz + (size_t)(us * 2) * 1024;
+  const float* xz1 = xz + (size_t)(us * 2 + 1) * 1024;
+
+  const int wu = us < nsl ? us : 0;
+  bf16x8 wf[KSH];
+  {
+    const uint16_t* p = W1k + (int64_t)(32 * wu + r) * D + DH * ch + 8 * h;
+#pragma unroll
+    for (int s2 = 0; s2 < KSH; ++s2) wf[s2] = *reinterpret_cast<const bf16x8*>(p + 16 * s2);
+  }
+  const float w2n = w2[32 * wu + r];
+#pragma unroll
+  for (int s2 = 0; s2 < KSH; ++s2) asm volatile("" ::"v"(wf[s2]));
+  asm volatile("" ::"v"(w2n));
+  f32x16 dw[NCTH];
+#pragma unroll
+  for (int c = 0; c < NCTH; ++c)
+#pragma unroll
+    for (int g = 0; g < 16; ++g) dw[c][g] = 0.f;
+  float dw2_acc = 0.f, db2_acc = 0.f, db1_acc = 0.f;
+  float du_keep = 0.f;
+  int64_t b_keep = -1;
+  float* const dmy = dummy + (size_t)blockIdx.x * 512 + tid;
+  auto store_du = [&]() {  // half ch of dUp: the ch = 0 wave's full row sum, zeros from ch = 1
+    float* dst = (b_keep >= 0 && us < nsl && h == 0) ? dUp + ((size_t)ch * B + b_keep) * A + 32 * us + r : dmy;
+    const float v = ch == 0 ? du_keep : 0.f;
+    asm volatile("global_store_dword %0, %1, off" ::"v"(dst), "v"(v) : "memory");
+  };
+  auto issue_ids = [&](int64_t b, int e) {
+    const int64_t bc = b < B ? b : 0;
+    const int i = lane < LP ? lane : 0;
+    glds4_asm(ids + bc * L + (i < L ? i : 0), lds_u32(idring + e * 64));
+  };
+  auto issue_data = [&](int64_t b, int sl, int e) {
+    float* sp = slot0 + sl * SLOT_F;
+    uint16_t* img = reinterpret_cast<uint16_t*>(sp + 4 * 128);
+#pragma unroll
+    for (int k = 0; k < NPW; ++k) {
+      const int u = w + 8 * k;
+      const int p = u * 64 + lane;
+      const int row = p / CPR, pc = p % CPR;
+      const int cc = pc ^ kswz<CPR>(row);
+      const int32_t idv0 = idring[e * 64 + row];
+      const int32_t idr = row < L && b < B ? idv0 : -1;
+      const uint16_t* src = (idr >= 0 && idr < n_table) ? table + (int64_t)idr * D + cc * 8 : zero_row(b, row) + cc * 8;
+      glds16_asm(src, lds_u32(img + u * 64 * 8));
+    }
+    const int64_t bc = b < B ? b : 0;
+    {  // small piece w of [dp0, dp1, dp2, dp3, al0, u0, u1, (u1 again: unused slot)]
+      const float* base;
+      int i, lim;
+      float* dst;
+      if (w < 4) { base = dpooled + bc * D; i = 64 * w + lane; lim = D; dst = sp + 64 * w; }
+      else if (w == 4) { base = alpha + bc * L; i = lane; lim = L; dst = sp + 256; }
+      else { base = U + bc * A; i = 64 * ((w - 5) & 1) + lane; lim = A; dst = sp + 384 + 64 * ((w - 5) & 1); }
+      if (w == 7) dst = sp + 320;  // the alpha slot's unused second half (LP <= 64)
+      glds4_asm(base + (i < lim ? i : 0), lds_u32(dst));
+    }
+  };
+
+  const int64_t grid = gridDim.x;
+  int64_t b = blockIdx.x;
+#pragma unroll
+  for (int k = 0; k < X; ++k) issue_ids(b + k * grid, k);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    store_du();
+    issue_ids(b + (k + X) * grid, (k + X) % RING);
+    issue_data(b + k * grid, k, k);
+  }
+  int sl = 0, e = P % RING;
+  for (; b < B; b += grid) {
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"((P - 1) * N_D) : "memory");
+    store_du();
+    issue_ids(b + (P + X) * grid, e + X < RING ? e + X : e + X - RING);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(X * N_D) : "memory");
+    issue_data(b + P * grid, sl + P < NSLOT ? sl + P : sl + P - NSLOT, e);
+    e = e + 1 < RING ? e + 1 : 0;
+
+    const float* sp = slot0 + sl * SLOT_F;
+    const float* sdp = sp;
+    const float* sal = sp + 256;
+    const float* sU = sp + 384;
+    const unsigned char* img = reinterpret_cast<const unsigned char*>(sp + 512);
+    {  // dalpha[row] = dpooled . K[row]: wave w owns rows [w R, (w+1) R)
+      constexpr int R = LP / 8, LPR = 64 / R, CHK = CPR / LPR;
+      const int row = w * R + lane / LPR, part = lane % LPR;
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < CHK; ++k) {
+        const int cc = part * CHK + k;
+        const uint4 kv = *reinterpret_cast<const uint4*>(img + row * 2 * D + 16 * (cc ^ kswz<CPR>(row)));
+        const float4 d0 = *reinterpret_cast<const float4*>(sdp + 8 * cc);
+        const float4 d1 = *reinterpret_cast<const float4*>(sdp + 8 * cc + 4);
+        acc = fmaf(d0.x, __uint_as_float(kv.x << 16), acc);
+        acc = fmaf(d0.y, __uint_as_float(kv.x & 0xFFFF0000u), acc);
+        acc = fmaf(d0.z, __uint_as_float(kv.y << 16), acc);
+        acc = fmaf(d0.w, __uint_as_float(kv.y & 0xFFFF0000u), acc);
+        acc = fmaf(d1.x, __uint_as_float(kv.z << 16), acc);
+        acc = fmaf(d1.y, __uint_as_float(kv.z & 0xFFFF0000u), acc);
+        acc = fmaf(d1.z, __uint_as_float(kv.w << 16), acc);
+        acc = fmaf(d1.w, __uint_as_float(kv.w & 0xFFFF0000u), acc);
+      }
+#pragma unroll
+      for (int o = 1; o < LPR; o <<= 1) acc += __shfl_xor(acc, o, 64);
+      if (part == 0) dabuf[row] = acc;
+    }
+    // partial z of this half's columns for row tile c (MFMA), exchanged through LDS
+    auto zpart = [&](int c) {
+      f32x16 acc;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) acc[g] = 0.f;
+#pragma unroll
+      for (int s2 = 0; s2 < KSH; ++s2) {
+        const bf16x8 kf =
+            *reinterpret_cast<const bf16x8*>(img + KImg<true, D>::off(32 * c + r, DH * ch + 16 * s2 + 8 * h));
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, wf[s2], acc, 0, 0, 0);
+      }
+      return acc;
+    };
+    auto zput = [&](const f32x16& acc) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        *reinterpret_cast<float4*>(xzw + j * 256 + 4 * lane) =
+            make_float4(acc[4 * j], acc[4 * j + 1], acc[4 * j + 2], acc[4 * j + 3]);
+    };
+    zput(zpart(0));
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // dalpha and both halves' partial z
+    float du = 0.f;
+    {  // every wave runs the tile loop (its barriers); a wave without units (A < 128) stores nothing
+      const float un = sU[32 * wu + r];
+      float da[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) da[c] = dabuf[32 * c + r];
+      float t = 0.f;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int row = 32 * c + r;
+        t += (row < L && h == 0) ? sal[row] * da[c] : 0.f;
+      }
+      const float cdot = wave_sum(t);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int row = 32 * c + r;
+        if (h == 0) {
+          const float ds = row < L ? sal[row] * (da[c] - cdot) : 0.f;
+          dsbuf[row] = ds;
+          if (w == 0) db2_acc += ds;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        if (c > 0) {  // every partner has read tile c - 1's partial: publish tile c's
+          const f32x16 zp = zpart(c);
+          asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+          zput(zp);
+          asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+        f32x16 dz;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float4 p0 = *reinterpret_cast<const float4*>(xz0 + j * 256 + 4 * lane);
+          const float4 p1 = *reinterpret_cast<const float4*>(xz1 + j * 256 + 4 * lane);
+          const float4 d4 = *reinterpret_cast<const float4*>(dsbuf + 32 * c + 8 * j + 4 * h);
+          const float zz[4] = {un + (p0.x + p1.x), un + (p0.y + p1.y), un + (p0.z + p1.z), un + (p0.w + p1.w)};
+          const float dsv[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int g = 4 * j + i;
+            const float z = zz[i];
+            if (ch == 0) dw2_acc = fmaf(dsv[i], fmaxf(z, 0.f), dw2_acc);
+            const float v = z > 0.f ? dsv[i] * w2n : 0.f;
+            dz[g] = v;
+            du += v;
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          bf16x8 af;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const bf16x2_hw pk = {(__bf16)dz[8 * s + 2 * j], (__bf16)dz[8 * s + 2 * j + 1]};
+            const uint32_t u = __builtin_bit_cast(uint32_t, pk);
+            af[2 * j] = (short)(u & 0xFFFF);
+            af[2 * j + 1] = (short)(u >> 16);
+          }
+          const int grp = lane >> 4, i16 = lane & 15;
+          const int rowq = 32 * c + 16 * s + 4 * h + (i16 >> 2);
+#pragma unroll
+          for (int cc = 0; cc < NCTH; ++cc) {
+            const int col = DH * ch + 32 * cc + 16 * (grp & 1) + 4 * (i16 & 3);
+            typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+            const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(img + KImg<true, D>::off(rowq, col)));
+            const bf16x4 hi =
+                __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(img + KImg<true, D>::off(rowq + 8, col)));
+            const bf16x8 bfr = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+            dw[cc] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, dw[cc], 0, 0, 0);
+          }
+        }
+      }
+      du += __shfl_xor(du, 32, 64);
+      if (ch == 0) db1_acc += du;
+    }
+    du_keep = du;
+    b_keep = b;
+    sl = sl == NSLOT - 1 ? 0 : sl + 1;
+  }
+  store_du();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup exits
+  float* slab = slabs + (size_t)blockIdx.x * slab_floats(A, D);
+  if (us < nsl) {
+#pragma unroll
+    for (int c = 0; c < NCTH; ++c)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) slab[(size_t)(32 * us + acc_row(g, h)) * D + DH * ch + 32 * c + r] = dw[c][g];
+    const float t2 = dw2_acc + __shfl_xor(dw2_acc, 32, 64);
+    if (ch == 0 && h == 0) {
+      slab[(size_t)A * D + 32 * us + r] = t2;
+      slab[slab_q_off(A, D) + (size_t)A * D + 32 * us + r] = db1_acc;
+    }
+  }
+  if (w == 0) {
+    const float tb2 = wave_sum(db2_acc);
+    if (lane == 0) slab[(size_t)A * D + A] = tb2;
   }
 }
 
@@ -1714,6 +2296,25 @@ extern "C" int nrk_din_attn_fwd(const void* keys, const int32_t* hist_ids, int64
   const size_t smem = fwd_smem(bf, d, L);
   NRK_CHECK_ARG(smem <= 160 * 1024, "din_fwd: L=%d d=%d needs %zu B LDS", L, d, smem);
   const bool wave_ok = bf && hist_ids && (d == 64 || d == 128);
+  const size_t pair_sm = ((size_t)((A + 63) & ~63) * 3 + (size_t)((L + 31) & ~31) * d + 4 * 128 + 2 * 256) * 4;
+  if (bf && hist_ids && d == 256 && pair_sm <= 80 * 1024) {  // L <= 64: a wave pair per sample, two WGs per CU
+    const size_t AP = (size_t)((A + 63) & ~63);
+    const size_t psm = pair_sm;
+    int grid = (int)cdiv(B, 2);
+    if (grid > 512) grid = 512;
+    const uint16_t* tb = static_cast<const uint16_t*>(keys);
+    const uint16_t* wk = static_cast<const uint16_t*>(W1k);
+    hipStream_t st = (hipStream_t)stream;
+    const int na = A / 32;
+#define NRK_FWD_PAIR(NN)                                                                                          \
+  hipLaunchKernelGGL((din_fwd_pair_kernel<256, NN>), dim3(grid), dim3(256), psm, st, tb, hist_ids, n_table, U, wk, \
+                     w2, B, L, pooled, alpha)
+    if (na == 1) NRK_FWD_PAIR(1); else if (na == 2) NRK_FWD_PAIR(2); else if (na == 3) NRK_FWD_PAIR(3);
+    else NRK_FWD_PAIR(4);
+#undef NRK_FWD_PAIR
+    NRK_CHECK_LAUNCH("din_fwd_pair_kernel");
+    return NRK_OK;
+  }
   if (wave_ok) {
     const int Lp = (L + 31) & ~31;
     const size_t AP = (size_t)((A + 63) & ~63);
@@ -1839,7 +2440,7 @@ extern "C" int nrk_din_batch(const int64_t* idx, int32_t B, const int32_t* hist_
                              int32_t dtype, int32_t d, const float* W1, const float* b1, int32_t A, int32_t* hist,
                              float* q, float* y, float* U, void* W1k_bf16, void* stream) {
   NRK_CHECK_ARG(dtype == NRK_DTYPE_BF16, "din_batch: the table must be bf16");
-  NRK_CHECK_ARG(d == 64 || d == 128, "din_batch: emb_dim %d unsupported (64, 128)", d);
+  NRK_CHECK_ARG(d == 64 || d == 128 || d == 256, "din_batch: emb_dim %d unsupported (64, 128, 256)", d);
   NRK_CHECK_ARG(A >= 32 && A <= 128 && A % 32 == 0, "din_batch: attn_units %d unsupported (32..128 step 32)", A);
   NRK_CHECK_ARG(L >= 1 && L <= 128 && B >= 0, "din_batch: bad L=%d / B=%d", L, B);
   if (B == 0) return NRK_OK;
@@ -1849,7 +2450,10 @@ extern "C" int nrk_din_batch(const int64_t* idx, int32_t B, const int32_t* hist_
   hipStream_t st = (hipStream_t)stream;
   const uint16_t* tb = static_cast<const uint16_t*>(table);
   uint16_t* wk = static_cast<uint16_t*>(W1k_bf16);
-  if (d == 128)
+  if (d == 256)
+    hipLaunchKernelGGL(din_batch_kernel<256>, dim3(grid), dim3(256), 0, st, idx, B, hist_all, tgt_all, lab_all, n_rows, L,
+                       tb, n_table, W1, b1, A, hist, q, y, U, wk);
+  else if (d == 128)
     hipLaunchKernelGGL(din_batch_kernel<128>, dim3(grid), dim3(256), 0, st, idx, B, hist_all, tgt_all, lab_all, n_rows, L,
                        tb, n_table, W1, b1, A, hist, q, y, U, wk);
   else
@@ -1859,18 +2463,21 @@ extern "C" int nrk_din_batch(const int64_t* idx, int32_t B, const int32_t* hist_
   return NRK_OK;
 }
 
-extern "C" int nrk_din_attn_bwd_params(const void* table, const int32_t* hist_ids, int64_t n_table, int32_t dtype,
-                                       const float* q, const float* U, const void* W1k, const float* w2, int32_t B,
-                                       int32_t L, int32_t d, int32_t A, const float* dpooled, const float* alpha,
-                                       float* gW1, float* gb1, float* gw2, float* gb2, float* dU, void* ws,
-                                       size_t ws_bytes, void* stream) {
+static int bwd_params_impl(const void* table, const int32_t* hist_ids, int64_t n_table, int32_t dtype,
+                           const float* q, const float* U, const void* W1k, const float* w2, int32_t B, int32_t L,
+                           int32_t d, int32_t A, const float* dpooled, const float* alpha, float* gW1, float* gb1,
+                           float* gw2, float* gb2, float* dU, void* ws, size_t ws_bytes, void* stream,
+                           const DpSrc* dps) {
   int rc = check_common(table, dtype, B, L, d, A);
   if (rc) return rc;
-  NRK_CHECK_ARG(dtype == NRK_DTYPE_BF16 && hist_ids != nullptr && (d == 64 || d == 128),
-                "din_bwd_params: needs a bf16 table, history ids and emb_dim 64 or 128");
+  NRK_CHECK_ARG(dtype == NRK_DTYPE_BF16 && hist_ids != nullptr &&
+                    (d == 64 || d == 128 || (d == 256 && dU == nullptr && L <= 64)),
+                "din_bwd_params: needs a bf16 table, history ids and emb_dim 64 or 128 (256: L <= 64, no dU output)");
   NRK_CHECK_ARG(B > 0, "din_bwd_params: empty batch");
-  NRK_CHECK_ARG(q && U && W1k && w2 && dpooled && alpha && gW1 && gb1 && gw2 && gb2 && ws,
+  NRK_CHECK_ARG(q && U && W1k && w2 && (dpooled || dps) && alpha && gW1 && gb1 && gw2 && gb2 && ws,
                 "din_bwd_params: null pointer");
+  NRK_CHECK_ARG(!dps || (dU == nullptr && (d == 64 || d == 128) && L <= 64),
+                "din_bwd_params_head: d=%d L=%d (needs d 64 or 128, L <= 64)", d, L);
   const int grid = din_grid(B, true);
   size_t woff[4];
   const size_t need = bwd_ws_parts(B, d, A, woff);
@@ -1886,34 +2493,76 @@ extern "C" int nrk_din_attn_bwd_params(const void* table, const int32_t* hist_id
   float* slabs = static_cast<float*>(ws);
   const uint16_t* tb = static_cast<const uint16_t*>(table);
   const uint16_t* wk = static_cast<const uint16_t*>(W1k);
-  if (dU == nullptr) {  // the fused train step: deep-prefetch kernels, dW1q formed here too
+  if (dU == nullptr && d == 256) {  // the reference's width: column-split 8-wave backward
+    const int LPk = Lp <= 32 ? 32 : 64;
+    constexpr int NS = 3, RING = 4;
+    const size_t dsm = (size_t)(NS * (4 * 128 + LPk * d / 2) + 8 * RING * 64 + 8 * 64 + 64 + 8 * 1024) * 4;
+    NRK_CHECK_ARG(dsm <= 160 * 1024, "din_bwd_params: L=%d d=%d needs %zu B LDS", L, d, dsm);
+    if (LPk == 32)
+      hipLaunchKernelGGL((din_bwd_deep8c_kernel<256, 32, NS>), dim3(grid), dim3(512), dsm, st, tb, hist_ids, n_table, U,
+                         wk, w2, B, L, A, dpooled, alpha, slabs, dUp, dmy);
+    else
+      hipLaunchKernelGGL((din_bwd_deep8c_kernel<256, 64, NS>), dim3(grid), dim3(512), dsm, st, tb, hist_ids, n_table, U,
+                         wk, w2, B, L, A, dpooled, alpha, slabs, dUp, dmy);
+    NRK_CHECK_LAUNCH("din_bwd_deep8c_kernel");
+    const int kchunk = (int)cdiv(B, DWQ_KC);
+    hipLaunchKernelGGL(din_dwq_kernel, dim3((unsigned)(A / 32 * (d / 32)), DWQ_KC), dim3(256), 0, st, dUp, q, B, A, d, d,
+                       kchunk, qpart_w8);
+    NRK_CHECK_LAUNCH("din_dwq_kernel");
+    qpart = qpart_w8;
+  } else if (dU == nullptr) {  // the fused train step: deep-prefetch kernels, dW1q formed here too
     const int LPk = Lp <= 32 ? 32 : Lp <= 64 ? 64 : 128;
     const int nslot = 4;
     const bool w8 = LPk * d >= 4096;  // >= 8 key-image pieces: one per wave
     size_t dsm = (size_t)(nslot * (4 * 128 + LPk * d / 2) + 4 * 4 * 128 + 5 * 128) * 4;
+    // deep8: 3 slots (2 samples in flight; 4 and 5 measured no faster, profiles/r03_din_ab.log)
+    constexpr int nslot8 = 3;
+    // dW1q folded into the 8-wave kernel (16 samples' dU / q rows in LDS) instead of the
+    // dU stores + din_dwq_kernel; NRK_DEEP8_FOLDQ=0: the old form (A/B hook)
+    const char* fq_env = getenv("NRK_DEEP8_FOLDQ");
+    const bool fold_q = !(fq_env && *fq_env == '0') && cdiv(B, grid) <= 16;
     if (w8) {
-      dsm = (size_t)(nslot * (4 * 128 + LPk * d / 2) + 8 * 4 * 128 + 9 * 128) * 4;
+      const int ring8 = (nslot8 - 1 > 3 ? nslot8 - 1 : 3) + 1;
+      dsm = (size_t)(nslot8 * (4 * 128 + LPk * d / 2) + 8 * ring8 * 128 + 9 * 128 + (fold_q ? 48 * 128 : 0) +
+                     (dps ? 32 * d + 6 * d : 0)) * 4;
       const size_t xneed = ((size_t)4 * 32 * d + 257) * 4;  // pair-combine exchange area (reuses the slots)
       if (dsm < xneed) dsm = xneed;
     }
     NRK_CHECK_ARG(dsm <= 160 * 1024, "din_bwd_params: L=%d d=%d needs %zu B LDS", L, d, dsm);
+#define NRK_BWD_DEEP8_V(DD, LL, FQV, FDPV)                                                                         \
+  hipLaunchKernelGGL((din_bwd_deep8_kernel<DD, LL, 3, FQV, FDPV>), dim3(grid), dim3(512), dsm, st, tb, hist_ids,     \
+                     n_table, U, wk, w2, B, L, A, dpooled, alpha, slabs, q, d, dUp, dmy, dpv)
+#define NRK_BWD_DEEP8_FDP(DD, LL)                                                                                   \
+  do {                                                                                                              \
+    if (fold_q) NRK_BWD_DEEP8_V(DD, LL, true, true); else NRK_BWD_DEEP8_V(DD, LL, false, true);                     \
+  } while (0)
 #define NRK_BWD_DEEP(DD, LL)                                                                                          \
   do {                                                                                                              \
-    if (w8)                                                                                                         \
-      hipLaunchKernelGGL((din_bwd_deep8_kernel<DD, LL, 3>), dim3(grid), dim3(512), dsm, st, tb, hist_ids, n_table, U, \
-                         wk, w2, B, L, A, dpooled, alpha, slabs, q, d, dUp, dmy);                                     \
-    else                                                                                                            \
+    if (w8) {                                                                                                       \
+      if (fold_q) NRK_BWD_DEEP8_V(DD, LL, true, false); else NRK_BWD_DEEP8_V(DD, LL, false, false);                 \
+    } else                                                                                                          \
       hipLaunchKernelGGL((din_bwd_deep_kernel<DD, LL, 4>), dim3(grid), dim3(256), dsm, st, tb, hist_ids, n_table, U, wk, \
                          w2, B, L, A, dpooled, alpha, slabs, q, d);                                                   \
   } while (0)
+    const DpSrc dpv = dps ? *dps : DpSrc{};
+    if (dps) {
+      NRK_CHECK_ARG(w8, "din_bwd_params_head: needs the 8-wave backward (L * d >= 4096)");
+      if (d == 128) {
+        if (LPk == 32) NRK_BWD_DEEP8_FDP(128, 32); else NRK_BWD_DEEP8_FDP(128, 64);
+      } else {
+        if (LPk == 32) NRK_BWD_DEEP8_FDP(64, 32); else NRK_BWD_DEEP8_FDP(64, 64);
+      }
+    } else
     if (d == 128) {
       if (LPk == 32) NRK_BWD_DEEP(128, 32); else if (LPk == 64) NRK_BWD_DEEP(128, 64); else NRK_BWD_DEEP(128, 128);
     } else {
       if (LPk == 32) NRK_BWD_DEEP(64, 32); else if (LPk == 64) NRK_BWD_DEEP(64, 64); else NRK_BWD_DEEP(64, 128);
     }
 #undef NRK_BWD_DEEP
+#undef NRK_BWD_DEEP8_FDP
+#undef NRK_BWD_DEEP8_V
     NRK_CHECK_LAUNCH("din_bwd_deep_kernel");
-    if (w8) {
+    if (w8 && !fold_q) {
       const int kchunk = (int)cdiv(B, DWQ_KC);
       hipLaunchKernelGGL(din_dwq_kernel, dim3((unsigned)(A / 32 * (d / 32)), DWQ_KC), dim3(256), 0, st, dUp, q, B, A, d, d,
                          kchunk, qpart_w8);
@@ -1934,4 +2583,34 @@ extern "C" int nrk_din_attn_bwd_params(const void* table, const int32_t* hist_id
                      grid, A, d, d, gW1, gb1, gw2, gb2, qpart, qpart ? DWQ_KC : 0);
   NRK_CHECK_LAUNCH("din_bwd_reduce_params_kernel");
   return NRK_OK;
+}
+
+extern "C" int nrk_din_attn_bwd_params(const void* table, const int32_t* hist_ids, int64_t n_table, int32_t dtype,
+                                       const float* q, const float* U, const void* W1k, const float* w2, int32_t B,
+                                       int32_t L, int32_t d, int32_t A, const float* dpooled, const float* alpha,
+                                       float* gW1, float* gb1, float* gw2, float* gb2, float* dU, void* ws,
+                                       size_t ws_bytes, void* stream) {
+  return bwd_params_impl(table, hist_ids, n_table, dtype, q, U, W1k, w2, B, L, d, A, dpooled, alpha, gW1, gb1, gw2,
+                         gb2, dU, ws, ws_bytes, stream, nullptr);
+}
+
+extern "C" int nrk_din_attn_bwd_params_head(const void* table, const int32_t* hist_ids, int64_t n_table,
+                                            int32_t dtype, const float* q, const float* U, const void* W1k,
+                                            const float* w2, int32_t B, int32_t L, int32_t d, int32_t A,
+                                            const float* pooled, const float* alpha, int32_t F,
+                                            const nrk_din_head_params* hp, const void* head_ws, size_t head_ws_bytes,
+                                            float* gW1, float* gb1, float* gw2, float* gb2, void* ws, size_t ws_bytes,
+                                            void* stream) {
+  NRK_CHECK_ARG(F == 32 && hp && pooled && head_ws, "din_bwd_params_head: needs F = 32, head params, pooled, head ws");
+  DpSrc dps{};
+  const float* da1 = nullptr;
+  int rc = nrk_din_head_ws_views(B, d, F, head_ws, head_ws_bytes, &dps.stat0, &dps.sum5, &da1);
+  if (rc) return rc;
+  dps.pooled = pooled;
+  dps.da1 = da1;
+  dps.w1 = hp->fc1_w;
+  dps.bn0w = hp->bn0_w;
+  dps.invB = 1.f / (float)B;
+  return bwd_params_impl(table, hist_ids, n_table, dtype, q, U, W1k, w2, B, L, d, A, nullptr, alpha, gW1, gb1, gw2,
+                         gb2, nullptr, ws, ws_bytes, stream, &dps);
 }

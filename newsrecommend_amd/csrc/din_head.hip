@@ -609,18 +609,21 @@ __global__ __launch_bounds__(256) void hf_stats0(HeadArgs a) {
 
 // LDS (floats): mean/inv [D2] x 2 | h0 [32][D2+4] | W1 [32][D2+4] | red [4][32][32] | d1 [32][33]
 // NX = D2 / 32: float4 of the block's x rows per thread (issued before the
-// prologue's partial sums, so the two memory round trips overlap)
+// prologue's partial sums, so the two memory round trips overlap).  D2 > 256
+// (d = 256, the reference's width): the W1 tile would not fit next to h0, so
+// the MFMA reads W1 rows from global memory (L2-resident, every block reads it)
 template <int NX>
 __global__ __launch_bounds__(256) void hf_fwd1(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   __shared__ double pro_tmp[256], pro_sum[1024];
   constexpr int D2 = NX * 32, hs = D2 + 4, q4 = D2 / 4;
+  constexpr bool W1_LDS = NX <= 8;
   const int t = threadIdx.x;
   float* mean = sm;
   float* inv = mean + D2;
   float* h0 = inv + D2;
   float* w1 = h0 + HR * hs;
-  float* red = w1 + HF * hs;
+  float* red = w1 + (W1_LDS ? HF * hs : 0);
   float* d1 = red + 4 * HR * HF;
   const int64_t r0 = (int64_t)blockIdx.x * HR;
   float4 xv[NX];
@@ -631,7 +634,7 @@ __global__ __launch_bounds__(256) void hf_fwd1(HeadArgs a) {
   }
   colsum_prologue(a.part0, a.nrg0, 2 * D2, 2 * D2, pro_tmp, pro_sum);
   bn_finalize(a, pro_sum, D2, mean, inv, a.stat0, a.p.bn0_rm, a.p.bn0_rv, a.p.bn0_nb, blockIdx.x == 0);
-  {  // W1 (L2-resident: every block reads it)
+  if constexpr (W1_LDS) {  // W1 (L2-resident: every block reads it)
     float4 wv[NX];
 #pragma unroll
     for (int u = 0; u < NX; ++u) wv[u] = *reinterpret_cast<const float4*>(a.p.fc1_w + 4 * (t + u * 256));
@@ -657,7 +660,7 @@ __global__ __launch_bounds__(256) void hf_fwd1(HeadArgs a) {
     const int lane = t & 63, w = t >> 6, i = lane & 31, h = lane >> 5;
     constexpr int kw = D2 / 8;
     const float* ar = h0 + i * hs + h * (D2 / 2) + w * kw;
-    const float* br = w1 + i * hs + h * (D2 / 2) + w * kw;
+    const float* br = (W1_LDS ? w1 + i * hs : a.p.fc1_w + (int64_t)i * D2) + h * (D2 / 2) + w * kw;
     f32x16 acc;
 #pragma unroll
     for (int g = 0; g < 16; ++g) acc[g] = 0.f;
@@ -1429,6 +1432,26 @@ static void head_sizes(int B, int d, int F, int nblk, size_t* off, size_t* total
   *total = o;
 }
 
+// The train-mode head's state the attention backward needs when it forms
+// dpooled itself (nrk_din_attn_bwd_params_head): BN0's finalised statistics
+// {mean [2d], invstd [2d]}, its backward sums {sum dh0 [2d], sum dh0 xhat0 [2d]}
+// (fp64) and da1 [B][F] (the gradient at fc.1's output), inside `ws` after
+// nrk_din_head_train on the fast path (F = 32).
+extern "C" int nrk_din_head_ws_views(int32_t B, int32_t d, int32_t F, const void* ws, size_t ws_bytes,
+                                     const float** stat0, const double** sum5, const float** da1) {
+  NRK_CHECK_ARG(ws && stat0 && sum5 && da1 && B > 1 && d > 0 && F >= 2, "din_head_ws_views: bad arguments");
+  size_t off[17], total = 0;
+  head_sizes(B, d, F, (int)cdiv(B, HR), off, &total);
+  if (ws_bytes < total) return fail(NRK_EWORKSPACE, "din_head_ws_views: workspace %zu < %zu", ws_bytes, total);
+  const char* w = static_cast<const char*>(ws);
+  *stat0 = reinterpret_cast<const float*>(w + off[6]);
+  const double* sb = reinterpret_cast<const double*>(w + off[15]);
+  const int D2_ = 2 * d, F2_ = F / 2;
+  *sum5 = sb + 2 * D2_ + 2 * F + 2 * F2_ + (3 * F2_ + 2) + (2 * F + F2_ * F + F2_);
+  *da1 = reinterpret_cast<const float*>(w + off[12]);
+  return NRK_OK;
+}
+
 extern "C" int nrk_din_head_workspace(int32_t B, int32_t d, int32_t F, size_t* ws_bytes) {
   NRK_CHECK_ARG(ws_bytes && B > 1 && d > 0 && F >= 2, "din_head_workspace: bad arguments");
   size_t off[17];
@@ -1444,7 +1467,10 @@ extern "C" int nrk_din_head_train(const float* q, const float* pooled, int64_t l
   NRK_CHECK_ARG(d > 0 && 2 * d <= 512 && F >= 2 && F <= 64 && F % 2 == 0 && ld_pooled >= d,
                 "din_head_train: unsupported d=%d F=%d ld=%lld", d, F, (long long)ld_pooled);
   NRK_CHECK_ARG(p_drop >= 0.f && p_drop < 1.f, "din_head_train: dropout %f", (double)p_drop);
-  NRK_CHECK_ARG(q && pooled && labels && step && prm && logits && loss && dpooled && ws, "din_head_train: null pointer");
+  NRK_CHECK_ARG(q && pooled && labels && step && prm && logits && loss && ws, "din_head_train: null pointer");
+  // dpooled == NULL (fast path only): the attention backward forms it from the
+  // workspace (nrk_din_attn_bwd_params_head), so the BN0-backward launch is skipped
+  NRK_CHECK_ARG(dpooled || (F == 32 && d % 32 == 0), "din_head_train: dpooled may be NULL only with F = 32");
   const int nblk = B / HR;
   size_t off[17], total = 0;
   head_sizes(B, d, F, nblk, off, &total);
@@ -1501,8 +1527,12 @@ extern "C" int nrk_din_head_train(const float* q, const float* pooled, int64_t l
   a.fast = F == HF && d % 32 == 0;
   a.nrg0 = nblk < 8 ? nblk : 8;
   if (a.fast) {
-    const size_t lf1 = ((size_t)2 * D2 + (size_t)(HR + HF) * (D2 + 4) + 4 * HR * HF + HR * (HF + 1)) * 4;
+    const size_t lf1 =
+        ((size_t)2 * D2 + (size_t)(HR + (D2 <= 256 ? HF : 0)) * (D2 + 4) + 4 * HR * HF + HR * (HF + 1)) * 4;
     const size_t lb1 = ((size_t)2 * D2 + (size_t)HR * (D2 + 4) + HR * (HF + 1) + 4 * HF) * 4;
+    // + the kernels' static LDS (hf_fwd1: 10 KB of prologue sums): every launch must fit 160 KB
+    NRK_CHECK_ARG(lf1 + 10240 <= 160 * 1024 && lb1 + 4096 <= 160 * 1024,
+                  "din_head_train: d=%d needs %zu / %zu B of LDS", d, lf1 + 10240, lb1 + 4096);
     const int s3_ = 3 * F2 + 2, s4_ = 2 * F + F2 * F + F2;
     hipLaunchKernelGGL(hf_stats0, dim3((unsigned)(D2 / 32 * a.nrg0)), dim3(256), 0, st, a);
     switch (D2) {  // the fast path needs d % 32 == 0, 2d <= 512
@@ -1529,7 +1559,7 @@ extern "C" int nrk_din_head_train(const float* q, const float* pooled, int64_t l
       default: hipLaunchKernelGGL(hf_bwd1<16>, dim3(nblk), dim3(256), lb1, st, a); break;
     }
     hipLaunchKernelGGL(hf_reduce, dim3((unsigned)(D2 / 4 + cdiv(s3_ + s4_, 64))), dim3(1024), 0, st, a);
-    hipLaunchKernelGGL(hf_bwd0, dim3(nblk), dim3(256), 0, st, a);
+    if (dpooled) hipLaunchKernelGGL(hf_bwd0, dim3(nblk), dim3(256), 0, st, a);
     NRK_CHECK_LAUNCH("din_head_train (fast)");
     return NRK_OK;
   }

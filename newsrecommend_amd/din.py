@@ -20,6 +20,7 @@ restatement, for CPU checks).
 from __future__ import annotations
 
 import ctypes
+import os
 import warnings
 
 import torch
@@ -481,19 +482,27 @@ class FusedTrainStep:
         _lib.check(L_.nrk_clip_adam_workspace(n, sz), "clip_adam_workspace")
         self.ws_opt = torch.zeros(max(sz.value, 1), dtype=torch.uint8, device=dev)  # holds a ticket: zeroed once
         self.n = n
-        # fast path (bf16 table, emb_dim 64/128): one batch-assembly kernel
+        # fast path (bf16 table, emb_dim 64/128/256): one batch-assembly kernel
         # (rows -> ids, labels, f32 query, U = q W1q^T + b1, bf16 W1k) and an
         # attention backward that also forms dW1q / db1 and writes every
         # attention gradient in place: no torch ops left inside the step
-        self.fast = (table.dtype == torch.bfloat16 and d in (64, 128) and Dk == d and hist_ids.shape[1] <= 128)
+        Lh = hist_ids.shape[1]
+        max_l = 64 if d == 256 else 128  # d = 256: the column-split backward holds L <= 64 rows
         why = [w for w, bad in (("table is not bf16", table.dtype != torch.bfloat16),
-                                (f"emb_dim {d} not in (64, 128)", d not in (64, 128)),
-                                (f"history length {hist_ids.shape[1]} > 128", hist_ids.shape[1] > 128)) if bad]
+                                (f"emb_dim {d} not in (64, 128, 256)", d not in (64, 128, 256)),
+                                (f"history length {Lh} > {max_l}", Lh > max_l)) if bad]
+        self.fast = not why
         # which path the step runs (the generic one has torch ops around the kernels)
         self.path = "fast" if self.fast else "generic: " + ", ".join(why)
         if not self.fast:
             warnings.warn(f"FusedTrainStep: {self.path} -> the generic step (torch GEMMs and gathers around the "
                           f"attention kernels), not the single-kernel-chain fast path", stacklevel=2)
+        # fast path, d 64/128, L <= 64 (8-wave backward): the attention backward
+        # forms dpooled from the head's state itself (nrk_din_attn_bwd_params_head;
+        # one launch and the dpooled round trip fewer).  NRK_DIN_FUSE_DP=0: A/B hook.
+        Lk = 32 if Lh <= 32 else 64
+        self.fuse_dp = (self.fast and d in (64, 128) and Lh <= 64 and Lk * d >= 4096 and self.F == 32
+                        and os.environ.get("NRK_DIN_FUSE_DP", "1") != "0")
         if self.fast:
             L = hist_ids.shape[1]
             self.hist_b = torch.empty((B, L), dtype=torch.int32, device=dev)
@@ -594,13 +603,22 @@ class FusedTrainStep:
             _lib.ptr(self.q_b), _lib.ptr(self.pooled), d, _lib.ptr(self.y_b), B, d, self.F, self.bn_momentum,
             self.bn_eps, self.p_drop,
             self.seed, _lib.ptr(self.step_t), ctypes.byref(self.hp), _lib.ptr(self.logits), _lib.ptr(loss),
-            _lib.ptr(self.dpooled), _lib.ptr(self.ws_head), self.ws_head.numel(), st), "din_head_train")
+            None if self.fuse_dp else _lib.ptr(self.dpooled), _lib.ptr(self.ws_head), self.ws_head.numel(), st),
+            "din_head_train")
         t0 = KernelTimer.mark("bwd")
-        _lib.check(L_.nrk_din_attn_bwd_params(
-            _lib.ptr(self.table), _lib.ptr(self.hist_b), N, dt, _lib.ptr(self.q_b), _lib.ptr(self.U_b),
-            _lib.ptr(self.W1k_b), _lib.ptr(w2), B, L, d, A, _lib.ptr(self.dpooled), _lib.ptr(self.alpha),
-            _lib.ptr(W1.grad), _lib.ptr(b1.grad), _lib.ptr(w2.grad), _lib.ptr(m.attn.attn[2].bias.grad), None,
-            _lib.ptr(self.ws_attn), self.ws_attn.numel(), st), "din_attn_bwd_params")
+        if self.fuse_dp:
+            _lib.check(L_.nrk_din_attn_bwd_params_head(
+                _lib.ptr(self.table), _lib.ptr(self.hist_b), N, dt, _lib.ptr(self.q_b), _lib.ptr(self.U_b),
+                _lib.ptr(self.W1k_b), _lib.ptr(w2), B, L, d, A, _lib.ptr(self.pooled), _lib.ptr(self.alpha), self.F,
+                ctypes.byref(self.hp), _lib.ptr(self.ws_head), self.ws_head.numel(), _lib.ptr(W1.grad),
+                _lib.ptr(b1.grad), _lib.ptr(w2.grad), _lib.ptr(m.attn.attn[2].bias.grad), _lib.ptr(self.ws_attn),
+                self.ws_attn.numel(), st), "din_attn_bwd_params_head")
+        else:
+            _lib.check(L_.nrk_din_attn_bwd_params(
+                _lib.ptr(self.table), _lib.ptr(self.hist_b), N, dt, _lib.ptr(self.q_b), _lib.ptr(self.U_b),
+                _lib.ptr(self.W1k_b), _lib.ptr(w2), B, L, d, A, _lib.ptr(self.dpooled), _lib.ptr(self.alpha),
+                _lib.ptr(W1.grad), _lib.ptr(b1.grad), _lib.ptr(w2.grad), _lib.ptr(m.attn.attn[2].bias.grad), None,
+                _lib.ptr(self.ws_attn), self.ws_attn.numel(), st), "din_attn_bwd_params")
         KernelTimer.push("bwd", t0)
         if self.grad_hook is not None:
             self.grad_hook(self.G)

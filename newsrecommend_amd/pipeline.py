@@ -203,7 +203,7 @@ rerank.path = None
 @torch.no_grad()
 def rerank_clusters(model, table: torch.Tensor, hist_rows: torch.Tensor, user_cluster: torch.Tensor,
                     cluster_off: torch.Tensor, cluster_rows: torch.Tensor, last_rows: torch.Tensor | None = None,
-                    k: int = 5, batch_samples: int = 1 << 22):
+                    k: int = 5, batch_samples: int = 1 << 22, append_missing: bool = False):
     """Retrieval.py:28-34 -> DIN.py:155-193 as the reference runs it: every
     user's candidates are the WHOLE cluster its profile is nearest to
     (cluster_candidates), so all users of cluster c share one ragged list,
@@ -214,9 +214,13 @@ def rerank_clusters(model, table: torch.Tensor, hist_rows: torch.Tensor, user_cl
     last_rows (U,) -- the row of each user's last click -- gives
     EvalDataset's labels (one-hot at the FIRST candidate equal to it, none when
     absent; DIN.py:27-31), the per-user BCE (DIN.py:176-177) and NDCG@k
-    (DIN.py:181-189, ndcg_at_k's tie rule).  Returns a dict: `logits` list of
-    (n_users_c, C_c) per cluster, `users` list of the user indices of each
-    group, and with last_rows `loss` (U,) f64 and `ndcg` (U,) f64."""
+    (DIN.py:181-189, ndcg_at_k's tie rule).  append_missing: the ground truth
+    (the last click) is appended to a user's list when the cluster lacks it
+    (finialize_retrieval.py:11-12): one extra column per group, -1 (padding,
+    excluded from the loss) where the cluster holds it.  Returns a dict:
+    `logits` list of (n_users_c, C_c [+1]) per cluster, `users` list of the
+    user indices of each group, and with last_rows `loss` (U,) f64 and
+    `ndcg` (U,) f64."""
     dev = table.device
     U = hist_rows.shape[0]
     uc = user_cluster.to(dev).long()
@@ -238,17 +242,25 @@ def rerank_clusters(model, table: torch.Tensor, hist_rows: torch.Tensor, user_cl
         us = order[lo:hi]
         cand = rows[oh[c]:oh[c + 1]]
         C = cand.numel()
-        lg = rerank(model, table, hist_rows[us], cand[None, :].expand(hi - lo, C), batch_samples=batch_samples)
+        cu = cand[None, :].expand(hi - lo, C)
+        if last_rows is not None and append_missing:
+            lu = last[us]
+            extra = torch.where((cu == lu[:, None]).any(1), torch.full_like(lu, -1), lu)
+            cu = torch.cat([cu, extra[:, None]], 1)
+        lg = rerank(model, table, hist_rows[us], cu, batch_samples=batch_samples)
         out["logits"].append(lg)
         out["users"].append(us)
         if last_rows is not None:
-            hit = cand[None, :] == last[us][:, None]
+            hit = (cu == last[us][:, None]) & (cu >= 0)
             first = torch.where(hit.any(1), hit.to(torch.int8).argmax(1), torch.full_like(us, -1))
-            lab = torch.zeros((hi - lo, C), dtype=torch.bool, device=dev)
+            lab = torch.zeros(cu.shape, dtype=torch.bool, device=dev)
             has = first >= 0
             lab[has.nonzero().squeeze(1), first[has]] = True
-            per = torch.nn.functional.binary_cross_entropy_with_logits(lg, lab.float(), reduction="none")
-            loss[us] = per.double().mean(1)
+            valid = cu >= 0
+            per = torch.nn.functional.binary_cross_entropy_with_logits(lg.clamp_min(-1e30), lab.float(),
+                                                                       reduction="none")
+            per = torch.where(valid, per.double(), torch.zeros_like(per, dtype=torch.float64))
+            loss[us] = per.sum(1) / valid.sum(1).double()
             ndcg[us] = ndcg_at_k(lg, lab, k)
     if last_rows is not None:
         out["loss"], out["ndcg"] = loss, ndcg

@@ -62,20 +62,26 @@ def _bn_inputs(cache, pooled, q):
     return [np.concatenate([q, pooled], 1), np.maximum(cache["pre.relu1"], 0), np.maximum(cache["pre.relu2"], 0)]
 
 
-def test_fused_train_step_fast_path_vs_oracle_c3_shape(gpu):
+@pytest.mark.parametrize("d,L,B,steps", [(128, 50, 512, 2), (256, 64, 64, 2), (256, 64, 4096, 1)])
+def test_fused_train_step_fast_path_vs_oracle_c3_shape(gpu, d, L, B, steps):
+    """(128, 50, 512): configs[2]'s shape.  (256, 64, 64) and (256, 64, 4096):
+    the reference's own training shape (DIN.py:16 EMBED_DIM from the 256-d
+    corpus of embedding_generate.py:14; main(): A 128, F 32, max_history 64,
+    batch 64, DIN.py:233-237) and the bench's batch at that shape."""
     from newsrecommend_amd.data import synthetic_click_rows
     from newsrecommend_amd.din import DIN, FusedTrainStep
     from oracle import din_oracle as o
 
     dev = torch.device("cuda")
-    d, A, F, L, B, N = 128, 128, 32, 50, 512, 6000
+    A, F, N = 128, 32, 6000
     lr, wd = 1.62e-3, 8.96e-5
     g = torch.Generator(device=dev).manual_seed(21)
     table = (torch.randn((N, d), generator=g, device=dev) * 0.5).to(torch.bfloat16)
-    hist, tgt, lab = synthetic_click_rows(4 * B, N, L, seed=9, device=dev)
+    hist, tgt, lab = synthetic_click_rows(max(4 * B, 2048), N, L, seed=9, device=dev)
     torch.manual_seed(3)
     model = DIN(d, A, F, 0.0).to(dev)
     fused = FusedTrainStep(model, table, hist, tgt, lab, B, lr=lr, weight_decay=wd, clip=1.0, graph=False)
+    print(f"FusedTrainStep path at d={d}, L={L}, B={B}: {fused.path}")
     assert fused.fast
     T = table.float().cpu().numpy().astype(np.float64)
     H, Tg, Y = hist.cpu().numpy(), tgt.cpu().numpy(), lab.cpu().numpy().reshape(-1, 1).astype(np.float64)
@@ -93,7 +99,7 @@ def test_fused_train_step_fast_path_vs_oracle_c3_shape(gpu):
     # moments, BN statistics before the step): a multi-step trajectory is not
     # comparable entry by entry, because Adam's sign-normalised first steps turn
     # gradient rounding in near-zero entries into +-lr parameter differences.
-    for s in range(2):
+    for s in range(steps):
         params = unflat(fused.P)
         state = {"step": s}
         for n, m_ in unflat(fused.M).items():
