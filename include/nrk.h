@@ -170,7 +170,11 @@ int nrk_din_attn_bwd_params_head(const void* table, const int32_t* hist_ids, int
                                  int32_t B, int32_t L, int32_t d, int32_t A, const float* pooled, const float* alpha,
                                  int32_t F, const struct nrk_din_head_params_s* hp, const void* head_ws,
                                  size_t head_ws_bytes, float* gW1, float* gb1, float* gw2, float* gb2,
-                                 void* ws, size_t ws_bytes, void* stream);
+                                 int64_t n_flat, double* norm_part, void* ws, size_t ws_bytes, void* stream);
+/*   norm_part (optional, device f64 [ceil(n_flat / 64)]): gW1 is then the base of
+ *   the model's flat gradient buffer of n_flat floats, [gW1 | gb1 | gw2 | gb2]
+ *   first and the head's (already final) gradients after; entry i receives the
+ *   sum of squares of flat entries [64 i, 64 i + 64), for nrk_clip_adam_partials. */
 
 /* One train batch from a device-resident click log (replaces TrainDataset.
  * __getitem__'s CPU gather, DIN.py:81-92, and the query GEMM of DIN.py:105-106):
@@ -184,6 +188,20 @@ int nrk_din_batch(const int64_t* idx, int32_t B, const int32_t* hist_all, const 
                   const float* lab_all, int64_t n_rows, int32_t L, const void* table, int64_t n_table,
                   int32_t dtype, int32_t d, const float* W1, const float* b1, int32_t A, int32_t* hist,
                   float* q, float* y, float* U, void* W1k_bf16, void* stream);
+/* W1 == NULL in nrk_din_batch: the gathers only (hist, q, y; b1 / U / W1k_bf16
+ * unused), e.g. for the rows of K steps at once; each step then forms
+ *   U [B][A] = q W1[:, :d]^T + b1 and W1k_bf16 from the gathered q [B][d] f32: */
+int nrk_din_batch_u(const float* q, int32_t B, int32_t d, const float* W1, const float* b1, int32_t A,
+                    float* U, void* W1k_bf16, void* stream);
+
+/* Diagnostics: the head-fused backward's per-workgroup phase timestamps
+ * (s_memrealtime ticks, 100 MHz; 8 per workgroup: entry, ids landed, first
+ * sample landed, loop done, dW1q flushed, exit), recorded while NRK_KTIME=1;
+ * then (values 32768 ..) per workgroup and wave 8 values: shader-clock cycles
+ * of the pipelined loop's stages {barrier wait, issue, A, B, C} and the
+ * iteration count.  Copies the first n (<= 9 x 32768) values to host memory.
+ * No reference counterpart. */
+int nrk_debug_ktimes(uint64_t* out, int64_t n);
 
 /* DIN attention for re-ranking (DIN.py:166-173: every candidate of a user
  * attends over the same history): pooled [nU*C][d] f32 for candidates whose
@@ -307,6 +325,15 @@ int nrk_clip_adam_workspace(int64_t n, size_t* ws_bytes);
 int nrk_clip_adam(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
                   float* step, float lr, const float* lr_dev, float beta1, float beta2, float eps, float weight_decay,
                   float max_norm, void* ws, size_t ws_bytes, void* stream);
+
+/* The same clip_grad_norm_ + Adam with the squared gradient norm given as f64
+ * partials (norm_part [n_part], e.g. from nrk_din_attn_bwd_params_head): no
+ * pass over all gradients per block; each block scales and updates only its
+ * own entries.  Workspace as nrk_clip_adam (zeroed once; its ticket). */
+int nrk_clip_adam_partials(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
+                           float* step, float lr, const float* lr_dev, float beta1, float beta2, float eps,
+                           float weight_decay, float max_norm, const double* norm_part, int32_t n_part,
+                           void* ws, size_t ws_bytes, void* stream);
 
 /* Row gather (table [N][d] dtype -> out [n][d] f32), id < 0 -> zeros.
  * Replaces the per-sample dict lookups of DIN.py:47-50,83 (target and

@@ -1112,6 +1112,16 @@ __device__ __forceinline__ void glds4_asm(const void* gsrc, uint32_t lds_dst) {
 // it forms dpooled itself (FDP): the head's state after nrk_din_head_train
 // (nrk_din_head_ws_views) and the forward's pooled rows.  stat0 / sum5 / bn0w /
 // w1 are indexed over the head's 2d input columns (the pooled half from d).
+// Per-workgroup phase timestamps (s_memrealtime, 100 MHz) of the head-fused
+// backward, for tools/din_step.py --ktime (NRK_KTIME=1): slot 8 b + i
+__device__ uint64_t g_ktime[4096 * 8];
+// per wave: shader-clock cycles spent in each stage of the pipelined loop (tools/din_step.py --ktime)
+__device__ uint64_t g_ktime2[4096 * 8 * 8];
+#define NRK_KT(on, i)                                                                         \
+  do {                                                                                        \
+    if ((on) && threadIdx.x == 0) g_ktime[(size_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+
 struct DpSrc {
   const float* pooled;  // [B][D]
   const float* da1;     // [B][32]
@@ -1120,6 +1130,7 @@ struct DpSrc {
   const double* sum5;   // {sum dh0 [2D], sum dh0 xhat0 [2D]}
   const float* bn0w;    // fc.0 weight [2D]
   float invB;
+  int ktime;             // record phase timestamps (g_ktime)
 };
 
 template <int D, int LP, int NSLOT>
@@ -1391,6 +1402,8 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8_kernel(
   float* colc = w1p + (FDP ? 32 * D : 0);
   float* dpl = colc + 5 * D;
   static_assert(!FDP || LP <= 64, "FDP: the da1 row takes the second alpha piece");
+  const bool kt = FDP && dps.ktime;
+  NRK_KT(kt, 0);
   if constexpr (FDP) {
     for (int i = tid; i < 32 * D; i += 512) w1p[i] = dps.w1[(size_t)(i / D) * 2 * D + D + i % D];
     for (int c = tid; c < D; c += 512) {
@@ -1498,6 +1511,7 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8_kernel(
 #pragma unroll
   for (int k = 0; k < X; ++k) issue_ids(b + k * grid, k);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  NRK_KT(kt, 1);
 #pragma unroll
   for (int k = 0; k < P; ++k) {
     store_du();  // nothing to store yet: the dummy slot (keeps every group the same size)
@@ -1508,6 +1522,7 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8_kernel(
   for (; b < B; b += grid) {
     // this wave's DMA group of sample b landed; all waves' after the barrier; slot of b - grid is free
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"((P - 1) * N_D) : "memory");
+    if (it == 0) NRK_KT(kt, 2);
     store_du();
     issue_ids(b + (P + X) * grid, e + X < RING ? e + X : e + X - RING);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(X * N_D) : "memory");  // ids of b + P grid landed
@@ -1648,6 +1663,7 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8_kernel(
     b_keep = b;
     sl = sl == NSLOT - 1 ? 0 : sl + 1;
   }
+  NRK_KT(kt, 3);
   store_du();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup exits
   if constexpr (FQ) {
@@ -1656,6 +1672,7 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8_kernel(
     else if (us < nsl) {  // no sample: a zero dW1q partial
       for (int i = lane; i < 32 * D; i += 64) sqs_slab[(size_t)(32 * us) * D + i] = 0.f;
     }
+    NRK_KT(kt, 4);
   }
   // combine the row-group pairs (rg 1 into rg 0, fixed order) through LDS
   float* xch = slot0;  // [4 unit slices][32][D] f32, reused for dW1k then dW1q
@@ -1699,6 +1716,352 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8_kernel(
     }
     if (rg == 0 && us == 0 && lane == 0) slab[(size_t)A * D + A] = tb2 + xs[256];
   }
+  NRK_KT(kt, 5);
+}
+
+// Software-pipelined form of the head-fused 8-wave backward (FQ + FDP, LP <= 64).  The
+// serial form runs dpooled, dalpha and the z / dW1k work of one sample between three
+// barriers; here each iteration runs the three stages on three samples behind ONE
+// barrier: A forms dpooled of sample i + 2 (all 512 threads, 4 lanes per column, the
+// thread's W1p column quarter and BN0 column constants in registers), B dalpha of
+// sample i + 1 (double-buffered dpl / dabuf), C the MFMA work of sample i.  Five
+// slots, data groups 4 samples ahead, ids 4 groups before their data.  Same outputs as
+// din_bwd_deep8_kernel<D, LP, *, true, true> up to the summation order of dpooled.
+template <int D, int LP>
+__global__ __launch_bounds__(512, 1) void din_bwd_deep8p_kernel(
+    const uint16_t* __restrict__ table, const int32_t* __restrict__ ids, int64_t n_table, const float* __restrict__ U,
+    const uint16_t* __restrict__ W1k, const float* __restrict__ w2, int B, int L, int A,
+    const float* __restrict__ alpha, float* __restrict__ slabs, const float* __restrict__ q, int dq, DpSrc dps) {
+  constexpr int CPR = D / 8, KS = D / 16, NCT = D / 32, NC = LP / 32;
+  constexpr int NPW = LP * CPR / 512;  // key-image DMA pieces per wave
+  static_assert(LP <= 64 && NPW >= 1, "deep8p: LP <= 64, L D >= 4096");
+  constexpr int N_D = NPW + 2;  // per wave and group: ids, keys, one small piece
+  constexpr int NSLOT = 5, P = 4, X = 4, RING = 5;
+  // slot (floats): pooled [128] | alpha [64], da1 [32..] | U [128] | q [128] | key image [LP][D] bf16
+  constexpr int SLOT_F = 4 * 128 + LP * D / 2;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int us = w & 3, rg = w >> 2;
+  const int nsl = A >> 5;
+  float* slot0 = reinterpret_cast<float*>(smem);
+  int32_t* const ring0 = reinterpret_cast<int32_t*>(slot0 + NSLOT * SLOT_F);
+  int32_t* idring = ring0 + w * RING * 64;                                  // [RING][64] per wave
+  float* dsbuf = reinterpret_cast<float*>(ring0 + 8 * RING * 64) + w * 64;  // [64] per wave
+  float* dabuf = reinterpret_cast<float*>(ring0 + 8 * RING * 64) + 8 * 64;  // [2][64]
+  float* dul = dabuf + 128;                                                 // [16][2 row groups][128]
+  float* ql = dul + 16 * 2 * 128;                                           // [16][128]
+  float* dpl = ql + 16 * 128;                                               // [2][D]
+  NRK_KT(dps.ktime, 0);
+
+  // stage A constants: column c, quarter p of the 32 fc.1 rows (rows 4 jj + p)
+  const bool a_act = tid < 4 * D;
+  const int ac = a_act ? tid >> 2 : 0, ap = tid & 3;
+  float w1r[8];
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) w1r[jj] = dps.w1[(size_t)(4 * jj + ap) * 2 * D + D + ac];
+  const float cm = dps.stat0[D + ac], civ = dps.stat0[3 * D + ac], cgw = dps.bn0w[D + ac];
+  const float csb = (float)dps.sum5[D + ac] * dps.invB, csg = (float)dps.sum5[3 * D + ac] * dps.invB;
+
+  WFrag<true, D> wf;
+  const int wu = us < nsl ? us : 0;
+  wf.load(W1k, 32 * wu + r, h);
+  const float w2n = w2[32 * wu + r];
+#pragma unroll
+  for (int s2 = 0; s2 < KS; ++s2) asm volatile("" ::"v"(wf.f[s2]));  // hipcc's waits for these land here
+  asm volatile("" ::"v"(w2n));
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) asm volatile("" ::"v"(w1r[jj]));
+  asm volatile("" ::"v"(cm), "v"(civ), "v"(cgw), "v"(csb), "v"(csg));
+  f32x16 dw[NCT];
+#pragma unroll
+  for (int c = 0; c < NCT; ++c)
+#pragma unroll
+    for (int g = 0; g < 16; ++g) dw[c][g] = 0.f;
+  float dw2_acc = 0.f, db2_acc = 0.f, db1_acc = 0.f;
+  float* const sqs_slab = slabs + (size_t)blockIdx.x * slab_floats(A, D) + slab_q_off(A, D);
+
+  auto issue_ids = [&](int64_t b, int e) {
+    const int64_t bc = b < B ? b : 0;
+    const int i = lane < L ? lane : 0;
+    glds4_asm(ids + bc * L + i, lds_u32(idring + e * 64));
+  };
+  auto issue_data = [&](int64_t b, int sl, int e) {
+    float* sp = slot0 + sl * SLOT_F;
+    uint16_t* img = reinterpret_cast<uint16_t*>(sp + 4 * 128);
+#pragma unroll
+    for (int k = 0; k < NPW; ++k) {
+      const int u = w + 8 * k;
+      const int p = u * 64 + lane;
+      const int row = p / CPR, pc = p % CPR;
+      const int cc = pc ^ kswz<CPR>(row);
+      const int32_t idv0 = idring[e * 64 + row];
+      const int32_t idr = row < L && b < B ? idv0 : -1;
+      const uint16_t* src = (idr >= 0 && idr < n_table) ? table + (int64_t)idr * D + cc * 8 : zero_row(b, row) + cc * 8;
+      glds16_asm(src, lds_u32(img + u * 64 * 8));
+    }
+    const int64_t bc = b < B ? b : 0;
+    {  // small piece w of [pooled0, pooled1, alpha, da1, u0, u1, q0, q1]
+      const int kind = w >> 1, part = w & 1;
+      const int i = part * 64 + lane;
+      const float* base = kind == 0 ? dps.pooled + bc * D : kind == 1 ? (part ? dps.da1 + bc * 32 : alpha + bc * L)
+                          : kind == 2 ? U + bc * A : q + bc * dq;
+      const int lim = kind == 0 ? D : kind == 1 ? (part ? 32 : L) : kind == 2 ? A : dq;
+      const int ii = kind == 1 ? lane : i;
+      glds4_asm(base + (ii < lim ? ii : 0), lds_u32(sp + kind * 128 + part * 64));
+    }
+  };
+  // stage A: dpooled[c] = iv g (sum_j da1[j] W1p[j][c] - sb - xhat sg), xhat = (pooled - m) iv
+  auto stage_a = [&](int sl, float* out) {
+    const float* sp = slot0 + sl * SLOT_F;
+    const float* da1s = sp + 192;
+    float acc = 0.f;
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) acc = fmaf(da1s[4 * jj + ap], w1r[jj], acc);
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+    if (a_act && ap == 0) {
+      const float xhat = (sp[ac] - cm) * civ;
+      out[ac] = civ * cgw * (acc - csb - xhat * csg);
+    }
+  };
+  // stage B: dalpha[row] = dpooled . K[row], wave w owns rows [w R, (w+1) R)
+  auto stage_b = [&](int sl, const float* sdp, float* out) {
+    const unsigned char* img = reinterpret_cast<const unsigned char*>(slot0 + sl * SLOT_F + 512);
+    constexpr int R = LP / 8, LPR = 64 / R, CH = CPR / LPR;
+    const int row = w * R + lane / LPR, part = lane % LPR;
+    float acc = 0.f;
+#pragma unroll
+    for (int ch = 0; ch < CH; ++ch) {
+      const int cc = part * CH + ch;
+      const uint4 kv = *reinterpret_cast<const uint4*>(img + row * 2 * D + 16 * (cc ^ kswz<CPR>(row)));
+      const float4 d0 = *reinterpret_cast<const float4*>(sdp + 8 * cc);
+      const float4 d1 = *reinterpret_cast<const float4*>(sdp + 8 * cc + 4);
+      acc = fmaf(d0.x, __uint_as_float(kv.x << 16), acc);
+      acc = fmaf(d0.y, __uint_as_float(kv.x & 0xFFFF0000u), acc);
+      acc = fmaf(d0.z, __uint_as_float(kv.y << 16), acc);
+      acc = fmaf(d0.w, __uint_as_float(kv.y & 0xFFFF0000u), acc);
+      acc = fmaf(d1.x, __uint_as_float(kv.z << 16), acc);
+      acc = fmaf(d1.y, __uint_as_float(kv.z & 0xFFFF0000u), acc);
+      acc = fmaf(d1.z, __uint_as_float(kv.w << 16), acc);
+      acc = fmaf(d1.w, __uint_as_float(kv.w & 0xFFFF0000u), acc);
+    }
+#pragma unroll
+    for (int o = 1; o < LPR; o <<= 1) acc += __shfl_xor(acc, o, 64);
+    if (part == 0) out[row] = acc;
+  };
+
+  const int64_t grid = gridDim.x;
+  const int64_t b0 = blockIdx.x;
+  const int n_it = b0 < B ? (int)((B - b0 + grid - 1) / grid) : 0;
+#pragma unroll
+  for (int k = 0; k < X; ++k) issue_ids(b0 + k * grid, k);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  NRK_KT(dps.ktime, 1);
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    issue_ids(b0 + (k + X) * grid, (k + X) % RING);
+    issue_data(b0 + k * grid, k, k);
+  }
+  // groups of samples 0, 1 landed (all waves' after the barrier)
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((P - 2) * N_D) : "memory");
+  stage_a(0, dpl);
+  stage_a(1, dpl + D);
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  stage_b(0, dpl, dabuf);
+  NRK_KT(dps.ktime, 2);
+
+  int sl = 0;                  // slot of sample i
+  uint64_t kacc[5] = {0, 0, 0, 0, 0}, kprev = dps.ktime ? __builtin_amdgcn_s_memtime() : 0;
+  auto kts = [&](int j) {
+    if (dps.ktime) {
+      const uint64_t now = __builtin_amdgcn_s_memtime();
+      kacc[j] += now - kprev;
+      kprev = now;
+    }
+  };
+  for (int i = 0; i < n_it; ++i) {
+    // group of sample i + 2 landed; stage results of iteration i - 1 visible; slot of i - 1 free
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"((P - 3) * N_D) : "memory");
+    kts(0);
+    {
+      const int e_new = (i + P + X) % RING, e_dat = (i + P) % RING;
+      issue_ids(b0 + (int64_t)(i + P + X) * grid, e_new);
+      issue_data(b0 + (int64_t)(i + P) * grid, sl == 0 ? NSLOT - 1 : sl - 1, e_dat);
+    }
+    kts(1);
+    const int sl1 = sl + 1 < NSLOT ? sl + 1 : sl + 1 - NSLOT, sl2 = sl + 2 < NSLOT ? sl + 2 : sl + 2 - NSLOT;
+    stage_a(sl2, dpl + (i & 1) * D);
+    if (dps.ktime) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    kts(2);
+    stage_b(sl1, dpl + ((i + 1) & 1) * D, dabuf + ((i + 1) & 1) * 64);
+    if (dps.ktime) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    kts(3);
+
+    // stage C: sample i
+    const float* sp = slot0 + sl * SLOT_F;
+    const float* sal = sp + 128;
+    const float* sU = sp + 256;
+    const float* dab = dabuf + (i & 1) * 64;
+    const unsigned char* img = reinterpret_cast<const unsigned char*>(sp + 512);
+    float du = 0.f;
+    if (us < nsl && rg < NC) {
+      const float un = sU[32 * us + r];
+      float da[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) da[c] = dab[32 * c + r];
+      float t = 0.f;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int row = 32 * c + r;
+        t += (row < L && h == 0) ? sal[row] * da[c] : 0.f;
+      }
+      const float cdot = wave_sum(t);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int row = 32 * c + r;
+        if (h == 0 && (c & 1) == rg) {
+          const float ds = row < L ? sal[row] * (da[c] - cdot) : 0.f;
+          dsbuf[row] = ds;
+          if (us == 0) db2_acc += ds;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        if ((c & 1) != rg) continue;
+        f32x16 acc;
+#pragma unroll
+        for (int g = 0; g < 16; ++g) acc[g] = un;
+#pragma unroll
+        for (int s2 = 0; s2 < KS; ++s2) {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(img + KImg<true, D>::off(32 * c + r, 16 * s2 + 8 * h));
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, wf.f[s2], acc, 0, 0, 0);
+        }
+        f32x16 dz;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float4 d4 = *reinterpret_cast<const float4*>(dsbuf + 32 * c + 8 * j + 4 * h);
+          const float dsv[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+          for (int i2 = 0; i2 < 4; ++i2) {
+            const int g = 4 * j + i2;
+            const float z = acc[g];
+            dw2_acc = fmaf(dsv[i2], fmaxf(z, 0.f), dw2_acc);
+            const float v = z > 0.f ? dsv[i2] * w2n : 0.f;
+            dz[g] = v;
+            du += v;
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          bf16x8 af;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {  // v_cvt_pk_bf16_f32 (round to nearest even)
+            const bf16x2_hw pk = {(__bf16)dz[8 * s + 2 * j], (__bf16)dz[8 * s + 2 * j + 1]};
+            const uint32_t u = __builtin_bit_cast(uint32_t, pk);
+            af[2 * j] = (short)(u & 0xFFFF);
+            af[2 * j + 1] = (short)(u >> 16);
+          }
+          const int grp = lane >> 4, i16 = lane & 15;
+          const int rowq = 32 * c + 16 * s + 4 * h + (i16 >> 2);
+#pragma unroll
+          for (int cc = 0; cc < NCT; ++cc) {
+            const int col = 32 * cc + 16 * (grp & 1) + 4 * (i16 & 3);
+            typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+            const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(img + KImg<true, D>::off(rowq, col)));
+            const bf16x4 hi =
+                __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(img + KImg<true, D>::off(rowq + 8, col)));
+            const bf16x8 bfr = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+            dw[cc] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, dw[cc], 0, 0, 0);
+          }
+        }
+      }
+      du += __shfl_xor(du, 32, 64);
+      db1_acc += du;
+    }
+    // stage this sample's dU rows (both row groups) and query row (host: <= 16 samples per workgroup)
+    if (h == 0 && us < nsl && i < 16) dul[i * 256 + rg * 128 + 32 * us + r] = du;
+    if (lane < 16 && i < 16) ql[i * 128 + 16 * w + lane] = sp[384 + 16 * w + lane];
+    sl = sl1;
+    if (dps.ktime) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    kts(4);
+  }
+  if (dps.ktime && lane == 0) {
+    uint64_t* kd = g_ktime2 + ((size_t)blockIdx.x * 8 + w) * 8;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) kd[j] = kacc[j];
+    kd[5] = (uint64_t)n_it;
+  }
+  NRK_KT(dps.ktime, 3);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");  // no LDS-DMA lands after this
+  // dW1q partial of the staged samples: wave (us, rg) owns tiles n = 32 us.., k = 32 (rg + 2 j)..
+  if (us < nsl) {
+    const int ns = n_it < 16 ? n_it : 16;
+#pragma unroll
+    for (int j = 0; j < (NCT + 1) / 2; ++j) {
+      const int tk = rg + 2 * j;
+      if (tk >= NCT) continue;
+      f32x16 acc;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) acc[g] = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        const int sm = 2 * kk + h;
+        const float av = sm < ns ? dul[sm * 256 + 32 * us + r] + dul[sm * 256 + 128 + 32 * us + r] : 0.f;
+        const float bv = sm < ns ? ql[sm * 128 + 32 * tk + r] : 0.f;
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int g = 0; g < 16; ++g) sqs_slab[(size_t)(32 * us + acc_row(g, h)) * D + 32 * tk + r] = acc[g];
+    }
+  }
+  NRK_KT(dps.ktime, 4);
+  // combine the row-group pairs (rg 1 into rg 0, fixed order) through LDS
+  float* xch = slot0;  // [4 unit slices][32][D] f32
+  const bool act = us < nsl;
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  if (rg == 1 && act) {
+#pragma unroll
+    for (int c = 0; c < NCT; ++c)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) xch[(size_t)(32 * us + acc_row(g, h)) * D + 32 * c + r] = dw[c][g];
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  if (rg == 0 && act) {
+#pragma unroll
+    for (int c = 0; c < NCT; ++c)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) dw[c][g] += xch[(size_t)(32 * us + acc_row(g, h)) * D + 32 * c + r];
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  float* xs = slot0 + 4 * 32 * D;  // [4][32] dw2, [4][32] db1, [1] db2 of the rg = 1 waves
+  {
+    const float t2 = dw2_acc + __shfl_xor(dw2_acc, 32, 64);
+    const float tb2 = wave_sum(db2_acc);
+    if (rg == 1 && act && h == 0) {
+      xs[32 * us + r] = t2;
+      xs[128 + 32 * us + r] = db1_acc;
+    }
+    if (rg == 1 && us == 0 && lane == 0) xs[256] = tb2;
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    float* slab = slabs + (size_t)blockIdx.x * slab_floats(A, D);
+    if (rg == 0 && act) {
+      float* sqs = slab + slab_q_off(A, D);
+#pragma unroll
+      for (int c = 0; c < NCT; ++c)
+#pragma unroll
+        for (int g = 0; g < 16; ++g) slab[(size_t)(32 * us + acc_row(g, h)) * D + 32 * c + r] = dw[c][g];
+      if (h == 0) {
+        slab[(size_t)A * D + 32 * us + r] = t2 + xs[32 * us + r];
+        sqs[(size_t)A * D + 32 * us + r] = db1_acc + xs[128 + 32 * us + r];
+      }
+    }
+    if (rg == 0 && us == 0 && lane == 0) slab[(size_t)A * D + A] = tb2 + xs[256];
+  }
+  NRK_KT(dps.ktime, 5);
 }
 
 // D = 256 variant of the 8-wave backward (the reference's training width):
@@ -2013,11 +2376,17 @@ __global__ __launch_bounds__(256) void din_dwq_kernel(const float* __restrict__ 
 // tensors: gW1 (A, 2d) = [dW1q | dW1k[:, :d]], gb1, gw2, gb2.  A block owns
 // 64 consecutive outputs of the layout {dW1q, dW1k, db1, dw2, db2}; its 8
 // waves each sum every 8th slab with 4 loads in flight, then combine.
+// norm_part (optional): gW1 is then the base of the model's flat gradient
+// buffer of n_flat floats ([gW1 | gb1 | gw2 | gb2 | the head's gradients, final
+// already]); block i also writes the fp64 sum of squares of flat entries
+// [64 i, 64 i + 64) to norm_part[i] (blocks past the attention outputs only read
+// the head's), so clip_grad_norm_ needs no second pass over the gradients.
 __global__ __launch_bounds__(512) void din_bwd_reduce_params_kernel(const float* __restrict__ slabs, int nslab, int A,
                                                                     int D, int d, float* __restrict__ gW1,
                                                                     float* __restrict__ gb1, float* __restrict__ gw2,
                                                                     float* __restrict__ gb2,
-                                                                    const float* __restrict__ qpart, int nkc) {
+                                                                    const float* __restrict__ qpart, int nkc,
+                                                                    int64_t n_flat, double* __restrict__ norm_part) {
   __shared__ float part[8][64];
   const size_t n = slab_floats(A, D);
   const size_t nw = (size_t)A * d;  // per half of W1
@@ -2054,13 +2423,22 @@ __global__ __launch_bounds__(512) void din_bwd_reduce_params_kernel(const float*
   }
   part[g][o] = (s0 + s1) + (s2 + s3);
   __syncthreads();
-  if (g == 0 && i < nout) {
-    const float t = ((part[0][o] + part[1][o]) + (part[2][o] + part[3][o])) +
-                    ((part[4][o] + part[5][o]) + (part[6][o] + part[7][o]));
-    if (i < 2 * nw) gW1[i] = t;
-    else if (i < 2 * nw + A) gb1[i - 2 * nw] = t;
-    else if (i < 2 * nw + 2 * A) gw2[i - 2 * nw - A] = t;
-    else gb2[0] = t;
+  if (g == 0) {
+    float t = 0.f;
+    if (i < nout) {
+      t = ((part[0][o] + part[1][o]) + (part[2][o] + part[3][o])) +
+          ((part[4][o] + part[5][o]) + (part[6][o] + part[7][o]));
+      if (i < 2 * nw) gW1[i] = t;
+      else if (i < 2 * nw + A) gb1[i - 2 * nw] = t;
+      else if (i < 2 * nw + 2 * A) gw2[i - 2 * nw - A] = t;
+      else gb2[0] = t;
+    } else if (norm_part != nullptr && (int64_t)i < n_flat) {
+      t = gW1[i];  // a head gradient (flat buffer)
+    }
+    if (norm_part != nullptr) {
+      const double sq = wave_sum((double)t * (double)t);
+      if (o == 0) norm_part[blockIdx.x] = sq;
+    }
   }
 }
 
@@ -2096,7 +2474,7 @@ __global__ __launch_bounds__(256) void din_bwd_reduce_kernel(const float* __rest
 //   and W1q is split three ways (hi + mid + lo bf16), so every product is the
 //   exact f32 product of the f32 weight and q, accumulated in f32;
 //   W1k (the key half of W1) -> bf16 for the attention kernels (grid-strided).
-template <int D>
+template <int D, bool DO_U>
 __global__ __launch_bounds__(256) void din_batch_kernel(const int64_t* __restrict__ idx, int B,
                                                         const int32_t* __restrict__ hist_all,
                                                         const int32_t* __restrict__ tgt_all,
@@ -2129,9 +2507,11 @@ __global__ __launch_bounds__(256) void din_batch_kernel(const int64_t* __restric
     s_row[tid] = row;
     s_tgt[tid] = t;
   }
-  for (int64_t e = (int64_t)blockIdx.x * 256 + tid; e < (int64_t)A * D; e += (int64_t)gridDim.x * 256) {
-    const int64_t n = e / D, k = e % D;
-    W1k_bf[e] = f32_to_bf16_rne(W1[n * 2 * D + D + k]);
+  if constexpr (DO_U) {
+    for (int64_t e = (int64_t)blockIdx.x * 256 + tid; e < (int64_t)A * D; e += (int64_t)gridDim.x * 256) {
+      const int64_t n = e / D, k = e % D;
+      W1k_bf[e] = f32_to_bf16_rne(W1[n * 2 * D + D + k]);
+    }
   }
   __syncthreads();
   for (int e0 = tid; e0 < 32 * L; e0 += 8 * 256) {  // 8 loads in flight per thread
@@ -2175,6 +2555,71 @@ __global__ __launch_bounds__(256) void din_batch_kernel(const int64_t* __restric
       *reinterpret_cast<float4*>(o) = lo4;
       *reinterpret_cast<float4*>(o + 4) = hi4;
     }
+  }
+  if constexpr (!DO_U) return;
+  for (int ws = w; ws < A / 32; ws += 4) {
+    f32x16 acc;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) acc[g] = 0.f;
+    const float* wrow = W1 + (int64_t)(32 * ws + r) * 2 * D;
+#pragma unroll
+    for (int s2 = 0; s2 < KS; ++s2) {
+      const float4 w0 = *reinterpret_cast<const float4*>(wrow + 16 * s2 + 8 * h);
+      const float4 w1 = *reinterpret_cast<const float4*>(wrow + 16 * s2 + 8 * h + 4);
+      const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      bf16x8 fh, fm, fl;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint16_t hb = f32_to_bf16_rne(wv[j]);
+        const float rem1 = wv[j] - bf16_to_f32(hb);
+        const uint16_t mb = f32_to_bf16_rne(rem1);
+        const uint16_t lb = f32_to_bf16_rne(rem1 - bf16_to_f32(mb));
+        fh[j] = (short)hb;
+        fm[j] = (short)mb;
+        fl[j] = (short)lb;
+      }
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fl, qf[s2], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fm, qf[s2], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fh, qf[s2], acc, 0, 0, 0);
+    }
+    if (b < B) {
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int n = 32 * ws + acc_row(g, h);
+        U[(int64_t)b * A + n] = acc[g] + b1[n];
+      }
+    }
+  }
+}
+
+// The per-step half of the train batch when the gathers of several steps ran
+// ahead (nrk_din_batch with W1 == NULL over K steps' rows): U = q W1q^T + b1
+// from the gathered f32 query rows (bf16-exact: rows of a bf16 table) and
+// W1k -> bf16, the same MFMA split as din_batch_kernel.
+template <int D>
+__global__ __launch_bounds__(256) void din_u_kernel(const float* __restrict__ q, int B, const float* __restrict__ W1,
+                                                    const float* __restrict__ b1, int A, float* __restrict__ U,
+                                                    uint16_t* __restrict__ W1k_bf) {
+  constexpr int KS = D / 16;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int b0 = blockIdx.x * 32;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + tid; e < (int64_t)A * D; e += (int64_t)gridDim.x * 256) {
+    const int64_t n = e / D, k = e % D;
+    W1k_bf[e] = f32_to_bf16_rne(W1[n * 2 * D + D + k]);
+  }
+  const int b = b0 + r;
+  bf16x8 qf[KS];
+#pragma unroll
+  for (int s2 = 0; s2 < KS; ++s2) {
+    float4 lo4 = make_float4(0.f, 0.f, 0.f, 0.f), hi4 = lo4;
+    if (b < B) {
+      lo4 = *reinterpret_cast<const float4*>(q + (int64_t)b * D + 16 * s2 + 8 * h);
+      hi4 = *reinterpret_cast<const float4*>(q + (int64_t)b * D + 16 * s2 + 8 * h + 4);
+    }
+    qf[s2][0] = (short)f32_to_bf16_rne(lo4.x); qf[s2][1] = (short)f32_to_bf16_rne(lo4.y);
+    qf[s2][2] = (short)f32_to_bf16_rne(lo4.z); qf[s2][3] = (short)f32_to_bf16_rne(lo4.w);
+    qf[s2][4] = (short)f32_to_bf16_rne(hi4.x); qf[s2][5] = (short)f32_to_bf16_rne(hi4.y);
+    qf[s2][6] = (short)f32_to_bf16_rne(hi4.z); qf[s2][7] = (short)f32_to_bf16_rne(hi4.w);
   }
   for (int ws = w; ws < A / 32; ws += 4) {
     f32x16 acc;
@@ -2444,21 +2889,24 @@ extern "C" int nrk_din_batch(const int64_t* idx, int32_t B, const int32_t* hist_
   NRK_CHECK_ARG(A >= 32 && A <= 128 && A % 32 == 0, "din_batch: attn_units %d unsupported (32..128 step 32)", A);
   NRK_CHECK_ARG(L >= 1 && L <= 128 && B >= 0, "din_batch: bad L=%d / B=%d", L, B);
   if (B == 0) return NRK_OK;
-  NRK_CHECK_ARG(idx && hist_all && tgt_all && lab_all && table && W1 && b1 && hist && q && y && U && W1k_bf16,
+  const bool do_u = W1 != nullptr;  // W1 == NULL: the gathers only (several steps' rows ahead; nrk_din_batch_u)
+  NRK_CHECK_ARG(idx && hist_all && tgt_all && lab_all && table && hist && q && y && (!do_u || (b1 && U && W1k_bf16)),
                 "din_batch: null pointer");
   const unsigned grid = (unsigned)cdiv(B, 32);
   hipStream_t st = (hipStream_t)stream;
   const uint16_t* tb = static_cast<const uint16_t*>(table);
   uint16_t* wk = static_cast<uint16_t*>(W1k_bf16);
-  if (d == 256)
-    hipLaunchKernelGGL(din_batch_kernel<256>, dim3(grid), dim3(256), 0, st, idx, B, hist_all, tgt_all, lab_all, n_rows, L,
-                       tb, n_table, W1, b1, A, hist, q, y, U, wk);
-  else if (d == 128)
-    hipLaunchKernelGGL(din_batch_kernel<128>, dim3(grid), dim3(256), 0, st, idx, B, hist_all, tgt_all, lab_all, n_rows, L,
-                       tb, n_table, W1, b1, A, hist, q, y, U, wk);
-  else
-    hipLaunchKernelGGL(din_batch_kernel<64>, dim3(grid), dim3(256), 0, st, idx, B, hist_all, tgt_all, lab_all, n_rows, L,
-                       tb, n_table, W1, b1, A, hist, q, y, U, wk);
+#define NRK_BATCH(DD)                                                                                               \
+  do {                                                                                                              \
+    if (do_u)                                                                                                       \
+      hipLaunchKernelGGL((din_batch_kernel<DD, true>), dim3(grid), dim3(256), 0, st, idx, B, hist_all, tgt_all,     \
+                         lab_all, n_rows, L, tb, n_table, W1, b1, A, hist, q, y, U, wk);                              \
+    else                                                                                                            \
+      hipLaunchKernelGGL((din_batch_kernel<DD, false>), dim3(grid), dim3(256), 0, st, idx, B, hist_all, tgt_all,    \
+                         lab_all, n_rows, L, tb, n_table, W1, b1, A, hist, q, y, U, wk);                              \
+  } while (0)
+  if (d == 256) NRK_BATCH(256); else if (d == 128) NRK_BATCH(128); else NRK_BATCH(64);
+#undef NRK_BATCH
   NRK_CHECK_LAUNCH("din_batch_kernel");
   return NRK_OK;
 }
@@ -2467,7 +2915,7 @@ static int bwd_params_impl(const void* table, const int32_t* hist_ids, int64_t n
                            const float* q, const float* U, const void* W1k, const float* w2, int32_t B, int32_t L,
                            int32_t d, int32_t A, const float* dpooled, const float* alpha, float* gW1, float* gb1,
                            float* gw2, float* gb2, float* dU, void* ws, size_t ws_bytes, void* stream,
-                           const DpSrc* dps) {
+                           const DpSrc* dps, int64_t n_flat = 0, double* norm_part = nullptr) {
   int rc = check_common(table, dtype, B, L, d, A);
   if (rc) return rc;
   NRK_CHECK_ARG(dtype == NRK_DTYPE_BF16 && hist_ids != nullptr &&
@@ -2516,7 +2964,9 @@ static int bwd_params_impl(const void* table, const int32_t* hist_ids, int64_t n
     const bool w8 = LPk * d >= 4096;  // >= 8 key-image pieces: one per wave
     size_t dsm = (size_t)(nslot * (4 * 128 + LPk * d / 2) + 4 * 4 * 128 + 5 * 128) * 4;
     // deep8: 3 slots (2 samples in flight; 4 and 5 measured no faster, profiles/r03_din_ab.log)
-    constexpr int nslot8 = 3;
+    // NRK_DEEP8_NSLOT=4 (A/B hook, head-fused form only): one more sample in flight
+    const char* ns_env = getenv("NRK_DEEP8_NSLOT");
+    const int nslot8 = (dps && ns_env && *ns_env == '4') ? 4 : 3;
     // dW1q folded into the 8-wave kernel (16 samples' dU / q rows in LDS) instead of the
     // dU stores + din_dwq_kernel; NRK_DEEP8_FOLDQ=0: the old form (A/B hook)
     const char* fq_env = getenv("NRK_DEEP8_FOLDQ");
@@ -2528,13 +2978,28 @@ static int bwd_params_impl(const void* table, const int32_t* hist_ids, int64_t n
       const size_t xneed = ((size_t)4 * 32 * d + 257) * 4;  // pair-combine exchange area (reuses the slots)
       if (dsm < xneed) dsm = xneed;
     }
+    // software-pipelined head-fused form (one barrier per sample); NRK_DEEP8_PIPE=1 (A/B hook)
+    const char* pp_env = getenv("NRK_DEEP8_PIPE");
+    const bool pipe8 = dps && w8 && fold_q && LPk <= 64 && (pp_env && *pp_env == '1');
+    if (pipe8) {
+      dsm = (size_t)(5 * (4 * 128 + LPk * d / 2) + 8 * 5 * 64 + 8 * 64 + 128 + 16 * 256 + 16 * 128 + 2 * d) * 4;
+      const size_t xneed = ((size_t)4 * 32 * d + 257) * 4;
+      if (dsm < xneed) dsm = xneed;
+    }
     NRK_CHECK_ARG(dsm <= 160 * 1024, "din_bwd_params: L=%d d=%d needs %zu B LDS", L, d, dsm);
 #define NRK_BWD_DEEP8_V(DD, LL, FQV, FDPV)                                                                         \
   hipLaunchKernelGGL((din_bwd_deep8_kernel<DD, LL, 3, FQV, FDPV>), dim3(grid), dim3(512), dsm, st, tb, hist_ids,     \
                      n_table, U, wk, w2, B, L, A, dpooled, alpha, slabs, q, d, dUp, dmy, dpv)
 #define NRK_BWD_DEEP8_FDP(DD, LL)                                                                                   \
   do {                                                                                                              \
-    if (fold_q) NRK_BWD_DEEP8_V(DD, LL, true, true); else NRK_BWD_DEEP8_V(DD, LL, false, true);                     \
+    if (pipe8)                                                                                                      \
+      hipLaunchKernelGGL((din_bwd_deep8p_kernel<DD, LL>), dim3(grid), dim3(512), dsm, st, tb, hist_ids, n_table, U, wk, \
+                         w2, B, L, A, alpha, slabs, q, d, dpv);                                                      \
+    else if (fold_q && nslot8 == 4)                                                                                 \
+      hipLaunchKernelGGL((din_bwd_deep8_kernel<DD, LL, 4, true, true>), dim3(grid), dim3(512), dsm, st, tb,         \
+                         hist_ids, n_table, U, wk, w2, B, L, A, dpooled, alpha, slabs, q, d, dUp, dmy, dpv);          \
+    else if (fold_q) NRK_BWD_DEEP8_V(DD, LL, true, true);                                                           \
+    else NRK_BWD_DEEP8_V(DD, LL, false, true);                                                                      \
   } while (0)
 #define NRK_BWD_DEEP(DD, LL)                                                                                          \
   do {                                                                                                              \
@@ -2550,7 +3015,7 @@ static int bwd_params_impl(const void* table, const int32_t* hist_ids, int64_t n
       if (d == 128) {
         if (LPk == 32) NRK_BWD_DEEP8_FDP(128, 32); else NRK_BWD_DEEP8_FDP(128, 64);
       } else {
-        if (LPk == 32) NRK_BWD_DEEP8_FDP(64, 32); else NRK_BWD_DEEP8_FDP(64, 64);
+        NRK_BWD_DEEP8_FDP(64, 64);  // w8: L d >= 4096, so LPk = 64 here
       }
     } else
     if (d == 128) {
@@ -2579,8 +3044,13 @@ static int bwd_params_impl(const void* table, const int32_t* hist_ids, int64_t n
     NRK_CHECK_LAUNCH("din_bwd_pipe_kernel");
   }
   const size_t nout = 2 * (size_t)A * d + 2 * (size_t)A + 1;
-  hipLaunchKernelGGL(din_bwd_reduce_params_kernel, dim3((unsigned)cdiv((int64_t)nout, 64)), dim3(512), 0, st, slabs,
-                     grid, A, d, d, gW1, gb1, gw2, gb2, qpart, qpart ? DWQ_KC : 0);
+  const int64_t nblk_out = cdiv(norm_part ? (n_flat > (int64_t)nout ? n_flat : (int64_t)nout) : (int64_t)nout, 64);
+  if (norm_part) {
+    NRK_CHECK_ARG(gb1 == gW1 + 2 * (size_t)A * d && gw2 == gb1 + A && gb2 == gw2 + A && n_flat >= (int64_t)nout,
+                  "din_bwd_params: norm partials need [gW1 | gb1 | gw2 | gb2] at the start of the flat buffer");
+  }
+  hipLaunchKernelGGL(din_bwd_reduce_params_kernel, dim3((unsigned)nblk_out), dim3(512), 0, st, slabs,
+                     grid, A, d, d, gW1, gb1, gw2, gb2, qpart, qpart ? DWQ_KC : 0, n_flat, norm_part);
   NRK_CHECK_LAUNCH("din_bwd_reduce_params_kernel");
   return NRK_OK;
 }
@@ -2599,8 +3069,8 @@ extern "C" int nrk_din_attn_bwd_params_head(const void* table, const int32_t* hi
                                             const float* w2, int32_t B, int32_t L, int32_t d, int32_t A,
                                             const float* pooled, const float* alpha, int32_t F,
                                             const nrk_din_head_params* hp, const void* head_ws, size_t head_ws_bytes,
-                                            float* gW1, float* gb1, float* gw2, float* gb2, void* ws, size_t ws_bytes,
-                                            void* stream) {
+                                            float* gW1, float* gb1, float* gw2, float* gb2, int64_t n_flat,
+                                            double* norm_part, void* ws, size_t ws_bytes, void* stream) {
   NRK_CHECK_ARG(F == 32 && hp && pooled && head_ws, "din_bwd_params_head: needs F = 32, head params, pooled, head ws");
   DpSrc dps{};
   const float* da1 = nullptr;
@@ -2611,6 +3081,38 @@ extern "C" int nrk_din_attn_bwd_params_head(const void* table, const int32_t* hi
   dps.w1 = hp->fc1_w;
   dps.bn0w = hp->bn0_w;
   dps.invB = 1.f / (float)B;
+  {
+    const char* kt = getenv("NRK_KTIME");
+    dps.ktime = kt && *kt == '1' && cdiv(B, 256) <= 4096;
+  }
   return bwd_params_impl(table, hist_ids, n_table, dtype, q, U, W1k, w2, B, L, d, A, nullptr, alpha, gW1, gb1, gw2,
-                         gb2, nullptr, ws, ws_bytes, stream, &dps);
+                         gb2, nullptr, ws, ws_bytes, stream, &dps, n_flat, norm_part);
+}
+
+extern "C" int nrk_debug_ktimes(uint64_t* out, int64_t n) {
+  NRK_CHECK_ARG(out && n >= 0, "debug_ktimes: bad arguments");
+  NRK_CHECK_ARG(n <= 4096 * 8 * 9, "debug_ktimes: n %lld > %d", (long long)n, 4096 * 8 * 9);
+  const int64_t n1 = n < 4096 * 8 ? n : 4096 * 8;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(nrk::g_ktime), (size_t)n1 * 8, 0, hipMemcpyDeviceToHost) != hipSuccess ||
+      (n > n1 && hipMemcpyFromSymbol(out + n1, HIP_SYMBOL(nrk::g_ktime2), (size_t)(n - n1) * 8, 0,
+                                     hipMemcpyDeviceToHost) != hipSuccess))
+    return fail(NRK_ELAUNCH, "debug_ktimes: copy failed");
+  return NRK_OK;
+}
+
+extern "C" int nrk_din_batch_u(const float* q, int32_t B, int32_t d, const float* W1, const float* b1, int32_t A,
+                               float* U, void* W1k_bf16, void* stream) {
+  NRK_CHECK_ARG(d == 64 || d == 128 || d == 256, "din_batch_u: emb_dim %d unsupported (64, 128, 256)", d);
+  NRK_CHECK_ARG(A >= 32 && A <= 128 && A % 32 == 0, "din_batch_u: attn_units %d unsupported (32..128 step 32)", A);
+  NRK_CHECK_ARG(B >= 0, "din_batch_u: bad B=%d", B);
+  if (B == 0) return NRK_OK;
+  NRK_CHECK_ARG(q && W1 && b1 && U && W1k_bf16, "din_batch_u: null pointer");
+  const unsigned grid = (unsigned)cdiv(B, 32);
+  hipStream_t st = (hipStream_t)stream;
+  uint16_t* wk = static_cast<uint16_t*>(W1k_bf16);
+  if (d == 256) hipLaunchKernelGGL(din_u_kernel<256>, dim3(grid), dim3(256), 0, st, q, B, W1, b1, A, U, wk);
+  else if (d == 128) hipLaunchKernelGGL(din_u_kernel<128>, dim3(grid), dim3(256), 0, st, q, B, W1, b1, A, U, wk);
+  else hipLaunchKernelGGL(din_u_kernel<64>, dim3(grid), dim3(256), 0, st, q, B, W1, b1, A, U, wk);
+  NRK_CHECK_LAUNCH("din_u_kernel");
+  return NRK_OK;
 }

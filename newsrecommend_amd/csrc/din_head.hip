@@ -759,6 +759,8 @@ __global__ __launch_bounds__(256) void hf_bwd1(HeadArgs a) {
   }
   __syncthreads();
   {  // G (32 x D2) = da1^T xhat0 over the block's 32 rows; wave w: column tiles w, w+4, ...
+     // stored column-major per block ([D2][32]: a column's 32 entries are one 128-B
+     // line), so hf_reduce reads whole lines of 4 columns per partial block
     const int lane = t & 63, w = t >> 6, i = lane & 31, h = lane >> 5;
     float* pg = a.pw1 + (int64_t)blockIdx.x * HF * D2;
     for (int ct = w; ct < D2 / 32; ct += 4) {
@@ -771,7 +773,7 @@ __global__ __launch_bounds__(256) void hf_bwd1(HeadArgs a) {
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(da[row * (HF + 1) + i], xh[row * hs + 32 * ct + i], acc, 0, 0, 0);
       }
 #pragma unroll
-      for (int g = 0; g < 16; ++g) pg[(int64_t)hacc_row(g, h) * D2 + 32 * ct + i] = acc[g];
+      for (int g = 0; g < 16; ++g) pg[(int64_t)(32 * ct + i) * HF + hacc_row(g, h)] = acc[g];
     }
   }
   if (t < HF) {
@@ -799,7 +801,8 @@ __global__ __launch_bounds__(1024) void hf_reduce(HeadArgs a) {
     __shared__ double red[8][32][4];
     __shared__ double sred[8][32];
     __shared__ double Gt[32][4], St[32];
-    const int ph = t >> 7, j = (t >> 2) & 31, cl = t & 3;
+    // j fastest: a wave's loads cover 2 columns x 32 rows = 64 consecutive floats of a partial block
+    const int ph = t >> 7, j = t & 31, cl = (t >> 5) & 3;
     const int c = 4 * cgp + cl;
     float wv[HF];  // W1 column of this block's column t (t < 4), loaded with the partials
     if (t < 4) {
@@ -812,7 +815,7 @@ __global__ __launch_bounds__(1024) void hf_reduce(HeadArgs a) {
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
         const int b = b0 + 8 * u;
-        v[u] = b < nblk ? a.pw1[(int64_t)b * HF * D2 + (int64_t)j * D2 + c] : 0.f;
+        v[u] = b < nblk ? a.pw1[(int64_t)b * HF * D2 + (int64_t)c * HF + j] : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < 16; ++u) acc += (double)v[u];
@@ -1402,6 +1405,65 @@ __global__ __launch_bounds__(1024) void clip_adam_fused_kernel(float* __restrict
   }
 }
 
+// clip_grad_norm_ + Adam with the squared norm given as fp64 partials (from
+// the kernels that wrote the gradients: din_bwd_reduce_params_kernel): every
+// block sums the nparts partials in a fixed order, then clips and updates ONLY
+// its own 1024 entries (stores its own slice of g: no cross-block read of g);
+// the block that draws the last ticket advances Adam's step count.
+__global__ __launch_bounds__(1024) void clip_adam_part_kernel(float* __restrict__ p, float* __restrict__ g,
+                                                             float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                             float* __restrict__ step, unsigned int* __restrict__ ticket,
+                                                             float lr, const float* __restrict__ lr_dev, float beta1,
+                                                             float beta2, float eps, float wd, float max_norm,
+                                                             const double* __restrict__ part, int nparts) {
+  __shared__ double red[17];
+  const int t = threadIdx.x;
+  const int64_t i = (int64_t)blockIdx.x * 1024 + t;
+  float gi = 0.f, pi = 0.f, mi = 0.f, vi = 0.f;
+  if (i < n) {
+    gi = g[i];
+    pi = p[i];
+    mi = m[i];
+    vi = v[i];
+  }
+  const float tstep = *step + 1.f;
+  if (lr_dev) lr = *lr_dev;
+  double s = 0.0;
+  for (int j = t; j < nparts; j += 1024) s += part[j];
+  const double ws = wave_sum(s);
+  if ((t & 63) == 0) red[t >> 6] = ws;
+  __syncthreads();
+  if (t == 0) {
+    double tot = 0.0;
+    for (int w = 0; w < 16; ++w) tot += red[w];
+    red[16] = tot;
+  }
+  __syncthreads();
+  const float norm = (float)sqrt(red[16]);
+  const float c = max_norm / (norm + 1e-6f);
+  const float coef = c < 1.f ? c : 1.f;
+  const float bc1 = 1.f - powf(beta1, tstep), bc2 = 1.f - powf(beta2, tstep);
+  const float step_size = lr / bc1, bc2_sqrt = sqrtf(bc2);
+  if (i < n) {
+    gi *= coef;
+    g[i] = gi;  // clip_grad_norm_ scales the stored gradients (this block's own entries)
+    gi = gi + wd * pi;
+    mi = mi + (gi - mi) * (1.f - beta1);
+    vi = vi * beta2 + (1.f - beta2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    p[i] = pi - step_size * (mi / denom);
+  }
+  if (t == 0) {
+    __threadfence();
+    if (atomicAdd(ticket, 1u) == gridDim.x - 1) {  // every block read *step before its ticket
+      *step = tstep;
+      *ticket = 0u;
+    }
+  }
+}
+
 }  // namespace nrk
 
 using namespace nrk;
@@ -1633,5 +1695,20 @@ extern "C" int nrk_clip_adam(float* params, float* grads, float* exp_avg, float*
   hipLaunchKernelGGL(clip_adam_kernel, dim3(nb), dim3(256), 0, st, params, grads, exp_avg, exp_avg_sq, n, part, ns,
                      step, lr, lr_dev, beta1, beta2, eps, weight_decay, max_norm);
   NRK_CHECK_LAUNCH("clip_adam_kernel");
+  return NRK_OK;
+}
+
+extern "C" int nrk_clip_adam_partials(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
+                                      float* step, float lr, const float* lr_dev, float beta1, float beta2, float eps,
+                                      float weight_decay, float max_norm, const double* norm_part, int32_t n_part,
+                                      void* ws, size_t ws_bytes, void* stream) {
+  NRK_CHECK_ARG(n > 0 && params && grads && exp_avg && exp_avg_sq && step && ws && norm_part && n_part > 0,
+                "clip_adam_partials: bad arguments");
+  if (ws_bytes < 256 * 8 + 256) return fail(NRK_EWORKSPACE, "clip_adam_partials: workspace %zu < 2304", ws_bytes);
+  unsigned int* ticket = reinterpret_cast<unsigned int*>(static_cast<char*>(ws) + 256 * 8);
+  hipLaunchKernelGGL(clip_adam_part_kernel, dim3((unsigned)cdiv(n, (int64_t)1024)), dim3(1024), 0, (hipStream_t)stream,
+                     params, grads, exp_avg, exp_avg_sq, n, step, ticket, lr, lr_dev, beta1, beta2, eps, weight_decay,
+                     max_norm, norm_part, n_part);
+  NRK_CHECK_LAUNCH("clip_adam_part_kernel");
   return NRK_OK;
 }

@@ -1894,6 +1894,7 @@ extern "C" int nrk_topk_merge(const double* S_parts, const int64_t* I_parts, int
 namespace nrk {
 struct IvfPlan {
   int dp, qt, M, waves, wq, nqt;
+  int wavesB;               // phase B (collect) waves per workgroup: wq = wavesB x 32 x qt
   int qtA, wqA;             // phase A query tiles per wave / queries per work item
   int nA, chA, cmaxA, R;    // phase A: lane maxima (+positions) over the nA nearest lists, R seeds
   int chB, cmaxB, cap;      // phase B: all probed lists, collect above e_k - B
@@ -1909,11 +1910,15 @@ static IvfPlan make_ivf_plan(int64_t nq, int nprobe, int nlist, int64_t max_list
   memset(&p, 0, sizeof(p));
   p.dp = padded_dim(d);
   p.waves = 4;
-  if (k <= 8) { p.M = 4; p.qt = 2; }
-  else if (k <= 24) { p.M = 8; p.qt = 1; }
-  else { p.M = 16; p.qt = 1; }
-  if (p.dp == 256) p.qt = 1;
-  p.wq = p.waves * 32 * p.qt;
+  p.M = 1;  // neither phase keeps lane lists (mode 4: lane maxima, mode 3: collect)
+  // phase B: two query tiles per wave at k <= 8 (one at DP = 256 or k > 8), 4 waves
+  // (256 probing queries per work item at configs[3]).  NRK_IVF_COLLECT_WAVES=8
+  // (A/B hook): 512 per item; configs[3] fetch 6.0 -> 4.0 GB per launch but the
+  // list segments' padding grows 3.66 -> 4.11 padded TF and the screen runs 3.36 ->
+  // 3.79 ms (profiles/r03_ivf_collect_ab.log): the screen is MFMA-bound, not HBM-bound
+  p.qt = (k <= 8 && p.dp != 256) ? 2 : 1;
+  p.wavesB = (p.dp >= 64 && test_hook("NRK_IVF_COLLECT_WAVES", 4) == 8) ? 8 : 4;
+  p.wq = p.wavesB * 32 * p.qt;
   // phase A (lane maxima over the nA nearest lists) runs one query tile per
   // wave: half the work-item padding of the grouped queries and a lighter
   // epilogue.  Phase B keeps p.qt (two tiles share each A fragment).
@@ -2144,10 +2149,10 @@ extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe,
   mark(1);
   if (n > 0) {
     // ---- phase B: collect every probed item at or above e_k - B_q
-    screen_fn fbk = pick_screen(p.dp, p.qt, p.M, l2 != 0, 3);
+    screen_fn fbk = p.wavesB == 8 ? pick_screen_collect8(p.dp, l2 != 0) : pick_screen(p.dp, p.qt, p.M, l2 != 0, 3);
     if (!fbk) return fail(NRK_EUNSUPPORTED, "ivf_search: no collect kernel for dp=%d", p.dp);
     IvfScreen isb{work, list_off, seg, sp, nlist, p.chB, p.cmaxB, thr, ccnt, cpos, p.cap, nprobe};
-    hipLaunchKernelGGL(fbk, dim3((unsigned)p.ubB), dim3(p.waves * 64), 0, st, qi, xbh_ivf, meta_ivf, nq, n, 0, 0, 0, 1,
+    hipLaunchKernelGGL(fbk, dim3((unsigned)p.ubB), dim3(p.wavesB * 64), 0, st, qi, xbh_ivf, meta_ivf, nq, n, 0, 0, 0, 1,
                        nullptr, nullptr, nullptr, nullptr, isb);
     NRK_CHECK_LAUNCH("screen_kernel (ivf collect)");
   }

@@ -116,12 +116,12 @@ struct IvfScreen {
 // (returning global atomics in the epilogue would stall the wave for ~1 us).
 template <int WQ>
 struct CollectLds {
-  static constexpr int CAP = 1024;
+  static constexpr int CAP = 4 * WQ;
   int n;
   int qcnt[WQ];
   int qid[WQ];
   int base[WQ];
-  int2 ent[CAP];  // {row | rank << 8, position}
+  int2 ent[CAP];  // {row | rank << 10, position}
 };
 struct NoLds {};
 
@@ -135,7 +135,7 @@ struct NoLds {};
 // TIL: items per tile (deferred IP main pass may use 128: half the barriers).
 template <int DP, int QT, int M, int WAVES, bool L2, int MODE, bool AFRAG_GROUP = true, bool DEFER = false,
           int TIL = 64>
-__global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
+__global__ __launch_bounds__(WAVES * 64, (MODE == 3 && WAVES == 8) ? 1 : 2) void screen_kernel(
     const uint16_t* __restrict__ qh, const uint16_t* __restrict__ xbh, const float* __restrict__ xmeta,
     int64_t nq, int64_t nb, int64_t chunk, int nch, int nqt, int tstride, float* __restrict__ part_s,
     int* __restrict__ part_i, float* __restrict__ part_t, const float* __restrict__ tau_q, IvfScreen iv) {
@@ -146,6 +146,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
   constexpr int NT = WAVES * 64;
   constexpr int GPT = TCH / NT;      // glds instructions per thread per tile
   static_assert(TCH % NT == 0, "tile must split evenly over the workgroup");
+  static_assert(WAVES * 32 * QT <= 1024, "collect rows: 10 bits");
   constexpr int KS = DP / 16;
   constexpr int WQ = WAVES * 32 * QT;
   constexpr int BUF = TI * DP + 2 * TI;  // uint16 per buffer: rows + TI float norms
@@ -316,7 +317,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
                     if (e < CollectLds<WQ>::CAP) {
                       const int row = (w * QT + t) * 32 + r;
                       const int rank = atomicAdd(&cl.qcnt[row], 1);
-                      cl.ent[e] = make_int2(row | (rank << 8), (int)(i0 + ir));
+                      cl.ent[e] = make_int2(row | (rank << 10), (int)(i0 + ir));
                     } else if (__builtin_nontemporal_load(&iv.cand_cnt[cq[t]]) <= iv.cap) {
                       // staging full: append directly (stop once the query overflowed)
                       const int pos = atomicAdd(&iv.cand_cnt[cq[t]], 1);
@@ -414,7 +415,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
                 if (e < CollectLds<WQ>::CAP) {
                   const int row = (w * QT + t) * 32 + r;
                   const int rank = atomicAdd(&cl.qcnt[row], 1);
-                  cl.ent[e] = make_int2(row | (rank << 8), pos);
+                  cl.ent[e] = make_int2(row | (rank << 10), pos);
                 } else if (__builtin_nontemporal_load(&iv.cand_cnt[cq[t]]) <= iv.cap) {
                   const int slot = atomicAdd(&iv.cand_cnt[cq[t]], 1);
                   if (slot < iv.cap) iv.cand_pos[(int64_t)cq[t] * iv.cap + slot] = pos;
@@ -590,7 +591,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen_kernel(
       const int ne = cl.n < CollectLds<WQ>::CAP ? cl.n : CollectLds<WQ>::CAP;
       for (int e = tid; e < ne; e += NT) {
         const int2 en = cl.ent[e];
-        const int row = en.x & 255, dst = cl.base[row] + (en.x >> 8);
+        const int row = en.x & 1023, dst = cl.base[row] + (en.x >> 10);
         if (dst < iv.cap) iv.cand_pos[(int64_t)cl.qid[row] * iv.cap + dst] = en.y;
       }
       continue;
@@ -682,10 +683,34 @@ screen_fn pick_screen_dp256(int qt, int M, bool l2, int mode);
 // k = 200: 18.8 -> 21.6 ms; each lane stream admits ~30 items above tau.)
 screen_fn pick_screen_dp256_w8(int M, bool l2, int mode);
 
+// IVF collect (mode 3) with 8 waves per workgroup (one register budget of 256
+// per lane): 512 probing queries per work item (256 at DP = 256), so most lists'
+// chunks are read by ONE work item instead of ~2.3 (each chunk's query tiles
+// ran desynchronised on the persistent grid and re-fetched it from HBM).
+screen_fn pick_screen_dp32_c8(bool l2);
+screen_fn pick_screen_dp64_c8(bool l2);
+screen_fn pick_screen_dp128_c8(bool l2);
+screen_fn pick_screen_dp256_c8(bool l2);
+
 #define NRK_SCREEN_DP(DP)                                                  \
   screen_fn pick_screen_dp##DP(int qt, int M, bool l2, int mode) {         \
     return l2 ? screen_for<DP, true>(qt, M, mode) : screen_for<DP, false>(qt, M, mode); \
+  }                                                                        \
+  screen_fn pick_screen_dp##DP##_c8(bool l2) {                             \
+    constexpr int Q = DP == 256 ? 1 : 2;                                   \
+    if constexpr (DP < 64) return nullptr; /* a 64-row tile is 256 chunks */ \
+    else return l2 ? screen_kernel<DP, Q, 1, 8, true, 3, true> : screen_kernel<DP, Q, 1, 8, false, 3, true>; \
   }
+
+inline screen_fn pick_screen_collect8(int dp, bool l2) {
+  switch (dp) {
+    case 32: return pick_screen_dp32_c8(l2);
+    case 64: return pick_screen_dp64_c8(l2);
+    case 128: return pick_screen_dp128_c8(l2);
+    case 256: return pick_screen_dp256_c8(l2);
+  }
+  return nullptr;
+}
 
 inline screen_fn pick_screen(int dp, int qt, int M, bool l2, int mode) {
   switch (dp) {

@@ -503,11 +503,21 @@ class FusedTrainStep:
         Lk = 32 if Lh <= 32 else 64
         self.fuse_dp = (self.fast and d in (64, 128) and Lh <= 64 and Lk * d >= 4096 and self.F == 32
                         and os.environ.get("NRK_DIN_FUSE_DP", "1") != "0")
+        # with fuse_dp and no grad_hook, the gradient reduction also writes the
+        # squared-norm partials clip_grad_norm_ reads (nrk_clip_adam_partials)
+        self.norm_part = (torch.zeros(-(-n // 64), dtype=torch.float64, device=dev)
+                          if self.fuse_dp and grad_hook is None else None)
+        # gathers ahead (fast path): one nrk_din_batch launch assembles the rows of
+        # all K steps of a graph (history ids, query rows, labels: nothing there
+        # depends on the parameters); each step then only forms U and bf16 W1k
+        # (nrk_din_batch_u).  NRK_DIN_GATHER_AHEAD=0: one full batch kernel per step.
+        self.gather_ahead = self.fast and os.environ.get("NRK_DIN_GATHER_AHEAD", "1") != "0"
         if self.fast:
             L = hist_ids.shape[1]
-            self.hist_b = torch.empty((B, L), dtype=torch.int32, device=dev)
-            self.q_b = torch.empty((B, d), dtype=torch.float32, device=dev)
-            self.y_b = torch.empty(B, dtype=torch.float32, device=dev)
+            self.hist_k = torch.empty((self.K, B, L), dtype=torch.int32, device=dev)
+            self.q_k = torch.empty((self.K, B, d), dtype=torch.float32, device=dev)
+            self.y_k = torch.empty((self.K, B), dtype=torch.float32, device=dev)
+            self.hist_b, self.q_b, self.y_b = self.hist_k[0], self.q_k[0], self.y_k[0]
             self.U_b = torch.empty((B, A), dtype=torch.float32, device=dev)
             self.W1k_b = torch.empty((A, d), dtype=torch.bfloat16, device=dev)
         self.graph = self.graph_k = None
@@ -526,17 +536,19 @@ class FusedTrainStep:
                 self.graph_k = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(self.graph_k):
                     for k in range(self.K):
-                        self._body(k)
+                        self._body(k, gather_n=self.K if k == 0 else 0)
             with torch.no_grad():  # capture ran real steps: restore the model and optimizer state
                 for t, s in zip((self.P, self.M, self.V, self.step_t), snap):
                     t.copy_(s)
                 for k, v in model.named_buffers():
                     v.copy_(bufs[k])
 
-    def _body(self, k=0):
+    def _body(self, k=0, gather_n=1):
+        """Step k of a K-step sequence; gather_n > 0: first assemble the rows of
+        steps k .. k + gather_n - 1 (fast path with gathers ahead)."""
         idx, loss = self.idx_ring[k], self.loss_ring[k]
         if self.fast:
-            return self._body_fast(idx, loss)
+            return self._body_fast(k, idx, loss, gather_n)
         L_ = _lib.load()
         m = self.model
         dev = self.table.device
@@ -579,7 +591,7 @@ class FusedTrainStep:
             _lib.ptr(self.ws_opt),
             self.ws_opt.numel(), st), "clip_adam")
 
-    def _body_fast(self, idx, loss):
+    def _body_fast(self, k, idx, loss, gather_n):
         L_ = _lib.load()
         m = self.model
         st = _lib.stream(self.table.device)
@@ -589,11 +601,21 @@ class FusedTrainStep:
         dt = _lib.NRK_DTYPE_BF16
         W1, b1 = m.attn.attn[0].weight, m.attn.attn[0].bias
         w2 = m.attn.attn[2].weight
-        _lib.check(L_.nrk_din_batch(
-            _lib.ptr(idx), B, _lib.ptr(self.hist_all), _lib.ptr(self.tgt_all), _lib.ptr(self.lab_all),
-            self.hist_all.shape[0], L, _lib.ptr(self.table), N, dt, d, _lib.ptr(W1), _lib.ptr(b1), A,
-            _lib.ptr(self.hist_b), _lib.ptr(self.q_b), _lib.ptr(self.y_b), _lib.ptr(self.U_b), _lib.ptr(self.W1k_b),
-            st), "din_batch")
+        self.hist_b, self.q_b, self.y_b = self.hist_k[k], self.q_k[k], self.y_k[k]
+        if self.gather_ahead:
+            if gather_n > 0:
+                _lib.check(L_.nrk_din_batch(
+                    _lib.ptr(self.idx_ring[k]), gather_n * B, _lib.ptr(self.hist_all), _lib.ptr(self.tgt_all),
+                    _lib.ptr(self.lab_all), self.hist_all.shape[0], L, _lib.ptr(self.table), N, dt, d, None, None, A,
+                    _lib.ptr(self.hist_b), _lib.ptr(self.q_b), _lib.ptr(self.y_b), None, None, st), "din_batch")
+            _lib.check(L_.nrk_din_batch_u(_lib.ptr(self.q_b), B, d, _lib.ptr(W1), _lib.ptr(b1), A, _lib.ptr(self.U_b),
+                                          _lib.ptr(self.W1k_b), st), "din_batch_u")
+        else:
+            _lib.check(L_.nrk_din_batch(
+                _lib.ptr(idx), B, _lib.ptr(self.hist_all), _lib.ptr(self.tgt_all), _lib.ptr(self.lab_all),
+                self.hist_all.shape[0], L, _lib.ptr(self.table), N, dt, d, _lib.ptr(W1), _lib.ptr(b1), A,
+                _lib.ptr(self.hist_b), _lib.ptr(self.q_b), _lib.ptr(self.y_b), _lib.ptr(self.U_b),
+                _lib.ptr(self.W1k_b), st), "din_batch")
         t0 = KernelTimer.mark("fwd")
         _lib.check(L_.nrk_din_attn_fwd(
             _lib.ptr(self.table), _lib.ptr(self.hist_b), N, dt, _lib.ptr(self.U_b), _lib.ptr(self.W1k_b), _lib.ptr(w2),
@@ -611,8 +633,9 @@ class FusedTrainStep:
                 _lib.ptr(self.table), _lib.ptr(self.hist_b), N, dt, _lib.ptr(self.q_b), _lib.ptr(self.U_b),
                 _lib.ptr(self.W1k_b), _lib.ptr(w2), B, L, d, A, _lib.ptr(self.pooled), _lib.ptr(self.alpha), self.F,
                 ctypes.byref(self.hp), _lib.ptr(self.ws_head), self.ws_head.numel(), _lib.ptr(W1.grad),
-                _lib.ptr(b1.grad), _lib.ptr(w2.grad), _lib.ptr(m.attn.attn[2].bias.grad), _lib.ptr(self.ws_attn),
-                self.ws_attn.numel(), st), "din_attn_bwd_params_head")
+                _lib.ptr(b1.grad), _lib.ptr(w2.grad), _lib.ptr(m.attn.attn[2].bias.grad), self.n,
+                _lib.ptr(self.norm_part), _lib.ptr(self.ws_attn), self.ws_attn.numel(), st),
+                "din_attn_bwd_params_head")
         else:
             _lib.check(L_.nrk_din_attn_bwd_params(
                 _lib.ptr(self.table), _lib.ptr(self.hist_b), N, dt, _lib.ptr(self.q_b), _lib.ptr(self.U_b),
@@ -622,6 +645,13 @@ class FusedTrainStep:
         KernelTimer.push("bwd", t0)
         if self.grad_hook is not None:
             self.grad_hook(self.G)
+        if self.norm_part is not None:
+            _lib.check(L_.nrk_clip_adam_partials(
+                _lib.ptr(self.P), _lib.ptr(self.G), _lib.ptr(self.M), _lib.ptr(self.V), self.n, _lib.ptr(self.step_t),
+                self._lr_host, _lib.ptr(self.lr_t), self.betas[0], self.betas[1], self.eps, self.wd, self.clip,
+                _lib.ptr(self.norm_part), self.norm_part.numel(), _lib.ptr(self.ws_opt), self.ws_opt.numel(), st),
+                "clip_adam_partials")
+            return
         _lib.check(L_.nrk_clip_adam(
             _lib.ptr(self.P), _lib.ptr(self.G), _lib.ptr(self.M), _lib.ptr(self.V), self.n, _lib.ptr(self.step_t),
             self._lr_host, _lib.ptr(self.lr_t), self.betas[0], self.betas[1], self.eps, self.wd, self.clip,
@@ -700,7 +730,7 @@ class FusedTrainStep:
             self.graph.replay()
         else:
             for k in range(self.K):
-                self._body(k)
+                self._body(k, gather_n=self.K if k == 0 else 0)
         return self.loss_ring
 
 

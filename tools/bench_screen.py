@@ -16,10 +16,21 @@ ap.add_argument("--k", type=int, default=5)
 ap.add_argument("--metric", default="ip")
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--rounds", type=int, default=3)
+ap.add_argument("--queries", choices=["corpus", "profiles"], default="corpus",
+                help="profiles: bench.py e2e's user profiles (mean of 1..50 Zipf-drawn corpus rows)")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 xb = clustered_corpus(a.nb, a.d, seed=1234, device=dev)
-xq = clustered_corpus(a.nq, a.d, seed=4321, device=dev)
+if a.queries == "corpus":
+    xq = clustered_corpus(a.nq, a.d, seed=4321, device=dev)
+else:  # as bench.py bench_e2e
+    from newsrecommend_amd.data import zipf_ids
+    g = torch.Generator(device=dev).manual_seed(11)
+    L = 50
+    hist = zipf_ids(a.nq * L, a.nb, generator=g, device=dev).view(a.nq, L).long()
+    lens = torch.randint(1, L + 1, (a.nq,), generator=g, device=dev)
+    valid = (torch.arange(L, device=dev)[None] < lens[:, None]).unsqueeze(-1)
+    xq = (xb.to(torch.bfloat16)[hist].float() * valid).sum(1) / valid.sum(1)
 idx = nf.IndexFlat(a.d, 0 if a.metric == "ip" else 1, device=dev)
 idx.add(xb)
 grid = [[(v.split("=")[0], x) for x in v.split("=")[1].split(",")] for v in a.vars] or [[("NONE", "0")]]

@@ -15,7 +15,10 @@ ap.add_argument("--drop", type=float, default=0.36)
 ap.add_argument("--items", type=int, default=2_000_000)
 ap.add_argument("--rows", type=int, default=1_000_000)
 ap.add_argument("--k", type=int, default=1, help="steps per graph launch (FusedTrainStep.step_many)")
+ap.add_argument("--ktime", action="store_true", help="per-workgroup phase times of the head-fused backward")
 a = ap.parse_args()
+if a.ktime:
+    os.environ["NRK_KTIME"] = "1"
 dev = torch.device("cuda", 0)
 g = torch.Generator(device=dev).manual_seed(1)
 table = (torch.randn((a.items, 128), generator=g, device=dev) * 0.5).to(torch.bfloat16)
@@ -36,3 +39,27 @@ for s in range(0, a.steps, a.k):
 torch.cuda.synchronize()
 dt = (time.perf_counter() - t0) / a.steps
 print(f"B={a.B}: {dt * 1e6:.1f} us/step = {a.B / dt / 1e6:.2f} M samples/s, loss {loss.item():.4f}", flush=True)
+if a.ktime:
+    import ctypes
+    import numpy as np
+    from newsrecommend_amd import _lib
+    nwg = 256
+    buf = np.zeros(4096 * 8 + nwg * 64, dtype=np.uint64)
+    _lib.check(_lib.load().nrk_debug_ktimes(buf.ctypes.data, buf.size), "debug_ktimes")
+    t = buf[:nwg * 8].reshape(nwg, 8).astype(np.int64)
+    t0 = t[:, 0].min()
+    us = (t - t0) / 100.0  # 100 MHz ticks -> us
+    names = ["entry", "ids", "first", "loop", "flush", "exit"]
+    for i, n in enumerate(names):
+        c = us[:, i]
+        print(f"  {n:6s} min {c.min():7.2f} med {np.median(c):7.2f} max {c.max():7.2f} us", flush=True)
+    d = us[:, 3] - us[:, 2]
+    print(f"  loop span per WG: min {d.min():.2f} med {np.median(d):.2f} max {d.max():.2f} us", flush=True)
+    if os.environ.get("NRK_DEEP8_PIPE") == "1":
+        k2 = buf[4096 * 8:].reshape(nwg, 8, 8).astype(np.float64)
+        nit = k2[:, :, 5].max()
+        for j, n in enumerate(["wait+barrier", "issue", "stage A", "stage B", "stage C"]):
+            c = k2[:, :, j] / np.maximum(k2[:, :, 5], 1)  # cycles per iteration
+            print(f"  {n:13s} cycles/iter: wave0 med {np.median(c[:, 0]):7.0f}  all-waves med {np.median(c):7.0f} "
+                  f"max {c.max():7.0f}", flush=True)
+        print(f"  iterations per WG {nit:.0f}", flush=True)
