@@ -199,8 +199,10 @@ int nrk_din_batch_u(const float* q, int32_t B, int32_t d, const float* W1, const
  * sample landed, loop done, dW1q flushed, exit), recorded while NRK_KTIME=1;
  * then (values 32768 ..) per workgroup and wave 8 values: shader-clock cycles
  * of the pipelined loop's stages {barrier wait, issue, A, B, C} and the
- * iteration count.  Copies the first n (<= 9 x 32768) values to host memory.
- * No reference counterpart. */
+ * iteration count; then (values 294912 ..) the d <= 128 forward's wave 0 of
+ * each workgroup: entry, then per sample "rows landed" / "done" (8 values per
+ * workgroup, 1024 workgroups).  Copies the first n (<= 303104) values to host
+ * memory.  No reference counterpart. */
 int nrk_debug_ktimes(uint64_t* out, int64_t n);
 
 /* DIN attention for re-ranking (DIN.py:166-173: every candidate of a user

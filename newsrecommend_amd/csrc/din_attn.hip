@@ -272,6 +272,18 @@ __device__ __forceinline__ const uint16_t* zero_row(int64_t b, int row) {
   return g_zero_rows + (((int)b * 37 + row) & 255) * 256;
 }
 
+// Per-workgroup phase timestamps (s_memrealtime, 100 MHz) of the head-fused
+// backward, for tools/din_step.py --ktime (NRK_KTIME=1): slot 8 b + i
+__device__ uint64_t g_ktime[4096 * 8];
+// per wave: shader-clock cycles spent in each stage of the pipelined loop (tools/din_step.py --ktime)
+__device__ uint64_t g_ktime2[4096 * 8 * 8];
+// forward (din_fwd_wave_kernel), wave 0 of each workgroup: entry, per sample landed / done
+__device__ uint64_t g_ktime3[1024 * 8];
+#define NRK_KT(on, i)                                                                         \
+  do {                                                                                        \
+    if ((on) && threadIdx.x == 0) g_ktime[(size_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+
 template <int D, int NA, int NBUF>
 __global__ __launch_bounds__(256, 2) void din_fwd_wave_kernel(const uint16_t* __restrict__ table,
                                                                const int32_t* __restrict__ ids, int64_t n_table,
@@ -279,7 +291,7 @@ __global__ __launch_bounds__(256, 2) void din_fwd_wave_kernel(const uint16_t* __
                                                                const uint16_t* __restrict__ W1k,
                                                                const float* __restrict__ w2, int B, int L,
                                                                float* __restrict__ pooled,
-                                                               float* __restrict__ alpha) {
+                                                               float* __restrict__ alpha, int kt) {
   constexpr int CPR = D / 8, KS = D / 16, A = 32 * NA;
   constexpr int DPL = D / 64;         // pooled dims per lane
   constexpr int AP = (A + 63) & ~63;  // U slot padded to whole 64-lane DMA pieces
@@ -347,12 +359,19 @@ __global__ __launch_bounds__(256, 2) void din_fwd_wave_kernel(const uint16_t* __
   int b = blockIdx.x * 4 + wv;
   int32_t c0, c1, n0 = -1, n1 = -1;
   uint64_t cv0, cv1, nv0 = 0, nv1 = 0;
+  int kslot = 1;
+  auto ktf = [&](int j) {  // wave 0 of each workgroup: phase timestamps (tools/din_step.py --ktime)
+    if (kt && wv == 0 && lane == 0 && blockIdx.x < 1024 && j < 8)
+      g_ktime3[(size_t)blockIdx.x * 8 + j] = __builtin_amdgcn_s_memrealtime();
+  };
+  ktf(0);
   load_ids(b, c0, c1, cv0, cv1);
   if (b < B) issue(b, 0, c0, c1, cv0, cv1);
   if (NBUF == 2) load_ids(b + nw, n0, n1, nv0, nv1);
   int sl = 0;
   for (; b < B; b += nw) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this sample's rows (and the next ids) landed
+    ktf(kslot++);
     const int bn = b + nw;
     // this sample: compacted valid rows [0, nv), the padding row nv (zero
     // key, npad = L - nv slots) when nv < L, nct tiles of 32 rows
@@ -405,14 +424,14 @@ __global__ __launch_bounds__(256, 2) void din_fwd_wave_kernel(const uint16_t* __
             part = fmaf(wv4.w, fmaxf(acc[4 * j + 3], 0.f), part);
           }
         }
-        part += __shfl_xor(part, 32, 64);
+        part = half_swap_sum(part);
         sc[c] = (row < nr) ? part : -INFINITY;
       }
     }
     // ---- softmax over the L slots (DIN.py:108, padding included): rows < nv
     // once each, the padding row nv for its npad slots
     float m = fmaxf(fmaxf(sc[0], sc[1]), fmaxf(sc[2], sc[3]));
-    m = wave_max(m);
+    m = wave_max_fast(m);
     float e[4], sum = 0.f;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -420,7 +439,7 @@ __global__ __launch_bounds__(256, 2) void din_fwd_wave_kernel(const uint16_t* __
       e[c] = c < nct && row < nr ? expf(sc[c] - m) : 0.f;
       sum += h == 0 ? (row < nv ? e[c] : (float)npad * e[c]) : 0.f;
     }
-    sum = wave_sum(sum);
+    sum = wave_sum_fast(sum);
 #pragma unroll
     for (int c = 0; c < 4; ++c) e[c] = e[c] / sum;
     {  // alpha in slot order: a valid slot's compacted row, or the padding row
@@ -478,6 +497,7 @@ __global__ __launch_bounds__(256, 2) void din_fwd_wave_kernel(const uint16_t* __
     }
     // slot reuse: every LDS read of this sample is done before the DMA after next
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    ktf(kslot++);
     if constexpr (NBUF == 2) {
       sl ^= 1;
     } else {
@@ -625,7 +645,7 @@ __global__ __launch_bounds__(256, 2) void din_fwd_pair_kernel(const uint16_t* __
             part = fmaf(wv4.w, fmaxf(acc[i][4 * j + 3], 0.f), part);
           }
         }
-        part += __shfl_xor(part, 32, 64);
+        part = half_swap_sum(part);
         if (h == 0) xch[hu * 128 + row] = part;
       }
     }
@@ -638,7 +658,7 @@ __global__ __launch_bounds__(256, 2) void din_fwd_pair_kernel(const uint16_t* __
       sc[c] = (c < nct && row < nr) ? xch[row] + xch[128 + row] : -INFINITY;
     }
     float m = fmaxf(fmaxf(sc[0], sc[1]), fmaxf(sc[2], sc[3]));
-    m = wave_max(m);
+    m = wave_max_fast(m);
     float e[4], sum = 0.f;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -646,7 +666,7 @@ __global__ __launch_bounds__(256, 2) void din_fwd_pair_kernel(const uint16_t* __
       e[c] = c < nct && row < nr ? expf(sc[c] - m) : 0.f;
       sum += h == 0 ? (row < nv ? e[c] : (float)npad * e[c]) : 0.f;
     }
-    sum = wave_sum(sum);
+    sum = wave_sum_fast(sum);
 #pragma unroll
     for (int c = 0; c < 4; ++c) e[c] = e[c] / sum;
     if (act && hu == 0) {
@@ -1112,16 +1132,6 @@ __device__ __forceinline__ void glds4_asm(const void* gsrc, uint32_t lds_dst) {
 // it forms dpooled itself (FDP): the head's state after nrk_din_head_train
 // (nrk_din_head_ws_views) and the forward's pooled rows.  stat0 / sum5 / bn0w /
 // w1 are indexed over the head's 2d input columns (the pooled half from d).
-// Per-workgroup phase timestamps (s_memrealtime, 100 MHz) of the head-fused
-// backward, for tools/din_step.py --ktime (NRK_KTIME=1): slot 8 b + i
-__device__ uint64_t g_ktime[4096 * 8];
-// per wave: shader-clock cycles spent in each stage of the pipelined loop (tools/din_step.py --ktime)
-__device__ uint64_t g_ktime2[4096 * 8 * 8];
-#define NRK_KT(on, i)                                                                         \
-  do {                                                                                        \
-    if ((on) && threadIdx.x == 0) g_ktime[(size_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
-
 struct DpSrc {
   const float* pooled;  // [B][D]
   const float* da1;     // [B][32]
@@ -1571,8 +1581,7 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8_kernel(
         acc = fmaf(d1.z, __uint_as_float(kv.w << 16), acc);
         acc = fmaf(d1.w, __uint_as_float(kv.w & 0xFFFF0000u), acc);
       }
-#pragma unroll
-      for (int o = 1; o < LPR; o <<= 1) acc += __shfl_xor(acc, o, 64);
+      acc = group_sum<LPR>(acc);
       if (part == 0) dabuf[row] = acc;
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -1588,7 +1597,7 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8_kernel(
         const int row = 32 * c + r;
         t += (row < L && h == 0) ? sal[row] * da[c] : 0.f;
       }
-      const float cdot = wave_sum(t);
+      const float cdot = wave_sum_fast(t);
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         const int row = 32 * c + r;
@@ -1651,7 +1660,7 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8_kernel(
           }
         }
       }
-      du += __shfl_xor(du, 32, 64);
+      du = half_swap_sum(du);
       db1_acc += du;
     }
     if constexpr (FQ) {  // stage this sample's dU rows (both row groups) and query row
@@ -1786,6 +1795,17 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8p_kernel(
     const int i = lane < L ? lane : 0;
     glds4_asm(ids + bc * L + i, lds_u32(idring + e * 64));
   };
+  // this wave's small piece of [pooled0, pooled1, alpha, da1, u0, u1, q0, q1]: wave-uniform source
+  // array, row stride (= its length) and lane offset
+  const int skind = w >> 1, spart = w & 1;
+  const float* const sbase =
+      skind == 0 ? dps.pooled : skind == 1 ? (spart ? dps.da1 : alpha) : skind == 2 ? U : q;
+  const int sstride = skind == 0 ? D : skind == 1 ? (spart ? 32 : L) : skind == 2 ? A : dq;
+  const int sii = skind == 1 ? lane : spart * 64 + lane;
+  const int soff = sii < sstride ? sii : 0;
+  // per slot 2 bits: 32-row tile c of the sample holds only zero key rows (padding
+  // slots, rows >= L, invalid ids), so its z = U exactly and its dW1k term is zero
+  uint32_t zmask = 0;
   auto issue_data = [&](int64_t b, int sl, int e) {
     float* sp = slot0 + sl * SLOT_F;
     uint16_t* img = reinterpret_cast<uint16_t*>(sp + 4 * 128);
@@ -1801,14 +1821,12 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8p_kernel(
       glds16_asm(src, lds_u32(img + u * 64 * 8));
     }
     const int64_t bc = b < B ? b : 0;
-    {  // small piece w of [pooled0, pooled1, alpha, da1, u0, u1, q0, q1]
-      const int kind = w >> 1, part = w & 1;
-      const int i = part * 64 + lane;
-      const float* base = kind == 0 ? dps.pooled + bc * D : kind == 1 ? (part ? dps.da1 + bc * 32 : alpha + bc * L)
-                          : kind == 2 ? U + bc * A : q + bc * dq;
-      const int lim = kind == 0 ? D : kind == 1 ? (part ? 32 : L) : kind == 2 ? A : dq;
-      const int ii = kind == 1 ? lane : i;
-      glds4_asm(base + (ii < lim ? ii : 0), lds_u32(sp + kind * 128 + part * 64));
+    glds4_asm(sbase + bc * sstride + soff, lds_u32(sp + skind * 128 + spart * 64));
+    {
+      const int32_t idl = idring[e * 64 + lane];
+      const uint64_t vm = __ballot(lane < L && b < B && idl >= 0 && idl < n_table);
+      const uint32_t zb = ((uint32_t)vm == 0u ? 1u : 0u) | ((uint32_t)(vm >> 32) == 0u ? 2u : 0u);
+      zmask = (zmask & ~(3u << (2 * sl))) | (zb << (2 * sl));
     }
   };
   // stage A: dpooled[c] = iv g (sum_j da1[j] W1p[j][c] - sb - xhat sg), xhat = (pooled - m) iv
@@ -1818,8 +1836,7 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8p_kernel(
     float acc = 0.f;
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) acc = fmaf(da1s[4 * jj + ap], w1r[jj], acc);
-    acc += __shfl_xor(acc, 1, 64);
-    acc += __shfl_xor(acc, 2, 64);
+    acc = quad_sum(acc);
     if (a_act && ap == 0) {
       const float xhat = (sp[ac] - cm) * civ;
       out[ac] = civ * cgw * (acc - csb - xhat * csg);
@@ -1846,8 +1863,7 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8p_kernel(
       acc = fmaf(d1.z, __uint_as_float(kv.w << 16), acc);
       acc = fmaf(d1.w, __uint_as_float(kv.w & 0xFFFF0000u), acc);
     }
-#pragma unroll
-    for (int o = 1; o < LPR; o <<= 1) acc += __shfl_xor(acc, o, 64);
+    acc = group_sum<LPR>(acc);
     if (part == 0) out[row] = acc;
   };
 
@@ -1884,17 +1900,19 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8p_kernel(
     // group of sample i + 2 landed; stage results of iteration i - 1 visible; slot of i - 1 free
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"((P - 3) * N_D) : "memory");
     kts(0);
-    {
+    // diagnostics (NRK_KTIME_DIAG, timing runs only): 2 = no DMA issue, 4 = no stage A / B, 8 = no stage C
+    const int diag = dps.ktime >> 1;
+    if (!(diag & 1)) {
       const int e_new = (i + P + X) % RING, e_dat = (i + P) % RING;
       issue_ids(b0 + (int64_t)(i + P + X) * grid, e_new);
       issue_data(b0 + (int64_t)(i + P) * grid, sl == 0 ? NSLOT - 1 : sl - 1, e_dat);
     }
     kts(1);
     const int sl1 = sl + 1 < NSLOT ? sl + 1 : sl + 1 - NSLOT, sl2 = sl + 2 < NSLOT ? sl + 2 : sl + 2 - NSLOT;
-    stage_a(sl2, dpl + (i & 1) * D);
+    if (!(diag & 2)) stage_a(sl2, dpl + (i & 1) * D);
     if (dps.ktime) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     kts(2);
-    stage_b(sl1, dpl + ((i + 1) & 1) * D, dabuf + ((i + 1) & 1) * 64);
+    if (!(diag & 2)) stage_b(sl1, dpl + ((i + 1) & 1) * D, dabuf + ((i + 1) & 1) * 64);
     if (dps.ktime) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     kts(3);
 
@@ -1905,7 +1923,7 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8p_kernel(
     const float* dab = dabuf + (i & 1) * 64;
     const unsigned char* img = reinterpret_cast<const unsigned char*>(sp + 512);
     float du = 0.f;
-    if (us < nsl && rg < NC) {
+    if (us < nsl && rg < NC && !(diag & 4)) {
       const float un = sU[32 * us + r];
       float da[NC];
 #pragma unroll
@@ -1916,7 +1934,7 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8p_kernel(
         const int row = 32 * c + r;
         t += (row < L && h == 0) ? sal[row] * da[c] : 0.f;
       }
-      const float cdot = wave_sum(t);
+      const float cdot = wave_sum_fast(t);
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         const int row = 32 * c + r;
@@ -1932,13 +1950,16 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8p_kernel(
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         if ((c & 1) != rg) continue;
+        const bool kz = (zmask >> (2 * sl + c)) & 1u;  // zero keys: z = U, no dW1k term (bit-exact)
         f32x16 acc;
 #pragma unroll
         for (int g = 0; g < 16; ++g) acc[g] = un;
+        if (!kz) {
 #pragma unroll
-        for (int s2 = 0; s2 < KS; ++s2) {
-          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(img + KImg<true, D>::off(32 * c + r, 16 * s2 + 8 * h));
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, wf.f[s2], acc, 0, 0, 0);
+          for (int s2 = 0; s2 < KS; ++s2) {
+            const bf16x8 kf = *reinterpret_cast<const bf16x8*>(img + KImg<true, D>::off(32 * c + r, 16 * s2 + 8 * h));
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, wf.f[s2], acc, 0, 0, 0);
+          }
         }
         f32x16 dz;
 #pragma unroll
@@ -1957,6 +1978,7 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8p_kernel(
         }
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
+          if (kz) break;
           bf16x8 af;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {  // v_cvt_pk_bf16_f32 (round to nearest even)
@@ -1979,7 +2001,7 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8p_kernel(
           }
         }
       }
-      du += __shfl_xor(du, 32, 64);
+      du = half_swap_sum(du);
       db1_acc += du;
     }
     // stage this sample's dU rows (both row groups) and query row (host: <= 16 samples per workgroup)
@@ -2206,8 +2228,7 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8c_kernel(
         acc = fmaf(d1.z, __uint_as_float(kv.w << 16), acc);
         acc = fmaf(d1.w, __uint_as_float(kv.w & 0xFFFF0000u), acc);
       }
-#pragma unroll
-      for (int o = 1; o < LPR; o <<= 1) acc += __shfl_xor(acc, o, 64);
+      acc = group_sum<LPR>(acc);
       if (part == 0) dabuf[row] = acc;
     }
     // partial z of this half's columns for row tile c (MFMA), exchanged through LDS
@@ -2243,7 +2264,7 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8c_kernel(
         const int row = 32 * c + r;
         t += (row < L && h == 0) ? sal[row] * da[c] : 0.f;
       }
-      const float cdot = wave_sum(t);
+      const float cdot = wave_sum_fast(t);
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         const int row = 32 * c + r;
@@ -2306,7 +2327,7 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8c_kernel(
           }
         }
       }
-      du += __shfl_xor(du, 32, 64);
+      du = half_swap_sum(du);
       if (ch == 0) db1_acc += du;
     }
     du_keep = du;
@@ -2772,9 +2793,11 @@ extern "C" int nrk_din_attn_fwd(const void* keys, const int32_t* hist_ids, int64
     const uint16_t* tb = static_cast<const uint16_t*>(keys);
     const uint16_t* wk = static_cast<const uint16_t*>(W1k);
     hipStream_t st = (hipStream_t)stream;
+    const char* kte = getenv("NRK_KTIME");
+    const int kt = kte && *kte == '1';
 #define NRK_FWD_WAVE(DD, NN)                                                                                        \
   hipLaunchKernelGGL((din_fwd_wave_kernel<DD, NN, 1>), dim3(grid), dim3(256), wsm, st, tb, hist_ids, n_table, U, wk, \
-                     w2, B, L, pooled, alpha)
+                     w2, B, L, pooled, alpha, kt)
     const int na = A / 32;
     if (d == 128) {
       if (na == 1) NRK_FWD_WAVE(128, 1); else if (na == 2) NRK_FWD_WAVE(128, 2);
@@ -3083,7 +3106,8 @@ extern "C" int nrk_din_attn_bwd_params_head(const void* table, const int32_t* hi
   dps.invB = 1.f / (float)B;
   {
     const char* kt = getenv("NRK_KTIME");
-    dps.ktime = kt && *kt == '1' && cdiv(B, 256) <= 4096;
+    const char* kd = getenv("NRK_KTIME_DIAG");
+    dps.ktime = (kt && *kt == '1' && cdiv(B, 256) <= 4096) ? 1 | ((kd ? atoi(kd) : 0) & 14) : 0;
   }
   return bwd_params_impl(table, hist_ids, n_table, dtype, q, U, W1k, w2, B, L, d, A, nullptr, alpha, gW1, gb1, gw2,
                          gb2, nullptr, ws, ws_bytes, stream, &dps, n_flat, norm_part);
@@ -3091,11 +3115,14 @@ extern "C" int nrk_din_attn_bwd_params_head(const void* table, const int32_t* hi
 
 extern "C" int nrk_debug_ktimes(uint64_t* out, int64_t n) {
   NRK_CHECK_ARG(out && n >= 0, "debug_ktimes: bad arguments");
-  NRK_CHECK_ARG(n <= 4096 * 8 * 9, "debug_ktimes: n %lld > %d", (long long)n, 4096 * 8 * 9);
-  const int64_t n1 = n < 4096 * 8 ? n : 4096 * 8;
+  const int64_t e1 = 4096 * 8, e2 = e1 + 4096 * 8 * 8, e3 = e2 + 1024 * 8;
+  NRK_CHECK_ARG(n <= e3, "debug_ktimes: n %lld > %lld", (long long)n, (long long)e3);
+  const int64_t n1 = n < e1 ? n : e1, n2 = n < e2 ? n - n1 : e2 - e1, n3 = n - n1 - n2;
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(nrk::g_ktime), (size_t)n1 * 8, 0, hipMemcpyDeviceToHost) != hipSuccess ||
-      (n > n1 && hipMemcpyFromSymbol(out + n1, HIP_SYMBOL(nrk::g_ktime2), (size_t)(n - n1) * 8, 0,
-                                     hipMemcpyDeviceToHost) != hipSuccess))
+      (n2 > 0 && hipMemcpyFromSymbol(out + e1, HIP_SYMBOL(nrk::g_ktime2), (size_t)n2 * 8, 0, hipMemcpyDeviceToHost) !=
+                     hipSuccess) ||
+      (n3 > 0 && hipMemcpyFromSymbol(out + e2, HIP_SYMBOL(nrk::g_ktime3), (size_t)n3 * 8, 0, hipMemcpyDeviceToHost) !=
+                     hipSuccess))
     return fail(NRK_ELAUNCH, "debug_ktimes: copy failed");
   return NRK_OK;
 }

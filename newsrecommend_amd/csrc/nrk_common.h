@@ -79,6 +79,59 @@ __device__ inline float wave_max(float v) {
   return v;
 }
 
+// Cross-lane sums on the VALU (DPP row ops and the CDNA4 half-row / half-wave
+// swaps) instead of ds_bpermute (an LDS round trip, ~100 cycles, per step):
+// every lane of the group receives the group's sum, in a fixed order.
+#define NRK_DPP(v, ctrl) __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), (ctrl), 0xf, 0xf, false))
+// sum over each quad (lanes 4k..4k+3)
+__device__ __forceinline__ float quad_sum(float v) {
+  v += NRK_DPP(v, 0xB1);  // quad_perm [1,0,3,2]
+  v += NRK_DPP(v, 0x4E);  // quad_perm [2,3,0,1]
+  return v;
+}
+// sum over each 8-lane group
+__device__ __forceinline__ float oct_sum(float v) {
+  v = quad_sum(v);
+  return v + NRK_DPP(v, 0x141);  // row_half_mirror: quad 0 <-> quad 1 of each 8
+}
+// sum over each row of 16 lanes
+__device__ __forceinline__ float row_sum16(float v) {
+  v = oct_sum(v);
+  return v + NRK_DPP(v, 0x140);  // row_mirror: the two 8-lane halves of the row
+}
+__device__ __forceinline__ float wave_sum_fast(float v);
+// sum over each group of N consecutive lanes (N in {4, 8, 16, 64})
+template <int N>
+__device__ __forceinline__ float group_sum(float v) {
+  static_assert(N == 4 || N == 8 || N == 16 || N == 64, "group_sum: N");
+  if constexpr (N == 4) return quad_sum(v);
+  else if constexpr (N == 8) return oct_sum(v);
+  else if constexpr (N == 16) return row_sum16(v);
+  else return wave_sum_fast(v);
+}
+// v[i] + v[i ^ 32]
+__device__ __forceinline__ float half_swap_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// sum over the wave (every lane)
+__device__ __forceinline__ float wave_sum_fast(float v) {
+  v = row_sum16(v);
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(r[0]) + __uint_as_float(r[1]);  // rows 2k <-> 2k+1
+  return half_swap_sum(v);
+}
+__device__ __forceinline__ float wave_max_fast(float v) {
+  v = fmaxf(v, NRK_DPP(v, 0xB1));
+  v = fmaxf(v, NRK_DPP(v, 0x4E));
+  v = fmaxf(v, NRK_DPP(v, 0x141));
+  v = fmaxf(v, NRK_DPP(v, 0x140));
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
 // Position of the (j+1)-th set bit of m (j < popcount(m)): history slot of
 // compacted row j (the DIN kernels score valid rows first, padding once).
 __device__ __forceinline__ int nth_set_bit(uint64_t m, int j) {

@@ -8,9 +8,13 @@ NRK_SCREEN_DP(256)
 screen_fn pick_screen_dp256_w8(int M, bool l2, int mode) {
   // IP: epilogue deferred into the next MFMA chain (configs[4] retrieve
   // 21.7 -> 19.8 ms), 64-item tiles (128 would spill); L2 keeps the direct
-  // epilogue.  The k = 200 form (M = 16) reads the corpus once (FETCH_SIZE
-  // 5.3 GB per launch at 10M x 256, profiles/r02_pmc_screen_k200.json); its
-  // cost over the k = 5 form is the lane-list insertions.
+  // epilogue.  The k = 200 form (M = 16) fetches 9.0-9.2 GB per launch at
+  // 10M x 256 under bench.py (its user-profile queries; 5.26 GB with corpus-row
+  // queries: profiles/r03_k200_query_distribution.log) against the 5.12 GB
+  // corpus (most likely the 16 query tiles sharing a chunk progress unevenly
+  // with these queries and re-fetch rows that left L2).  It runs at 560 GB/s, MFMA-bound
+  // (16.0 ms with the profile queries, 16.5 ms with corpus rows); its cost over
+  // the k = 5 form is the lane-list insertions.
   if (mode == 1)
     return l2 ? screen_kernel<256, 1, 1, 8, true, 1, false> : screen_kernel<256, 1, 1, 8, false, 1, false, true, 64>;
   if (M == 4)

@@ -44,7 +44,7 @@ if a.ktime:
     import numpy as np
     from newsrecommend_amd import _lib
     nwg = 256
-    buf = np.zeros(4096 * 8 + nwg * 64, dtype=np.uint64)
+    buf = np.zeros(4096 * 8 * 9 + 1024 * 8, dtype=np.uint64)
     _lib.check(_lib.load().nrk_debug_ktimes(buf.ctypes.data, buf.size), "debug_ktimes")
     t = buf[:nwg * 8].reshape(nwg, 8).astype(np.int64)
     t0 = t[:, 0].min()
@@ -56,10 +56,17 @@ if a.ktime:
     d = us[:, 3] - us[:, 2]
     print(f"  loop span per WG: min {d.min():.2f} med {np.median(d):.2f} max {d.max():.2f} us", flush=True)
     if os.environ.get("NRK_DEEP8_PIPE") == "1":
-        k2 = buf[4096 * 8:].reshape(nwg, 8, 8).astype(np.float64)
+        k2 = buf[4096 * 8:4096 * 8 + nwg * 64].reshape(nwg, 8, 8).astype(np.float64)
         nit = k2[:, :, 5].max()
         for j, n in enumerate(["wait+barrier", "issue", "stage A", "stage B", "stage C"]):
             c = k2[:, :, j] / np.maximum(k2[:, :, 5], 1)  # cycles per iteration
             print(f"  {n:13s} cycles/iter: wave0 med {np.median(c[:, 0]):7.0f}  all-waves med {np.median(c):7.0f} "
                   f"max {c.max():7.0f}", flush=True)
         print(f"  iterations per WG {nit:.0f}", flush=True)
+    f = buf[4096 * 8 * 9:].reshape(1024, 8).astype(np.int64)
+    f = f[:min(512, (a.B + 3) // 4)]  # the d = 128 forward's grid
+    fu = (f - f[:, 0].min()) / 100.0
+    for j, n in enumerate(["fwd entry", "s0 landed", "s0 done", "s1 landed", "s1 done", "s2 landed", "s2 done"]):
+        c = fu[:, j]
+        if (f[:, j] > 0).all():
+            print(f"  {n:10s} min {c.min():7.2f} med {np.median(c):7.2f} max {c.max():7.2f} us", flush=True)
