@@ -397,7 +397,7 @@ __global__ __launch_bounds__(256, 2) void din_fwd_wave_kernel(const uint16_t* __
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       sc[c] = -INFINITY;
-      if (c < nct) {
+      if (c < nct && !(kt & 2)) {  // (kt & 2: timing diagnostics only, scores skipped)
         bf16x8 kf[KS];
         const int row = 32 * c + r;
 #pragma unroll
@@ -465,7 +465,7 @@ __global__ __launch_bounds__(256, 2) void din_fwd_wave_kernel(const uint16_t* __
     float acc2[DPL];
 #pragma unroll
     for (int j = 0; j < DPL; ++j) acc2[j] = 0.f;
-    const int L8 = (nv + 7) & ~7;
+    const int L8 = (kt & 4) ? 0 : (nv + 7) & ~7;  // (kt & 4: timing diagnostics only, pooling skipped)
     for (int row0 = 0; row0 < L8; row0 += 8) {
       const int c = row0 >> 5;
       const float ec = c == 0 ? e[0] : c == 1 ? e[1] : c == 2 ? e[2] : e[3];
@@ -2794,7 +2794,8 @@ extern "C" int nrk_din_attn_fwd(const void* keys, const int32_t* hist_ids, int64
     const uint16_t* wk = static_cast<const uint16_t*>(W1k);
     hipStream_t st = (hipStream_t)stream;
     const char* kte = getenv("NRK_KTIME");
-    const int kt = kte && *kte == '1';
+    const char* kfd = getenv("NRK_KTIME_FWD_DIAG");
+    const int kt = (kte && *kte == '1') ? 1 | ((kfd ? atoi(kfd) : 0) & 6) : 0;
 #define NRK_FWD_WAVE(DD, NN)                                                                                        \
   hipLaunchKernelGGL((din_fwd_wave_kernel<DD, NN, 1>), dim3(grid), dim3(256), wsm, st, tb, hist_ids, n_table, U, wk, \
                      w2, B, L, pooled, alpha, kt)
