@@ -760,7 +760,8 @@ def bench_din(args, rank, world, dev):
         "final_loss": float(loss.reshape(-1)[0].item()),
         "kernels_ms": {"attn_fwd": fwd_ms, "attn_bwd (deep8 + dwq + reduce)" if fused else "attn_bwd+reduce": bwd_ms},
         "roofline_step": {"bound": "hbm", "achieved": step_gbs, "peak": HBM_GBS, "unit": "GB/s",
-                          "frac": step_gbs / HBM_GBS, "traffic": None,
+                          "frac": step_gbs / HBM_GBS,
+                          "traffic": _pmc_traffic(f"din_step:{din_key}") if fused and graphed else None,
                           "algorithmic": f"{STEP_BYTES} B/sample (SURVEY.md 8d: L*d*2 + d*2 + 4*(L+1) + 4) x "
                                          f"samples/s over the whole step"},
         "roofline_fwd": {"bound": "hbm", "achieved": fwd_gbs, "peak": HBM_GBS, "unit": "GB/s",

@@ -520,8 +520,8 @@ __global__ __launch_bounds__(256, 2) void din_fwd_wave_kernel(const uint16_t* __
 // half of the 256 columns.  Four waves = two samples per workgroup, two
 // workgroups per CU (LDS).  Same math and padding-row compaction as
 // din_fwd_wave_kernel.
-template <int D, int NA>
-__global__ __launch_bounds__(256, 2) void din_fwd_pair_kernel(const uint16_t* __restrict__ table,
+template <int D, int NA, int MINB = 2>
+__global__ __launch_bounds__(256, MINB) void din_fwd_pair_kernel(const uint16_t* __restrict__ table,
                                                                const int32_t* __restrict__ ids, int64_t n_table,
                                                                const float* __restrict__ U,
                                                                const uint16_t* __restrict__ W1k,
@@ -531,7 +531,7 @@ __global__ __launch_bounds__(256, 2) void din_fwd_pair_kernel(const uint16_t* __
   constexpr int CPR = D / 8, KS = D / 16, A = 32 * NA;
   constexpr int NAH = (NA + 1) / 2;   // unit tiles per wave half
   constexpr int DH = D / 2, DPL = DH / 64;  // pooled columns per wave half / per lane
-  static_assert(DPL == 2, "pair kernel: D = 256");
+  static_assert(DPL == 2 || DPL == 1, "pair kernel: D = 128 or 256");
   constexpr int AP = (A + 63) & ~63;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -696,17 +696,29 @@ __global__ __launch_bounds__(256, 2) void din_fwd_pair_kernel(const uint16_t* __
         const float ec = c == 0 ? e[0] : c == 1 ? e[1] : c == 2 ? e[2] : e[3];
         uint32_t u[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
-          u[i] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const unsigned char*>(img) +
-                                                    KImg<true, D>::off(row0 + i, DH * hu + 2 * lane));
+        for (int i = 0; i < 8; ++i) {
+          if constexpr (DPL == 2)
+            u[i] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const unsigned char*>(img) +
+                                                      KImg<true, D>::off(row0 + i, DH * hu + 2 * lane));
+          else
+            u[i] = *reinterpret_cast<const uint16_t*>(reinterpret_cast<const unsigned char*>(img) +
+                                                      KImg<true, D>::off(row0 + i, DH * hu + lane));
+        }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const float al = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ec), (row0 + i) & 31));
-          acc2[0] = fmaf(al, __uint_as_float(u[i] << 16), acc2[0]);
-          acc2[1] = fmaf(al, __uint_as_float(u[i] & 0xFFFF0000u), acc2[1]);
+          if constexpr (DPL == 2) {
+            acc2[0] = fmaf(al, __uint_as_float(u[i] << 16), acc2[0]);
+            acc2[1] = fmaf(al, __uint_as_float(u[i] & 0xFFFF0000u), acc2[1]);
+          } else {
+            acc2[0] = fmaf(al, __uint_as_float(u[i] << 16), acc2[0]);
+          }
         }
       }
-      *reinterpret_cast<float2*>(pooled + (int64_t)b * D + DH * hu + 2 * lane) = make_float2(acc2[0], acc2[1]);
+      if constexpr (DPL == 2)
+        *reinterpret_cast<float2*>(pooled + (int64_t)b * D + DH * hu + 2 * lane) = make_float2(acc2[0], acc2[1]);
+      else
+        pooled[(int64_t)b * D + DH * hu + lane] = acc2[0];
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __syncthreads();  // every read of the pair's image and exchange is done: refill
@@ -2774,6 +2786,29 @@ extern "C" int nrk_din_attn_fwd(const void* keys, const int32_t* hist_ids, int64
     const int na = A / 32;
 #define NRK_FWD_PAIR(NN)                                                                                          \
   hipLaunchKernelGGL((din_fwd_pair_kernel<256, NN>), dim3(grid), dim3(256), psm, st, tb, hist_ids, n_table, U, wk, \
+                     w2, B, L, pooled, alpha)
+    if (na == 1) NRK_FWD_PAIR(1); else if (na == 2) NRK_FWD_PAIR(2); else if (na == 3) NRK_FWD_PAIR(3);
+    else NRK_FWD_PAIR(4);
+#undef NRK_FWD_PAIR
+    NRK_CHECK_LAUNCH("din_fwd_pair_kernel");
+    return NRK_OK;
+  }
+  // d = 128: a wave pair per sample (each wave half the unit tiles: 168 VGPRs, three
+  // workgroups = 12 waves per CU): 153.4 -> 151.5 us per train step against one wave
+  // per sample at 8 waves per CU (profiles/r03_din_fwd_pair_ab.log).  NRK_DIN_FWD_PAIR=0:
+  // the wave-per-sample kernel (A/B hook; it carries the --ktime stamps)
+  const char* fp_env = getenv("NRK_DIN_FWD_PAIR");
+  if (wave_ok && d == 128 && !(fp_env && *fp_env == '0')) {
+    const size_t psm = pair_sm;
+    NRK_CHECK_ARG(3 * psm <= 160 * 1024, "din_fwd: L=%d d=%d needs %zu B LDS (pair)", L, d, psm);
+    int grid = (int)cdiv(B, 2);
+    if (grid > 768) grid = 768;
+    const uint16_t* tb = static_cast<const uint16_t*>(keys);
+    const uint16_t* wk = static_cast<const uint16_t*>(W1k);
+    hipStream_t st = (hipStream_t)stream;
+    const int na = A / 32;
+#define NRK_FWD_PAIR(NN)                                                                                          \
+  hipLaunchKernelGGL((din_fwd_pair_kernel<128, NN, 3>), dim3(grid), dim3(256), psm, st, tb, hist_ids, n_table, U, wk, \
                      w2, B, L, pooled, alpha)
     if (na == 1) NRK_FWD_PAIR(1); else if (na == 2) NRK_FWD_PAIR(2); else if (na == 3) NRK_FWD_PAIR(3);
     else NRK_FWD_PAIR(4);

@@ -15,10 +15,13 @@ ap.add_argument("--drop", type=float, default=0.36)
 ap.add_argument("--items", type=int, default=2_000_000)
 ap.add_argument("--rows", type=int, default=1_000_000)
 ap.add_argument("--k", type=int, default=1, help="steps per graph launch (FusedTrainStep.step_many)")
-ap.add_argument("--ktime", action="store_true", help="per-workgroup phase times of the head-fused backward")
+ap.add_argument("--ktime", action="store_true",
+                help="per-workgroup phase times of the head-fused backward and (NRK_DIN_FWD_PAIR=0, set here) "
+                     "of the wave-per-sample forward")
 a = ap.parse_args()
 if a.ktime:
     os.environ["NRK_KTIME"] = "1"
+    os.environ.setdefault("NRK_DIN_FWD_PAIR", "0")
 dev = torch.device("cuda", 0)
 g = torch.Generator(device=dev).manual_seed(1)
 table = (torch.randn((a.items, 128), generator=g, device=dev) * 0.5).to(torch.bfloat16)
