@@ -202,6 +202,15 @@ __global__ __launch_bounds__(WAVES * 64, (MODE == 3 && WAVES == 8) ? 1 : 2) void
   #pragma unroll
       for (int s = 0; s < KS; ++s) qf[t][s] = src[2 * s];
     }
+    // query tiles of this wave holding a real row (IVF: padding rows are a suffix of the segment)
+    int nact = QT;
+    if constexpr (MODE >= 2) {
+      nact = 0;
+  #pragma unroll
+      for (int t = 0; t < QT; ++t)
+        if (__any(iv.slot_pair[seg0 + qidx[t]] >= 0)) nact = t + 1;
+      nact = __builtin_amdgcn_readfirstlane(nact);
+    }
     float ls[QT][M + 1];
     int li[QT][M + 1];
     float tau[QT];
@@ -254,9 +263,14 @@ __global__ __launch_bounds__(WAVES * 64, (MODE == 3 && WAVES == 8) ? 1 : 2) void
       }
     };
 
-    // one 64-item tile (buffer index is a compile-time constant: immediate LDS offsets)
-    auto compute = [&](int it, auto buf_c) {
+    // one 64-item tile (buffer index is a compile-time constant: immediate LDS offsets).
+    // NACT: query tiles of this wave that hold any real row (IVF modes: a list's
+    // gathered segment is padded to the workgroup's rows, padding is a suffix, so a
+    // wave past the list's last prober skips its MFMAs and leaves the SIMD's MFMA
+    // pipe to the co-resident workgroup's wave)
+    auto compute = [&](int it, auto buf_c, auto nact_c) {
       constexpr int buf = decltype(buf_c)::value;
+      constexpr int NACT = decltype(nact_c)::value;
       const uint16_t* tl = lds + buf * BUF;
       const float* lnorm = reinterpret_cast<const float*>(tl + TI * DP);
       const int64_t i0 = ibeg + (int64_t)it * tstride * TI;
@@ -279,19 +293,19 @@ __global__ __launch_bounds__(WAVES * 64, (MODE == 3 && WAVES == 8) ? 1 : 2) void
   #pragma unroll
         for (int s = 0; s < KS; ++s) {
   #pragma unroll
-          for (int t = 0; t < QT; ++t)
+          for (int t = 0; t < NACT; ++t)
             acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], qf[t][s], acc[t], 0, 0, 0);
         }
-        if constexpr (AFRAG_GROUP) {  // scheduler: the KS LDS reads first, then the MFMA chain
+        if constexpr (AFRAG_GROUP && NACT > 0) {  // scheduler: the KS LDS reads first, then the MFMA chain
           __builtin_amdgcn_sched_group_barrier(0x100, KS, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, KS * QT, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, KS * NACT, 0);
         }
         // Epilogue.  MASKED only for the (rare) partial last tile of a chunk: a
         // wave-uniform branch, so full tiles carry no per-score selects.
         auto epilogue = [&](auto masked_tag) {
           constexpr bool MASKED = decltype(masked_tag)::value;
   #pragma unroll
-          for (int t = 0; t < QT; ++t) {
+          for (int t = 0; t < NACT; ++t) {
             float sc[16];
   #pragma unroll
             for (int g = 0; g < 16; ++g) {
@@ -371,7 +385,10 @@ __global__ __launch_bounds__(WAVES * 64, (MODE == 3 && WAVES == 8) ? 1 : 2) void
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();  // tile `it` landed; everyone is done with the other buffer
       if (it + 1 < ntiles) issue_tile(it + 1, std::integral_constant<int, buf ^ 1>{});
-      compute(it, buf_c);
+      if (nact == QT) compute(it, buf_c, std::integral_constant<int, QT>{});
+      else if constexpr (QT > 1) {
+        if (nact == 1) compute(it, buf_c, std::integral_constant<int, 1>{});
+      }
     };
     // ---- deferred epilogue (DEFER): see the comment at the template ----
     constexpr int NSUB = TI / 32;  // sub-tiles per tile (2 or 4)

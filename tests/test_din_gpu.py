@@ -370,6 +370,41 @@ def test_din_batch_kernel(gpu, d, A, L):
     assert (U - U_ref).abs().max().item() < 2e-5 * max(1.0, U_ref.abs().max().item())
 
 
+@pytest.mark.parametrize("A,L,B", [(128, 50, 4096), (64, 20, 97), (96, 64, 1000)])
+def test_fwd_pair_d128_matches_wave_kernel(gpu, A, L, B, monkeypatch):
+    """d = 128: the wave-pair forward (default) against the wave-per-sample
+    kernel (NRK_DIN_FWD_PAIR=0): the partial scores of the two unit halves are
+    summed in another order, so pooled / alpha agree to f32 rounding."""
+    from newsrecommend_amd import _lib
+    from newsrecommend_amd.data import synthetic_click_rows
+
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(8)
+    d, N = 128, 6000
+    L_ = _lib.load()
+    table = (torch.randn((N, d), generator=g, device=dev) * 0.5).to(torch.bfloat16)
+    hist, _, _ = synthetic_click_rows(B, N, L, seed=4, device=dev)
+    hist = hist.to(torch.int32).contiguous()
+    hist[3, :] = -1  # an empty history
+    U = torch.randn((B, A), generator=g, device=dev) * 0.3
+    wk = (torch.randn((A, d), generator=g, device=dev) * 0.1).to(torch.bfloat16)
+    w2 = torch.randn(A, generator=g, device=dev) * 0.3
+    outs = []
+    for pair in ("0", "1"):
+        monkeypatch.setenv("NRK_DIN_FWD_PAIR", pair)
+        pooled = torch.full((B, d), float("nan"), device=dev)
+        alpha = torch.full((B, L), float("nan"), device=dev)
+        _lib.check(L_.nrk_din_attn_fwd(
+            _lib.ptr(table), _lib.ptr(hist), N, _lib.NRK_DTYPE_BF16, _lib.ptr(U), _lib.ptr(wk), _lib.ptr(w2), 0.0, B,
+            L, d, A, _lib.ptr(pooled), _lib.ptr(alpha), _lib.stream(dev)), "din_attn_fwd")
+        torch.cuda.synchronize()
+        outs.append((pooled, alpha))
+    (p0, a0), (p1, a1) = outs
+    assert torch.isfinite(p1).all() and torch.isfinite(a1).all()
+    assert (a0 - a1).abs().max().item() < 1e-5
+    assert (p0 - p1).abs().max().item() < 1e-5 * max(1.0, p0.abs().max().item())
+
+
 def test_fused_train_step_generic_path_matches_eager(gpu):
     """emb_dim 48 (zero-padded to the 64 kernel: the FusedTrainStep path
     without the batch-assembly kernel) still equals the eager loop."""
