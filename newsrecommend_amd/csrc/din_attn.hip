@@ -1740,6 +1740,334 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8_kernel(
   NRK_KT(kt, 5);
 }
 
+// Two-stream form of the head-fused 8-wave backward (FQ + FDP, LP <= 64): the
+// workgroup's samples alternate between two groups of four waves (g = w >> 2),
+// each group runs ONE sample per iteration with all four waves (us = w & 3: 32
+// attention units each, every row tile of the sample), so one barrier-separated
+// iteration advances two samples and a sample whose second row tile holds only
+// zero keys (padding, rows >= L) costs its group one tile, not a partner wave's
+// idle tile.  The per-group dW1k / dw2 / db1 accumulators meet in a fixed order
+// at the end, as the row-group pairs of din_bwd_deep8_kernel do.
+template <int D, int LP>
+__global__ __launch_bounds__(512, 1) void din_bwd_deep8g_kernel(
+    const uint16_t* __restrict__ table, const int32_t* __restrict__ ids, int64_t n_table, const float* __restrict__ U,
+    const uint16_t* __restrict__ W1k, const float* __restrict__ w2, int B, int L, int A,
+    const float* __restrict__ alpha, float* __restrict__ slabs, const float* __restrict__ q, int dq, DpSrc dps) {
+  constexpr int CPR = D / 8, KS = D / 16, NCT = D / 32, NC = LP / 32;
+  constexpr int NPW = LP * CPR / 256;  // key-image DMA pieces per wave (four waves per sample)
+  static_assert(LP <= 64 && NPW >= 1, "deep8g: LP <= 64, L D >= 2048");
+  constexpr int N_D = NPW + 2 + 1;     // per wave and iteration: keys, two small pieces, ids
+  constexpr int NSLOT = 3, P = NSLOT - 1, X = 3, RING = X + 1;
+  static_assert(X * N_D < 64, "vmcnt range");
+  // slot (floats): pooled [128] | alpha [64], da1 [32..] | U [128] | q [128] | key image [LP][D] bf16
+  constexpr int SLOT_F = 4 * 128 + LP * D / 2;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int us = w & 3, g = w >> 2, gt = tid & 255;
+  const int nsl = A >> 5;
+  float* slot0 = reinterpret_cast<float*>(smem) + g * NSLOT * SLOT_F;  // this group's slots
+  int32_t* const ring0 = reinterpret_cast<int32_t*>(reinterpret_cast<float*>(smem) + 2 * NSLOT * SLOT_F);
+  int32_t* idring = ring0 + w * RING * 64;                                  // [RING][64] per wave
+  float* dsbuf = reinterpret_cast<float*>(ring0 + 8 * RING * 64) + w * 64;  // [64] per wave
+  float* dabuf = reinterpret_cast<float*>(ring0 + 8 * RING * 64) + 8 * 64 + g * 64;  // [64] per group
+  float* dul = reinterpret_cast<float*>(ring0 + 8 * RING * 64) + 8 * 64 + 2 * 64;    // [16][128] dU rows
+  float* ql = dul + 16 * 128;                                                        // [16][128] query rows
+  float* dpl = ql + 16 * 128;                                                        // [2 groups][D]
+  float* w1p = dpl + 2 * D;                                                          // [32][D] fc.1 pooled half
+  float* colc = w1p + 32 * D;                                                        // [5][D]
+  const bool kt = dps.ktime;
+  NRK_KT(kt, 0);
+  for (int i = tid; i < 32 * D; i += 512) w1p[i] = dps.w1[(size_t)(i / D) * 2 * D + D + i % D];
+  for (int c = tid; c < D; c += 512) {
+    colc[c] = dps.stat0[D + c];
+    colc[D + c] = dps.stat0[3 * D + c];
+    colc[2 * D + c] = dps.bn0w[D + c];
+    colc[3 * D + c] = (float)dps.sum5[D + c] * dps.invB;
+    colc[4 * D + c] = (float)dps.sum5[3 * D + c] * dps.invB;
+  }
+  WFrag<true, D> wf;
+  const int wu = us < nsl ? us : 0;
+  wf.load(W1k, 32 * wu + r, h);
+  const float w2n = w2[32 * wu + r];
+  f32x16 dw[NCT];
+#pragma unroll
+  for (int c = 0; c < NCT; ++c)
+#pragma unroll
+    for (int gg = 0; gg < 16; ++gg) dw[c][gg] = 0.f;
+  float dw2_acc = 0.f, db2_acc = 0.f, db1_acc = 0.f;
+  float* const sqs_slab = slabs + (size_t)blockIdx.x * slab_floats(A, D) + slab_q_off(A, D);
+
+  // this wave's two small pieces of [pooled0, pooled1, alpha, da1, u0, u1, q0, q1]: kind us
+  const float* const sbase = us == 0 ? dps.pooled : us == 2 ? U : q;
+  const int sstride = us == 0 ? D : us == 2 ? A : dq;
+  uint32_t zmask = 0;  // per slot 2 bits: row tile c holds only zero keys (z = U, no dW1k term)
+  auto issue_ids = [&](int64_t b, int e) {
+    const int64_t bc = b < B ? b : 0;
+    const int i = lane < L ? lane : 0;
+    glds4_asm(ids + bc * L + i, lds_u32(idring + e * 64));
+  };
+  auto issue_data = [&](int64_t b, int sl, int e) {
+    float* sp = slot0 + sl * SLOT_F;
+    uint16_t* img = reinterpret_cast<uint16_t*>(sp + 4 * 128);
+#pragma unroll
+    for (int k = 0; k < NPW; ++k) {
+      const int u = us + 4 * k;
+      const int p = u * 64 + lane;
+      const int row = p / CPR, pc = p % CPR;
+      const int cc = pc ^ kswz<CPR>(row);
+      const int32_t idv0 = idring[e * 64 + row];
+      const int32_t idr = row < L && b < B ? idv0 : -1;
+      const uint16_t* src = (idr >= 0 && idr < n_table) ? table + (int64_t)idr * D + cc * 8 : zero_row(b, row) + cc * 8;
+      glds16_asm(src, lds_u32(img + u * 64 * 8));
+    }
+    const int64_t bc = b < B ? b : 0;
+    if (us == 1) {  // alpha [L], da1 [32]
+      glds4_asm(alpha + bc * L + (lane < L ? lane : 0), lds_u32(sp + 128));
+      glds4_asm(dps.da1 + bc * 32 + (lane < 32 ? lane : 0), lds_u32(sp + 192));
+    } else {
+#pragma unroll
+      for (int part = 0; part < 2; ++part) {
+        const int i = part * 64 + lane;
+        glds4_asm(sbase + bc * sstride + (i < sstride ? i : 0), lds_u32(sp + us * 128 + part * 64));
+      }
+    }
+    const int32_t idl = idring[e * 64 + lane];
+    const uint64_t vm = __ballot(lane < L && b < B && idl >= 0 && idl < n_table);
+    const uint32_t zb = ((uint32_t)vm == 0u ? 1u : 0u) | ((uint32_t)(vm >> 32) == 0u ? 2u : 0u);
+    zmask = (zmask & ~(3u << (2 * sl))) | (zb << (2 * sl));
+  };
+
+  const int64_t grid = gridDim.x;
+  const int64_t b0 = blockIdx.x;
+  const int ns_wg = b0 < B ? (int)((B - b0 + grid - 1) / grid) : 0;  // samples of this workgroup
+  const int n_it = (ns_wg + 1) >> 1;
+  auto sample = [&](int j) { return b0 + (int64_t)(2 * j + g) * grid; };  // group g's j-th sample
+#pragma unroll
+  for (int k = 0; k < X; ++k) issue_ids(sample(k), k);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  NRK_KT(kt, 1);
+#pragma unroll
+  for (int k = 0; k < P; ++k) {
+    issue_ids(sample(k + X), (k + X) % RING);
+    issue_data(sample(k), k, k);
+  }
+  int sl = 0, e = P % RING;  // e: ring entry holding the ids of sample(j + P)
+  for (int j = 0; j < n_it; ++j) {
+    // this wave's DMA group of sample(j) landed; all waves' after the barrier; slot of sample(j - 1) is free
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"((P - 1) * N_D) : "memory");
+    if (j == 0) NRK_KT(kt, 2);
+    issue_ids(sample(j + P + X), e + X < RING ? e + X : e + X - RING);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(X * N_D) : "memory");  // ids of sample(j + P) landed
+    issue_data(sample(j + P), sl + P < NSLOT ? sl + P : sl + P - NSLOT, e);
+    e = e + 1 < RING ? e + 1 : 0;
+
+    const int64_t bs = sample(j);
+    const bool act = bs < B;  // group 1 may run past the workgroup's last sample
+    const float* sp = slot0 + sl * SLOT_F;
+    const float* sal = sp + 128;
+    const float* sU = sp + 256;
+    const unsigned char* img = reinterpret_cast<const unsigned char*>(sp + 512);
+    float* sdp = dpl + g * D;
+    if (gt < D) {  // dpooled[c] = iv g (sum_j da1[j] W1p[j][c] - sb - xhat sg), xhat = (pooled - m) iv
+      const float* da1s = sp + 192;
+      float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f;
+#pragma unroll
+      for (int jj = 0; jj < 32; jj += 4) {
+        c0 = fmaf(da1s[jj], w1p[jj * D + gt], c0);
+        c1 = fmaf(da1s[jj + 1], w1p[(jj + 1) * D + gt], c1);
+        c2 = fmaf(da1s[jj + 2], w1p[(jj + 2) * D + gt], c2);
+        c3 = fmaf(da1s[jj + 3], w1p[(jj + 3) * D + gt], c3);
+      }
+      const float acc = (c0 + c1) + (c2 + c3);
+      const float m = colc[gt], iv = colc[D + gt], gw = colc[2 * D + gt];
+      const float xhat = (sp[gt] - m) * iv;
+      sdp[gt] = iv * gw * (acc - colc[3 * D + gt] - xhat * colc[4 * D + gt]);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    {  // dalpha[row] = dpooled . K[row]: wave us of the group owns rows [us R, (us+1) R)
+      constexpr int R = LP / 4, LPR = 64 / R, CH = CPR / LPR;
+      const int row = us * R + lane / LPR, part = lane % LPR;
+      float acc = 0.f;
+#pragma unroll
+      for (int ch = 0; ch < CH; ++ch) {
+        const int cc = part * CH + ch;
+        const uint4 kv = *reinterpret_cast<const uint4*>(img + row * 2 * D + 16 * (cc ^ kswz<CPR>(row)));
+        const float4 d0 = *reinterpret_cast<const float4*>(sdp + 8 * cc);
+        const float4 d1 = *reinterpret_cast<const float4*>(sdp + 8 * cc + 4);
+        acc = fmaf(d0.x, __uint_as_float(kv.x << 16), acc);
+        acc = fmaf(d0.y, __uint_as_float(kv.x & 0xFFFF0000u), acc);
+        acc = fmaf(d0.z, __uint_as_float(kv.y << 16), acc);
+        acc = fmaf(d0.w, __uint_as_float(kv.y & 0xFFFF0000u), acc);
+        acc = fmaf(d1.x, __uint_as_float(kv.z << 16), acc);
+        acc = fmaf(d1.y, __uint_as_float(kv.z & 0xFFFF0000u), acc);
+        acc = fmaf(d1.z, __uint_as_float(kv.w << 16), acc);
+        acc = fmaf(d1.w, __uint_as_float(kv.w & 0xFFFF0000u), acc);
+      }
+      acc = group_sum<LPR>(acc);
+      if (part == 0) dabuf[row] = acc;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    float du = 0.f;
+    if (act && us < nsl) {
+      const float un = sU[32 * us + r];
+      float da[NC];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) da[c] = dabuf[32 * c + r];
+      float t = 0.f;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int row = 32 * c + r;
+        t += (row < L && h == 0) ? sal[row] * da[c] : 0.f;
+      }
+      const float cdot = wave_sum_fast(t);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int row = 32 * c + r;
+        if (h == 0) {
+          const float ds = row < L ? sal[row] * (da[c] - cdot) : 0.f;
+          dsbuf[row] = ds;
+          if (us == 0) db2_acc += ds;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 1
+      for (int c = 0; c < NC; ++c) {  // (not unrolled: the two tiles' registers would overlap)
+        const bool kz = (zmask >> (2 * sl + c)) & 1u;  // zero keys: z = U exactly, no dW1k term
+        f32x16 acc;
+#pragma unroll
+        for (int gg = 0; gg < 16; ++gg) acc[gg] = un;
+        if (!kz) {
+#pragma unroll
+          for (int s2 = 0; s2 < KS; ++s2) {
+            const bf16x8 kf = *reinterpret_cast<const bf16x8*>(img + KImg<true, D>::off(32 * c + r, 16 * s2 + 8 * h));
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, wf.f[s2], acc, 0, 0, 0);
+          }
+        }
+        f32x16 dz;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const float4 d4 = *reinterpret_cast<const float4*>(dsbuf + 32 * c + 8 * jj + 4 * h);
+          const float dsv[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+          for (int i2 = 0; i2 < 4; ++i2) {
+            const int gg = 4 * jj + i2;
+            const float z = acc[gg];
+            dw2_acc = fmaf(dsv[i2], fmaxf(z, 0.f), dw2_acc);
+            const float v = z > 0.f ? dsv[i2] * w2n : 0.f;
+            dz[gg] = v;
+            du += v;
+          }
+        }
+        if (kz) continue;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          bf16x8 af;
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {  // v_cvt_pk_bf16_f32 (round to nearest even)
+            const bf16x2_hw pk = {(__bf16)dz[8 * s + 2 * jj], (__bf16)dz[8 * s + 2 * jj + 1]};
+            const uint32_t u = __builtin_bit_cast(uint32_t, pk);
+            af[2 * jj] = (short)(u & 0xFFFF);
+            af[2 * jj + 1] = (short)(u >> 16);
+          }
+          const int grp = lane >> 4, i16 = lane & 15;
+          const int rowq = 32 * c + 16 * s + 4 * h + (i16 >> 2);
+#pragma unroll
+          for (int cc = 0; cc < NCT; ++cc) {
+            const int col = 32 * cc + 16 * (grp & 1) + 4 * (i16 & 3);
+            typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+            const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(img + KImg<true, D>::off(rowq, col)));
+            const bf16x4 hi =
+                __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(img + KImg<true, D>::off(rowq + 8, col)));
+            const bf16x8 bfr = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+            dw[cc] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, dw[cc], 0, 0, 0);
+          }
+        }
+      }
+      du = half_swap_sum(du);
+      db1_acc += du;
+    }
+    {  // stage this sample's dU row and query row (sample index 2 j + g of the workgroup; host: <= 16)
+      const int si = 2 * j + g;
+      if (act && si < 16) {
+        if (h == 0 && us < nsl) dul[si * 128 + 32 * us + r] = du;
+        if (lane < 32) ql[si * 128 + 32 * us + lane] = sp[384 + 32 * us + lane];
+      }
+    }
+    sl = sl == NSLOT - 1 ? 0 : sl + 1;
+  }
+  NRK_KT(kt, 3);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");  // no LDS-DMA lands after this
+  {  // dW1q partial of the staged samples: wave (us, g) owns tiles n = 32 us.., k = 32 (g + 2 jj)..
+    const int ns = ns_wg < 16 ? ns_wg : 16;
+    if (us < nsl) {
+#pragma unroll
+      for (int jj = 0; jj < (NCT + 1) / 2; ++jj) {
+        const int tk = g + 2 * jj;
+        if (tk >= NCT) continue;
+        f32x16 acc;
+#pragma unroll
+        for (int gg = 0; gg < 16; ++gg) acc[gg] = 0.f;
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) {
+          const int sm = 2 * kk + h;
+          const float av = sm < ns ? dul[sm * 128 + 32 * us + r] : 0.f;
+          const float bv = sm < ns ? ql[sm * 128 + 32 * tk + r] : 0.f;
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int gg = 0; gg < 16; ++gg) sqs_slab[(size_t)(32 * us + acc_row(gg, h)) * D + 32 * tk + r] = acc[gg];
+      }
+    }
+  }
+  NRK_KT(kt, 4);
+  // combine the groups (g 1 into g 0, fixed order) through LDS
+  float* xch = reinterpret_cast<float*>(smem);  // [4 unit slices][32][D] f32
+  const bool wact = us < nsl;
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  if (g == 1 && wact) {
+#pragma unroll
+    for (int c = 0; c < NCT; ++c)
+#pragma unroll
+      for (int gg = 0; gg < 16; ++gg) xch[(size_t)(32 * us + acc_row(gg, h)) * D + 32 * c + r] = dw[c][gg];
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  if (g == 0 && wact) {
+#pragma unroll
+    for (int c = 0; c < NCT; ++c)
+#pragma unroll
+      for (int gg = 0; gg < 16; ++gg) dw[c][gg] += xch[(size_t)(32 * us + acc_row(gg, h)) * D + 32 * c + r];
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  float* xs = xch + 4 * 32 * D;  // [4][32] dw2, [4][32] db1, [1] db2 of group 1
+  {
+    const float t2 = half_swap_sum(dw2_acc);
+    const float tb2 = wave_sum_fast(db2_acc);
+    if (g == 1 && wact && h == 0) {
+      xs[32 * us + r] = t2;
+      xs[128 + 32 * us + r] = db1_acc;
+    }
+    if (g == 1 && us == 0 && lane == 0) xs[256] = tb2;
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    float* slab = slabs + (size_t)blockIdx.x * slab_floats(A, D);
+    if (g == 0 && wact) {
+      float* sqs = slab + slab_q_off(A, D);
+#pragma unroll
+      for (int c = 0; c < NCT; ++c)
+#pragma unroll
+        for (int gg = 0; gg < 16; ++gg) slab[(size_t)(32 * us + acc_row(gg, h)) * D + 32 * c + r] = dw[c][gg];
+      if (h == 0) {
+        slab[(size_t)A * D + 32 * us + r] = t2 + xs[32 * us + r];
+        sqs[(size_t)A * D + 32 * us + r] = db1_acc + xs[128 + 32 * us + r];
+      }
+    }
+    if (g == 0 && us == 0 && lane == 0) slab[(size_t)A * D + A] = tb2 + xs[256];
+  }
+  NRK_KT(kt, 5);
+}
+
 // Software-pipelined form of the head-fused 8-wave backward (FQ + FDP, LP <= 64).  The
 // serial form runs dpooled, dalpha and the z / dW1k work of one sample between three
 // barriers; here each iteration runs the three stages on three samples behind ONE
@@ -3045,6 +3373,17 @@ static int bwd_params_impl(const void* table, const int32_t* hist_ids, int64_t n
       const size_t xneed = ((size_t)4 * 32 * d + 257) * 4;
       if (dsm < xneed) dsm = xneed;
     }
+    // two-stream form (two groups of four waves, one sample each per iteration): 151.5 ->
+    // 148.1 us per train step at B = 4096 (profiles/r03_deep8_groups_ab.log).
+    // NRK_DEEP8_GROUPS=0: the row-group-split form (A/B hook)
+    const char* gr_env = getenv("NRK_DEEP8_GROUPS");
+    const bool group8 = !pipe8 && dps && w8 && fold_q && LPk <= 64 && LPk * d >= 2048 * 2 && !(gr_env && *gr_env == '0');
+    if (group8) {
+      dsm = (size_t)(2 * 3 * (4 * 128 + LPk * d / 2) + 8 * 4 * 64 + 8 * 64 + 2 * 64 + 2 * 16 * 128 + 2 * d + 32 * d +
+                     5 * d) * 4;
+      const size_t xneed = ((size_t)4 * 32 * d + 257) * 4;
+      if (dsm < xneed) dsm = xneed;
+    }
     NRK_CHECK_ARG(dsm <= 160 * 1024, "din_bwd_params: L=%d d=%d needs %zu B LDS", L, d, dsm);
 #define NRK_BWD_DEEP8_V(DD, LL, FQV, FDPV)                                                                         \
   hipLaunchKernelGGL((din_bwd_deep8_kernel<DD, LL, 3, FQV, FDPV>), dim3(grid), dim3(512), dsm, st, tb, hist_ids,     \
@@ -3053,6 +3392,9 @@ static int bwd_params_impl(const void* table, const int32_t* hist_ids, int64_t n
   do {                                                                                                              \
     if (pipe8)                                                                                                      \
       hipLaunchKernelGGL((din_bwd_deep8p_kernel<DD, LL>), dim3(grid), dim3(512), dsm, st, tb, hist_ids, n_table, U, wk, \
+                         w2, B, L, A, alpha, slabs, q, d, dpv);                                                      \
+    else if (group8)                                                                                                \
+      hipLaunchKernelGGL((din_bwd_deep8g_kernel<DD, LL>), dim3(grid), dim3(512), dsm, st, tb, hist_ids, n_table, U, wk, \
                          w2, B, L, A, alpha, slabs, q, d, dpv);                                                      \
     else if (fold_q && nslot8 == 4)                                                                                 \
       hipLaunchKernelGGL((din_bwd_deep8_kernel<DD, LL, 4, true, true>), dim3(grid), dim3(512), dsm, st, tb,         \
