@@ -41,7 +41,7 @@ def _newer(target, deps):
 
 
 def build_lib(force: bool = False) -> str:
-    headers = [os.path.join(CSRC, "nrk_common.h"), os.path.join(CSRC, "screen.h"), os.path.join(ROOT, "include", "nrk.h")]
+    headers = [os.path.join(CSRC, "nrk_common.h"), os.path.join(CSRC, "screen.h"), os.path.join(CSRC, "screen16.h"), os.path.join(ROOT, "include", "nrk.h")]
     objdir = os.path.join(CSRC, "build")
     os.makedirs(objdir, exist_ok=True)
     jobs = []

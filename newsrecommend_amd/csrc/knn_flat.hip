@@ -20,7 +20,7 @@
 
 #include <type_traits>
 
-#include "screen.h"
+#include "screen16.h"
 
 namespace nrk {
 
@@ -1814,6 +1814,11 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
   }
 
   screen_fn fn = p.waves == 8 ? pick_screen_dp256_w8(p.M, l2 != 0, 0) : pick_screen(p.dp, p.qt, p.M, l2 != 0, 0);
+  if (const int v16 = l2 ? 0 : test_hook("NRK_SCREEN16", 1)) {  // inner product: the 16x16x32 main pass where built
+    screen_fn f16 = p.waves == 8 ? (p.dp == 256 ? pick_screen16_dp256_w8(p.M, v16) : nullptr)
+                                 : (p.dp == 128 ? pick_screen16_dp128(p.qt, p.M, v16) : nullptr);
+    if (f16) fn = f16;
+  }
   if (!fn) return fail(NRK_EUNSUPPORTED, "knn_flat: no screen kernel for dp=%d", p.dp);
   const int nblk = p.nqt * p.nch;
   mark(1);

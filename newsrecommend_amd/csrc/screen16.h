@@ -1,0 +1,270 @@
+// screen16.h — the flat inner-product main pass (K-GEMM-TOPK, screen MODE 0) on
+// v_mfma_f32_16x16x32_bf16.  Same contract, grid, LDS staging and outputs as
+// screen_kernel<DP, QT, M, WAVES, false, 0, *, true, TIL> (screen.h): every
+// (query, chunk) gets two lane streams of M candidates + their (M+1)-th score.
+//
+// Why a second form: per FLOP the 16x16x32 instruction takes the same cycles
+// as 32x32x16, but on random data the chip holds a higher clock under it
+// (MI355X_MICROARCH.md: ~1.12-1.15x FLOP/s in bare loops), and the main pass is
+// MFMA-bound.
+//
+// Layout.  A = items (16 rows), B = queries (16 columns), K = 32 per MFMA.  A
+// wave's QT tiles of 32 queries are 2 QT half-tiles of 16; lane l holds query
+// (l & 15) of every half-tile and items 4 (l >> 4) + v (v < 4) of every 16-item
+// half of a 32-item sub-tile, so each (query, chunk) is scanned by FOUR lane
+// streams (lane groups g = l >> 4).  At the end the lists of groups g and g ^ 2
+// (lanes l and l ^ 32) are merged into one top-(M+1) list: the merged (M+1)-th
+// score bounds every item either stream left out (each stream's own (M+1)-th
+// entry is in the union the merged list is the top of), so the two merged
+// streams per (query, chunk) satisfy exactly what merge_rescore_kernel assumes
+// of the two lane halves of the 32x32 form.
+#pragma once
+
+#include "screen.h"
+
+namespace nrk {
+
+// sorted (descending score, ascending id on ties) insertion for list merges
+template <int N>
+__device__ __forceinline__ void list_insert_tie(float (&ls)[N], int (&li)[N], float v, int id) {
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const bool gt = v > ls[j] || (v == ls[j] && id < li[j]);
+    const float ts = gt ? v : ls[j];
+    const int ti = gt ? id : li[j];
+    v = gt ? ls[j] : v;
+    id = gt ? li[j] : id;
+    ls[j] = ts;
+    li[j] = ti;
+  }
+}
+
+template <int DP, int QT, int M, int WAVES, int TIL, bool SCHED = true>
+__global__ __launch_bounds__(WAVES * 64, 2) void screen16_kernel(
+    const uint16_t* __restrict__ qh, const uint16_t* __restrict__ xbh, const float* __restrict__ xmeta, int64_t nq,
+    int64_t nb, int64_t chunk, int nch, int nqt, int tstride, float* __restrict__ part_s, int* __restrict__ part_i,
+    float* __restrict__ part_t, const float* __restrict__ tau_q, IvfScreen iv) {
+  (void)xmeta;
+  (void)tstride;
+  (void)iv;
+  constexpr int CPR = DP / 8;   // 16-B chunks per row
+  constexpr int TI = TIL;       // items per tile between barriers
+  constexpr int NSUB = TI / 32; // 32-item sub-tiles per tile
+  static_assert(NSUB % 2 == 0, "sub-tiles alternate between two accumulator sets");
+  constexpr int TCH = TI * CPR;
+  constexpr int NT = WAVES * 64;
+  constexpr int GPT = TCH / NT;
+  static_assert(TCH % NT == 0, "tile must split evenly over the workgroup");
+  constexpr int KS2 = DP / 32;  // K steps of 32
+  constexpr int NQ2 = 2 * QT;   // 16-query half-tiles per wave
+  constexpr int WQ = WAVES * 32 * QT;
+  constexpr int BUF = TI * DP;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BUF];
+
+  const int nblk = gridDim.x, b = blockIdx.x;
+  const int xg = b & 7, jj = b >> 3, q8 = nblk >> 3, r8 = nblk & 7;
+  const int logical = (xg < r8 ? xg * (q8 + 1) : r8 * (q8 + 1) + (xg - r8) * q8) + jj;
+  const int c = logical / nqt, qt = logical - c * nqt;
+  const int64_t ibeg = (int64_t)c * chunk;
+  const int64_t iend = ibeg + chunk < nb ? ibeg + chunk : nb;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int q16 = lane & 15, g = lane >> 4;
+  const int ntiles = (int)cdiv(iend - ibeg, TI);
+
+  bf16x8 qf[NQ2][KS2];
+  int64_t qidx[NQ2];
+  float tau[NQ2];
+  float ls[NQ2][M + 1];
+  int li[NQ2][M + 1];
+#pragma unroll
+  for (int t = 0; t < NQ2; ++t) {
+    qidx[t] = (int64_t)qt * WQ + (int64_t)w * QT * 32 + 16 * t + q16;  // < nq_pad (zero rows)
+    const bf16x8* src = reinterpret_cast<const bf16x8*>(qh + qidx[t] * DP + 8 * g);
+#pragma unroll
+    for (int s = 0; s < KS2; ++s) qf[t][s] = src[4 * s];
+    tau[t] = (tau_q && qidx[t] < nq) ? tau_q[qidx[t]] : -INFINITY;
+#pragma unroll
+    for (int j = 0; j <= M; ++j) {
+      ls[t][j] = -INFINITY;
+      li[t][j] = -1;
+    }
+  }
+
+  const int64_t cnt = iend - ibeg > 0 ? iend - ibeg : 0;
+  const BufRsrc xrs = make_rsrc(xbh + ibeg * DP, (int)(cnt * DP * 2));
+  int voff[GPT];
+#pragma unroll
+  for (int u = 0; u < GPT; ++u) {
+    const int p = u * NT + tid;
+    const int row = p / CPR, pc = p % CPR;
+    voff[u] = row * DP * 2 + 16 * (pc ^ swz<CPR>(row));
+  }
+  auto issue_tile = [&](int it, auto buf_c) {
+    constexpr int buf = decltype(buf_c)::value;
+    const int soff = it * TI * DP * 2;
+#pragma unroll
+    for (int u = 0; u < GPT; ++u) buffer_load_lds16(xrs, lds + buf * BUF + (u * NT + w * 64) * 8, voff[u], soff);
+  };
+  // A fragment: row `row` of a tile image, K step s (lane group g reads chunk 4 s + g)
+  auto afrag = [&](const uint16_t* tl, int row, int s) {
+    return *reinterpret_cast<const bf16x8*>(tl + row * DP + 8 * ((4 * s + g) ^ swz<CPR>(row)));
+  };
+
+  // deferred epilogue: sub-tile s's scores are reduced while sub-tile s+1's
+  // MFMA chain runs (A: even sub-tiles, B: odd ones)
+  f32x4 accA[NQ2][2], accB[NQ2][2];
+  int64_t baseA = -1, baseB = -1;
+  int nvA = 0, nvB = 0;
+  bf16x8 af[2][KS2];
+  auto mask_rows = [&](f32x4 (&pa)[NQ2][2], int nv) __attribute__((always_inline)) {
+#pragma unroll
+    for (int t = 0; t < NQ2; ++t)
+#pragma unroll
+      for (int ih = 0; ih < 2; ++ih)
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          if (16 * ih + 4 * g + v >= nv) pa[t][ih][v] = -INFINITY;
+  };
+  auto tree = [&](f32x4 (&pa)[NQ2][2], float (&m2)[NQ2][2], float (&m)[NQ2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int t = 0; t < NQ2; ++t) {
+#pragma unroll
+      for (int ih = 0; ih < 2; ++ih)
+        m2[t][ih] = fmax_ieee(fmax_ieee(pa[t][ih][0], pa[t][ih][1]), fmax_ieee(pa[t][ih][2], pa[t][ih][3]));
+      m[t] = fmax_ieee(m2[t][0], m2[t][1]);
+    }
+  };
+  auto drain = [&](f32x4 (&pa)[NQ2][2], int64_t pbase, const float (&m2)[NQ2][2], const float (&m)[NQ2])
+      __attribute__((always_inline)) {
+    bool hit = false;
+#pragma unroll
+    for (int t = 0; t < NQ2; ++t) hit |= m[t] > fmaxf(ls[t][M], tau[t]);
+    if (!__any(hit)) return;
+#pragma unroll
+    for (int t = 0; t < NQ2; ++t) {
+      if (__any(m[t] > fmaxf(ls[t][M], tau[t]))) {
+#pragma unroll
+        for (int ih = 0; ih < 2; ++ih) {
+          if (__any(m2[t][ih] > fmaxf(ls[t][M], tau[t]))) {
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+              const float thr = fmaxf(ls[t][M], tau[t]);
+              if (pa[t][ih][v] > thr)
+                list_insert<M + 1>(ls[t], li[t], pa[t][ih][v], (int)(pbase + 16 * ih + 4 * g + v));
+            }
+          }
+        }
+      }
+    }
+  };
+  auto sub_tile = [&](auto st_c, int64_t i0, int nvalid, const uint16_t* next_tl) __attribute__((always_inline)) {
+    constexpr int st = decltype(st_c)::value;
+    constexpr int par = st & 1;
+    f32x4(&cur)[NQ2][2] = par ? accB : accA;
+    f32x4(&pend)[NQ2][2] = par ? accA : accB;
+    const int64_t pbase = par ? baseA : baseB;
+    const int pnv = par ? nvA : nvB;
+    if (pbase >= 0 && pnv < 32) mask_rows(pend, pnv);
+    // next sub-tile: the next 32 rows of this tile, or rows 0..31 of the next tile
+    const int nrow = (st + 1 < NSUB ? 32 * (st + 1) : 0) + q16;
+    const f32x4 zero = {};
+#pragma unroll
+    for (int s = 0; s < KS2; ++s) {
+#pragma unroll
+      for (int ih = 0; ih < 2; ++ih) {
+#pragma unroll
+        for (int t = 0; t < NQ2; ++t)
+          cur[t][ih] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ih][s], qf[t][s], s == 0 ? zero : cur[t][ih], 0, 0, 0);
+        af[ih][s] = afrag(next_tl, nrow + 16 * ih, s);
+      }
+    }
+    float m2[NQ2][2], m[NQ2];
+    tree(pend, m2, m);
+#pragma unroll
+    for (int t = 0; t < NQ2; ++t) m[t] = pbase >= 0 ? m[t] : -INFINITY;  // nothing pending: drain is a no-op
+    if constexpr (SCHED) {
+#pragma unroll
+      for (int s = 0; s < 2 * KS2; ++s) {
+        __builtin_amdgcn_sched_group_barrier(0x008, NQ2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 2 * NQ2 > 6 ? 6 : 2 * NQ2, 0);
+      }
+    }
+    drain(pend, pbase, m2, m);
+    if constexpr (par == 0) {
+      baseA = i0 + 32 * st;
+      nvA = nvalid - 32 * st;
+    } else {
+      baseB = i0 + 32 * st;
+      nvB = nvalid - 32 * st;
+    }
+  };
+  auto tile_d = [&](int it, auto buf_c) __attribute__((always_inline)) {
+    constexpr int buf = decltype(buf_c)::value;
+    const uint16_t* tl = lds + buf * BUF;
+    const int64_t i0 = ibeg + (int64_t)it * TI;
+    const int nvalid = (int)((iend - i0) < TI ? (iend - i0) : TI);
+    sub_tile(std::integral_constant<int, 0>{}, i0, nvalid, tl);
+    if constexpr (NSUB == 4) {
+      sub_tile(std::integral_constant<int, 1>{}, i0, nvalid, tl);
+      sub_tile(std::integral_constant<int, 2>{}, i0, nvalid, tl);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // tile it+1 landed; every wave is done with buffer buf
+    if (it + 2 < ntiles) issue_tile(it + 2, buf_c);
+    sub_tile(std::integral_constant<int, NSUB - 1>{}, i0, nvalid, lds + (buf ^ 1) * BUF);
+  };
+  if (ntiles > 0) {
+    issue_tile(0, std::integral_constant<int, 0>{});
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // tile 0 landed
+    if (ntiles > 1) issue_tile(1, std::integral_constant<int, 1>{});
+#pragma unroll
+    for (int ih = 0; ih < 2; ++ih)
+#pragma unroll
+      for (int s = 0; s < KS2; ++s) af[ih][s] = afrag(lds, 16 * ih + q16, s);
+  }
+  for (int it = 0; it < ntiles; it += 2) {
+    tile_d(it, std::integral_constant<int, 0>{});
+    if (it + 1 < ntiles) tile_d(it + 1, std::integral_constant<int, 1>{});
+  }
+  if (baseB >= 0) {  // the last sub-tile's epilogue
+    if (nvB < 32) mask_rows(accB, nvB);
+    float m2[NQ2][2], m[NQ2];
+    tree(accB, m2, m);
+    drain(accB, baseB, m2, m);
+  }
+
+  // merge the streams of lane groups g and g ^ 2, write from groups 0 and 1
+#pragma unroll
+  for (int t = 0; t < NQ2; ++t) {
+    float ps[M + 1];
+    int pi[M + 1];
+#pragma unroll
+    for (int j = 0; j <= M; ++j) {
+      ps[j] = __shfl_xor(ls[t][j], 32);
+      pi[j] = __shfl_xor(li[t][j], 32);
+    }
+    if (g < 2) {
+#pragma unroll
+      for (int j = 0; j <= M; ++j) list_insert_tie<M + 1>(ls[t], li[t], ps[j], pi[j]);
+      const int64_t qi = qidx[t];
+      if (qi < nq) {
+        const int64_t base = (qi * nch + c) * 2 + g;
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+          part_s[base * M + j] = ls[t][j];
+          part_i[base * M + j] = li[t][j];
+        }
+        part_t[base] = ls[t][M];
+      }
+    }
+  }
+}
+
+// the 16x16x32 main pass for (DP, qt, M), or nullptr (no such form: use screen.h's)
+screen_fn pick_screen16_dp128(int qt, int M, int var);
+screen_fn pick_screen16_dp256_w8(int M, int var);
+
+}  // namespace nrk

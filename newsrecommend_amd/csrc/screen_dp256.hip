@@ -1,9 +1,18 @@
 // screen_dp256.hip — screen_kernel instantiations for padded dim 256 (screen.h);
 // one translation unit per padded dimension so the build compiles them in parallel.
-#include "screen.h"
+#include "screen16.h"
 
 namespace nrk {
 NRK_SCREEN_DP(256)
+
+// 16x16x32 main pass at DP = 256 (8 waves, 64-item tiles), M = 4 only (N1):
+// 15.69 ms vs 15.82 for the 32x32x16 kernel (10M x 256, k = 5; the compiler's
+// own schedule 15.97, var 2).  M = 16 (k = 200) spills 32 VGPRs and ran 34.8 vs
+// 16.7 ms: it keeps the 32x32x16 kernel.
+screen_fn pick_screen16_dp256_w8(int M, int var) {
+  if (M != 4) return nullptr;
+  return var == 2 ? screen16_kernel<256, 1, 4, 8, 64, false> : screen16_kernel<256, 1, 4, 8, 64, true>;
+}
 
 screen_fn pick_screen_dp256_w8(int M, bool l2, int mode) {
   // IP: epilogue deferred into the next MFMA chain (configs[4] retrieve

@@ -55,6 +55,18 @@ def test_screen_partial_chunk_tiles(gpu, metric, d, k):
     _check(xq, xb, k, metric, gpu)
 
 
+@pytest.mark.parametrize("form", ["0", "2"])
+@pytest.mark.parametrize("d,n", [(128, 60_001), (128, 70_003), (256, 60_001), (256, 70_003)])
+def test_screen_main_pass_forms(gpu, monkeypatch, form, d, n):
+    """The inner-product main pass runs on the 16x16x32 kernel (screen16.h) by
+    default at k <= 8 for d 128 / 256; the 32x32x16 kernel (NRK_SCREEN16=0) and
+    the alternate 16x16x32 schedule (=2) give the oracle's results too, with and
+    without partial last tiles."""
+    monkeypatch.setenv("NRK_SCREEN16", form)
+    xq, xb = _mixture(n, 300, d, seed=d + n % 7)
+    _check(xq, xb, 5, ko.METRIC_IP, gpu)
+
+
 @pytest.mark.parametrize("metric", [ko.METRIC_IP, ko.METRIC_L2])
 def test_collect_pass_dense_neighbourhoods(gpu, metric):
     """Few, dense clusters (8 centres, 400k rows): neighbours closer together
