@@ -204,6 +204,9 @@ int nrk_din_batch_u(const float* q, int32_t B, int32_t d, const float* W1, const
  * workgroup, 1024 workgroups).  Copies the first n (<= 303104) values to host
  * memory.  No reference counterpart. */
 int nrk_debug_ktimes(uint64_t* out, int64_t n);
+/* The same for the fast head's kernels (NRK_KTIME=1 at nrk_din_head_train):
+ * out [8 kernels][128 blocks][8 slots] of s_memrealtime ticks (100 MHz), n <= 8192. */
+int nrk_debug_head_ktimes(uint64_t* out, int64_t n);
 
 /* DIN attention for re-ranking (DIN.py:166-173: every candidate of a user
  * attends over the same history): pooled [nU*C][d] f32 for candidates whose

@@ -65,6 +65,7 @@ SIGNATURES = {
     "nrk_din_head_ws_views": (ctypes.c_int, [c_i32, c_i32, c_i32, c_p, c_size, c_p, c_p, c_p]),
     "nrk_din_batch_u": (ctypes.c_int, [c_p, c_i32, c_i32, c_p, c_p, c_i32, c_p, c_p, c_p]),
     "nrk_debug_ktimes": (ctypes.c_int, [c_p, c_i64]),
+    "nrk_debug_head_ktimes": (ctypes.c_int, [c_p, c_i64]),
     "nrk_din_batch": (ctypes.c_int, [c_p, c_i32, c_p, c_p, c_p, c_i64, c_i32, c_p, c_i64, c_i32, c_i32, c_p, c_p,
                                      c_i32, c_p, c_p, c_p, c_p, c_p, c_p]),
     "nrk_din_rerank_attn": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_i32, c_i32, c_p, c_i32, c_i32, c_i32, c_p, c_p,

@@ -20,6 +20,7 @@
 // Activations are recomputed in the backward kernels from the stored
 // pre-activations a1/a2 and the counter-based dropout masks.
 #include <math.h>
+#include <stdlib.h>
 
 #include "nrk_common.h"
 
@@ -47,7 +48,19 @@ struct HeadArgs {
   float* dpooled;
   int fast;  // F == 32 fast path: statistics reduced in each consumer's prologue
   int nrg0;  // row groups of hf_stats0
+  int ktime; // diagnostic phase stamps (NRK_KTIME=1, g_hkt)
 };
+
+// Diagnostic phase stamps of the fast head's kernels (NRK_KTIME=1, read by
+// nrk_debug_head_ktimes; tools/din_step.py --hktime): g_hkt[kernel][block][slot]
+// = s_memrealtime (100 MHz) from thread 0 of blocks < 128.  Nothing reads
+// them back on the device; results are unaffected.
+__device__ uint64_t g_hkt[8 * 128 * 8];
+#define NRK_HKT(a, k, i)                                                                          \
+  do {                                                                                            \
+    if ((a).ktime && threadIdx.x == 0 && blockIdx.x < 128)                                        \
+      g_hkt[((k) * 128 + blockIdx.x) * 8 + (i)] = __builtin_amdgcn_s_memrealtime();              \
+  } while (0)
 
 __device__ __forceinline__ float hx(const HeadArgs& a, int64_t r, int c) {
   return c < a.d ? a.q[r * a.d + c] : a.pooled[r * a.ld + (c - a.d)];
@@ -111,6 +124,47 @@ __device__ void bn_finalize(const HeadArgs& a, const double* sum, int C, float* 
     }
   }
   if (publish && threadIdx.x == 0 && nb) *nb += 1;
+}
+
+// bn_finalize with the designated block's running statistics loaded at kernel
+// entry (pre_rm / pre_rv: columns t and t + blockDim.x of thread t, C <= 2 x
+// blockDim.x), so the publish adds no memory round trip at the kernel's tail
+struct RunStatPre {
+  float rm[2], rv[2];
+  int64_t nb;
+};
+__device__ __forceinline__ RunStatPre run_stat_pre(const float* rm, const float* rv, const int64_t* nb, int C,
+                                                   bool publish) {
+  RunStatPre r{};
+  r.nb = publish && threadIdx.x == 0 && nb ? *nb : 0;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int c = threadIdx.x + u * blockDim.x;
+    r.rm[u] = publish && c < C ? rm[c] : 0.f;
+    r.rv[u] = publish && c < C ? rv[c] : 0.f;
+  }
+  return r;
+}
+__device__ void bn_finalize_pre(const HeadArgs& a, const double* sum, int C, float* s_mean, float* s_inv, float* stat,
+                                float* rm, float* rv, int64_t* nb, bool publish, const RunStatPre& pre) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int c = threadIdx.x + u * blockDim.x;
+    if (c >= C) break;
+    const double mean = sum[c] / a.B;
+    double var = sum[C + c] / a.B - mean * mean;
+    if (var < 0) var = 0;
+    const float inv = (float)(1.0 / sqrt(var + (double)a.eps));
+    s_mean[c] = (float)mean;
+    s_inv[c] = inv;
+    if (publish) {
+      stat[c] = (float)mean;
+      stat[C + c] = inv;
+      rm[c] = (1.f - a.momentum) * pre.rm[u] + a.momentum * (float)mean;
+      rv[c] = (1.f - a.momentum) * pre.rv[u] + a.momentum * (float)(var * a.B / (a.B - 1));
+    }
+  }
+  if (publish && threadIdx.x == 0 && nb) *nb = pre.nb + 1;
 }
 
 __device__ __forceinline__ void load_stat(const float* stat, int C, float* s_mean, float* s_inv) {
@@ -582,6 +636,7 @@ constexpr int HF = 32;  // fc_units of the fast path
 __device__ __forceinline__ int hacc_row(int g, int h) { return (g & 3) + 8 * (g >> 2) + 4 * h; }
 
 __global__ __launch_bounds__(256) void hf_stats0(HeadArgs a) {
+  NRK_HKT(a, 0, 0);
   const int ncg = a.D2 / 32;
   const int cg = blockIdx.x % ncg, rg = blockIdx.x / ncg;
   const int cl = threadIdx.x & 31, ph = threadIdx.x >> 5;
@@ -595,6 +650,7 @@ __global__ __launch_bounds__(256) void hf_stats0(HeadArgs a) {
     sv += v;
     ssv += v * v;
   }
+  NRK_HKT(a, 0, 1);
   __shared__ double red[2][8][32];
   red[0][ph][cl] = sv;
   red[1][ph][cl] = ssv;
@@ -605,6 +661,7 @@ __global__ __launch_bounds__(256) void hf_stats0(HeadArgs a) {
     for (int q = 0; q < 8; ++q) t += red[wch][q][cl];
     a.part0[(int64_t)rg * 2 * a.D2 + wch * a.D2 + c] = t;
   }
+  NRK_HKT(a, 0, 7);
 }
 
 // LDS (floats): mean/inv [D2] x 2 | h0 [32][D2+4] | W1 [32][D2+4] | red [4][32][32] | d1 [32][33]
@@ -625,6 +682,7 @@ __global__ __launch_bounds__(256) void hf_fwd1(HeadArgs a) {
   float* w1 = h0 + HR * hs;
   float* red = w1 + (W1_LDS ? HF * hs : 0);
   float* d1 = red + 4 * HR * HF;
+  NRK_HKT(a, 1, 0);
   const int64_t r0 = (int64_t)blockIdx.x * HR;
   float4 xv[NX];
 #pragma unroll
@@ -632,8 +690,13 @@ __global__ __launch_bounds__(256) void hf_fwd1(HeadArgs a) {
     const int e = t + u * 256;
     xv[u] = hx4(a, r0 + e / q4, 4 * (e % q4));
   }
+  // the step counter and block 0's running statistics are loaded with the rows,
+  // ahead of the prologue's partial sums (W1 after: measured slower ahead of them)
+  const float stepv = *a.step;
+  const RunStatPre rsp = run_stat_pre(a.p.bn0_rm, a.p.bn0_rv, a.p.bn0_nb, D2, blockIdx.x == 0);
   colsum_prologue(a.part0, a.nrg0, 2 * D2, 2 * D2, pro_tmp, pro_sum);
-  bn_finalize(a, pro_sum, D2, mean, inv, a.stat0, a.p.bn0_rm, a.p.bn0_rv, a.p.bn0_nb, blockIdx.x == 0);
+  NRK_HKT(a, 1, 1);
+  bn_finalize_pre(a, pro_sum, D2, mean, inv, a.stat0, a.p.bn0_rm, a.p.bn0_rv, a.p.bn0_nb, blockIdx.x == 0, rsp);
   if constexpr (W1_LDS) {  // W1 (L2-resident: every block reads it)
     float4 wv[NX];
 #pragma unroll
@@ -645,6 +708,7 @@ __global__ __launch_bounds__(256) void hf_fwd1(HeadArgs a) {
     }
   }
   __syncthreads();  // mean / inv published
+  NRK_HKT(a, 1, 2);
 #pragma unroll
   for (int u = 0; u < NX; ++u) {
     const int e = t + u * 256, row = e / q4, c = 4 * (e % q4);
@@ -656,6 +720,7 @@ __global__ __launch_bounds__(256) void hf_fwd1(HeadArgs a) {
     *reinterpret_cast<float4*>(h0 + row * hs + c) = x;
   }
   __syncthreads();
+  NRK_HKT(a, 1, 3);
   {  // a1 = h0 W1^T: lane half h covers k in [h D2/2, (h+1) D2/2), wave w a quarter of that
     const int lane = t & 63, w = t >> 6, i = lane & 31, h = lane >> 5;
     constexpr int kw = D2 / 8;
@@ -676,13 +741,15 @@ __global__ __launch_bounds__(256) void hf_fwd1(HeadArgs a) {
     for (int g = 0; g < 16; ++g) red[w * HR * HF + hacc_row(g, h) * HF + i] = acc[g];
   }
   __syncthreads();
+  NRK_HKT(a, 1, 4);
   for (int o = t; o < HR * HF; o += 256) {
     const int r = o / HF, j = o % HF;
     const float v = ((red[o] + red[HR * HF + o]) + (red[2 * HR * HF + o] + red[3 * HR * HF + o])) + a.p.fc1_b[j];
     a.a1[(r0 + r) * HF + j] = v;
-    d1[r * (HF + 1) + j] = fmaxf(v, 0.f) * keep_scale(a, 1, r0 + r, j);
+    d1[r * (HF + 1) + j] = fmaxf(v, 0.f) * keep_scale_s(a, stepv, 1, r0 + r, j);
   }
   __syncthreads();
+  NRK_HKT(a, 1, 5);
   if (t < 2 * HF) {
     const int j = t % HF, sq = t / HF;
     double acc = 0.0;
@@ -692,6 +759,7 @@ __global__ __launch_bounds__(256) void hf_fwd1(HeadArgs a) {
     }
     a.part1[(int64_t)blockIdx.x * 2 * HF + sq * HF + j] = acc;
   }
+  NRK_HKT(a, 1, 7);
 }
 
 // LDS (floats): m0/i0 [D2] x 2 | xhat0 [32][D2+4] | da1 [32][33] | m1/i1/sb1/sg1 [32] x 4
@@ -709,6 +777,7 @@ __global__ __launch_bounds__(256) void hf_bwd1(HeadArgs a) {
   float* i1 = m1 + HF;
   float* sb1 = i1 + HF;
   float* sg1 = sb1 + HF;
+  NRK_HKT(a, 5, 0);
   const int64_t r0 = (int64_t)blockIdx.x * HR;
   const int s4 = 2 * HF + a.F2 * HF + a.F2;
   constexpr int q4 = D2 / 4;
@@ -726,6 +795,7 @@ __global__ __launch_bounds__(256) void hf_bwd1(HeadArgs a) {
     a1v[u] = a.a1[r0 * HF + e];
     dhv[u] = a.dh1[r0 * HF + e];
   }
+  const float stepv = *a.step;
   load_stat(a.stat0, D2, m0, i0);
   load_stat(a.stat1, HF, m1, i1);
   colsum_prologue(a.part4, a.nblk, s4, 2 * HF, pro_tmp, pro_sum);
@@ -733,6 +803,7 @@ __global__ __launch_bounds__(256) void hf_bwd1(HeadArgs a) {
     sb1[t] = (float)pro_sum[t];
     sg1[t] = (float)pro_sum[HF + t];
   }
+  NRK_HKT(a, 5, 1);
   __syncthreads();
 #pragma unroll
   for (int u = 0; u < NX; ++u) {
@@ -749,7 +820,7 @@ __global__ __launch_bounds__(256) void hf_bwd1(HeadArgs a) {
 #pragma unroll
     for (int u = 0; u < HR * HF / 256; ++u) {
       const int e = t + u * 256, r = e / HF, j = e % HF;
-      const float ks = keep_scale(a, 1, r0 + r, j);
+      const float ks = keep_scale_s(a, stepv, 1, r0 + r, j);
       const float xhat = (fmaxf(a1v[u], 0.f) * ks - m1[j]) * i1[j];
       const float dd1 = i1[j] * a.p.bn1_w[j] * (dhv[u] - sb1[j] * invB - xhat * sg1[j] * invB);
       const float v = a1v[u] > 0.f ? dd1 * ks : 0.f;
@@ -758,6 +829,7 @@ __global__ __launch_bounds__(256) void hf_bwd1(HeadArgs a) {
     }
   }
   __syncthreads();
+  NRK_HKT(a, 5, 2);
   {  // G (32 x D2) = da1^T xhat0 over the block's 32 rows; wave w: column tiles w, w+4, ...
      // stored column-major per block ([D2][32]: a column's 32 entries are one 128-B
      // line), so hf_reduce reads whole lines of 4 columns per partial block
@@ -776,11 +848,13 @@ __global__ __launch_bounds__(256) void hf_bwd1(HeadArgs a) {
       for (int g = 0; g < 16; ++g) pg[(int64_t)(32 * ct + i) * HF + hacc_row(g, h)] = acc[g];
     }
   }
+  NRK_HKT(a, 5, 3);
   if (t < HF) {
     double acc = 0.0;
     for (int r = 0; r < HR; ++r) acc += da[r * (HF + 1) + t];
     a.part5[(int64_t)blockIdx.x * HF + t] = acc;
   }
+  NRK_HKT(a, 5, 7);
 }
 
 // Every head gradient from the block partials (fixed order, fp64).
@@ -790,6 +864,7 @@ __global__ __launch_bounds__(256) void hf_bwd1(HeadArgs a) {
 //   (also kept in sum5 for hf_bwd0).  Blocks after: 64 columns each of the
 //   small layers' partials (part3: bn2, fc3, loss; part4: bn1, fc2).
 __global__ __launch_bounds__(1024) void hf_reduce(HeadArgs a) {
+  NRK_HKT(a, 6, 0);
   const int D2 = a.D2, F2 = a.F2, t = threadIdx.x, nblk = a.nblk;
   const int nA = D2 / 4;
   if ((int)blockIdx.x < nA) {
@@ -837,6 +912,7 @@ __global__ __launch_bounds__(1024) void hf_reduce(HeadArgs a) {
       sred[p2][j2] = s2;
     }
     __syncthreads();
+    NRK_HKT(a, 6, 1);
     if (t < 128) {
       const int jj = t >> 2, cc = t & 3;
       double g = 0.0;
@@ -866,6 +942,7 @@ __global__ __launch_bounds__(1024) void hf_reduce(HeadArgs a) {
       a.sum5[col] = sb;
       a.sum5[D2 + col] = sg;
     }
+    NRK_HKT(a, 6, 7);
     if (cgp == 0 && t < HF) a.p.g_fc1_b[t] = (float)St[t];
     return;
   }
@@ -926,6 +1003,7 @@ __global__ __launch_bounds__(256) void hf_fwd2(HeadArgs a) {
   __shared__ float mean[HF], inv[HF], b2s[HF2];
   __shared__ double red[2][16][HF2];
   __shared__ double pro_tmp[256], pro_sum[2 * HF];
+  NRK_HKT(a, 2, 0);
   const int t = threadIdx.x;
   const int64_t r0 = (int64_t)blockIdx.x * HR;
   const float stepv = *a.step;
@@ -934,8 +1012,10 @@ __global__ __launch_bounds__(256) void hf_fwd2(HeadArgs a) {
   if (t < HF2 * HF / 4) wv = reinterpret_cast<const float4*>(a.p.fc2_w)[t];
   const float gw = t < HF ? a.p.bn1_w[t] : 0.f, gb = t < HF ? a.p.bn1_b[t] : 0.f;
   if (t < HF2) b2s[t] = a.p.fc2_b[t];
+  const RunStatPre rsp = run_stat_pre(a.p.bn1_rm, a.p.bn1_rv, a.p.bn1_nb, HF, blockIdx.x == 0);
   colsum_prologue(a.part1, a.nblk, 2 * HF, 2 * HF, pro_tmp, pro_sum);
-  bn_finalize(a, pro_sum, HF, mean, inv, a.stat1, a.p.bn1_rm, a.p.bn1_rv, a.p.bn1_nb, blockIdx.x == 0);
+  NRK_HKT(a, 2, 1);
+  bn_finalize_pre(a, pro_sum, HF, mean, inv, a.stat1, a.p.bn1_rm, a.p.bn1_rv, a.p.bn1_nb, blockIdx.x == 0, rsp);
   __shared__ float gws[HF], gbs[HF];
   if (t < HF) {
     gws[t] = gw;
@@ -954,6 +1034,7 @@ __global__ __launch_bounds__(256) void hf_fwd2(HeadArgs a) {
     if (t < HF2 * HF / 4) *reinterpret_cast<float4*>(&w2[t >> 3][(t & 7) * 4]) = wv;
   }
   __syncthreads();
+  NRK_HKT(a, 2, 2);
 #pragma unroll
   for (int u = 0; u < 2; ++u) {  // a2 = h1 W2^T + b2: 512 outputs
     const int o = t + 256 * u, r = o >> 4, k = o & 15;
@@ -976,6 +1057,7 @@ __global__ __launch_bounds__(256) void hf_fwd2(HeadArgs a) {
     d2[r][k] = fmaxf(acc, 0.f) * keep_scale_s(a, stepv, 2, r0 + r, k);
   }
   __syncthreads();
+  NRK_HKT(a, 2, 3);
   {  // BN2 partial sums: 16 columns x 16 groups of 2 rows
     const int k = t & 15, g = t >> 4;
     const double v0 = d2[2 * g][k], v1 = d2[2 * g + 1][k];
@@ -990,6 +1072,7 @@ __global__ __launch_bounds__(256) void hf_fwd2(HeadArgs a) {
     for (int g = 0; g < 16; ++g) s += red[which][g][k];
     a.part2[(int64_t)blockIdx.x * 2 * HF2 + which * HF2 + k] = s;
   }
+  NRK_HKT(a, 2, 7);
 }
 
 // BN2 (prologue sums) -> Linear(16, 1) -> BCEWithLogits (mean); dlogit;
@@ -999,6 +1082,7 @@ __global__ __launch_bounds__(256) void hf_fwd3(HeadArgs a) {
   __shared__ float mean[HF2], inv[HF2], w3[HF2], gw2[HF2], gb2[HF2], dl[HR], lo[HR];
   __shared__ double red[3][16][HF2];
   __shared__ double pro_tmp[256], pro_sum[2 * HF2];
+  NRK_HKT(a, 3, 0);
   const int t = threadIdx.x;
   const int64_t r0 = (int64_t)blockIdx.x * HR;
   const float stepv = *a.step;
@@ -1011,8 +1095,10 @@ __global__ __launch_bounds__(256) void hf_fwd3(HeadArgs a) {
     gw2[t] = a.p.bn2_w[t];
     gb2[t] = a.p.bn2_b[t];
   }
+  const RunStatPre rsp = run_stat_pre(a.p.bn2_rm, a.p.bn2_rv, a.p.bn2_nb, HF2, blockIdx.x == 0);
   colsum_prologue(a.part2, a.nblk, 2 * HF2, 2 * HF2, pro_tmp, pro_sum);
-  bn_finalize(a, pro_sum, HF2, mean, inv, a.stat2, a.p.bn2_rm, a.p.bn2_rv, a.p.bn2_nb, blockIdx.x == 0);
+  NRK_HKT(a, 3, 1);
+  bn_finalize_pre(a, pro_sum, HF2, mean, inv, a.stat2, a.p.bn2_rm, a.p.bn2_rv, a.p.bn2_nb, blockIdx.x == 0, rsp);
   __syncthreads();
   if (t < HR * HF2 / 4) {
     const int r = t >> 2, k0 = (t & 3) * 4;
@@ -1027,6 +1113,7 @@ __global__ __launch_bounds__(256) void hf_fwd3(HeadArgs a) {
     }
   }
   __syncthreads();
+  NRK_HKT(a, 3, 2);
   if (t < HR) {
     float z = b3;
 #pragma unroll
@@ -1057,6 +1144,7 @@ __global__ __launch_bounds__(256) void hf_fwd3(HeadArgs a) {
     red[2][g][k] = sw;
   }
   __syncthreads();
+  NRK_HKT(a, 3, 3);
   double* pp = a.part3 + (int64_t)blockIdx.x * (3 * HF2 + 2);
   if (t < 3 * HF2) {
     const int which = t >> 4, k = t & 15;
@@ -1073,6 +1161,7 @@ __global__ __launch_bounds__(256) void hf_fwd3(HeadArgs a) {
       pp[3 * HF2 + 1] = ls;
     }
   }
+  NRK_HKT(a, 3, 7);
 }
 
 // BN2 backward (prologue sums) -> Dropout/ReLU backward -> Linear(32, 16)
@@ -1085,6 +1174,7 @@ __global__ __launch_bounds__(256) void hf_bwd2(HeadArgs a) {
   __shared__ float m1[HF], i1[HF], g1[HF], b1[HF], m2[HF2], i2[HF2], g2[HF2], sb2[HF2], sg2[HF2];
   __shared__ double red[2][8][HF];
   __shared__ double pro_tmp[256], pro_sum[2 * HF2];
+  NRK_HKT(a, 4, 0);
   const int t = threadIdx.x;
   const int64_t r0 = (int64_t)blockIdx.x * HR;
   const float stepv = *a.step;
@@ -1108,6 +1198,7 @@ __global__ __launch_bounds__(256) void hf_bwd2(HeadArgs a) {
     g2[k] = a.p.bn2_w[k];
   }
   colsum_prologue(a.part3, a.nblk, 3 * HF2 + 2, 2 * HF2, pro_tmp, pro_sum);
+  NRK_HKT(a, 4, 1);
   if (t < HF2) {
     sb2[t] = (float)pro_sum[t];
     sg2[t] = (float)pro_sum[HF2 + t];
@@ -1144,6 +1235,7 @@ __global__ __launch_bounds__(256) void hf_bwd2(HeadArgs a) {
     w2[wr][wc + 3] = wv.w;
   }
   __syncthreads();
+  NRK_HKT(a, 4, 2);
   double* pp = a.part4 + (int64_t)blockIdx.x * (2 * HF + HF2 * HF + HF2);
 #pragma unroll
   for (int u = 0; u < 2; ++u) {  // dW2[k][j] = sum_r da2[r][k] h1[r][j] (fp64, rows in order)
@@ -1176,6 +1268,7 @@ __global__ __launch_bounds__(256) void hf_bwd2(HeadArgs a) {
     }
     reinterpret_cast<float4*>(a.dh1 + r0 * HF)[t] = make_float4(dh[0], dh[1], dh[2], dh[3]);
   }
+  NRK_HKT(a, 4, 3);
   __syncthreads();  // h1 is re-used below as the dh1 image
   {
     const int r = t >> 3, j0 = (t & 7) * 4;
@@ -1203,6 +1296,7 @@ __global__ __launch_bounds__(256) void hf_bwd2(HeadArgs a) {
     for (int g = 0; g < 8; ++g) s += red[which][g][j];
     pp[which * HF + j] = s;
   }
+  NRK_HKT(a, 4, 7);
 }
 
 // dpooled = BN0 backward of dh0's pooled half, dh0 = da1 W1 on MFMA
@@ -1588,6 +1682,10 @@ extern "C" int nrk_din_head_train(const float* q, const float* pooled, int64_t l
   const int D2 = 2 * d, F2 = F / 2;
   a.fast = F == HF && d % 32 == 0;
   a.nrg0 = nblk < 8 ? nblk : 8;
+  {
+    const char* kt = getenv("NRK_KTIME");
+    a.ktime = kt && *kt == '1';
+  }
   if (a.fast) {
     const size_t lf1 =
         ((size_t)2 * D2 + (size_t)(HR + (D2 <= 256 ? HF : 0)) * (D2 + 4) + 4 * HR * HF + HR * (HF + 1)) * 4;
@@ -1660,6 +1758,13 @@ extern "C" int nrk_din_head_train(const float* q, const float* pooled, int64_t l
   const int ntot = F * D2 + F + D2 + F2 * F + F2 + F + F2 + 1 + F2;
   hipLaunchKernelGGL(head_grads, dim3((unsigned)cdiv(ntot, 256)), dim3(256), 0, st, a);
   NRK_CHECK_LAUNCH("head_grads");
+  return NRK_OK;
+}
+
+extern "C" int nrk_debug_head_ktimes(uint64_t* out, int64_t n) {
+  NRK_CHECK_ARG(out && n >= 0 && n <= 8 * 128 * 8, "debug_head_ktimes: bad arguments");
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(nrk::g_hkt), (size_t)n * 8, 0, hipMemcpyDeviceToHost) != hipSuccess)
+    return fail(NRK_ELAUNCH, "debug_head_ktimes: copy failed");
   return NRK_OK;
 }
 

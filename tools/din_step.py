@@ -18,7 +18,11 @@ ap.add_argument("--k", type=int, default=1, help="steps per graph launch (FusedT
 ap.add_argument("--ktime", action="store_true",
                 help="per-workgroup phase times of the head-fused backward and (NRK_DIN_FWD_PAIR=0, set here) "
                      "of the wave-per-sample forward")
+ap.add_argument("--hktime", action="store_true",
+                help="per-block phase stamps of the fast head's kernels (nrk_debug_head_ktimes)")
 a = ap.parse_args()
+if a.hktime:
+    os.environ["NRK_KTIME"] = "1"
 if a.ktime:
     os.environ["NRK_KTIME"] = "1"
     os.environ.setdefault("NRK_DIN_FWD_PAIR", "0")
@@ -73,3 +77,19 @@ if a.ktime:
         c = fu[:, j]
         if (f[:, j] > 0).all():
             print(f"  {n:10s} min {c.min():7.2f} med {np.median(c):7.2f} max {c.max():7.2f} us", flush=True)
+if a.hktime:
+    import numpy as np
+    from newsrecommend_amd import _lib
+    buf = np.zeros(8 * 128 * 8, dtype=np.uint64)
+    _lib.check(_lib.load().nrk_debug_head_ktimes(buf.ctypes.data, buf.size), "debug_head_ktimes")
+    t = buf.reshape(8, 128, 8).astype(np.int64)
+    names = ["stats0", "fwd1", "fwd2", "fwd3", "bwd2", "bwd1", "reduce"]
+    base = t[0, :, 0][t[0, :, 0] > 0].min()
+    for k, n in enumerate(names):
+        blk = t[k][t[k, :, 0] > 0]
+        if len(blk) == 0:
+            continue
+        us = (blk - base) / 100.0
+        cols = [f"s{i}: med {np.median(us[:, i]):7.2f} [{us[:, i].min():7.2f}, {us[:, i].max():7.2f}]"
+                for i in range(8) if (blk[:, i] > 0).all()]
+        print(f"  {n:7s} " + "  ".join(cols), flush=True)
