@@ -2983,6 +2983,9 @@ __global__ __launch_bounds__(256) void din_u_kernel(const float* __restrict__ q,
     qf[s2][6] = (short)f32_to_bf16_rne(hi4.z); qf[s2][7] = (short)f32_to_bf16_rne(hi4.w);
   }
   for (int ws = w; ws < A / 32; ws += 4) {
+    float bv[16];  // b1 of this lane's output units, loaded ahead of the MFMA chain
+#pragma unroll
+    for (int g = 0; g < 16; ++g) bv[g] = b1[32 * ws + acc_row(g, h)];
     f32x16 acc;
 #pragma unroll
     for (int g = 0; g < 16; ++g) acc[g] = 0.f;
@@ -3009,10 +3012,7 @@ __global__ __launch_bounds__(256) void din_u_kernel(const float* __restrict__ q,
     }
     if (b < B) {
 #pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        const int n = 32 * ws + acc_row(g, h);
-        U[(int64_t)b * A + n] = acc[g] + b1[n];
-      }
+      for (int g = 0; g < 16; ++g) U[(int64_t)b * A + 32 * ws + acc_row(g, h)] = acc[g] + bv[g];
     }
   }
 }

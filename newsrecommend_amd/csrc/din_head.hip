@@ -43,6 +43,8 @@ struct HeadArgs {
   double *sum0, *sum1, *sum2, *sum3, *sum4, *sum5, *sumw1;  // the partials summed over blocks
   float *stat0, *stat1, *stat2;  // finalised {mean, invstd} per feature
   float *a1, *a2, *dh2, *dh1, *dh0, *pw1;
+  uint32_t* mask1;  // fast head, dropout > 0: fc.2 dropout keep bits, one word per row (hf_fwd1)
+  uint16_t* mask2;  // fc.6 dropout keep bits, 16 per row (hf_fwd2)
   float* logits;
   float* loss;
   float* dpooled;
@@ -78,6 +80,12 @@ __device__ __forceinline__ float keep_scale_s(const HeadArgs& a, float stepv, in
   z ^= z >> 31;
   const float u = (float)(z >> 40) * (1.0f / 16777216.0f);
   return u >= a.p_drop ? 1.f / (1.f - a.p_drop) : 0.f;
+}
+// the keep scale of bit `bit` of a stored mask word (the same value keep_scale_s
+// gave when the word was formed)
+__device__ __forceinline__ float keep_bit(const HeadArgs& a, uint32_t word, int bit) {
+  if (a.p_drop <= 0.f) return 1.f;
+  return (word >> bit) & 1u ? 1.f / (1.f - a.p_drop) : 0.f;
 }
 __device__ __forceinline__ float keep_scale(const HeadArgs& a, int layer, int64_t r, int c) {
   return keep_scale_s(a, *a.step, layer, r, c);
@@ -694,6 +702,12 @@ __global__ __launch_bounds__(256) void hf_fwd1(HeadArgs a) {
   // ahead of the prologue's partial sums (W1 after: measured slower ahead of them)
   const float stepv = *a.step;
   const RunStatPre rsp = run_stat_pre(a.p.bn0_rm, a.p.bn0_rv, a.p.bn0_nb, D2, blockIdx.x == 0);
+  // this thread's BN0 affine columns (4 (t % q4) .. +3 for every u when 256 % q4 == 0)
+  // and fc.1 bias entry (t % 32 for every output it writes), loaded with the rows
+  constexpr bool G0_PRE = 256 % q4 == 0;
+  const float4 g0 = G0_PRE ? *reinterpret_cast<const float4*>(a.p.bn0_w + 4 * (t % q4)) : float4{};
+  const float4 be0 = G0_PRE ? *reinterpret_cast<const float4*>(a.p.bn0_b + 4 * (t % q4)) : float4{};
+  const float b1j = a.p.fc1_b[t % HF];
   colsum_prologue(a.part0, a.nrg0, 2 * D2, 2 * D2, pro_tmp, pro_sum);
   NRK_HKT(a, 1, 1);
   bn_finalize_pre(a, pro_sum, D2, mean, inv, a.stat0, a.p.bn0_rm, a.p.bn0_rv, a.p.bn0_nb, blockIdx.x == 0, rsp);
@@ -713,10 +727,12 @@ __global__ __launch_bounds__(256) void hf_fwd1(HeadArgs a) {
   for (int u = 0; u < NX; ++u) {
     const int e = t + u * 256, row = e / q4, c = 4 * (e % q4);
     float4 x = xv[u];
-    x.x = (x.x - mean[c]) * inv[c] * a.p.bn0_w[c] + a.p.bn0_b[c];
-    x.y = (x.y - mean[c + 1]) * inv[c + 1] * a.p.bn0_w[c + 1] + a.p.bn0_b[c + 1];
-    x.z = (x.z - mean[c + 2]) * inv[c + 2] * a.p.bn0_w[c + 2] + a.p.bn0_b[c + 2];
-    x.w = (x.w - mean[c + 3]) * inv[c + 3] * a.p.bn0_w[c + 3] + a.p.bn0_b[c + 3];
+    const float4 gu = G0_PRE ? g0 : *reinterpret_cast<const float4*>(a.p.bn0_w + c);
+    const float4 bu = G0_PRE ? be0 : *reinterpret_cast<const float4*>(a.p.bn0_b + c);
+    x.x = (x.x - mean[c]) * inv[c] * gu.x + bu.x;
+    x.y = (x.y - mean[c + 1]) * inv[c + 1] * gu.y + bu.y;
+    x.z = (x.z - mean[c + 2]) * inv[c + 2] * gu.z + bu.z;
+    x.w = (x.w - mean[c + 3]) * inv[c + 3] * gu.w + bu.w;
     *reinterpret_cast<float4*>(h0 + row * hs + c) = x;
   }
   __syncthreads();
@@ -744,20 +760,29 @@ __global__ __launch_bounds__(256) void hf_fwd1(HeadArgs a) {
   NRK_HKT(a, 1, 4);
   for (int o = t; o < HR * HF; o += 256) {
     const int r = o / HF, j = o % HF;
-    const float v = ((red[o] + red[HR * HF + o]) + (red[2 * HR * HF + o] + red[3 * HR * HF + o])) + a.p.fc1_b[j];
+    const float v = ((red[o] + red[HR * HF + o]) + (red[2 * HR * HF + o] + red[3 * HR * HF + o])) + b1j;
     a.a1[(r0 + r) * HF + j] = v;
-    d1[r * (HF + 1) + j] = fmaxf(v, 0.f) * keep_scale_s(a, stepv, 1, r0 + r, j);
+    const float ks = keep_scale_s(a, stepv, 1, r0 + r, j);
+    d1[r * (HF + 1) + j] = fmaxf(v, 0.f) * ks;
+    if (a.p_drop > 0.f) {  // the keep bits of this wave's two rows, for the later kernels
+      const uint64_t bits = __ballot(ks != 0.f);
+      if ((t & 63) == 0) *reinterpret_cast<uint64_t*>(a.mask1 + r0 + r) = bits;
+    }
   }
   __syncthreads();
   NRK_HKT(a, 1, 5);
-  if (t < 2 * HF) {
-    const int j = t % HF, sq = t / HF;
+  {  // BN1 partial sums: {sum, sum sq} x 32 columns x 4 row groups of 8, combined in a fixed order
+    __shared__ double p1[4][2 * HF];
+    const int o = t & 63, rq = t >> 6, j = o % HF, sq = o / HF;
     double acc = 0.0;
-    for (int r = 0; r < HR; ++r) {
+#pragma unroll
+    for (int r = 8 * rq; r < 8 * rq + 8; ++r) {
       const double v = d1[r * (HF + 1) + j];
       acc += sq ? v * v : v;
     }
-    a.part1[(int64_t)blockIdx.x * 2 * HF + sq * HF + j] = acc;
+    p1[rq][o] = acc;
+    __syncthreads();
+    if (t < 2 * HF) a.part1[(int64_t)blockIdx.x * 2 * HF + t] = (p1[0][t] + p1[1][t]) + (p1[2][t] + p1[3][t]);
   }
   NRK_HKT(a, 1, 7);
 }
@@ -795,7 +820,10 @@ __global__ __launch_bounds__(256) void hf_bwd1(HeadArgs a) {
     a1v[u] = a.a1[r0 * HF + e];
     dhv[u] = a.dh1[r0 * HF + e];
   }
-  const float stepv = *a.step;
+  const float g1j = a.p.bn1_w[t % HF];  // the BN1 weight of every element this thread forms
+  uint32_t mw[HR * HF / 256];           // fc.2 keep bits of rows (t >> 5) + 8 u
+#pragma unroll
+  for (int u = 0; u < HR * HF / 256; ++u) mw[u] = a.p_drop > 0.f ? a.mask1[r0 + (t >> 5) + 8 * u] : 0u;
   load_stat(a.stat0, D2, m0, i0);
   load_stat(a.stat1, HF, m1, i1);
   colsum_prologue(a.part4, a.nblk, s4, 2 * HF, pro_tmp, pro_sum);
@@ -820,9 +848,9 @@ __global__ __launch_bounds__(256) void hf_bwd1(HeadArgs a) {
 #pragma unroll
     for (int u = 0; u < HR * HF / 256; ++u) {
       const int e = t + u * 256, r = e / HF, j = e % HF;
-      const float ks = keep_scale_s(a, stepv, 1, r0 + r, j);
+      const float ks = keep_bit(a, mw[u], j);
       const float xhat = (fmaxf(a1v[u], 0.f) * ks - m1[j]) * i1[j];
-      const float dd1 = i1[j] * a.p.bn1_w[j] * (dhv[u] - sb1[j] * invB - xhat * sg1[j] * invB);
+      const float dd1 = i1[j] * g1j * (dhv[u] - sb1[j] * invB - xhat * sg1[j] * invB);
       const float v = a1v[u] > 0.f ? dd1 * ks : 0.f;
       da[r * (HF + 1) + j] = v;
       a.dh1[(r0 + r) * HF + j] = v;  // da1 replaces dh1 (same thread, same element)
@@ -849,10 +877,17 @@ __global__ __launch_bounds__(256) void hf_bwd1(HeadArgs a) {
     }
   }
   NRK_HKT(a, 5, 3);
-  if (t < HF) {
+  {  // sum da1 over the block's rows: 32 columns x 8 row groups of 4, fixed-order combine
+    __shared__ double p5[8][HF];
+    const int j = t & 31, rq = t >> 5;
     double acc = 0.0;
-    for (int r = 0; r < HR; ++r) acc += da[r * (HF + 1) + t];
-    a.part5[(int64_t)blockIdx.x * HF + t] = acc;
+#pragma unroll
+    for (int r = 4 * rq; r < 4 * rq + 4; ++r) acc += da[r * (HF + 1) + j];
+    p5[rq][j] = acc;
+    __syncthreads();
+    if (t < HF)
+      a.part5[(int64_t)blockIdx.x * HF + t] = ((p5[0][t] + p5[1][t]) + (p5[2][t] + p5[3][t])) +
+                                             ((p5[4][t] + p5[5][t]) + (p5[6][t] + p5[7][t]));
   }
   NRK_HKT(a, 5, 7);
 }
@@ -880,6 +915,8 @@ __global__ __launch_bounds__(1024) void hf_reduce(HeadArgs a) {
     const int ph = t >> 7, j = t & 31, cl = (t >> 5) & 3;
     const int c = 4 * cgp + cl;
     float wv[HF];  // W1 column of this block's column t (t < 4), loaded with the partials
+    const int colp = 4 * cgp + (t & 3);  // BN0 affine of output column (t < 128), loaded with the partials
+    const float bw0 = t < 128 ? a.p.bn0_w[colp] : 0.f, bb0 = t < 128 ? a.p.bn0_b[colp] : 0.f;
     if (t < 4) {
 #pragma unroll
       for (int jj = 0; jj < HF; ++jj) wv[jj] = a.p.fc1_w[(int64_t)jj * D2 + 4 * cgp + t];
@@ -927,7 +964,7 @@ __global__ __launch_bounds__(1024) void hf_reduce(HeadArgs a) {
     __syncthreads();
     if (t < 128) {
       const int jj = t >> 2, cc = t & 3, col = 4 * cgp + cc;
-      a.p.g_fc1_w[(int64_t)jj * D2 + col] = (float)(a.p.bn0_w[col] * Gt[jj][cc] + a.p.bn0_b[col] * St[jj]);
+      a.p.g_fc1_w[(int64_t)jj * D2 + col] = (float)(bw0 * Gt[jj][cc] + bb0 * St[jj]);
     }
     if (t < 4) {
       const int col = 4 * cgp + t;
@@ -1008,6 +1045,7 @@ __global__ __launch_bounds__(256) void hf_fwd2(HeadArgs a) {
   const int64_t r0 = (int64_t)blockIdx.x * HR;
   const float stepv = *a.step;
   const float4 av = reinterpret_cast<const float4*>(a.a1 + r0 * HF)[t];  // row t/8, cols 4(t%8)..
+  const uint32_t mw1 = a.p_drop > 0.f ? a.mask1[r0 + (t >> 3)] : 0u;      // its fc.2 keep bits
   float4 wv = make_float4(0.f, 0.f, 0.f, 0.f);
   if (t < HF2 * HF / 4) wv = reinterpret_cast<const float4*>(a.p.fc2_w)[t];
   const float gw = t < HF ? a.p.bn1_w[t] : 0.f, gb = t < HF ? a.p.bn1_b[t] : 0.f;
@@ -1028,7 +1066,7 @@ __global__ __launch_bounds__(256) void hf_fwd2(HeadArgs a) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int j = j0 + u;
-      const float d1 = fmaxf(x[u], 0.f) * keep_scale_s(a, stepv, 1, r0 + r, j);
+      const float d1 = fmaxf(x[u], 0.f) * keep_bit(a, mw1, j);
       h1[r][j] = (d1 - mean[j]) * inv[j] * gws[j] + gbs[j];
     }
     if (t < HF2 * HF / 4) *reinterpret_cast<float4*>(&w2[t >> 3][(t & 7) * 4]) = wv;
@@ -1054,7 +1092,12 @@ __global__ __launch_bounds__(256) void hf_fwd2(HeadArgs a) {
     }
     const float acc = (c0 + c1) + (c2 + c3);
     a.a2[(r0 + r) * HF2 + k] = acc;
-    d2[r][k] = fmaxf(acc, 0.f) * keep_scale_s(a, stepv, 2, r0 + r, k);
+    const float ks = keep_scale_s(a, stepv, 2, r0 + r, k);
+    d2[r][k] = fmaxf(acc, 0.f) * ks;
+    if (a.p_drop > 0.f) {  // the keep bits of this wave's four rows
+      const uint64_t bits = __ballot(ks != 0.f);
+      if ((t & 63) == 0) *reinterpret_cast<uint64_t*>(a.mask2 + r0 + r) = bits;
+    }
   }
   __syncthreads();
   NRK_HKT(a, 2, 3);
@@ -1085,10 +1128,10 @@ __global__ __launch_bounds__(256) void hf_fwd3(HeadArgs a) {
   NRK_HKT(a, 3, 0);
   const int t = threadIdx.x;
   const int64_t r0 = (int64_t)blockIdx.x * HR;
-  const float stepv = *a.step;
   float4 av = make_float4(0.f, 0.f, 0.f, 0.f);
   if (t < HR * HF2 / 4) av = reinterpret_cast<const float4*>(a.a2 + r0 * HF2)[t];  // row t/4, cols 4(t%4)..
   const float yv = t < HR ? a.y[r0 + t] : 0.f;
+  const uint32_t mw2 = a.p_drop > 0.f && t < HR * HF2 / 4 ? a.mask2[r0 + (t >> 2)] : 0u;  // fc.6 keep bits
   const float b3 = a.p.fc3_b[0];
   if (t < HF2) {
     w3[t] = a.p.fc3_w[t];
@@ -1106,7 +1149,7 @@ __global__ __launch_bounds__(256) void hf_fwd3(HeadArgs a) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int k = k0 + u;
-      const float d2 = fmaxf(x4[u], 0.f) * keep_scale_s(a, stepv, 2, r0 + r, k);
+      const float d2 = fmaxf(x4[u], 0.f) * keep_bit(a, mw2, k);
       const float x = (d2 - mean[k]) * inv[k];
       xh[r][k] = x;
       h2[r][k] = x * gw2[k] + gb2[k];
@@ -1177,9 +1220,10 @@ __global__ __launch_bounds__(256) void hf_bwd2(HeadArgs a) {
   NRK_HKT(a, 4, 0);
   const int t = threadIdx.x;
   const int64_t r0 = (int64_t)blockIdx.x * HR;
-  const float stepv = *a.step;
   // every load of the block first
   const float4 a1v = reinterpret_cast<const float4*>(a.a1 + r0 * HF)[t];  // row t/8, cols 4(t%8)..
+  const uint32_t mw1 = a.p_drop > 0.f ? a.mask1[r0 + (t >> 3)] : 0u;
+  const uint32_t mw2 = a.p_drop > 0.f && t < HR * HF2 / 4 ? a.mask2[r0 + (t >> 2)] : 0u;
   float4 a2v = make_float4(0.f, 0.f, 0.f, 0.f), dhv = a2v, wv = a2v;
   if (t < HR * HF2 / 4) {
     a2v = reinterpret_cast<const float4*>(a.a2 + r0 * HF2)[t];  // row t/4, cols 4(t%4)..
@@ -1211,7 +1255,7 @@ __global__ __launch_bounds__(256) void hf_bwd2(HeadArgs a) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int j = j0 + u;
-      const float d1 = fmaxf(x4[u], 0.f) * keep_scale_s(a, stepv, 1, r0 + r, j);
+      const float d1 = fmaxf(x4[u], 0.f) * keep_bit(a, mw1, j);
       const float x = (d1 - m1[j]) * i1[j];
       xh1[r][j] = x;
       h1[r][j] = x * g1[j] + b1[j];
@@ -1223,7 +1267,7 @@ __global__ __launch_bounds__(256) void hf_bwd2(HeadArgs a) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int k = k0 + u;
-      const float ks = keep_scale_s(a, stepv, 2, r0 + r, k);
+      const float ks = keep_bit(a, mw2, k);
       const float xhat = (fmaxf(a4[u], 0.f) * ks - m2[k]) * i2[k];
       const float dd2 = i2[k] * g2[k] * (d4[u] - sb2[k] * invB - xhat * sg2[k] * invB);
       da2[r][k] = a4[u] > 0.f ? dd2 * ks : 0.f;
@@ -1585,6 +1629,8 @@ static void head_sizes(int B, int d, int F, int nblk, size_t* off, size_t* total
   take(13, (size_t)B * D2 * 4);                        // dh0
   take(14, (size_t)nblk * F * D2 * 4);                 // pw1
   take(15, (size_t)(2 * D2 + 2 * F + 2 * F2 + (3 * F2 + 2) + (2 * F + F2 * F + F2) + (2 * D2 + F) + F * D2) * 8);
+  take(16, (size_t)B * 4);                             // mask1
+  take(17, (size_t)B * 2);                             // mask2
   *total = o;
 }
 
@@ -1596,7 +1642,7 @@ static void head_sizes(int B, int d, int F, int nblk, size_t* off, size_t* total
 extern "C" int nrk_din_head_ws_views(int32_t B, int32_t d, int32_t F, const void* ws, size_t ws_bytes,
                                      const float** stat0, const double** sum5, const float** da1) {
   NRK_CHECK_ARG(ws && stat0 && sum5 && da1 && B > 1 && d > 0 && F >= 2, "din_head_ws_views: bad arguments");
-  size_t off[17], total = 0;
+  size_t off[18], total = 0;
   head_sizes(B, d, F, (int)cdiv(B, HR), off, &total);
   if (ws_bytes < total) return fail(NRK_EWORKSPACE, "din_head_ws_views: workspace %zu < %zu", ws_bytes, total);
   const char* w = static_cast<const char*>(ws);
@@ -1610,7 +1656,7 @@ extern "C" int nrk_din_head_ws_views(int32_t B, int32_t d, int32_t F, const void
 
 extern "C" int nrk_din_head_workspace(int32_t B, int32_t d, int32_t F, size_t* ws_bytes) {
   NRK_CHECK_ARG(ws_bytes && B > 1 && d > 0 && F >= 2, "din_head_workspace: bad arguments");
-  size_t off[17];
+  size_t off[18];
   head_sizes(B, d, F, (int)cdiv(B, HR), off, ws_bytes);
   return NRK_OK;
 }
@@ -1628,7 +1674,7 @@ extern "C" int nrk_din_head_train(const float* q, const float* pooled, int64_t l
   // workspace (nrk_din_attn_bwd_params_head), so the BN0-backward launch is skipped
   NRK_CHECK_ARG(dpooled || (F == 32 && d % 32 == 0), "din_head_train: dpooled may be NULL only with F = 32");
   const int nblk = B / HR;
-  size_t off[17], total = 0;
+  size_t off[18], total = 0;
   head_sizes(B, d, F, nblk, off, &total);
   if (ws_bytes < total) return fail(NRK_EWORKSPACE, "din_head_train: workspace %zu < %zu", ws_bytes, total);
   char* w = static_cast<char*>(ws);
@@ -1664,6 +1710,8 @@ extern "C" int nrk_din_head_train(const float* q, const float* pooled, int64_t l
   a.dh1 = reinterpret_cast<float*>(w + off[12]);
   a.dh0 = reinterpret_cast<float*>(w + off[13]);
   a.pw1 = reinterpret_cast<float*>(w + off[14]);
+  a.mask1 = reinterpret_cast<uint32_t*>(w + off[16]);
+  a.mask2 = reinterpret_cast<uint16_t*>(w + off[17]);
   {
     double* sb = reinterpret_cast<double*>(w + off[15]);
     const int D2_ = 2 * d, F2_ = F / 2;

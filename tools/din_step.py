@@ -90,6 +90,10 @@ if a.hktime:
         if len(blk) == 0:
             continue
         us = (blk - base) / 100.0
-        cols = [f"s{i}: med {np.median(us[:, i]):7.2f} [{us[:, i].min():7.2f}, {us[:, i].max():7.2f}]"
-                for i in range(8) if (blk[:, i] > 0).all()]
+        cols = []
+        for i in range(8):
+            ok = blk[:, i] > 0  # blocks that stamp slot i (hf_reduce: the G blocks only past s0)
+            if ok.any():
+                v = us[ok, i]
+                cols.append(f"s{i}: med {np.median(v):7.2f} [{v.min():7.2f}, {v.max():7.2f}]")
         print(f"  {n:7s} " + "  ".join(cols), flush=True)
