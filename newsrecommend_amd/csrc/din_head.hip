@@ -43,6 +43,7 @@ struct HeadArgs {
   double *sum0, *sum1, *sum2, *sum3, *sum4, *sum5, *sumw1;  // the partials summed over blocks
   float *stat0, *stat1, *stat2;  // finalised {mean, invstd} per feature
   float *a1, *a2, *dh2, *dh1, *dh0, *pw1;
+  float* da1;       // fast head: the gradient at fc.1's output [B][32] (hf_bwd1; the dh0 region)
   uint32_t* mask1;  // fast head, dropout > 0: fc.2 dropout keep bits, one word per row (hf_fwd1)
   uint16_t* mask2;  // fc.6 dropout keep bits, 16 per row (hf_fwd2)
   float* logits;
@@ -787,31 +788,36 @@ __global__ __launch_bounds__(256) void hf_fwd1(HeadArgs a) {
   NRK_HKT(a, 1, 7);
 }
 
-// LDS (floats): m0/i0 [D2] x 2 | xhat0 [32][D2+4] | da1 [32][33] | m1/i1/sb1/sg1 [32] x 4
-template <int NX>
+// LDS (floats): m0/i0 [DC] x 2 | xhat0 [32][DC+4] | da1 [32][33] | m1/i1/sb1/sg1 [32] x 4 | gT [DC][36]
+// CS column splits: block b covers rows 32 (b / CS) .. and the DC = D2 / CS columns
+// from (b % CS) DC (every split forms the block's da1; split 0 writes it and its sum),
+// so the x̂0 loads and the G MFMAs of a row block spread over CS CUs
+template <int NX, int CS>
 __global__ __launch_bounds__(256) void hf_bwd1(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   __shared__ double pro_tmp[256], pro_sum[64];
-  constexpr int D2 = NX * 32, hs = D2 + 4;
+  constexpr int D2 = NX * 32, DC = D2 / CS, hs = DC + 4;
+  static_assert(NX % CS == 0, "column split of whole 32-column tiles");
   const int t = threadIdx.x;
+  const int rb = (int)blockIdx.x / CS, hh = (int)blockIdx.x % CS, cbase = hh * DC;
   float* m0 = sm;
-  float* i0 = m0 + D2;
-  float* xh = i0 + D2;
+  float* i0 = m0 + DC;
+  float* xh = i0 + DC;
   float* da = xh + HR * hs;
   float* m1 = da + HR * (HF + 1);
   float* i1 = m1 + HF;
   float* sb1 = i1 + HF;
   float* sg1 = sb1 + HF;
   NRK_HKT(a, 5, 0);
-  const int64_t r0 = (int64_t)blockIdx.x * HR;
+  const int64_t r0 = (int64_t)rb * HR;
   const int s4 = 2 * HF + a.F2 * HF + a.F2;
-  constexpr int q4 = D2 / 4;
+  constexpr int q4 = DC / 4;
   // every load of the block's rows first, then the prologue's partial sums
-  float4 xv[NX];
+  float4 xv[NX / CS];
 #pragma unroll
-  for (int u = 0; u < NX; ++u) {
+  for (int u = 0; u < NX / CS; ++u) {
     const int e = t + u * 256;
-    xv[u] = hx4(a, r0 + e / q4, 4 * (e % q4));
+    xv[u] = hx4(a, r0 + e / q4, cbase + 4 * (e % q4));
   }
   float a1v[HR * HF / 256], dhv[HR * HF / 256];
 #pragma unroll
@@ -824,7 +830,10 @@ __global__ __launch_bounds__(256) void hf_bwd1(HeadArgs a) {
   uint32_t mw[HR * HF / 256];           // fc.2 keep bits of rows (t >> 5) + 8 u
 #pragma unroll
   for (int u = 0; u < HR * HF / 256; ++u) mw[u] = a.p_drop > 0.f ? a.mask1[r0 + (t >> 5) + 8 * u] : 0u;
-  load_stat(a.stat0, D2, m0, i0);
+  for (int c = t; c < DC; c += 256) {
+    m0[c] = a.stat0[cbase + c];
+    i0[c] = a.stat0[D2 + cbase + c];
+  }
   load_stat(a.stat1, HF, m1, i1);
   colsum_prologue(a.part4, a.nblk, s4, 2 * HF, pro_tmp, pro_sum);
   if (t < HF) {
@@ -834,7 +843,7 @@ __global__ __launch_bounds__(256) void hf_bwd1(HeadArgs a) {
   NRK_HKT(a, 5, 1);
   __syncthreads();
 #pragma unroll
-  for (int u = 0; u < NX; ++u) {
+  for (int u = 0; u < NX / CS; ++u) {
     const int e = t + u * 256, row = e / q4, c = 4 * (e % q4);
     float4 x = xv[u];
     x.x = (x.x - m0[c]) * i0[c];
@@ -853,17 +862,19 @@ __global__ __launch_bounds__(256) void hf_bwd1(HeadArgs a) {
       const float dd1 = i1[j] * g1j * (dhv[u] - sb1[j] * invB - xhat * sg1[j] * invB);
       const float v = a1v[u] > 0.f ? dd1 * ks : 0.f;
       da[r * (HF + 1) + j] = v;
-      a.dh1[(r0 + r) * HF + j] = v;  // da1 replaces dh1 (same thread, same element)
+      if (hh == 0) a.da1[(r0 + r) * HF + j] = v;  // (not in place: the other split still reads dh1)
     }
   }
   __syncthreads();
   NRK_HKT(a, 5, 2);
-  {  // G (32 x D2) = da1^T xhat0 over the block's 32 rows; wave w: column tiles w, w+4, ...
-     // stored column-major per block ([D2][32]: a column's 32 entries are one 128-B
-     // line), so hf_reduce reads whole lines of 4 columns per partial block
+  {  // G (32 x DC) = da1^T xhat0 over the block's 32 rows; wave w: column tiles w, w+4, ...
+     // stored column-major per row block ([D2][32]: a column's 32 entries are one 128-B
+     // line, hf_reduce_c1 reads one line per partial block).  The tile goes through
+     // LDS (gT [DC][36]) so the global stores are whole lines: scattered 4-B stores
+     // of 64 lines per instruction left partially written lines
     const int lane = t & 63, w = t >> 6, i = lane & 31, h = lane >> 5;
-    float* pg = a.pw1 + (int64_t)blockIdx.x * HF * D2;
-    for (int ct = w; ct < D2 / 32; ct += 4) {
+    float* gT = sg1 + HF;  // [DC][36] after the BN1 constants
+    for (int ct = w; ct < DC / 32; ct += 4) {
       f32x16 acc;
 #pragma unroll
       for (int g = 0; g < 16; ++g) acc[g] = 0.f;
@@ -873,11 +884,18 @@ __global__ __launch_bounds__(256) void hf_bwd1(HeadArgs a) {
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(da[row * (HF + 1) + i], xh[row * hs + 32 * ct + i], acc, 0, 0, 0);
       }
 #pragma unroll
-      for (int g = 0; g < 16; ++g) pg[(int64_t)(32 * ct + i) * HF + hacc_row(g, h)] = acc[g];
+      for (int g = 0; g < 16; ++g) gT[(32 * ct + i) * 36 + hacc_row(g, h)] = acc[g];
+    }
+    __syncthreads();
+    float4* pg4 = reinterpret_cast<float4*>(a.pw1 + (int64_t)rb * HF * D2 + (int64_t)cbase * HF);
+#pragma unroll 4
+    for (int e = t; e < DC * HF / 4; e += 256) {
+      const int c = e >> 3, qd = e & 7;
+      pg4[e] = *reinterpret_cast<const float4*>(gT + c * 36 + 4 * qd);
     }
   }
   NRK_HKT(a, 5, 3);
-  {  // sum da1 over the block's rows: 32 columns x 8 row groups of 4, fixed-order combine
+  if (hh == 0) {  // sum da1 over the block's rows: 32 columns x 8 row groups of 4, fixed-order combine
     __shared__ double p5[8][HF];
     const int j = t & 31, rq = t >> 5;
     double acc = 0.0;
@@ -886,8 +904,8 @@ __global__ __launch_bounds__(256) void hf_bwd1(HeadArgs a) {
     p5[rq][j] = acc;
     __syncthreads();
     if (t < HF)
-      a.part5[(int64_t)blockIdx.x * HF + t] = ((p5[0][t] + p5[1][t]) + (p5[2][t] + p5[3][t])) +
-                                             ((p5[4][t] + p5[5][t]) + (p5[6][t] + p5[7][t]));
+      a.part5[(int64_t)rb * HF + t] = ((p5[0][t] + p5[1][t]) + (p5[2][t] + p5[3][t])) +
+                                      ((p5[4][t] + p5[5][t]) + (p5[6][t] + p5[7][t]));
   }
   NRK_HKT(a, 5, 7);
 }
@@ -1009,6 +1027,109 @@ __global__ __launch_bounds__(1024) void hf_reduce(HeadArgs a) {
   if (t < 64 && valid) {
     double v = 0.0;
     for (int p2 = 0; p2 < 16; ++p2) v += sr[p2][t];
+    if (q < s3) {
+      if (q < F2) a.p.g_bn2_b[q] = (float)v;
+      else if (q < 2 * F2) a.p.g_bn2_w[q - F2] = (float)v;
+      else if (q < 3 * F2) a.p.g_fc3_w[q - 2 * F2] = (float)v;
+      else if (q == 3 * F2) a.p.g_fc3_b[0] = (float)v;
+      else *a.loss = (float)(v / a.B);
+    } else {
+      const int o = q - s3;
+      if (o < HF) a.p.g_bn1_b[o] = (float)v;
+      else if (o < 2 * HF) a.p.g_bn1_w[o - HF] = (float)v;
+      else if (o < 2 * HF + F2 * HF) a.p.g_fc2_w[o - 2 * HF] = (float)v;
+      else a.p.g_fc2_b[o - 2 * HF - F2 * HF] = (float)v;
+    }
+  }
+}
+
+// hf_reduce with ONE column of G per block (256 threads = 8 phases x 32 j, all 16
+// loads of a thread in flight at once): the 4 MB of G partials are read by D2
+// blocks spread over the chip instead of D2 / 4 (hf_reduce's G phase took 5.8 us
+// on 64 blocks).  g_fc1_w[j][c] = bn0_w[c] G[j][c] + bn0_b[c] S[j],
+// g_bn0_b[c] = sum_j W1[j][c] S[j], g_bn0_w[c] = sum_j W1[j][c] G[j][c] (and sum5).
+// Blocks after: 64 columns each of the small layers' partials, 4 phases.
+__global__ __launch_bounds__(256) void hf_reduce_c1(HeadArgs a) {
+  NRK_HKT(a, 6, 0);
+  const int D2 = a.D2, F2 = a.F2, t = threadIdx.x, nblk = a.nblk;
+  if ((int)blockIdx.x < D2) {
+    const int c = blockIdx.x;
+    __shared__ double red[8][32], sred[8][32], Gt[32], St[32];
+    const int ph = t >> 5, j = t & 31;
+    const float wj = t < 32 ? a.p.fc1_w[(int64_t)j * D2 + c] : 0.f;
+    const float bw0 = a.p.bn0_w[c], bb0 = a.p.bn0_b[c];
+    double acc = 0.0, s5 = 0.0;
+    for (int b0 = ph; b0 < nblk; b0 += 8 * 16) {
+      float v[16];
+      double w5[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int b = b0 + 8 * u;
+        v[u] = b < nblk ? a.pw1[(int64_t)b * HF * D2 + (int64_t)c * HF + j] : 0.f;
+        w5[u] = b < nblk ? a.part5[(int64_t)b * HF + j] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        acc += (double)v[u];
+        s5 += w5[u];
+      }
+    }
+    red[ph][j] = acc;
+    sred[ph][j] = s5;
+    __syncthreads();
+    NRK_HKT(a, 6, 1);
+    if (t < 32) {
+      double g = 0.0, s = 0.0;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        g += red[q][t];
+        s += sred[q][t];
+      }
+      Gt[t] = g;
+      St[t] = s;
+      a.p.g_fc1_w[(int64_t)t * D2 + c] = (float)(bw0 * g + bb0 * s);
+    }
+    __syncthreads();
+    if (t < 64) {  // sums over j on wave 0 (lanes 32..63 add zeros)
+      double sb = t < 32 ? (double)wj * St[t] : 0.0, sg = t < 32 ? (double)wj * Gt[t] : 0.0;
+      sb = wave_sum(sb);
+      sg = wave_sum(sg);
+      if (t == 0) {
+        a.p.g_bn0_b[c] = (float)sb;
+        a.p.g_bn0_w[c] = (float)sg;
+        a.sum5[c] = sb;
+        a.sum5[D2 + c] = sg;
+      }
+    }
+    if (c == 0 && t < HF) a.p.g_fc1_b[t] = (float)St[t];
+    NRK_HKT(a, 6, 7);
+    return;
+  }
+  // small layers: column q of the concatenation [part3 (3F2+2) | part4 (2F + F2 F + F2)]
+  __shared__ double sr[4][64];
+  const int s3 = 3 * F2 + 2, s4 = 2 * HF + F2 * HF + F2;
+  const int cl = t & 63, ph = t >> 6;
+  const int q = ((int)blockIdx.x - D2) * 64 + cl;
+  const bool valid = q < s3 + s4;
+  double acc = 0.0;
+  if (valid) {
+    const double* src = q < s3 ? a.part3 + q : a.part4 + (q - s3);
+    const int stride = q < s3 ? s3 : s4;
+    for (int b0 = ph; b0 < nblk; b0 += 4 * 32) {
+      double v[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) {
+        const int b = b0 + 4 * u;
+        v[u] = b < nblk ? src[(int64_t)b * stride] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 32; ++u) acc += v[u];
+    }
+  }
+  sr[ph][cl] = acc;
+  __syncthreads();
+  if (t < 64 && valid) {
+    const double v = (sr[0][t] + sr[1][t]) + (sr[2][t] + sr[3][t]);
     if (q < s3) {
       if (q < F2) a.p.g_bn2_b[q] = (float)v;
       else if (q < 2 * F2) a.p.g_bn2_w[q - F2] = (float)v;
@@ -1349,7 +1470,7 @@ __global__ __launch_bounds__(256) void hf_bwd0(HeadArgs a) {
   __shared__ float da[HR][HF + 1];
   const int D2 = a.D2, d = a.d, ld = (int)a.ld, t = threadIdx.x;
   const int64_t r0 = (int64_t)blockIdx.x * HR;
-  for (int e = t; e < HR * HF; e += 256) da[e / HF][e % HF] = a.dh1[(r0 + e / HF) * HF + e % HF];
+  for (int e = t; e < HR * HF; e += 256) da[e / HF][e % HF] = a.da1[(r0 + e / HF) * HF + e % HF];
   for (int e = t; e < HR * (ld - d); e += 256) a.dpooled[(r0 + e / (ld - d)) * ld + d + e % (ld - d)] = 0.f;
   __syncthreads();
   const float invB = 1.f / (float)a.B;
@@ -1650,7 +1771,7 @@ extern "C" int nrk_din_head_ws_views(int32_t B, int32_t d, int32_t F, const void
   const double* sb = reinterpret_cast<const double*>(w + off[15]);
   const int D2_ = 2 * d, F2_ = F / 2;
   *sum5 = sb + 2 * D2_ + 2 * F + 2 * F2_ + (3 * F2_ + 2) + (2 * F + F2_ * F + F2_);
-  *da1 = reinterpret_cast<const float*>(w + off[12]);
+  *da1 = reinterpret_cast<const float*>(w + off[13]);  // hf_bwd1's da1 (the dh0 region, unused by the fast head)
   return NRK_OK;
 }
 
@@ -1709,6 +1830,7 @@ extern "C" int nrk_din_head_train(const float* q, const float* pooled, int64_t l
   a.dh2 = reinterpret_cast<float*>(w + off[11]);
   a.dh1 = reinterpret_cast<float*>(w + off[12]);
   a.dh0 = reinterpret_cast<float*>(w + off[13]);
+  a.da1 = a.dh0;
   a.pw1 = reinterpret_cast<float*>(w + off[14]);
   a.mask1 = reinterpret_cast<uint32_t*>(w + off[16]);
   a.mask2 = reinterpret_cast<uint16_t*>(w + off[17]);
@@ -1737,7 +1859,7 @@ extern "C" int nrk_din_head_train(const float* q, const float* pooled, int64_t l
   if (a.fast) {
     const size_t lf1 =
         ((size_t)2 * D2 + (size_t)(HR + (D2 <= 256 ? HF : 0)) * (D2 + 4) + 4 * HR * HF + HR * (HF + 1)) * 4;
-    const size_t lb1 = ((size_t)2 * D2 + (size_t)HR * (D2 + 4) + HR * (HF + 1) + 4 * HF) * 4;
+    const size_t lb1 = ((size_t)2 * D2 + (size_t)HR * (D2 + 4) + HR * (HF + 1) + 4 * HF + (size_t)D2 * 36) * 4;
     // + the kernels' static LDS (hf_fwd1: 10 KB of prologue sums): every launch must fit 160 KB
     NRK_CHECK_ARG(lf1 + 10240 <= 160 * 1024 && lb1 + 4096 <= 160 * 1024,
                   "din_head_train: d=%d needs %zu / %zu B of LDS", d, lf1 + 10240, lb1 + 4096);
@@ -1756,17 +1878,33 @@ extern "C" int nrk_din_head_train(const float* q, const float* pooled, int64_t l
     hipLaunchKernelGGL(hf_fwd2, dim3(nblk), dim3(256), 0, st, a);
     hipLaunchKernelGGL(hf_fwd3, dim3(nblk), dim3(256), 0, st, a);
     hipLaunchKernelGGL(hf_bwd2, dim3(nblk), dim3(256), 0, st, a);
+    // NRK_DIN_BWD1_SPLIT=1: one block per 32-row block (A/B hook); default 2 column splits
+    const char* cs_env = getenv("NRK_DIN_BWD1_SPLIT");
+    const int cs = (cs_env && *cs_env == '1') || (D2 / 32) % 2 ? 1 : 2;
+    const size_t lb1c = ((size_t)2 * (D2 / cs) + (size_t)HR * (D2 / cs + 4) + HR * (HF + 1) + 4 * HF +
+                         (size_t)(D2 / cs) * 36) * 4;
+#define NRK_HF_BWD1(NXV)                                                                                    \
+  do {                                                                                                      \
+    if (cs == 2) hipLaunchKernelGGL((hf_bwd1<NXV, ((NXV) % 2 ? 1 : 2)>), dim3(2 * nblk), dim3(256), lb1c, st, a); \
+    else hipLaunchKernelGGL((hf_bwd1<NXV, 1>), dim3(nblk), dim3(256), lb1c, st, a);                        \
+  } while (0)
     switch (D2) {
-      case 64: hipLaunchKernelGGL(hf_bwd1<2>, dim3(nblk), dim3(256), lb1, st, a); break;
-      case 128: hipLaunchKernelGGL(hf_bwd1<4>, dim3(nblk), dim3(256), lb1, st, a); break;
-      case 192: hipLaunchKernelGGL(hf_bwd1<6>, dim3(nblk), dim3(256), lb1, st, a); break;
-      case 256: hipLaunchKernelGGL(hf_bwd1<8>, dim3(nblk), dim3(256), lb1, st, a); break;
-      case 320: hipLaunchKernelGGL(hf_bwd1<10>, dim3(nblk), dim3(256), lb1, st, a); break;
-      case 384: hipLaunchKernelGGL(hf_bwd1<12>, dim3(nblk), dim3(256), lb1, st, a); break;
-      case 448: hipLaunchKernelGGL(hf_bwd1<14>, dim3(nblk), dim3(256), lb1, st, a); break;
-      default: hipLaunchKernelGGL(hf_bwd1<16>, dim3(nblk), dim3(256), lb1, st, a); break;
+      case 64: NRK_HF_BWD1(2); break;
+      case 128: NRK_HF_BWD1(4); break;
+      case 192: NRK_HF_BWD1(6); break;
+      case 256: NRK_HF_BWD1(8); break;
+      case 320: NRK_HF_BWD1(10); break;
+      case 384: NRK_HF_BWD1(12); break;
+      case 448: NRK_HF_BWD1(14); break;
+      default: NRK_HF_BWD1(16); break;
     }
-    hipLaunchKernelGGL(hf_reduce, dim3((unsigned)(D2 / 4 + cdiv(s3_ + s4_, 64))), dim3(1024), 0, st, a);
+#undef NRK_HF_BWD1
+    // NRK_DIN_HEAD_REDUCE=4: the 4-column form (A/B hook)
+    const char* hr_env = getenv("NRK_DIN_HEAD_REDUCE");
+    if (hr_env && *hr_env == '4')
+      hipLaunchKernelGGL(hf_reduce, dim3((unsigned)(D2 / 4 + cdiv(s3_ + s4_, 64))), dim3(1024), 0, st, a);
+    else
+      hipLaunchKernelGGL(hf_reduce_c1, dim3((unsigned)(D2 + cdiv(s3_ + s4_, 64))), dim3(256), 0, st, a);
     if (dpooled) hipLaunchKernelGGL(hf_bwd0, dim3(nblk), dim3(256), 0, st, a);
     NRK_CHECK_LAUNCH("din_head_train (fast)");
     return NRK_OK;
