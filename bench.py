@@ -767,7 +767,7 @@ def bench_din(args, rank, world, dev):
                    "step": (f"fused head/optimizer kernels, one hip graph per {DIN_STEPS_PER_GRAPH} steps" if graphed else
                             "fused head/optimizer kernels + RCCL grad all_reduce") if fused else "eager torch"},
         "final_loss": float(loss.reshape(-1)[0].item()),
-        "kernels_ms": {"attn_fwd": fwd_ms, "attn_bwd (deep8 + dwq + reduce)" if fused else "attn_bwd+reduce": bwd_ms},
+        "kernels_ms": {"attn_fwd": fwd_ms, "attn_bwd (8-wave + reduce)" if fused else "attn_bwd+reduce": bwd_ms},
         "roofline_step": {"bound": "hbm", "achieved": step_gbs, "peak": HBM_GBS, "unit": "GB/s",
                           "frac": step_gbs / HBM_GBS,
                           "traffic": _pmc_traffic(f"din_step:{din_key}") if fused and graphed else None,
