@@ -2826,6 +2826,20 @@ __global__ __launch_bounds__(256) void din_bwd_reduce_kernel(const float* __rest
   }
 }
 
+// w = hi + mid + lo exactly, each part a bf16 (truncation split: hi keeps w's top
+// 8 significant bits, w - hi is exact in f32 with <= 16 of them, mid its top 8,
+// the remaining <= 8 bits are exactly a bf16), so q·hi + q·mid + q·lo are exact
+// f32 products for a bf16 q.  Six integer/float ops instead of three RNE roundings.
+__device__ __forceinline__ void split3_bf16(float w, short* hi, short* mid, short* lo) {
+  const uint32_t hb = __float_as_uint(w) & 0xFFFF0000u;
+  const float rem = w - __uint_as_float(hb);
+  const uint32_t mb = __float_as_uint(rem) & 0xFFFF0000u;
+  const float low = rem - __uint_as_float(mb);
+  *hi = (short)(hb >> 16);
+  *mid = (short)(mb >> 16);
+  *lo = (short)(__float_as_uint(low) >> 16);
+}
+
 // ========================================================== train batch ==
 // One DIN train batch assembled from the device-resident click log, replacing
 // TrainDataset.__getitem__'s CPU gather (DIN.py:81-92) and the query half of
@@ -2931,13 +2945,11 @@ __global__ __launch_bounds__(256) void din_batch_kernel(const int64_t* __restric
       bf16x8 fh, fm, fl;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const uint16_t hb = f32_to_bf16_rne(wv[j]);
-        const float rem1 = wv[j] - bf16_to_f32(hb);
-        const uint16_t mb = f32_to_bf16_rne(rem1);
-        const uint16_t lb = f32_to_bf16_rne(rem1 - bf16_to_f32(mb));
-        fh[j] = (short)hb;
-        fm[j] = (short)mb;
-        fl[j] = (short)lb;
+        short h1, m1, l1;
+        split3_bf16(wv[j], &h1, &m1, &l1);
+        fh[j] = h1;
+        fm[j] = m1;
+        fl[j] = l1;
       }
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fl, qf[s2], acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fm, qf[s2], acc, 0, 0, 0);
@@ -2998,13 +3010,11 @@ __global__ __launch_bounds__(256) void din_u_kernel(const float* __restrict__ q,
       bf16x8 fh, fm, fl;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const uint16_t hb = f32_to_bf16_rne(wv[j]);
-        const float rem1 = wv[j] - bf16_to_f32(hb);
-        const uint16_t mb = f32_to_bf16_rne(rem1);
-        const uint16_t lb = f32_to_bf16_rne(rem1 - bf16_to_f32(mb));
-        fh[j] = (short)hb;
-        fm[j] = (short)mb;
-        fl[j] = (short)lb;
+        short h1, m1, l1;
+        split3_bf16(wv[j], &h1, &m1, &l1);
+        fh[j] = h1;
+        fm[j] = m1;
+        fl[j] = l1;
       }
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fl, qf[s2], acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fm, qf[s2], acc, 0, 0, 0);

@@ -1851,7 +1851,11 @@ extern "C" int nrk_din_head_train(const float* q, const float* pooled, int64_t l
   hipStream_t st = (hipStream_t)stream;
   const int D2 = 2 * d, F2 = F / 2;
   a.fast = F == HF && d % 32 == 0;
-  a.nrg0 = nblk < 8 ? nblk : 8;
+  {  // row groups of hf_stats0 (NRK_DIN_NRG0=8 / 32: A/B hook)
+    const char* rg_env = getenv("NRK_DIN_NRG0");
+    const int want = rg_env && *rg_env ? atoi(rg_env) : 16;  // 16: measured -0.9 us vs 8, 32 no better
+    a.nrg0 = (want == 8 || want == 16 || want == 32) && nblk >= want ? want : (nblk < 8 ? nblk : 8);
+  }
   {
     const char* kt = getenv("NRK_KTIME");
     a.ktime = kt && *kt == '1';
