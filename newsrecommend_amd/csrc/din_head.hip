@@ -189,6 +189,25 @@ __device__ __forceinline__ void load_stat(const float* stat, int C, float* s_mea
 __device__ void colsum_prologue(const double* __restrict__ part, int nblk, int stride, int ncol,
                                 double* s_tmp /*[256]*/, double* s_out) {
   const int t = threadIdx.x;
+  if (ncol > 256 && ncol <= 512 && nblk <= 16) {  // hf_fwd1's BN0 sums: both columns' loads in one round
+    double v[2][16];
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int c = t + 256 * k;
+        v[k][u] = c < ncol && u < nblk ? part[(int64_t)u * stride + c] : 0.0;
+      }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      double acc = 0.0;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) acc += v[k][u];
+      if (t + 256 * k < ncol) s_out[t + 256 * k] = acc;
+    }
+    __syncthreads();
+    return;
+  }
   if (ncol > 128) {
     for (int c = t; c < ncol; c += 256) {
       double acc = 0.0;
@@ -683,7 +702,11 @@ __global__ __launch_bounds__(256) void hf_fwd1(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   __shared__ double pro_tmp[256], pro_sum[1024];
   constexpr int D2 = NX * 32, hs = D2 + 4, q4 = D2 / 4;
-  constexpr bool W1_LDS = NX <= 8;
+  // W1 stays in registers (the lane's 32 x D2/8 slice: loaded right after the
+  // prologue's partial sums, in flight through the BN0 finalise and the h0 phase)
+  // where it fits; the LDS tile costs a dependent round trip before the h0 phase
+  constexpr bool W1_REG = NX <= 8;
+  constexpr bool W1_LDS = false;
   const int t = threadIdx.x;
   float* mean = sm;
   float* inv = mean + D2;
@@ -711,6 +734,13 @@ __global__ __launch_bounds__(256) void hf_fwd1(HeadArgs a) {
   const float b1j = a.p.fc1_b[t % HF];
   colsum_prologue(a.part0, a.nrg0, 2 * D2, 2 * D2, pro_tmp, pro_sum);
   NRK_HKT(a, 1, 1);
+  float4 w1r[W1_REG ? D2 / 32 : 1];
+  if constexpr (W1_REG) {
+    const int lane = t & 63, w = t >> 6, i = lane & 31, h = lane >> 5;
+    const float* br = a.p.fc1_w + (int64_t)i * D2 + h * (D2 / 2) + w * (D2 / 8);
+#pragma unroll
+    for (int u = 0; u < D2 / 32; ++u) w1r[u] = *reinterpret_cast<const float4*>(br + 4 * u);
+  }
   bn_finalize_pre(a, pro_sum, D2, mean, inv, a.stat0, a.p.bn0_rm, a.p.bn0_rv, a.p.bn0_nb, blockIdx.x == 0, rsp);
   if constexpr (W1_LDS) {  // W1 (L2-resident: every block reads it)
     float4 wv[NX];
@@ -746,9 +776,12 @@ __global__ __launch_bounds__(256) void hf_fwd1(HeadArgs a) {
     f32x16 acc;
 #pragma unroll
     for (int g = 0; g < 16; ++g) acc[g] = 0.f;
+#pragma unroll
     for (int kk = 0; kk < kw; kk += 4) {
       const float4 av = *reinterpret_cast<const float4*>(ar + kk);
-      const float4 bv = *reinterpret_cast<const float4*>(br + kk);
+      float4 bv;
+      if constexpr (W1_REG) bv = w1r[kk / 4];
+      else bv = *reinterpret_cast<const float4*>(br + kk);
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, bv.x, acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, bv.y, acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, bv.z, acc, 0, 0, 0);
