@@ -39,7 +39,10 @@ __device__ __forceinline__ void list_insert_tie(float (&ls)[N], int (&li)[N], fl
   }
 }
 
-template <int DP, int QT, int M, int WAVES, int TIL, bool SCHED = true>
+// PREF: the next sub-tile's A fragments are read during the current chain (2 x DP / 32
+// fragments live); PREF = false reads each K step's two fragments just before its
+// MFMAs (2 live), for the M = 16 lists that would not fit beside the prefetch
+template <int DP, int QT, int M, int WAVES, int TIL, bool SCHED = true, bool PREF = true>
 __global__ __launch_bounds__(WAVES * 64, 2) void screen16_kernel(
     const uint16_t* __restrict__ qh, const uint16_t* __restrict__ xbh, const float* __restrict__ xmeta, int64_t nq,
     int64_t nb, int64_t chunk, int nch, int nqt, int tstride, float* __restrict__ part_s, int* __restrict__ part_i,
@@ -116,7 +119,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_kernel(
   f32x4 accA[NQ2][2], accB[NQ2][2];
   int64_t baseA = -1, baseB = -1;
   int nvA = 0, nvB = 0;
-  bf16x8 af[2][KS2];
+  bf16x8 af[2][PREF ? KS2 : 1];
   auto mask_rows = [&](f32x4 (&pa)[NQ2][2], int nv) __attribute__((always_inline)) {
 #pragma unroll
     for (int t = 0; t < NQ2; ++t)
@@ -158,7 +161,8 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_kernel(
       }
     }
   };
-  auto sub_tile = [&](auto st_c, int64_t i0, int nvalid, const uint16_t* next_tl) __attribute__((always_inline)) {
+  auto sub_tile = [&](auto st_c, int64_t i0, int nvalid, const uint16_t* next_tl, const uint16_t* cur_tl)
+      __attribute__((always_inline)) {
     constexpr int st = decltype(st_c)::value;
     constexpr int par = st & 1;
     f32x4(&cur)[NQ2][2] = par ? accB : accA;
@@ -171,12 +175,17 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_kernel(
     const f32x4 zero = {};
 #pragma unroll
     for (int s = 0; s < KS2; ++s) {
+      if constexpr (!PREF) {
+        af[0][0] = afrag(cur_tl, 32 * st + q16, s);
+        af[1][0] = afrag(cur_tl, 32 * st + 16 + q16, s);
+      }
 #pragma unroll
       for (int ih = 0; ih < 2; ++ih) {
 #pragma unroll
         for (int t = 0; t < NQ2; ++t)
-          cur[t][ih] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ih][s], qf[t][s], s == 0 ? zero : cur[t][ih], 0, 0, 0);
-        af[ih][s] = afrag(next_tl, nrow + 16 * ih, s);
+          cur[t][ih] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ih][PREF ? s : 0], qf[t][s],
+                                                             s == 0 ? zero : cur[t][ih], 0, 0, 0);
+        if constexpr (PREF) af[ih][s] = afrag(next_tl, nrow + 16 * ih, s);
       }
     }
     float m2[NQ2][2], m[NQ2];
@@ -205,25 +214,34 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_kernel(
     const uint16_t* tl = lds + buf * BUF;
     const int64_t i0 = ibeg + (int64_t)it * TI;
     const int nvalid = (int)((iend - i0) < TI ? (iend - i0) : TI);
-    sub_tile(std::integral_constant<int, 0>{}, i0, nvalid, tl);
+    sub_tile(std::integral_constant<int, 0>{}, i0, nvalid, tl, tl);
     if constexpr (NSUB == 4) {
-      sub_tile(std::integral_constant<int, 1>{}, i0, nvalid, tl);
-      sub_tile(std::integral_constant<int, 2>{}, i0, nvalid, tl);
+      sub_tile(std::integral_constant<int, 1>{}, i0, nvalid, tl, tl);
+      sub_tile(std::integral_constant<int, 2>{}, i0, nvalid, tl, tl);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // tile it+1 landed; every wave is done with buffer buf
-    if (it + 2 < ntiles) issue_tile(it + 2, buf_c);
-    sub_tile(std::integral_constant<int, NSUB - 1>{}, i0, nvalid, lds + (buf ^ 1) * BUF);
+    if constexpr (PREF) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // tile it+1 landed; every wave is done with buffer buf
+      if (it + 2 < ntiles) issue_tile(it + 2, buf_c);
+      sub_tile(std::integral_constant<int, NSUB - 1>{}, i0, nvalid, lds + (buf ^ 1) * BUF, tl);
+    } else {  // the last sub-tile still reads buf: refill it only after
+      sub_tile(std::integral_constant<int, NSUB - 1>{}, i0, nvalid, tl, tl);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // tile it+1 landed; every wave is done with buffer buf
+      if (it + 2 < ntiles) issue_tile(it + 2, buf_c);
+    }
   };
   if (ntiles > 0) {
     issue_tile(0, std::integral_constant<int, 0>{});
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // tile 0 landed
     if (ntiles > 1) issue_tile(1, std::integral_constant<int, 1>{});
+    if constexpr (PREF) {
 #pragma unroll
-    for (int ih = 0; ih < 2; ++ih)
+      for (int ih = 0; ih < 2; ++ih)
 #pragma unroll
-      for (int s = 0; s < KS2; ++s) af[ih][s] = afrag(lds, 16 * ih + q16, s);
+        for (int s = 0; s < KS2; ++s) af[ih][s] = afrag(lds, 16 * ih + q16, s);
+    }
   }
   for (int it = 0; it < ntiles; it += 2) {
     tile_d(it, std::integral_constant<int, 0>{});
