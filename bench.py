@@ -147,7 +147,7 @@ def bench_flat(args, rank, world, dev):
         "stages_ms": {"query_prepare+tau_prepass": float(stage_ms[0]), "screen": screen_ms,
                       "merge_rescore": float(stage_ms[2]), "exact_fallback": float(stage_ms[3])},
         "fallback_queries": fallback[0], "exact_scan_queries": fallback[1],
-        "roofline": {"bound": "mfma", "kernel": _screen_kernel_name(args.metric, args.k, args.d),
+        "roofline": {"bound": "mfma", "kernel": _screen_kernel_name(nq, nb_local, args.d, args.k, metric),
                      "achieved": achieved, "peak": BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / BF16_DENSE_TFLOPS,
                      "traffic": _pmc_traffic(f"nb={args.nb},d={args.d},nq={args.nq},k={args.k},metric={args.metric},"
@@ -205,13 +205,16 @@ def _cpu_flat(args, xq, xb_host, metric, nb=None, d=None, k=None):
                       f"blocks + running top-k, {cores} threads), {dt:.1f} s"}
 
 
-def _screen_kernel_name(metric, k, d):
-    """The flat main-pass kernel libnrk runs for this search (knn_flat.hip):
-    inner product at k <= 8 and padded dim 128 / 256 on the 16x16x32 form
-    unless NRK_SCREEN16=0."""
-    if metric == "ip" and k <= 8 and d in (128, 256) and os.environ.get("NRK_SCREEN16", "1") != "0":
-        return "screen16_kernel (bf16 v_mfma_f32_16x16x32)"
-    return "screen_kernel (bf16 v_mfma_f32_32x32x16)"
+def _screen_kernel_name(nq, nb, d, k, metric):
+    """The flat main-pass kernel libnrk runs for this search, as the library
+    itself plans it (nrk_knn_flat_main_pass)."""
+    import ctypes
+
+    from newsrecommend_amd import _lib
+
+    buf = ctypes.create_string_buffer(256)
+    _lib.check(_lib.load().nrk_knn_flat_main_pass(nq, nb, d, k, metric, buf, 256), "knn_flat_main_pass")
+    return buf.value.decode()
 
 
 def _pmc_traffic(key):
@@ -395,7 +398,7 @@ def bench_n1(args, rank, world, dev, index, xb):
                       "merge_rescore": float(st[2]), "exact_fallback": float(st[3])},
         "fallback_queries": int(index.local.last_fallback.item()),
         "exact_scan_queries": int(index.local.last_exact_scan.item()),
-        "roofline": {"bound": "mfma", "kernel": _screen_kernel_name("ip", k, d) + ", dp 256, 8 waves",
+        "roofline": {"bound": "mfma", "kernel": _screen_kernel_name(nq, index.local.ntotal, d, k, 0),
                      "achieved": achieved, "peak": BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / BF16_DENSE_TFLOPS,
                      "traffic": _pmc_traffic(f"n1:nb={n},d={d},nq={nq},k={k},metric=ip,gpus={world}"),

@@ -62,6 +62,10 @@ int nrk_version(void);
  *            accumulated with atomic max, so zero it before the first prepare
  *            call of an index (prepare may be called on appended slices). */
 int nrk_padded_dim(int32_t d);
+/* Name of the main-pass kernel nrk_knn_flat runs for this shape (for
+ * benchmark records and profiles): writes a NUL-terminated string of at most
+ * len bytes into name.  No reference counterpart (faiss has no such query). */
+int nrk_knn_flat_main_pass(int64_t nq, int64_t nb, int32_t d, int32_t k, int32_t metric, char* name, size_t len);
 int nrk_flat_prepare(const float* xb, int64_t nb, int32_t d, uint16_t* xb_bf16,
                      float* xb_meta, float* stats, void* stream);
 
@@ -193,20 +197,6 @@ int nrk_din_batch(const int64_t* idx, int32_t B, const int32_t* hist_all, const 
  *   U [B][A] = q W1[:, :d]^T + b1 and W1k_bf16 from the gathered q [B][d] f32: */
 int nrk_din_batch_u(const float* q, int32_t B, int32_t d, const float* W1, const float* b1, int32_t A,
                     float* U, void* W1k_bf16, void* stream);
-
-/* Diagnostics: the head-fused backward's per-workgroup phase timestamps
- * (s_memrealtime ticks, 100 MHz; 8 per workgroup: entry, ids landed, first
- * sample landed, loop done, dW1q flushed, exit), recorded while NRK_KTIME=1;
- * then (values 32768 ..) per workgroup and wave 8 values: shader-clock cycles
- * of the pipelined loop's stages {barrier wait, issue, A, B, C} and the
- * iteration count; then (values 294912 ..) the d <= 128 forward's wave 0 of
- * each workgroup: entry, then per sample "rows landed" / "done" (8 values per
- * workgroup, 1024 workgroups).  Copies the first n (<= 303104) values to host
- * memory.  No reference counterpart. */
-int nrk_debug_ktimes(uint64_t* out, int64_t n);
-/* The same for the fast head's kernels (NRK_KTIME=1 at nrk_din_head_train):
- * out [8 kernels][128 blocks][8 slots] of s_memrealtime ticks (100 MHz), n <= 8192. */
-int nrk_debug_head_ktimes(uint64_t* out, int64_t n);
 
 /* DIN attention for re-ranking (DIN.py:166-173: every candidate of a user
  * attends over the same history): pooled [nU*C][d] f32 for candidates whose

@@ -31,6 +31,7 @@ SIGNATURES = {
     "nrk_last_error": (ctypes.c_char_p, []),
     "nrk_version": (ctypes.c_int, []),
     "nrk_padded_dim": (ctypes.c_int, [c_i32]),
+    "nrk_knn_flat_main_pass": (ctypes.c_int, [c_i64, c_i64, c_i32, c_i32, c_i32, ctypes.c_char_p, c_size]),
     "nrk_flat_prepare": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_p, c_p, c_p]),
     "nrk_knn_flat_workspace": (ctypes.c_int, [c_i64, c_i64, c_i32, c_i32, ctypes.POINTER(c_size)]),
     "nrk_knn_flat": (ctypes.c_int, [c_p, c_i64, c_p, c_p, c_p, c_p, c_i64, c_i32, c_i32, c_i32, c_p, c_p, c_p, c_i64,
@@ -64,8 +65,6 @@ SIGNATURES = {
                                               c_f32, c_p, c_i32, c_p, c_size, c_p]),
     "nrk_din_head_ws_views": (ctypes.c_int, [c_i32, c_i32, c_i32, c_p, c_size, c_p, c_p, c_p]),
     "nrk_din_batch_u": (ctypes.c_int, [c_p, c_i32, c_i32, c_p, c_p, c_i32, c_p, c_p, c_p]),
-    "nrk_debug_ktimes": (ctypes.c_int, [c_p, c_i64]),
-    "nrk_debug_head_ktimes": (ctypes.c_int, [c_p, c_i64]),
     "nrk_din_batch": (ctypes.c_int, [c_p, c_i32, c_p, c_p, c_p, c_i64, c_i32, c_p, c_i64, c_i32, c_i32, c_p, c_p,
                                      c_i32, c_p, c_p, c_p, c_p, c_p, c_p]),
     "nrk_din_rerank_attn": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_i32, c_i32, c_p, c_i32, c_i32, c_i32, c_p, c_p,

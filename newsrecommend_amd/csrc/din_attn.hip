@@ -272,18 +272,6 @@ __device__ __forceinline__ const uint16_t* zero_row(int64_t b, int row) {
   return g_zero_rows + (((int)b * 37 + row) & 255) * 256;
 }
 
-// Per-workgroup phase timestamps (s_memrealtime, 100 MHz) of the head-fused
-// backward, for tools/din_step.py --ktime (NRK_KTIME=1): slot 8 b + i
-__device__ uint64_t g_ktime[4096 * 8];
-// per wave: shader-clock cycles spent in each stage of the pipelined loop (tools/din_step.py --ktime)
-__device__ uint64_t g_ktime2[4096 * 8 * 8];
-// forward (din_fwd_wave_kernel), wave 0 of each workgroup: entry, per sample landed / done
-__device__ uint64_t g_ktime3[1024 * 8];
-#define NRK_KT(on, i)                                                                         \
-  do {                                                                                        \
-    if ((on) && threadIdx.x == 0) g_ktime[(size_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
-
 template <int D, int NA, int NBUF>
 __global__ __launch_bounds__(256, 2) void din_fwd_wave_kernel(const uint16_t* __restrict__ table,
                                                                const int32_t* __restrict__ ids, int64_t n_table,
@@ -291,7 +279,7 @@ __global__ __launch_bounds__(256, 2) void din_fwd_wave_kernel(const uint16_t* __
                                                                const uint16_t* __restrict__ W1k,
                                                                const float* __restrict__ w2, int B, int L,
                                                                float* __restrict__ pooled,
-                                                               float* __restrict__ alpha, int kt) {
+                                                               float* __restrict__ alpha) {
   constexpr int CPR = D / 8, KS = D / 16, A = 32 * NA;
   constexpr int DPL = D / 64;         // pooled dims per lane
   constexpr int AP = (A + 63) & ~63;  // U slot padded to whole 64-lane DMA pieces
@@ -359,19 +347,12 @@ __global__ __launch_bounds__(256, 2) void din_fwd_wave_kernel(const uint16_t* __
   int b = blockIdx.x * 4 + wv;
   int32_t c0, c1, n0 = -1, n1 = -1;
   uint64_t cv0, cv1, nv0 = 0, nv1 = 0;
-  int kslot = 1;
-  auto ktf = [&](int j) {  // wave 0 of each workgroup: phase timestamps (tools/din_step.py --ktime)
-    if (kt && wv == 0 && lane == 0 && blockIdx.x < 1024 && j < 8)
-      g_ktime3[(size_t)blockIdx.x * 8 + j] = __builtin_amdgcn_s_memrealtime();
-  };
-  ktf(0);
   load_ids(b, c0, c1, cv0, cv1);
   if (b < B) issue(b, 0, c0, c1, cv0, cv1);
   if (NBUF == 2) load_ids(b + nw, n0, n1, nv0, nv1);
   int sl = 0;
   for (; b < B; b += nw) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this sample's rows (and the next ids) landed
-    ktf(kslot++);
     const int bn = b + nw;
     // this sample: compacted valid rows [0, nv), the padding row nv (zero
     // key, npad = L - nv slots) when nv < L, nct tiles of 32 rows
@@ -397,7 +378,7 @@ __global__ __launch_bounds__(256, 2) void din_fwd_wave_kernel(const uint16_t* __
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       sc[c] = -INFINITY;
-      if (c < nct && !(kt & 2)) {  // (kt & 2: timing diagnostics only, scores skipped)
+      if (c < nct) {
         bf16x8 kf[KS];
         const int row = 32 * c + r;
 #pragma unroll
@@ -465,7 +446,7 @@ __global__ __launch_bounds__(256, 2) void din_fwd_wave_kernel(const uint16_t* __
     float acc2[DPL];
 #pragma unroll
     for (int j = 0; j < DPL; ++j) acc2[j] = 0.f;
-    const int L8 = (kt & 4) ? 0 : (nv + 7) & ~7;  // (kt & 4: timing diagnostics only, pooling skipped)
+    const int L8 = (nv + 7) & ~7;
     for (int row0 = 0; row0 < L8; row0 += 8) {
       const int c = row0 >> 5;
       const float ec = c == 0 ? e[0] : c == 1 ? e[1] : c == 2 ? e[2] : e[3];
@@ -497,7 +478,6 @@ __global__ __launch_bounds__(256, 2) void din_fwd_wave_kernel(const uint16_t* __
     }
     // slot reuse: every LDS read of this sample is done before the DMA after next
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    ktf(kslot++);
     if constexpr (NBUF == 2) {
       sl ^= 1;
     } else {
@@ -1152,7 +1132,6 @@ struct DpSrc {
   const double* sum5;   // {sum dh0 [2D], sum dh0 xhat0 [2D]}
   const float* bn0w;    // fc.0 weight [2D]
   float invB;
-  int ktime;             // record phase timestamps (g_ktime)
 };
 
 template <int D, int LP, int NSLOT>
@@ -1424,8 +1403,6 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8_kernel(
   float* colc = w1p + (FDP ? 32 * D : 0);
   float* dpl = colc + 5 * D;
   static_assert(!FDP || LP <= 64, "FDP: the da1 row takes the second alpha piece");
-  const bool kt = FDP && dps.ktime;
-  NRK_KT(kt, 0);
   if constexpr (FDP) {
     for (int i = tid; i < 32 * D; i += 512) w1p[i] = dps.w1[(size_t)(i / D) * 2 * D + D + i % D];
     for (int c = tid; c < D; c += 512) {
@@ -1533,7 +1510,6 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8_kernel(
 #pragma unroll
   for (int k = 0; k < X; ++k) issue_ids(b + k * grid, k);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  NRK_KT(kt, 1);
 #pragma unroll
   for (int k = 0; k < P; ++k) {
     store_du();  // nothing to store yet: the dummy slot (keeps every group the same size)
@@ -1544,7 +1520,6 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8_kernel(
   for (; b < B; b += grid) {
     // this wave's DMA group of sample b landed; all waves' after the barrier; slot of b - grid is free
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"((P - 1) * N_D) : "memory");
-    if (it == 0) NRK_KT(kt, 2);
     store_du();
     issue_ids(b + (P + X) * grid, e + X < RING ? e + X : e + X - RING);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(X * N_D) : "memory");  // ids of b + P grid landed
@@ -1684,7 +1659,6 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8_kernel(
     b_keep = b;
     sl = sl == NSLOT - 1 ? 0 : sl + 1;
   }
-  NRK_KT(kt, 3);
   store_du();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup exits
   if constexpr (FQ) {
@@ -1693,7 +1667,6 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8_kernel(
     else if (us < nsl) {  // no sample: a zero dW1q partial
       for (int i = lane; i < 32 * D; i += 64) sqs_slab[(size_t)(32 * us) * D + i] = 0.f;
     }
-    NRK_KT(kt, 4);
   }
   // combine the row-group pairs (rg 1 into rg 0, fixed order) through LDS
   float* xch = slot0;  // [4 unit slices][32][D] f32, reused for dW1k then dW1q
@@ -1737,7 +1710,6 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8_kernel(
     }
     if (rg == 0 && us == 0 && lane == 0) slab[(size_t)A * D + A] = tb2 + xs[256];
   }
-  NRK_KT(kt, 5);
 }
 
 // Two-stream form of the head-fused 8-wave backward (FQ + FDP, LP <= 64): the
@@ -1776,8 +1748,6 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8g_kernel(
   float* dpl = ql + 16 * 128;                                                        // [2 groups][D]
   float* w1p = dpl + 2 * D;                                                          // [32][D] fc.1 pooled half
   float* colc = w1p + 32 * D;                                                        // [5][D]
-  const bool kt = dps.ktime;
-  NRK_KT(kt, 0);
   for (int i = tid; i < 32 * D; i += 512) w1p[i] = dps.w1[(size_t)(i / D) * 2 * D + D + i % D];
   for (int c = tid; c < D; c += 512) {
     colc[c] = dps.stat0[D + c];
@@ -1846,7 +1816,6 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8g_kernel(
 #pragma unroll
   for (int k = 0; k < X; ++k) issue_ids(sample(k), k);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  NRK_KT(kt, 1);
 #pragma unroll
   for (int k = 0; k < P; ++k) {
     issue_ids(sample(k + X), (k + X) % RING);
@@ -1856,7 +1825,6 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8g_kernel(
   for (int j = 0; j < n_it; ++j) {
     // this wave's DMA group of sample(j) landed; all waves' after the barrier; slot of sample(j - 1) is free
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"((P - 1) * N_D) : "memory");
-    if (j == 0) NRK_KT(kt, 2);
     issue_ids(sample(j + P + X), e + X < RING ? e + X : e + X - RING);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(X * N_D) : "memory");  // ids of sample(j + P) landed
     issue_data(sample(j + P), sl + P < NSLOT ? sl + P : sl + P - NSLOT, e);
@@ -1998,7 +1966,6 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8g_kernel(
     }
     sl = sl == NSLOT - 1 ? 0 : sl + 1;
   }
-  NRK_KT(kt, 3);
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");  // no LDS-DMA lands after this
   {  // dW1q partial of the staged samples: wave (us, g) owns tiles n = 32 us.., k = 32 (g + 2 jj)..
     const int ns = ns_wg < 16 ? ns_wg : 16;
@@ -2022,7 +1989,6 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8g_kernel(
       }
     }
   }
-  NRK_KT(kt, 4);
   // combine the groups (g 1 into g 0, fixed order) through LDS
   float* xch = reinterpret_cast<float*>(smem);  // [4 unit slices][32][D] f32
   const bool wact = us < nsl;
@@ -2065,365 +2031,6 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8g_kernel(
     }
     if (g == 0 && us == 0 && lane == 0) slab[(size_t)A * D + A] = tb2 + xs[256];
   }
-  NRK_KT(kt, 5);
-}
-
-// Software-pipelined form of the head-fused 8-wave backward (FQ + FDP, LP <= 64).  The
-// serial form runs dpooled, dalpha and the z / dW1k work of one sample between three
-// barriers; here each iteration runs the three stages on three samples behind ONE
-// barrier: A forms dpooled of sample i + 2 (all 512 threads, 4 lanes per column, the
-// thread's W1p column quarter and BN0 column constants in registers), B dalpha of
-// sample i + 1 (double-buffered dpl / dabuf), C the MFMA work of sample i.  Five
-// slots, data groups 4 samples ahead, ids 4 groups before their data.  Same outputs as
-// din_bwd_deep8_kernel<D, LP, *, true, true> up to the summation order of dpooled.
-template <int D, int LP>
-__global__ __launch_bounds__(512, 1) void din_bwd_deep8p_kernel(
-    const uint16_t* __restrict__ table, const int32_t* __restrict__ ids, int64_t n_table, const float* __restrict__ U,
-    const uint16_t* __restrict__ W1k, const float* __restrict__ w2, int B, int L, int A,
-    const float* __restrict__ alpha, float* __restrict__ slabs, const float* __restrict__ q, int dq, DpSrc dps) {
-  constexpr int CPR = D / 8, KS = D / 16, NCT = D / 32, NC = LP / 32;
-  constexpr int NPW = LP * CPR / 512;  // key-image DMA pieces per wave
-  static_assert(LP <= 64 && NPW >= 1, "deep8p: LP <= 64, L D >= 4096");
-  constexpr int N_D = NPW + 2;  // per wave and group: ids, keys, one small piece
-  constexpr int NSLOT = 5, P = 4, X = 4, RING = 5;
-  // slot (floats): pooled [128] | alpha [64], da1 [32..] | U [128] | q [128] | key image [LP][D] bf16
-  constexpr int SLOT_F = 4 * 128 + LP * D / 2;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r = lane & 31;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int us = w & 3, rg = w >> 2;
-  const int nsl = A >> 5;
-  float* slot0 = reinterpret_cast<float*>(smem);
-  int32_t* const ring0 = reinterpret_cast<int32_t*>(slot0 + NSLOT * SLOT_F);
-  int32_t* idring = ring0 + w * RING * 64;                                  // [RING][64] per wave
-  float* dsbuf = reinterpret_cast<float*>(ring0 + 8 * RING * 64) + w * 64;  // [64] per wave
-  float* dabuf = reinterpret_cast<float*>(ring0 + 8 * RING * 64) + 8 * 64;  // [2][64]
-  float* dul = dabuf + 128;                                                 // [16][2 row groups][128]
-  float* ql = dul + 16 * 2 * 128;                                           // [16][128]
-  float* dpl = ql + 16 * 128;                                               // [2][D]
-  NRK_KT(dps.ktime, 0);
-
-  // stage A constants: column c, quarter p of the 32 fc.1 rows (rows 4 jj + p)
-  const bool a_act = tid < 4 * D;
-  const int ac = a_act ? tid >> 2 : 0, ap = tid & 3;
-  float w1r[8];
-#pragma unroll
-  for (int jj = 0; jj < 8; ++jj) w1r[jj] = dps.w1[(size_t)(4 * jj + ap) * 2 * D + D + ac];
-  const float cm = dps.stat0[D + ac], civ = dps.stat0[3 * D + ac], cgw = dps.bn0w[D + ac];
-  const float csb = (float)dps.sum5[D + ac] * dps.invB, csg = (float)dps.sum5[3 * D + ac] * dps.invB;
-
-  WFrag<true, D> wf;
-  const int wu = us < nsl ? us : 0;
-  wf.load(W1k, 32 * wu + r, h);
-  const float w2n = w2[32 * wu + r];
-#pragma unroll
-  for (int s2 = 0; s2 < KS; ++s2) asm volatile("" ::"v"(wf.f[s2]));  // hipcc's waits for these land here
-  asm volatile("" ::"v"(w2n));
-#pragma unroll
-  for (int jj = 0; jj < 8; ++jj) asm volatile("" ::"v"(w1r[jj]));
-  asm volatile("" ::"v"(cm), "v"(civ), "v"(cgw), "v"(csb), "v"(csg));
-  f32x16 dw[NCT];
-#pragma unroll
-  for (int c = 0; c < NCT; ++c)
-#pragma unroll
-    for (int g = 0; g < 16; ++g) dw[c][g] = 0.f;
-  float dw2_acc = 0.f, db2_acc = 0.f, db1_acc = 0.f;
-  float* const sqs_slab = slabs + (size_t)blockIdx.x * slab_floats(A, D) + slab_q_off(A, D);
-
-  auto issue_ids = [&](int64_t b, int e) {
-    const int64_t bc = b < B ? b : 0;
-    const int i = lane < L ? lane : 0;
-    glds4_asm(ids + bc * L + i, lds_u32(idring + e * 64));
-  };
-  // this wave's small piece of [pooled0, pooled1, alpha, da1, u0, u1, q0, q1]: wave-uniform source
-  // array, row stride (= its length) and lane offset
-  const int skind = w >> 1, spart = w & 1;
-  const float* const sbase =
-      skind == 0 ? dps.pooled : skind == 1 ? (spart ? dps.da1 : alpha) : skind == 2 ? U : q;
-  const int sstride = skind == 0 ? D : skind == 1 ? (spart ? 32 : L) : skind == 2 ? A : dq;
-  const int sii = skind == 1 ? lane : spart * 64 + lane;
-  const int soff = sii < sstride ? sii : 0;
-  // per slot 2 bits: 32-row tile c of the sample holds only zero key rows (padding
-  // slots, rows >= L, invalid ids), so its z = U exactly and its dW1k term is zero
-  uint32_t zmask = 0;
-  auto issue_data = [&](int64_t b, int sl, int e) {
-    float* sp = slot0 + sl * SLOT_F;
-    uint16_t* img = reinterpret_cast<uint16_t*>(sp + 4 * 128);
-#pragma unroll
-    for (int k = 0; k < NPW; ++k) {
-      const int u = w + 8 * k;
-      const int p = u * 64 + lane;
-      const int row = p / CPR, pc = p % CPR;
-      const int cc = pc ^ kswz<CPR>(row);
-      const int32_t idv0 = idring[e * 64 + row];
-      const int32_t idr = row < L && b < B ? idv0 : -1;
-      const uint16_t* src = (idr >= 0 && idr < n_table) ? table + (int64_t)idr * D + cc * 8 : zero_row(b, row) + cc * 8;
-      glds16_asm(src, lds_u32(img + u * 64 * 8));
-    }
-    const int64_t bc = b < B ? b : 0;
-    glds4_asm(sbase + bc * sstride + soff, lds_u32(sp + skind * 128 + spart * 64));
-    {
-      const int32_t idl = idring[e * 64 + lane];
-      const uint64_t vm = __ballot(lane < L && b < B && idl >= 0 && idl < n_table);
-      const uint32_t zb = ((uint32_t)vm == 0u ? 1u : 0u) | ((uint32_t)(vm >> 32) == 0u ? 2u : 0u);
-      zmask = (zmask & ~(3u << (2 * sl))) | (zb << (2 * sl));
-    }
-  };
-  // stage A: dpooled[c] = iv g (sum_j da1[j] W1p[j][c] - sb - xhat sg), xhat = (pooled - m) iv
-  auto stage_a = [&](int sl, float* out) {
-    const float* sp = slot0 + sl * SLOT_F;
-    const float* da1s = sp + 192;
-    float acc = 0.f;
-#pragma unroll
-    for (int jj = 0; jj < 8; ++jj) acc = fmaf(da1s[4 * jj + ap], w1r[jj], acc);
-    acc = quad_sum(acc);
-    if (a_act && ap == 0) {
-      const float xhat = (sp[ac] - cm) * civ;
-      out[ac] = civ * cgw * (acc - csb - xhat * csg);
-    }
-  };
-  // stage B: dalpha[row] = dpooled . K[row], wave w owns rows [w R, (w+1) R)
-  auto stage_b = [&](int sl, const float* sdp, float* out) {
-    const unsigned char* img = reinterpret_cast<const unsigned char*>(slot0 + sl * SLOT_F + 512);
-    constexpr int R = LP / 8, LPR = 64 / R, CH = CPR / LPR;
-    const int row = w * R + lane / LPR, part = lane % LPR;
-    float acc = 0.f;
-#pragma unroll
-    for (int ch = 0; ch < CH; ++ch) {
-      const int cc = part * CH + ch;
-      const uint4 kv = *reinterpret_cast<const uint4*>(img + row * 2 * D + 16 * (cc ^ kswz<CPR>(row)));
-      const float4 d0 = *reinterpret_cast<const float4*>(sdp + 8 * cc);
-      const float4 d1 = *reinterpret_cast<const float4*>(sdp + 8 * cc + 4);
-      acc = fmaf(d0.x, __uint_as_float(kv.x << 16), acc);
-      acc = fmaf(d0.y, __uint_as_float(kv.x & 0xFFFF0000u), acc);
-      acc = fmaf(d0.z, __uint_as_float(kv.y << 16), acc);
-      acc = fmaf(d0.w, __uint_as_float(kv.y & 0xFFFF0000u), acc);
-      acc = fmaf(d1.x, __uint_as_float(kv.z << 16), acc);
-      acc = fmaf(d1.y, __uint_as_float(kv.z & 0xFFFF0000u), acc);
-      acc = fmaf(d1.z, __uint_as_float(kv.w << 16), acc);
-      acc = fmaf(d1.w, __uint_as_float(kv.w & 0xFFFF0000u), acc);
-    }
-    acc = group_sum<LPR>(acc);
-    if (part == 0) out[row] = acc;
-  };
-
-  const int64_t grid = gridDim.x;
-  const int64_t b0 = blockIdx.x;
-  const int n_it = b0 < B ? (int)((B - b0 + grid - 1) / grid) : 0;
-#pragma unroll
-  for (int k = 0; k < X; ++k) issue_ids(b0 + k * grid, k);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  NRK_KT(dps.ktime, 1);
-#pragma unroll
-  for (int k = 0; k < P; ++k) {
-    issue_ids(b0 + (k + X) * grid, (k + X) % RING);
-    issue_data(b0 + k * grid, k, k);
-  }
-  // groups of samples 0, 1 landed (all waves' after the barrier)
-  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((P - 2) * N_D) : "memory");
-  stage_a(0, dpl);
-  stage_a(1, dpl + D);
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  stage_b(0, dpl, dabuf);
-  NRK_KT(dps.ktime, 2);
-
-  int sl = 0;                  // slot of sample i
-  uint64_t kacc[5] = {0, 0, 0, 0, 0}, kprev = dps.ktime ? __builtin_amdgcn_s_memtime() : 0;
-  auto kts = [&](int j) {
-    if (dps.ktime) {
-      const uint64_t now = __builtin_amdgcn_s_memtime();
-      kacc[j] += now - kprev;
-      kprev = now;
-    }
-  };
-  for (int i = 0; i < n_it; ++i) {
-    // group of sample i + 2 landed; stage results of iteration i - 1 visible; slot of i - 1 free
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"((P - 3) * N_D) : "memory");
-    kts(0);
-    // diagnostics (NRK_KTIME_DIAG, timing runs only): 2 = no DMA issue, 4 = no stage A / B, 8 = no stage C
-    const int diag = dps.ktime >> 1;
-    if (!(diag & 1)) {
-      const int e_new = (i + P + X) % RING, e_dat = (i + P) % RING;
-      issue_ids(b0 + (int64_t)(i + P + X) * grid, e_new);
-      issue_data(b0 + (int64_t)(i + P) * grid, sl == 0 ? NSLOT - 1 : sl - 1, e_dat);
-    }
-    kts(1);
-    const int sl1 = sl + 1 < NSLOT ? sl + 1 : sl + 1 - NSLOT, sl2 = sl + 2 < NSLOT ? sl + 2 : sl + 2 - NSLOT;
-    if (!(diag & 2)) stage_a(sl2, dpl + (i & 1) * D);
-    if (dps.ktime) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    kts(2);
-    if (!(diag & 2)) stage_b(sl1, dpl + ((i + 1) & 1) * D, dabuf + ((i + 1) & 1) * 64);
-    if (dps.ktime) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    kts(3);
-
-    // stage C: sample i
-    const float* sp = slot0 + sl * SLOT_F;
-    const float* sal = sp + 128;
-    const float* sU = sp + 256;
-    const float* dab = dabuf + (i & 1) * 64;
-    const unsigned char* img = reinterpret_cast<const unsigned char*>(sp + 512);
-    float du = 0.f;
-    if (us < nsl && rg < NC && !(diag & 4)) {
-      const float un = sU[32 * us + r];
-      float da[NC];
-#pragma unroll
-      for (int c = 0; c < NC; ++c) da[c] = dab[32 * c + r];
-      float t = 0.f;
-#pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        const int row = 32 * c + r;
-        t += (row < L && h == 0) ? sal[row] * da[c] : 0.f;
-      }
-      const float cdot = wave_sum_fast(t);
-#pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        const int row = 32 * c + r;
-        if (h == 0 && (c & 1) == rg) {
-          const float ds = row < L ? sal[row] * (da[c] - cdot) : 0.f;
-          dsbuf[row] = ds;
-          if (us == 0) db2_acc += ds;
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        if ((c & 1) != rg) continue;
-        const bool kz = (zmask >> (2 * sl + c)) & 1u;  // zero keys: z = U, no dW1k term (bit-exact)
-        f32x16 acc;
-#pragma unroll
-        for (int g = 0; g < 16; ++g) acc[g] = un;
-        if (!kz) {
-#pragma unroll
-          for (int s2 = 0; s2 < KS; ++s2) {
-            const bf16x8 kf = *reinterpret_cast<const bf16x8*>(img + KImg<true, D>::off(32 * c + r, 16 * s2 + 8 * h));
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, wf.f[s2], acc, 0, 0, 0);
-          }
-        }
-        f32x16 dz;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float4 d4 = *reinterpret_cast<const float4*>(dsbuf + 32 * c + 8 * j + 4 * h);
-          const float dsv[4] = {d4.x, d4.y, d4.z, d4.w};
-#pragma unroll
-          for (int i2 = 0; i2 < 4; ++i2) {
-            const int g = 4 * j + i2;
-            const float z = acc[g];
-            dw2_acc = fmaf(dsv[i2], fmaxf(z, 0.f), dw2_acc);
-            const float v = z > 0.f ? dsv[i2] * w2n : 0.f;
-            dz[g] = v;
-            du += v;
-          }
-        }
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          if (kz) break;
-          bf16x8 af;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {  // v_cvt_pk_bf16_f32 (round to nearest even)
-            const bf16x2_hw pk = {(__bf16)dz[8 * s + 2 * j], (__bf16)dz[8 * s + 2 * j + 1]};
-            const uint32_t u = __builtin_bit_cast(uint32_t, pk);
-            af[2 * j] = (short)(u & 0xFFFF);
-            af[2 * j + 1] = (short)(u >> 16);
-          }
-          const int grp = lane >> 4, i16 = lane & 15;
-          const int rowq = 32 * c + 16 * s + 4 * h + (i16 >> 2);
-#pragma unroll
-          for (int cc = 0; cc < NCT; ++cc) {
-            const int col = 32 * cc + 16 * (grp & 1) + 4 * (i16 & 3);
-            typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
-            const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(img + KImg<true, D>::off(rowq, col)));
-            const bf16x4 hi =
-                __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(img + KImg<true, D>::off(rowq + 8, col)));
-            const bf16x8 bfr = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-            dw[cc] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, dw[cc], 0, 0, 0);
-          }
-        }
-      }
-      du = half_swap_sum(du);
-      db1_acc += du;
-    }
-    // stage this sample's dU rows (both row groups) and query row (host: <= 16 samples per workgroup)
-    if (h == 0 && us < nsl && i < 16) dul[i * 256 + rg * 128 + 32 * us + r] = du;
-    if (lane < 16 && i < 16) ql[i * 128 + 16 * w + lane] = sp[384 + 16 * w + lane];
-    sl = sl1;
-    if (dps.ktime) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    kts(4);
-  }
-  if (dps.ktime && lane == 0) {
-    uint64_t* kd = g_ktime2 + ((size_t)blockIdx.x * 8 + w) * 8;
-#pragma unroll
-    for (int j = 0; j < 5; ++j) kd[j] = kacc[j];
-    kd[5] = (uint64_t)n_it;
-  }
-  NRK_KT(dps.ktime, 3);
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");  // no LDS-DMA lands after this
-  // dW1q partial of the staged samples: wave (us, rg) owns tiles n = 32 us.., k = 32 (rg + 2 j)..
-  if (us < nsl) {
-    const int ns = n_it < 16 ? n_it : 16;
-#pragma unroll
-    for (int j = 0; j < (NCT + 1) / 2; ++j) {
-      const int tk = rg + 2 * j;
-      if (tk >= NCT) continue;
-      f32x16 acc;
-#pragma unroll
-      for (int g = 0; g < 16; ++g) acc[g] = 0.f;
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
-        const int sm = 2 * kk + h;
-        const float av = sm < ns ? dul[sm * 256 + 32 * us + r] + dul[sm * 256 + 128 + 32 * us + r] : 0.f;
-        const float bv = sm < ns ? ql[sm * 128 + 32 * tk + r] : 0.f;
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
-      }
-#pragma unroll
-      for (int g = 0; g < 16; ++g) sqs_slab[(size_t)(32 * us + acc_row(g, h)) * D + 32 * tk + r] = acc[g];
-    }
-  }
-  NRK_KT(dps.ktime, 4);
-  // combine the row-group pairs (rg 1 into rg 0, fixed order) through LDS
-  float* xch = slot0;  // [4 unit slices][32][D] f32
-  const bool act = us < nsl;
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  if (rg == 1 && act) {
-#pragma unroll
-    for (int c = 0; c < NCT; ++c)
-#pragma unroll
-      for (int g = 0; g < 16; ++g) xch[(size_t)(32 * us + acc_row(g, h)) * D + 32 * c + r] = dw[c][g];
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  if (rg == 0 && act) {
-#pragma unroll
-    for (int c = 0; c < NCT; ++c)
-#pragma unroll
-      for (int g = 0; g < 16; ++g) dw[c][g] += xch[(size_t)(32 * us + acc_row(g, h)) * D + 32 * c + r];
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  float* xs = slot0 + 4 * 32 * D;  // [4][32] dw2, [4][32] db1, [1] db2 of the rg = 1 waves
-  {
-    const float t2 = dw2_acc + __shfl_xor(dw2_acc, 32, 64);
-    const float tb2 = wave_sum(db2_acc);
-    if (rg == 1 && act && h == 0) {
-      xs[32 * us + r] = t2;
-      xs[128 + 32 * us + r] = db1_acc;
-    }
-    if (rg == 1 && us == 0 && lane == 0) xs[256] = tb2;
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    float* slab = slabs + (size_t)blockIdx.x * slab_floats(A, D);
-    if (rg == 0 && act) {
-      float* sqs = slab + slab_q_off(A, D);
-#pragma unroll
-      for (int c = 0; c < NCT; ++c)
-#pragma unroll
-        for (int g = 0; g < 16; ++g) slab[(size_t)(32 * us + acc_row(g, h)) * D + 32 * c + r] = dw[c][g];
-      if (h == 0) {
-        slab[(size_t)A * D + 32 * us + r] = t2 + xs[32 * us + r];
-        sqs[(size_t)A * D + 32 * us + r] = db1_acc + xs[128 + 32 * us + r];
-      }
-    }
-    if (rg == 0 && us == 0 && lane == 0) slab[(size_t)A * D + A] = tb2 + xs[256];
-  }
-  NRK_KT(dps.ktime, 5);
 }
 
 // D = 256 variant of the 8-wave backward (the reference's training width):
@@ -3133,10 +2740,8 @@ extern "C" int nrk_din_attn_fwd(const void* keys, const int32_t* hist_ids, int64
   }
   // d = 128: a wave pair per sample (each wave half the unit tiles: 168 VGPRs, three
   // workgroups = 12 waves per CU): 153.4 -> 151.5 us per train step against one wave
-  // per sample at 8 waves per CU (profiles/r03_din_fwd_pair_ab.log).  NRK_DIN_FWD_PAIR=0:
-  // the wave-per-sample kernel (A/B hook; it carries the --ktime stamps)
-  const char* fp_env = getenv("NRK_DIN_FWD_PAIR");
-  if (wave_ok && d == 128 && !(fp_env && *fp_env == '0')) {
+  // per sample at 8 waves per CU (profiles/r03_din_fwd_pair_ab.log)
+  if (wave_ok && d == 128) {
     const size_t psm = pair_sm;
     NRK_CHECK_ARG(3 * psm <= 160 * 1024, "din_fwd: L=%d d=%d needs %zu B LDS (pair)", L, d, psm);
     int grid = (int)cdiv(B, 2);
@@ -3154,7 +2759,7 @@ extern "C" int nrk_din_attn_fwd(const void* keys, const int32_t* hist_ids, int64
     NRK_CHECK_LAUNCH("din_fwd_pair_kernel");
     return NRK_OK;
   }
-  if (wave_ok) {
+  if (wave_ok) {  // d = 64: one wave per sample
     const int Lp = (L + 31) & ~31;
     const size_t AP = (size_t)((A + 63) & ~63);
     const size_t slot = AP * 4 + (size_t)Lp * d * 2;
@@ -3166,20 +2771,12 @@ extern "C" int nrk_din_attn_fwd(const void* keys, const int32_t* hist_ids, int64
     const uint16_t* tb = static_cast<const uint16_t*>(keys);
     const uint16_t* wk = static_cast<const uint16_t*>(W1k);
     hipStream_t st = (hipStream_t)stream;
-    const char* kte = getenv("NRK_KTIME");
-    const char* kfd = getenv("NRK_KTIME_FWD_DIAG");
-    const int kt = (kte && *kte == '1') ? 1 | ((kfd ? atoi(kfd) : 0) & 6) : 0;
-#define NRK_FWD_WAVE(DD, NN)                                                                                        \
-  hipLaunchKernelGGL((din_fwd_wave_kernel<DD, NN, 1>), dim3(grid), dim3(256), wsm, st, tb, hist_ids, n_table, U, wk, \
-                     w2, B, L, pooled, alpha, kt)
     const int na = A / 32;
-    if (d == 128) {
-      if (na == 1) NRK_FWD_WAVE(128, 1); else if (na == 2) NRK_FWD_WAVE(128, 2);
-      else if (na == 3) NRK_FWD_WAVE(128, 3); else NRK_FWD_WAVE(128, 4);
-    } else {
-      if (na == 1) NRK_FWD_WAVE(64, 1); else if (na == 2) NRK_FWD_WAVE(64, 2);
-      else if (na == 3) NRK_FWD_WAVE(64, 3); else NRK_FWD_WAVE(64, 4);
-    }
+#define NRK_FWD_WAVE(NN)                                                                                            \
+  hipLaunchKernelGGL((din_fwd_wave_kernel<64, NN, 1>), dim3(grid), dim3(256), wsm, st, tb, hist_ids, n_table, U, wk,  \
+                     w2, B, L, pooled, alpha)
+    if (na == 1) NRK_FWD_WAVE(1); else if (na == 2) NRK_FWD_WAVE(2); else if (na == 3) NRK_FWD_WAVE(3);
+    else NRK_FWD_WAVE(4);
 #undef NRK_FWD_WAVE
   } else {
     NRK_DIN_DISPATCH(bf, d, {
@@ -3361,33 +2958,21 @@ static int bwd_params_impl(const void* table, const int32_t* hist_ids, int64_t n
     const bool w8 = LPk * d >= 4096;  // >= 8 key-image pieces: one per wave
     size_t dsm = (size_t)(nslot * (4 * 128 + LPk * d / 2) + 4 * 4 * 128 + 5 * 128) * 4;
     // deep8: 3 slots (2 samples in flight; 4 and 5 measured no faster, profiles/r03_din_ab.log)
-    // NRK_DEEP8_NSLOT=4 (A/B hook, head-fused form only): one more sample in flight
-    const char* ns_env = getenv("NRK_DEEP8_NSLOT");
-    const int nslot8 = (dps && ns_env && *ns_env == '4') ? 4 : 3;
-    // dW1q folded into the 8-wave kernel (16 samples' dU / q rows in LDS) instead of the
-    // dU stores + din_dwq_kernel; NRK_DEEP8_FOLDQ=0: the old form (A/B hook)
-    const char* fq_env = getenv("NRK_DEEP8_FOLDQ");
-    const bool fold_q = !(fq_env && *fq_env == '0') && cdiv(B, grid) <= 16;
+    constexpr int nslot8 = 3;
+    // dW1q folded into the 8-wave kernel (16 samples' dU / q rows in LDS) while a
+    // workgroup holds at most 16 samples; beyond, dU rows + din_dwq_kernel
+    const bool fold_q = cdiv(B, grid) <= 16;
     if (w8) {
-      const int ring8 = (nslot8 - 1 > 3 ? nslot8 - 1 : 3) + 1;
+      const int ring8 = 4;
       dsm = (size_t)(nslot8 * (4 * 128 + LPk * d / 2) + 8 * ring8 * 128 + 9 * 128 + (fold_q ? 48 * 128 : 0) +
                      (dps ? 32 * d + 6 * d : 0)) * 4;
       const size_t xneed = ((size_t)4 * 32 * d + 257) * 4;  // pair-combine exchange area (reuses the slots)
       if (dsm < xneed) dsm = xneed;
     }
-    // software-pipelined head-fused form (one barrier per sample); NRK_DEEP8_PIPE=1 (A/B hook)
-    const char* pp_env = getenv("NRK_DEEP8_PIPE");
-    const bool pipe8 = dps && w8 && fold_q && LPk <= 64 && (pp_env && *pp_env == '1');
-    if (pipe8) {
-      dsm = (size_t)(5 * (4 * 128 + LPk * d / 2) + 8 * 5 * 64 + 8 * 64 + 128 + 16 * 256 + 16 * 128 + 2 * d) * 4;
-      const size_t xneed = ((size_t)4 * 32 * d + 257) * 4;
-      if (dsm < xneed) dsm = xneed;
-    }
-    // two-stream form (two groups of four waves, one sample each per iteration): 151.5 ->
-    // 148.1 us per train step at B = 4096 (profiles/r03_deep8_groups_ab.log).
-    // NRK_DEEP8_GROUPS=0: the row-group-split form (A/B hook)
-    const char* gr_env = getenv("NRK_DEEP8_GROUPS");
-    const bool group8 = !pipe8 && dps && w8 && fold_q && LPk <= 64 && LPk * d >= 2048 * 2 && !(gr_env && *gr_env == '0');
+    // head-fused with dW1q folded: the two-stream form (two groups of four waves, one
+    // sample each per iteration): 151.5 -> 148.1 us per train step at B = 4096 against
+    // the row-group split (profiles/r03_deep8_groups_ab.log)
+    const bool group8 = dps && w8 && fold_q && LPk <= 64;
     if (group8) {
       dsm = (size_t)(2 * 3 * (4 * 128 + LPk * d / 2) + 8 * 4 * 64 + 8 * 64 + 2 * 64 + 2 * 16 * 128 + 2 * d + 32 * d +
                      5 * d) * 4;
@@ -3400,16 +2985,9 @@ static int bwd_params_impl(const void* table, const int32_t* hist_ids, int64_t n
                      n_table, U, wk, w2, B, L, A, dpooled, alpha, slabs, q, d, dUp, dmy, dpv)
 #define NRK_BWD_DEEP8_FDP(DD, LL)                                                                                   \
   do {                                                                                                              \
-    if (pipe8)                                                                                                      \
-      hipLaunchKernelGGL((din_bwd_deep8p_kernel<DD, LL>), dim3(grid), dim3(512), dsm, st, tb, hist_ids, n_table, U, wk, \
-                         w2, B, L, A, alpha, slabs, q, d, dpv);                                                      \
-    else if (group8)                                                                                                \
+    if (group8)                                                                                                     \
       hipLaunchKernelGGL((din_bwd_deep8g_kernel<DD, LL>), dim3(grid), dim3(512), dsm, st, tb, hist_ids, n_table, U, wk, \
                          w2, B, L, A, alpha, slabs, q, d, dpv);                                                      \
-    else if (fold_q && nslot8 == 4)                                                                                 \
-      hipLaunchKernelGGL((din_bwd_deep8_kernel<DD, LL, 4, true, true>), dim3(grid), dim3(512), dsm, st, tb,         \
-                         hist_ids, n_table, U, wk, w2, B, L, A, dpooled, alpha, slabs, q, d, dUp, dmy, dpv);          \
-    else if (fold_q) NRK_BWD_DEEP8_V(DD, LL, true, true);                                                           \
     else NRK_BWD_DEEP8_V(DD, LL, false, true);                                                                      \
   } while (0)
 #define NRK_BWD_DEEP(DD, LL)                                                                                          \
@@ -3492,27 +3070,8 @@ extern "C" int nrk_din_attn_bwd_params_head(const void* table, const int32_t* hi
   dps.w1 = hp->fc1_w;
   dps.bn0w = hp->bn0_w;
   dps.invB = 1.f / (float)B;
-  {
-    const char* kt = getenv("NRK_KTIME");
-    const char* kd = getenv("NRK_KTIME_DIAG");
-    dps.ktime = (kt && *kt == '1' && cdiv(B, 256) <= 4096) ? 1 | ((kd ? atoi(kd) : 0) & 14) : 0;
-  }
   return bwd_params_impl(table, hist_ids, n_table, dtype, q, U, W1k, w2, B, L, d, A, nullptr, alpha, gW1, gb1, gw2,
                          gb2, nullptr, ws, ws_bytes, stream, &dps, n_flat, norm_part);
-}
-
-extern "C" int nrk_debug_ktimes(uint64_t* out, int64_t n) {
-  NRK_CHECK_ARG(out && n >= 0, "debug_ktimes: bad arguments");
-  const int64_t e1 = 4096 * 8, e2 = e1 + 4096 * 8 * 8, e3 = e2 + 1024 * 8;
-  NRK_CHECK_ARG(n <= e3, "debug_ktimes: n %lld > %lld", (long long)n, (long long)e3);
-  const int64_t n1 = n < e1 ? n : e1, n2 = n < e2 ? n - n1 : e2 - e1, n3 = n - n1 - n2;
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(nrk::g_ktime), (size_t)n1 * 8, 0, hipMemcpyDeviceToHost) != hipSuccess ||
-      (n2 > 0 && hipMemcpyFromSymbol(out + e1, HIP_SYMBOL(nrk::g_ktime2), (size_t)n2 * 8, 0, hipMemcpyDeviceToHost) !=
-                     hipSuccess) ||
-      (n3 > 0 && hipMemcpyFromSymbol(out + e2, HIP_SYMBOL(nrk::g_ktime3), (size_t)n3 * 8, 0, hipMemcpyDeviceToHost) !=
-                     hipSuccess))
-    return fail(NRK_ELAUNCH, "debug_ktimes: copy failed");
-  return NRK_OK;
 }
 
 extern "C" int nrk_din_batch_u(const float* q, int32_t B, int32_t d, const float* W1, const float* b1, int32_t A,

@@ -51,19 +51,7 @@ struct HeadArgs {
   float* dpooled;
   int fast;  // F == 32 fast path: statistics reduced in each consumer's prologue
   int nrg0;  // row groups of hf_stats0
-  int ktime; // diagnostic phase stamps (NRK_KTIME=1, g_hkt)
 };
-
-// Diagnostic phase stamps of the fast head's kernels (NRK_KTIME=1, read by
-// nrk_debug_head_ktimes; tools/din_step.py --hktime): g_hkt[kernel][block][slot]
-// = s_memrealtime (100 MHz) from thread 0 of blocks < 128.  Nothing reads
-// them back on the device; results are unaffected.
-__device__ uint64_t g_hkt[8 * 128 * 8];
-#define NRK_HKT(a, k, i)                                                                          \
-  do {                                                                                            \
-    if ((a).ktime && threadIdx.x == 0 && blockIdx.x < 128)                                        \
-      g_hkt[((k) * 128 + blockIdx.x) * 8 + (i)] = __builtin_amdgcn_s_memrealtime();              \
-  } while (0)
 
 __device__ __forceinline__ float hx(const HeadArgs& a, int64_t r, int c) {
   return c < a.d ? a.q[r * a.d + c] : a.pooled[r * a.ld + (c - a.d)];
@@ -651,11 +639,11 @@ __global__ void head_grads(HeadArgs a) {
 // (fixed block order, fp64) instead of by a separate colsum launch, and the
 // two 2d-wide layers run on f32 MFMA (v_mfma_f32_32x32x2_f32: exact f32
 // products, f32 accumulation):
-//   hf_stats0  BN0 partial sums over 8 row groups x 32-column groups
+//   hf_stats0  BN0 partial sums over 16 row groups x 32-column groups
 //   hf_fwd1    BN0 -> Linear(2d,32) (MFMA, K split over the 4 waves) -> ReLU -> Dropout
 //   head_fwd2 / head_fwd3 / head_bwd2 (a.fast: prologue sums)
 //   hf_bwd1    BN1 bwd -> da1;  G = da1^T xhat0 per block (MFMA), sum da1
-//   hf_reduce  G, sum da1 and the small layers' partials -> every head gradient;
+//   hf_reduce_c1  G, sum da1 and the small layers' partials -> every head gradient;
 //              BN0's backward sums follow from G: sum_r dh0 = W1^T sum da1,
 //              sum_r dh0 xhat0 = sum_j W1[j] G[j]  (dh0 = da1 W1, never stored)
 //   hf_bwd0    dh0 (pooled half) = da1 W1 (MFMA) -> BN0 bwd -> dpooled
@@ -664,7 +652,6 @@ constexpr int HF = 32;  // fc_units of the fast path
 __device__ __forceinline__ int hacc_row(int g, int h) { return (g & 3) + 8 * (g >> 2) + 4 * h; }
 
 __global__ __launch_bounds__(256) void hf_stats0(HeadArgs a) {
-  NRK_HKT(a, 0, 0);
   const int ncg = a.D2 / 32;
   const int cg = blockIdx.x % ncg, rg = blockIdx.x / ncg;
   const int cl = threadIdx.x & 31, ph = threadIdx.x >> 5;
@@ -678,7 +665,6 @@ __global__ __launch_bounds__(256) void hf_stats0(HeadArgs a) {
     sv += v;
     ssv += v * v;
   }
-  NRK_HKT(a, 0, 1);
   __shared__ double red[2][8][32];
   red[0][ph][cl] = sv;
   red[1][ph][cl] = ssv;
@@ -689,14 +675,14 @@ __global__ __launch_bounds__(256) void hf_stats0(HeadArgs a) {
     for (int q = 0; q < 8; ++q) t += red[wch][q][cl];
     a.part0[(int64_t)rg * 2 * a.D2 + wch * a.D2 + c] = t;
   }
-  NRK_HKT(a, 0, 7);
 }
 
-// LDS (floats): mean/inv [D2] x 2 | h0 [32][D2+4] | W1 [32][D2+4] | red [4][32][32] | d1 [32][33]
+// LDS (floats): mean/inv [D2] x 2 | h0 [32][D2+4] | red [4][32][32] | d1 [32][33]
 // NX = D2 / 32: float4 of the block's x rows per thread (issued before the
-// prologue's partial sums, so the two memory round trips overlap).  D2 > 256
-// (d = 256, the reference's width): the W1 tile would not fit next to h0, so
-// the MFMA reads W1 rows from global memory (L2-resident, every block reads it)
+// prologue's partial sums, so the two memory round trips overlap).  W1 (fc.1
+// weight, L2-resident: every block reads it) goes to registers for D2 <= 256; for
+// D2 > 256 (d = 256, the reference's width) the MFMA reads its rows from global
+// memory.  (An LDS tile of W1 cost a dependent round trip before the h0 phase.)
 template <int NX>
 __global__ __launch_bounds__(256) void hf_fwd1(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -706,15 +692,12 @@ __global__ __launch_bounds__(256) void hf_fwd1(HeadArgs a) {
   // prologue's partial sums, in flight through the BN0 finalise and the h0 phase)
   // where it fits; the LDS tile costs a dependent round trip before the h0 phase
   constexpr bool W1_REG = NX <= 8;
-  constexpr bool W1_LDS = false;
   const int t = threadIdx.x;
   float* mean = sm;
   float* inv = mean + D2;
   float* h0 = inv + D2;
-  float* w1 = h0 + HR * hs;
-  float* red = w1 + (W1_LDS ? HF * hs : 0);
+  float* red = h0 + HR * hs;
   float* d1 = red + 4 * HR * HF;
-  NRK_HKT(a, 1, 0);
   const int64_t r0 = (int64_t)blockIdx.x * HR;
   float4 xv[NX];
 #pragma unroll
@@ -733,7 +716,6 @@ __global__ __launch_bounds__(256) void hf_fwd1(HeadArgs a) {
   const float4 be0 = G0_PRE ? *reinterpret_cast<const float4*>(a.p.bn0_b + 4 * (t % q4)) : float4{};
   const float b1j = a.p.fc1_b[t % HF];
   colsum_prologue(a.part0, a.nrg0, 2 * D2, 2 * D2, pro_tmp, pro_sum);
-  NRK_HKT(a, 1, 1);
   float4 w1r[W1_REG ? D2 / 32 : 1];
   if constexpr (W1_REG) {
     const int lane = t & 63, w = t >> 6, i = lane & 31, h = lane >> 5;
@@ -742,18 +724,7 @@ __global__ __launch_bounds__(256) void hf_fwd1(HeadArgs a) {
     for (int u = 0; u < D2 / 32; ++u) w1r[u] = *reinterpret_cast<const float4*>(br + 4 * u);
   }
   bn_finalize_pre(a, pro_sum, D2, mean, inv, a.stat0, a.p.bn0_rm, a.p.bn0_rv, a.p.bn0_nb, blockIdx.x == 0, rsp);
-  if constexpr (W1_LDS) {  // W1 (L2-resident: every block reads it)
-    float4 wv[NX];
-#pragma unroll
-    for (int u = 0; u < NX; ++u) wv[u] = *reinterpret_cast<const float4*>(a.p.fc1_w + 4 * (t + u * 256));
-#pragma unroll
-    for (int u = 0; u < NX; ++u) {
-      const int e = t + u * 256;
-      *reinterpret_cast<float4*>(w1 + (e / q4) * hs + 4 * (e % q4)) = wv[u];
-    }
-  }
   __syncthreads();  // mean / inv published
-  NRK_HKT(a, 1, 2);
 #pragma unroll
   for (int u = 0; u < NX; ++u) {
     const int e = t + u * 256, row = e / q4, c = 4 * (e % q4);
@@ -767,12 +738,11 @@ __global__ __launch_bounds__(256) void hf_fwd1(HeadArgs a) {
     *reinterpret_cast<float4*>(h0 + row * hs + c) = x;
   }
   __syncthreads();
-  NRK_HKT(a, 1, 3);
   {  // a1 = h0 W1^T: lane half h covers k in [h D2/2, (h+1) D2/2), wave w a quarter of that
     const int lane = t & 63, w = t >> 6, i = lane & 31, h = lane >> 5;
     constexpr int kw = D2 / 8;
     const float* ar = h0 + i * hs + h * (D2 / 2) + w * kw;
-    const float* br = (W1_LDS ? w1 + i * hs : a.p.fc1_w + (int64_t)i * D2) + h * (D2 / 2) + w * kw;
+    const float* br = a.p.fc1_w + (int64_t)i * D2 + h * (D2 / 2) + w * kw;
     f32x16 acc;
 #pragma unroll
     for (int g = 0; g < 16; ++g) acc[g] = 0.f;
@@ -791,7 +761,6 @@ __global__ __launch_bounds__(256) void hf_fwd1(HeadArgs a) {
     for (int g = 0; g < 16; ++g) red[w * HR * HF + hacc_row(g, h) * HF + i] = acc[g];
   }
   __syncthreads();
-  NRK_HKT(a, 1, 4);
   for (int o = t; o < HR * HF; o += 256) {
     const int r = o / HF, j = o % HF;
     const float v = ((red[o] + red[HR * HF + o]) + (red[2 * HR * HF + o] + red[3 * HR * HF + o])) + b1j;
@@ -804,7 +773,6 @@ __global__ __launch_bounds__(256) void hf_fwd1(HeadArgs a) {
     }
   }
   __syncthreads();
-  NRK_HKT(a, 1, 5);
   {  // BN1 partial sums: {sum, sum sq} x 32 columns x 4 row groups of 8, combined in a fixed order
     __shared__ double p1[4][2 * HF];
     const int o = t & 63, rq = t >> 6, j = o % HF, sq = o / HF;
@@ -818,7 +786,6 @@ __global__ __launch_bounds__(256) void hf_fwd1(HeadArgs a) {
     __syncthreads();
     if (t < 2 * HF) a.part1[(int64_t)blockIdx.x * 2 * HF + t] = (p1[0][t] + p1[1][t]) + (p1[2][t] + p1[3][t]);
   }
-  NRK_HKT(a, 1, 7);
 }
 
 // LDS (floats): m0/i0 [DC] x 2 | xhat0 [32][DC+4] | da1 [32][33] | m1/i1/sb1/sg1 [32] x 4 | gT [DC][36]
@@ -841,7 +808,6 @@ __global__ __launch_bounds__(256) void hf_bwd1(HeadArgs a) {
   float* i1 = m1 + HF;
   float* sb1 = i1 + HF;
   float* sg1 = sb1 + HF;
-  NRK_HKT(a, 5, 0);
   const int64_t r0 = (int64_t)rb * HR;
   const int s4 = 2 * HF + a.F2 * HF + a.F2;
   constexpr int q4 = DC / 4;
@@ -873,7 +839,6 @@ __global__ __launch_bounds__(256) void hf_bwd1(HeadArgs a) {
     sb1[t] = (float)pro_sum[t];
     sg1[t] = (float)pro_sum[HF + t];
   }
-  NRK_HKT(a, 5, 1);
   __syncthreads();
 #pragma unroll
   for (int u = 0; u < NX / CS; ++u) {
@@ -899,7 +864,6 @@ __global__ __launch_bounds__(256) void hf_bwd1(HeadArgs a) {
     }
   }
   __syncthreads();
-  NRK_HKT(a, 5, 2);
   {  // G (32 x DC) = da1^T xhat0 over the block's 32 rows; wave w: column tiles w, w+4, ...
      // stored column-major per row block ([D2][32]: a column's 32 entries are one 128-B
      // line, hf_reduce_c1 reads one line per partial block).  The tile goes through
@@ -927,7 +891,6 @@ __global__ __launch_bounds__(256) void hf_bwd1(HeadArgs a) {
       pg4[e] = *reinterpret_cast<const float4*>(gT + c * 36 + 4 * qd);
     }
   }
-  NRK_HKT(a, 5, 3);
   if (hh == 0) {  // sum da1 over the block's rows: 32 columns x 8 row groups of 4, fixed-order combine
     __shared__ double p5[8][HF];
     const int j = t & 31, rq = t >> 5;
@@ -940,150 +903,15 @@ __global__ __launch_bounds__(256) void hf_bwd1(HeadArgs a) {
       a.part5[(int64_t)rb * HF + t] = ((p5[0][t] + p5[1][t]) + (p5[2][t] + p5[3][t])) +
                                       ((p5[4][t] + p5[5][t]) + (p5[6][t] + p5[7][t]));
   }
-  NRK_HKT(a, 5, 7);
 }
 
-// Every head gradient from the block partials (fixed order, fp64).
-// Blocks [0, D2/4): 4 columns c of G each (1024 threads = 8 phases x 32 j x 4 c):
-//   g_fc1_w[j][c] = bn0_w[c] G[j][c] + bn0_b[c] S[j]   (S = sum da1 = g_fc1_b)
-//   g_bn0_b[c] = sum_j W1[j][c] S[j],  g_bn0_w[c] = sum_j W1[j][c] G[j][c]
-//   (also kept in sum5 for hf_bwd0).  Blocks after: 64 columns each of the
-//   small layers' partials (part3: bn2, fc3, loss; part4: bn1, fc2).
-__global__ __launch_bounds__(1024) void hf_reduce(HeadArgs a) {
-  NRK_HKT(a, 6, 0);
-  const int D2 = a.D2, F2 = a.F2, t = threadIdx.x, nblk = a.nblk;
-  const int nA = D2 / 4;
-  if ((int)blockIdx.x < nA) {
-    // XCD-aware column groups: blocks b, b+8, ... run on one XCD (round-robin
-    // dispatch), so give them adjacent 4-column groups: each XCD's L2 then
-    // fetches whole 128-B lines of the partial rows once, instead of all 8 XCDs
-    // fetching every line for their 16-B pieces
-    const int cgp = nA % 8 == 0 ? ((int)blockIdx.x % 8) * (nA / 8) + (int)blockIdx.x / 8 : (int)blockIdx.x;
-    __shared__ double red[8][32][4];
-    __shared__ double sred[8][32];
-    __shared__ double Gt[32][4], St[32];
-    // j fastest: a wave's loads cover 2 columns x 32 rows = 64 consecutive floats of a partial block
-    const int ph = t >> 7, j = t & 31, cl = (t >> 5) & 3;
-    const int c = 4 * cgp + cl;
-    float wv[HF];  // W1 column of this block's column t (t < 4), loaded with the partials
-    const int colp = 4 * cgp + (t & 3);  // BN0 affine of output column (t < 128), loaded with the partials
-    const float bw0 = t < 128 ? a.p.bn0_w[colp] : 0.f, bb0 = t < 128 ? a.p.bn0_b[colp] : 0.f;
-    if (t < 4) {
-#pragma unroll
-      for (int jj = 0; jj < HF; ++jj) wv[jj] = a.p.fc1_w[(int64_t)jj * D2 + 4 * cgp + t];
-    }
-    double acc = 0.0;
-    for (int b0 = ph; b0 < nblk; b0 += 8 * 16) {
-      float v[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int b = b0 + 8 * u;
-        v[u] = b < nblk ? a.pw1[(int64_t)b * HF * D2 + (int64_t)c * HF + j] : 0.f;
-      }
-#pragma unroll
-      for (int u = 0; u < 16; ++u) acc += (double)v[u];
-    }
-    red[ph][j][cl] = acc;
-    if (t < 256) {
-      const int j2 = t & 31, p2 = t >> 5;
-      double s2 = 0.0;
-      for (int b0 = p2; b0 < nblk; b0 += 8 * 16) {
-        double v[16];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) {
-          const int b = b0 + 8 * u;
-          v[u] = b < nblk ? a.part5[(int64_t)b * HF + j2] : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < 16; ++u) s2 += v[u];
-      }
-      sred[p2][j2] = s2;
-    }
-    __syncthreads();
-    NRK_HKT(a, 6, 1);
-    if (t < 128) {
-      const int jj = t >> 2, cc = t & 3;
-      double g = 0.0;
-      for (int q = 0; q < 8; ++q) g += red[q][jj][cc];
-      Gt[jj][cc] = g;
-    }
-    if (t < 32) {
-      double s2 = 0.0;
-      for (int q = 0; q < 8; ++q) s2 += sred[q][t];
-      St[t] = s2;
-    }
-    __syncthreads();
-    if (t < 128) {
-      const int jj = t >> 2, cc = t & 3, col = 4 * cgp + cc;
-      a.p.g_fc1_w[(int64_t)jj * D2 + col] = (float)(bw0 * Gt[jj][cc] + bb0 * St[jj]);
-    }
-    if (t < 4) {
-      const int col = 4 * cgp + t;
-      double sb = 0.0, sg = 0.0;
-#pragma unroll
-      for (int jj = 0; jj < HF; ++jj) {
-        sb += (double)wv[jj] * St[jj];
-        sg += (double)wv[jj] * Gt[jj][t];
-      }
-      a.p.g_bn0_b[col] = (float)sb;
-      a.p.g_bn0_w[col] = (float)sg;
-      a.sum5[col] = sb;
-      a.sum5[D2 + col] = sg;
-    }
-    NRK_HKT(a, 6, 7);
-    if (cgp == 0 && t < HF) a.p.g_fc1_b[t] = (float)St[t];
-    return;
-  }
-  // small layers: column q of the concatenation [part3 (3F2+2) | part4 (2F + F2 F + F2)]
-  __shared__ double sr[16][64];
-  const int s3 = 3 * F2 + 2, s4 = 2 * HF + F2 * HF + F2;
-  const int cl = t & 63, ph = t >> 6;
-  const int q = ((int)blockIdx.x - nA) * 64 + cl;
-  const bool valid = q < s3 + s4;
-  double acc = 0.0;
-  if (valid) {
-    const double* src = q < s3 ? a.part3 + q : a.part4 + (q - s3);
-    const int stride = q < s3 ? s3 : s4;
-    for (int b0 = ph; b0 < nblk; b0 += 16 * 16) {
-      double v[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int b = b0 + 16 * u;
-        v[u] = b < nblk ? src[(int64_t)b * stride] : 0.0;
-      }
-#pragma unroll
-      for (int u = 0; u < 16; ++u) acc += v[u];
-    }
-  }
-  sr[ph][cl] = acc;
-  __syncthreads();
-  if (t < 64 && valid) {
-    double v = 0.0;
-    for (int p2 = 0; p2 < 16; ++p2) v += sr[p2][t];
-    if (q < s3) {
-      if (q < F2) a.p.g_bn2_b[q] = (float)v;
-      else if (q < 2 * F2) a.p.g_bn2_w[q - F2] = (float)v;
-      else if (q < 3 * F2) a.p.g_fc3_w[q - 2 * F2] = (float)v;
-      else if (q == 3 * F2) a.p.g_fc3_b[0] = (float)v;
-      else *a.loss = (float)(v / a.B);
-    } else {
-      const int o = q - s3;
-      if (o < HF) a.p.g_bn1_b[o] = (float)v;
-      else if (o < 2 * HF) a.p.g_bn1_w[o - HF] = (float)v;
-      else if (o < 2 * HF + F2 * HF) a.p.g_fc2_w[o - 2 * HF] = (float)v;
-      else a.p.g_fc2_b[o - 2 * HF - F2 * HF] = (float)v;
-    }
-  }
-}
-
-// hf_reduce with ONE column of G per block (256 threads = 8 phases x 32 j, all 16
-// loads of a thread in flight at once): the 4 MB of G partials are read by D2
-// blocks spread over the chip instead of D2 / 4 (hf_reduce's G phase took 5.8 us
-// on 64 blocks).  g_fc1_w[j][c] = bn0_w[c] G[j][c] + bn0_b[c] S[j],
+// Every head gradient from the block partials (fixed order, fp64), ONE column of
+// G per block (256 threads = 8 phases x 32 j, all 16 loads of a thread in flight
+// at once): the 4 MB of G partials are read by D2 blocks spread over the chip (a
+// 4-column form on D2 / 4 blocks spent 5.8 us in its G phase).  g_fc1_w[j][c] = bn0_w[c] G[j][c] + bn0_b[c] S[j],
 // g_bn0_b[c] = sum_j W1[j][c] S[j], g_bn0_w[c] = sum_j W1[j][c] G[j][c] (and sum5).
 // Blocks after: 64 columns each of the small layers' partials, 4 phases.
 __global__ __launch_bounds__(256) void hf_reduce_c1(HeadArgs a) {
-  NRK_HKT(a, 6, 0);
   const int D2 = a.D2, F2 = a.F2, t = threadIdx.x, nblk = a.nblk;
   if ((int)blockIdx.x < D2) {
     const int c = blockIdx.x;
@@ -1110,7 +938,6 @@ __global__ __launch_bounds__(256) void hf_reduce_c1(HeadArgs a) {
     red[ph][j] = acc;
     sred[ph][j] = s5;
     __syncthreads();
-    NRK_HKT(a, 6, 1);
     if (t < 32) {
       double g = 0.0, s = 0.0;
 #pragma unroll
@@ -1135,7 +962,6 @@ __global__ __launch_bounds__(256) void hf_reduce_c1(HeadArgs a) {
       }
     }
     if (c == 0 && t < HF) a.p.g_fc1_b[t] = (float)St[t];
-    NRK_HKT(a, 6, 7);
     return;
   }
   // small layers: column q of the concatenation [part3 (3F2+2) | part4 (2F + F2 F + F2)]
@@ -1194,7 +1020,6 @@ __global__ __launch_bounds__(256) void hf_fwd2(HeadArgs a) {
   __shared__ float mean[HF], inv[HF], b2s[HF2];
   __shared__ double red[2][16][HF2];
   __shared__ double pro_tmp[256], pro_sum[2 * HF];
-  NRK_HKT(a, 2, 0);
   const int t = threadIdx.x;
   const int64_t r0 = (int64_t)blockIdx.x * HR;
   const float stepv = *a.step;
@@ -1206,7 +1031,6 @@ __global__ __launch_bounds__(256) void hf_fwd2(HeadArgs a) {
   if (t < HF2) b2s[t] = a.p.fc2_b[t];
   const RunStatPre rsp = run_stat_pre(a.p.bn1_rm, a.p.bn1_rv, a.p.bn1_nb, HF, blockIdx.x == 0);
   colsum_prologue(a.part1, a.nblk, 2 * HF, 2 * HF, pro_tmp, pro_sum);
-  NRK_HKT(a, 2, 1);
   bn_finalize_pre(a, pro_sum, HF, mean, inv, a.stat1, a.p.bn1_rm, a.p.bn1_rv, a.p.bn1_nb, blockIdx.x == 0, rsp);
   __shared__ float gws[HF], gbs[HF];
   if (t < HF) {
@@ -1226,7 +1050,6 @@ __global__ __launch_bounds__(256) void hf_fwd2(HeadArgs a) {
     if (t < HF2 * HF / 4) *reinterpret_cast<float4*>(&w2[t >> 3][(t & 7) * 4]) = wv;
   }
   __syncthreads();
-  NRK_HKT(a, 2, 2);
 #pragma unroll
   for (int u = 0; u < 2; ++u) {  // a2 = h1 W2^T + b2: 512 outputs
     const int o = t + 256 * u, r = o >> 4, k = o & 15;
@@ -1254,7 +1077,6 @@ __global__ __launch_bounds__(256) void hf_fwd2(HeadArgs a) {
     }
   }
   __syncthreads();
-  NRK_HKT(a, 2, 3);
   {  // BN2 partial sums: 16 columns x 16 groups of 2 rows
     const int k = t & 15, g = t >> 4;
     const double v0 = d2[2 * g][k], v1 = d2[2 * g + 1][k];
@@ -1269,7 +1091,6 @@ __global__ __launch_bounds__(256) void hf_fwd2(HeadArgs a) {
     for (int g = 0; g < 16; ++g) s += red[which][g][k];
     a.part2[(int64_t)blockIdx.x * 2 * HF2 + which * HF2 + k] = s;
   }
-  NRK_HKT(a, 2, 7);
 }
 
 // BN2 (prologue sums) -> Linear(16, 1) -> BCEWithLogits (mean); dlogit;
@@ -1279,7 +1100,6 @@ __global__ __launch_bounds__(256) void hf_fwd3(HeadArgs a) {
   __shared__ float mean[HF2], inv[HF2], w3[HF2], gw2[HF2], gb2[HF2], dl[HR], lo[HR];
   __shared__ double red[3][16][HF2];
   __shared__ double pro_tmp[256], pro_sum[2 * HF2];
-  NRK_HKT(a, 3, 0);
   const int t = threadIdx.x;
   const int64_t r0 = (int64_t)blockIdx.x * HR;
   float4 av = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1294,7 +1114,6 @@ __global__ __launch_bounds__(256) void hf_fwd3(HeadArgs a) {
   }
   const RunStatPre rsp = run_stat_pre(a.p.bn2_rm, a.p.bn2_rv, a.p.bn2_nb, HF2, blockIdx.x == 0);
   colsum_prologue(a.part2, a.nblk, 2 * HF2, 2 * HF2, pro_tmp, pro_sum);
-  NRK_HKT(a, 3, 1);
   bn_finalize_pre(a, pro_sum, HF2, mean, inv, a.stat2, a.p.bn2_rm, a.p.bn2_rv, a.p.bn2_nb, blockIdx.x == 0, rsp);
   __syncthreads();
   if (t < HR * HF2 / 4) {
@@ -1310,7 +1129,6 @@ __global__ __launch_bounds__(256) void hf_fwd3(HeadArgs a) {
     }
   }
   __syncthreads();
-  NRK_HKT(a, 3, 2);
   if (t < HR) {
     float z = b3;
 #pragma unroll
@@ -1341,7 +1159,6 @@ __global__ __launch_bounds__(256) void hf_fwd3(HeadArgs a) {
     red[2][g][k] = sw;
   }
   __syncthreads();
-  NRK_HKT(a, 3, 3);
   double* pp = a.part3 + (int64_t)blockIdx.x * (3 * HF2 + 2);
   if (t < 3 * HF2) {
     const int which = t >> 4, k = t & 15;
@@ -1358,7 +1175,6 @@ __global__ __launch_bounds__(256) void hf_fwd3(HeadArgs a) {
       pp[3 * HF2 + 1] = ls;
     }
   }
-  NRK_HKT(a, 3, 7);
 }
 
 // BN2 backward (prologue sums) -> Dropout/ReLU backward -> Linear(32, 16)
@@ -1371,7 +1187,6 @@ __global__ __launch_bounds__(256) void hf_bwd2(HeadArgs a) {
   __shared__ float m1[HF], i1[HF], g1[HF], b1[HF], m2[HF2], i2[HF2], g2[HF2], sb2[HF2], sg2[HF2];
   __shared__ double red[2][8][HF];
   __shared__ double pro_tmp[256], pro_sum[2 * HF2];
-  NRK_HKT(a, 4, 0);
   const int t = threadIdx.x;
   const int64_t r0 = (int64_t)blockIdx.x * HR;
   // every load of the block first
@@ -1396,7 +1211,6 @@ __global__ __launch_bounds__(256) void hf_bwd2(HeadArgs a) {
     g2[k] = a.p.bn2_w[k];
   }
   colsum_prologue(a.part3, a.nblk, 3 * HF2 + 2, 2 * HF2, pro_tmp, pro_sum);
-  NRK_HKT(a, 4, 1);
   if (t < HF2) {
     sb2[t] = (float)pro_sum[t];
     sg2[t] = (float)pro_sum[HF2 + t];
@@ -1433,7 +1247,6 @@ __global__ __launch_bounds__(256) void hf_bwd2(HeadArgs a) {
     w2[wr][wc + 3] = wv.w;
   }
   __syncthreads();
-  NRK_HKT(a, 4, 2);
   double* pp = a.part4 + (int64_t)blockIdx.x * (2 * HF + HF2 * HF + HF2);
 #pragma unroll
   for (int u = 0; u < 2; ++u) {  // dW2[k][j] = sum_r da2[r][k] h1[r][j] (fp64, rows in order)
@@ -1466,7 +1279,6 @@ __global__ __launch_bounds__(256) void hf_bwd2(HeadArgs a) {
     }
     reinterpret_cast<float4*>(a.dh1 + r0 * HF)[t] = make_float4(dh[0], dh[1], dh[2], dh[3]);
   }
-  NRK_HKT(a, 4, 3);
   __syncthreads();  // h1 is re-used below as the dh1 image
   {
     const int r = t >> 3, j0 = (t & 7) * 4;
@@ -1494,7 +1306,6 @@ __global__ __launch_bounds__(256) void hf_bwd2(HeadArgs a) {
     for (int g = 0; g < 8; ++g) s += red[which][g][j];
     pp[which * HF + j] = s;
   }
-  NRK_HKT(a, 4, 7);
 }
 
 // dpooled = BN0 backward of dh0's pooled half, dh0 = da1 W1 on MFMA
@@ -1884,18 +1695,11 @@ extern "C" int nrk_din_head_train(const float* q, const float* pooled, int64_t l
   hipStream_t st = (hipStream_t)stream;
   const int D2 = 2 * d, F2 = F / 2;
   a.fast = F == HF && d % 32 == 0;
-  {  // row groups of hf_stats0 (NRK_DIN_NRG0=8 / 32: A/B hook)
-    const char* rg_env = getenv("NRK_DIN_NRG0");
-    const int want = rg_env && *rg_env ? atoi(rg_env) : 16;  // 16: measured -0.9 us vs 8, 32 no better
-    a.nrg0 = (want == 8 || want == 16 || want == 32) && nblk >= want ? want : (nblk < 8 ? nblk : 8);
-  }
-  {
-    const char* kt = getenv("NRK_KTIME");
-    a.ktime = kt && *kt == '1';
-  }
+  // row groups of hf_stats0: 16 (measured -0.9 us vs 8, 32 no better)
+  a.nrg0 = nblk >= 16 ? 16 : (nblk < 8 ? nblk : 8);
   if (a.fast) {
     const size_t lf1 =
-        ((size_t)2 * D2 + (size_t)(HR + (D2 <= 256 ? HF : 0)) * (D2 + 4) + 4 * HR * HF + HR * (HF + 1)) * 4;
+        ((size_t)2 * D2 + (size_t)HR * (D2 + 4) + 4 * HR * HF + HR * (HF + 1)) * 4;
     const size_t lb1 = ((size_t)2 * D2 + (size_t)HR * (D2 + 4) + HR * (HF + 1) + 4 * HF + (size_t)D2 * 36) * 4;
     // + the kernels' static LDS (hf_fwd1: 10 KB of prologue sums): every launch must fit 160 KB
     NRK_CHECK_ARG(lf1 + 10240 <= 160 * 1024 && lb1 + 4096 <= 160 * 1024,
@@ -1915,9 +1719,8 @@ extern "C" int nrk_din_head_train(const float* q, const float* pooled, int64_t l
     hipLaunchKernelGGL(hf_fwd2, dim3(nblk), dim3(256), 0, st, a);
     hipLaunchKernelGGL(hf_fwd3, dim3(nblk), dim3(256), 0, st, a);
     hipLaunchKernelGGL(hf_bwd2, dim3(nblk), dim3(256), 0, st, a);
-    // NRK_DIN_BWD1_SPLIT=1: one block per 32-row block (A/B hook); default 2 column splits
-    const char* cs_env = getenv("NRK_DIN_BWD1_SPLIT");
-    const int cs = (cs_env && *cs_env == '1') || (D2 / 32) % 2 ? 1 : 2;
+    // two column halves per 32-row block (one block per row block measured slower)
+    const int cs = (D2 / 32) % 2 ? 1 : 2;
     const size_t lb1c = ((size_t)2 * (D2 / cs) + (size_t)HR * (D2 / cs + 4) + HR * (HF + 1) + 4 * HF +
                          (size_t)(D2 / cs) * 36) * 4;
 #define NRK_HF_BWD1(NXV)                                                                                    \
@@ -1936,12 +1739,7 @@ extern "C" int nrk_din_head_train(const float* q, const float* pooled, int64_t l
       default: NRK_HF_BWD1(16); break;
     }
 #undef NRK_HF_BWD1
-    // NRK_DIN_HEAD_REDUCE=4: the 4-column form (A/B hook)
-    const char* hr_env = getenv("NRK_DIN_HEAD_REDUCE");
-    if (hr_env && *hr_env == '4')
-      hipLaunchKernelGGL(hf_reduce, dim3((unsigned)(D2 / 4 + cdiv(s3_ + s4_, 64))), dim3(1024), 0, st, a);
-    else
-      hipLaunchKernelGGL(hf_reduce_c1, dim3((unsigned)(D2 + cdiv(s3_ + s4_, 64))), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(hf_reduce_c1, dim3((unsigned)(D2 + cdiv(s3_ + s4_, 64))), dim3(256), 0, st, a);
     if (dpooled) hipLaunchKernelGGL(hf_bwd0, dim3(nblk), dim3(256), 0, st, a);
     NRK_CHECK_LAUNCH("din_head_train (fast)");
     return NRK_OK;
@@ -1981,13 +1779,6 @@ extern "C" int nrk_din_head_train(const float* q, const float* pooled, int64_t l
   const int ntot = F * D2 + F + D2 + F2 * F + F2 + F + F2 + 1 + F2;
   hipLaunchKernelGGL(head_grads, dim3((unsigned)cdiv(ntot, 256)), dim3(256), 0, st, a);
   NRK_CHECK_LAUNCH("head_grads");
-  return NRK_OK;
-}
-
-extern "C" int nrk_debug_head_ktimes(uint64_t* out, int64_t n) {
-  NRK_CHECK_ARG(out && n >= 0 && n <= 8 * 128 * 8, "debug_head_ktimes: bad arguments");
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(nrk::g_hkt), (size_t)n * 8, 0, hipMemcpyDeviceToHost) != hipSuccess)
-    return fail(NRK_ELAUNCH, "debug_head_ktimes: copy failed");
   return NRK_OK;
 }
 

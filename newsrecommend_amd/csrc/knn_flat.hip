@@ -1700,6 +1700,39 @@ static int exact_launch(const float* xq, int64_t nq, const float* xb, int64_t nb
 
 extern "C" int nrk_padded_dim(int32_t d) { return padded_dim(d); }
 
+// The flat search's main-pass screen kernel for a plan.  Inner product: the
+// 16x16x32 form where built (NRK_SCREEN16=0: the 32x32x16 kernel, which every
+// other form runs; a test hook).
+static screen_fn main_pass(const FlatPlan& p, bool l2, bool* s16) {
+  *s16 = false;
+  screen_fn fn = p.waves == 8 ? pick_screen_dp256_w8(p.M, l2, 0) : pick_screen(p.dp, p.qt, p.M, l2, 0);
+  if (!l2 && test_hook("NRK_SCREEN16", 1)) {
+    screen_fn f16 = p.waves == 8 ? (p.dp == 256 ? pick_screen16_dp256_w8(p.M) : nullptr)
+                                 : (p.dp == 128 ? pick_screen16_dp128(p.qt, p.M) : nullptr);
+    if (f16) {
+      fn = f16;
+      *s16 = true;
+    }
+  }
+  return fn;
+}
+
+extern "C" int nrk_knn_flat_main_pass(int64_t nq, int64_t nb, int32_t d, int32_t k, int32_t metric, char* name,
+                                      size_t len) {
+  NRK_CHECK_ARG(name && len > 0 && nq >= 0 && nb >= 0 && d > 0 && k > 0, "knn_flat_main_pass: bad arguments");
+  const FlatPlan p = make_plan(nq, nb, d, k);
+  const bool l2 = metric == NRK_METRIC_L2;
+  if (p.small) snprintf(name, len, "small_exact (fp64 tile GEMM, no screen)");
+  else if (p.exact_only) snprintf(name, len, "exact_topk_kernel (fp64 brute force, no screen)");
+  else {
+    bool s16 = false;
+    (void)main_pass(p, l2, &s16);
+    snprintf(name, len, "%s<dp %d, qt %d, M %d, %d waves, %s> (bf16 v_mfma_f32_%s)", s16 ? "screen16_kernel" : "screen_kernel",
+             p.dp, p.qt, p.M, p.waves, l2 ? "L2" : "IP", s16 ? "16x16x32" : "32x32x16");
+  }
+  return NRK_OK;
+}
+
 extern "C" int nrk_flat_prepare(const float* xb, int64_t nb, int32_t d, uint16_t* xb_bf16, float* xb_meta,
                                 float* stats, void* stream) {
   NRK_CHECK_ARG(d > 0 && nb >= 0, "flat_prepare: bad shape nb=%lld d=%d", (long long)nb, d);
@@ -1813,12 +1846,8 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
     NRK_CHECK_LAUNCH("tau_select_kernel");
   }
 
-  screen_fn fn = p.waves == 8 ? pick_screen_dp256_w8(p.M, l2 != 0, 0) : pick_screen(p.dp, p.qt, p.M, l2 != 0, 0);
-  if (const int v16 = l2 ? 0 : test_hook("NRK_SCREEN16", 1)) {  // inner product: the 16x16x32 main pass where built
-    screen_fn f16 = p.waves == 8 ? (p.dp == 256 ? pick_screen16_dp256_w8(p.M, v16) : nullptr)
-                                 : (p.dp == 128 ? pick_screen16_dp128(p.qt, p.M, v16) : nullptr);
-    if (f16) fn = f16;
-  }
+  bool s16 = false;
+  screen_fn fn = main_pass(p, l2 != 0, &s16);
   if (!fn) return fail(NRK_EUNSUPPORTED, "knn_flat: no screen kernel for dp=%d", p.dp);
   const int nblk = p.nqt * p.nch;
   mark(1);
@@ -1917,12 +1946,12 @@ static IvfPlan make_ivf_plan(int64_t nq, int nprobe, int nlist, int64_t max_list
   p.waves = 4;
   p.M = 1;  // neither phase keeps lane lists (mode 4: lane maxima, mode 3: collect)
   // phase B: two query tiles per wave at k <= 8 (one at DP = 256 or k > 8), 4 waves
-  // (256 probing queries per work item at configs[3]).  NRK_IVF_COLLECT_WAVES=8
-  // (A/B hook): 512 per item; configs[3] fetch 6.0 -> 4.0 GB per launch but the
-  // list segments' padding grows 3.66 -> 4.11 padded TF and the screen runs 3.36 ->
-  // 3.79 ms (profiles/r03_ivf_collect_ab.log): the screen is MFMA-bound, not HBM-bound
+  // (256 probing queries per work item at configs[3]).  8 waves (512 per item) cut
+  // the configs[3] fetch 6.0 -> 4.0 GB per launch but padded the list segments more
+  // (3.66 -> 4.11 padded TF) and ran 3.36 -> 3.79 ms (profiles/r03_ivf_collect_ab.log):
+  // the screen is MFMA-bound, not HBM-bound
   p.qt = (k <= 8 && p.dp != 256) ? 2 : 1;
-  p.wavesB = (p.dp >= 64 && test_hook("NRK_IVF_COLLECT_WAVES", 4) == 8) ? 8 : 4;
+  p.wavesB = 4;
   p.wq = p.wavesB * 32 * p.qt;
   // phase A (lane maxima over the nA nearest lists) runs one query tile per
   // wave: half the work-item padding of the grouped queries and a lighter
@@ -2154,7 +2183,7 @@ extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe,
   mark(1);
   if (n > 0) {
     // ---- phase B: collect every probed item at or above e_k - B_q
-    screen_fn fbk = p.wavesB == 8 ? pick_screen_collect8(p.dp, l2 != 0) : pick_screen(p.dp, p.qt, p.M, l2 != 0, 3);
+    screen_fn fbk = pick_screen(p.dp, p.qt, p.M, l2 != 0, 3);
     if (!fbk) return fail(NRK_EUNSUPPORTED, "ivf_search: no collect kernel for dp=%d", p.dp);
     IvfScreen isb{work, list_off, seg, sp, nlist, p.chB, p.cmaxB, thr, ccnt, cpos, p.cap, nprobe};
     hipLaunchKernelGGL(fbk, dim3((unsigned)p.ubB), dim3(p.wavesB * 64), 0, st, qi, xbh_ivf, meta_ivf, nq, n, 0, 0, 0, 1,

@@ -116,7 +116,7 @@ struct IvfScreen {
 // (returning global atomics in the epilogue would stall the wave for ~1 us).
 template <int WQ>
 struct CollectLds {
-  static constexpr int CAP = 4 * WQ;
+  static constexpr int CAP = 4 * WQ > 1024 ? 4 * WQ : 1024;  // the QT = 1 forms keep 1024 entries
   int n;
   int qcnt[WQ];
   int qid[WQ];
@@ -700,34 +700,10 @@ screen_fn pick_screen_dp256(int qt, int M, bool l2, int mode);
 // k = 200: 18.8 -> 21.6 ms; each lane stream admits ~30 items above tau.)
 screen_fn pick_screen_dp256_w8(int M, bool l2, int mode);
 
-// IVF collect (mode 3) with 8 waves per workgroup (one register budget of 256
-// per lane): 512 probing queries per work item (256 at DP = 256), so most lists'
-// chunks are read by ONE work item instead of ~2.3 (each chunk's query tiles
-// ran desynchronised on the persistent grid and re-fetched it from HBM).
-screen_fn pick_screen_dp32_c8(bool l2);
-screen_fn pick_screen_dp64_c8(bool l2);
-screen_fn pick_screen_dp128_c8(bool l2);
-screen_fn pick_screen_dp256_c8(bool l2);
-
 #define NRK_SCREEN_DP(DP)                                                  \
   screen_fn pick_screen_dp##DP(int qt, int M, bool l2, int mode) {         \
     return l2 ? screen_for<DP, true>(qt, M, mode) : screen_for<DP, false>(qt, M, mode); \
-  }                                                                        \
-  screen_fn pick_screen_dp##DP##_c8(bool l2) {                             \
-    constexpr int Q = DP == 256 ? 1 : 2;                                   \
-    if constexpr (DP < 64) return nullptr; /* a 64-row tile is 256 chunks */ \
-    else return l2 ? screen_kernel<DP, Q, 1, 8, true, 3, true> : screen_kernel<DP, Q, 1, 8, false, 3, true>; \
   }
-
-inline screen_fn pick_screen_collect8(int dp, bool l2) {
-  switch (dp) {
-    case 32: return pick_screen_dp32_c8(l2);
-    case 64: return pick_screen_dp64_c8(l2);
-    case 128: return pick_screen_dp128_c8(l2);
-    case 256: return pick_screen_dp256_c8(l2);
-  }
-  return nullptr;
-}
 
 inline screen_fn pick_screen(int dp, int qt, int M, bool l2, int mode) {
   switch (dp) {

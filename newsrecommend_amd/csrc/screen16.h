@@ -282,7 +282,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_kernel(
 }
 
 // the 16x16x32 main pass for (DP, qt, M), or nullptr (no such form: use screen.h's)
-screen_fn pick_screen16_dp128(int qt, int M, int var);
-screen_fn pick_screen16_dp256_w8(int M, int var);
+screen_fn pick_screen16_dp128(int qt, int M);
+screen_fn pick_screen16_dp256_w8(int M);
 
 }  // namespace nrk

@@ -7,11 +7,11 @@ NRK_SCREEN_DP(128)
 
 // 16x16x32 main pass (screen16.h), the k <= 8 form only (2 query tiles, M = 4).
 // A/B on one box (tools/bench_screen.py, configs[1]): 128-item tiles with the
-// compiler's own schedule 0.810 ms vs the 32x32x16 kernel's 0.830 ms;
-// with sched_group_barrier interleaving 0.812, 64-item tiles 0.817 (var 2).
-// M = 8 / 16 keep the 32x32x16 kernel (unmeasured here).
-screen_fn pick_screen16_dp128(int qt, int M, int var) {
+// compiler's own schedule 0.810 ms vs the 32x32x16 kernel's 0.830 ms (with
+// sched_group_barrier interleaving 0.812, 64-item tiles 0.817: not kept).
+// M = 8 / 16 keep the 32x32x16 kernel.
+screen_fn pick_screen16_dp128(int qt, int M) {
   if (M != 4 || qt != 2) return nullptr;
-  return var == 2 ? screen16_kernel<128, 2, 4, 4, 128, true> : screen16_kernel<128, 2, 4, 4, 128, false>;
+  return screen16_kernel<128, 2, 4, 4, 128, false>;
 }
 }  // namespace nrk

@@ -5,17 +5,13 @@
 namespace nrk {
 NRK_SCREEN_DP(256)
 
-// 16x16x32 main pass at DP = 256 (8 waves, 64-item tiles), M = 4 only (N1):
-// 15.69 ms vs 15.82 for the 32x32x16 kernel (10M x 256, k = 5; the compiler's
-// own schedule 15.97, var 2).  M = 16 (k = 200) spills 32 VGPRs and ran 34.8 vs
-// 16.7 ms: it keeps the 32x32x16 kernel.
-screen_fn pick_screen16_dp256_w8(int M, int var) {
-  // k = 200 with the A fragments read per K step (no prefetch: 228 VGPRs, no spill):
-  // 17.40 vs 15.87 ms for the 32x32x16 kernel (profile queries, one-process A/B), so
-  // only behind NRK_SCREEN16=3
-  if (M == 16) return var == 3 ? screen16_kernel<256, 1, 16, 8, 64, true, false> : nullptr;
-  if (M != 4) return nullptr;
-  return var == 2 ? screen16_kernel<256, 1, 4, 8, 64, false> : screen16_kernel<256, 1, 4, 8, 64, true>;
+// 16x16x32 main pass at DP = 256 (8 waves, 64-item tiles, sched_group_barrier
+// interleave), M = 4 only (N1): 15.69 ms vs 15.82 for the 32x32x16 kernel (10M x
+// 256, k = 5; the compiler's own schedule 15.97).  M = 16 (k = 200) keeps the
+// 32x32x16 kernel: the 16x16x32 form spills 32 VGPRs there (34.8 vs 16.7 ms), and
+// reading the A fragments per K step instead (228 VGPRs) ran 17.40 vs 15.87 ms.
+screen_fn pick_screen16_dp256_w8(int M) {
+  return M == 4 ? screen16_kernel<256, 1, 4, 8, 64, true> : nullptr;
 }
 
 screen_fn pick_screen_dp256_w8(int M, bool l2, int mode) {

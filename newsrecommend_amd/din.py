@@ -510,8 +510,7 @@ class FusedTrainStep:
         # gathers ahead (fast path): one nrk_din_batch launch assembles the rows of
         # all K steps of a graph (history ids, query rows, labels: nothing there
         # depends on the parameters); each step then only forms U and bf16 W1k
-        # (nrk_din_batch_u).  NRK_DIN_GATHER_AHEAD=0: one full batch kernel per step.
-        self.gather_ahead = self.fast and os.environ.get("NRK_DIN_GATHER_AHEAD", "1") != "0"
+        # (nrk_din_batch_u).
         if self.fast:
             L = hist_ids.shape[1]
             self.hist_k = torch.empty((self.K, B, L), dtype=torch.int32, device=dev)
@@ -602,20 +601,13 @@ class FusedTrainStep:
         W1, b1 = m.attn.attn[0].weight, m.attn.attn[0].bias
         w2 = m.attn.attn[2].weight
         self.hist_b, self.q_b, self.y_b = self.hist_k[k], self.q_k[k], self.y_k[k]
-        if self.gather_ahead:
-            if gather_n > 0:
-                _lib.check(L_.nrk_din_batch(
-                    _lib.ptr(self.idx_ring[k]), gather_n * B, _lib.ptr(self.hist_all), _lib.ptr(self.tgt_all),
-                    _lib.ptr(self.lab_all), self.hist_all.shape[0], L, _lib.ptr(self.table), N, dt, d, None, None, A,
-                    _lib.ptr(self.hist_b), _lib.ptr(self.q_b), _lib.ptr(self.y_b), None, None, st), "din_batch")
-            _lib.check(L_.nrk_din_batch_u(_lib.ptr(self.q_b), B, d, _lib.ptr(W1), _lib.ptr(b1), A, _lib.ptr(self.U_b),
-                                          _lib.ptr(self.W1k_b), st), "din_batch_u")
-        else:
+        if gather_n > 0:
             _lib.check(L_.nrk_din_batch(
-                _lib.ptr(idx), B, _lib.ptr(self.hist_all), _lib.ptr(self.tgt_all), _lib.ptr(self.lab_all),
-                self.hist_all.shape[0], L, _lib.ptr(self.table), N, dt, d, _lib.ptr(W1), _lib.ptr(b1), A,
-                _lib.ptr(self.hist_b), _lib.ptr(self.q_b), _lib.ptr(self.y_b), _lib.ptr(self.U_b),
-                _lib.ptr(self.W1k_b), st), "din_batch")
+                _lib.ptr(self.idx_ring[k]), gather_n * B, _lib.ptr(self.hist_all), _lib.ptr(self.tgt_all),
+                _lib.ptr(self.lab_all), self.hist_all.shape[0], L, _lib.ptr(self.table), N, dt, d, None, None, A,
+                _lib.ptr(self.hist_b), _lib.ptr(self.q_b), _lib.ptr(self.y_b), None, None, st), "din_batch")
+        _lib.check(L_.nrk_din_batch_u(_lib.ptr(self.q_b), B, d, _lib.ptr(W1), _lib.ptr(b1), A, _lib.ptr(self.U_b),
+                                      _lib.ptr(self.W1k_b), st), "din_batch_u")
         t0 = KernelTimer.mark("fwd")
         _lib.check(L_.nrk_din_attn_fwd(
             _lib.ptr(self.table), _lib.ptr(self.hist_b), N, dt, _lib.ptr(self.U_b), _lib.ptr(self.W1k_b), _lib.ptr(w2),

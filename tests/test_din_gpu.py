@@ -370,17 +370,20 @@ def test_din_batch_kernel(gpu, d, A, L):
     assert (U - U_ref).abs().max().item() < 2e-5 * max(1.0, U_ref.abs().max().item())
 
 
-@pytest.mark.parametrize("A,L,B", [(128, 50, 4096), (64, 20, 97), (96, 64, 1000)])
-def test_fwd_pair_d128_matches_wave_kernel(gpu, A, L, B, monkeypatch):
-    """d = 128: the wave-pair forward (default) against the wave-per-sample
-    kernel (NRK_DIN_FWD_PAIR=0): the partial scores of the two unit halves are
-    summed in another order, so pooled / alpha agree to f32 rounding."""
+@pytest.mark.parametrize("d,A,L,B", [(128, 128, 50, 4096), (128, 64, 20, 97), (128, 96, 64, 1000),
+                                     (64, 128, 50, 513), (256, 128, 64, 300)])
+def test_fwd_fast_kernels_vs_f64(gpu, d, A, L, B):
+    """The bf16 attention forwards nrk_din_attn_fwd picks (d = 128 / 256: the
+    wave-pair kernel, d = 64: one wave per sample) against the same arithmetic
+    in float64 on the kernels' inputs (bf16 rows and W1k are exact in f64):
+    z = U + W1k k, s = relu(z) w2, alpha = softmax over all L slots (padding
+    included, DIN.py:108), pooled = alpha K.  What remains is f32 accumulation."""
     from newsrecommend_amd import _lib
     from newsrecommend_amd.data import synthetic_click_rows
 
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(8)
-    d, N = 128, 6000
+    N = 6000
     L_ = _lib.load()
     table = (torch.randn((N, d), generator=g, device=dev) * 0.5).to(torch.bfloat16)
     hist, _, _ = synthetic_click_rows(B, N, L, seed=4, device=dev)
@@ -389,20 +392,19 @@ def test_fwd_pair_d128_matches_wave_kernel(gpu, A, L, B, monkeypatch):
     U = torch.randn((B, A), generator=g, device=dev) * 0.3
     wk = (torch.randn((A, d), generator=g, device=dev) * 0.1).to(torch.bfloat16)
     w2 = torch.randn(A, generator=g, device=dev) * 0.3
-    outs = []
-    for pair in ("0", "1"):
-        monkeypatch.setenv("NRK_DIN_FWD_PAIR", pair)
-        pooled = torch.full((B, d), float("nan"), device=dev)
-        alpha = torch.full((B, L), float("nan"), device=dev)
-        _lib.check(L_.nrk_din_attn_fwd(
-            _lib.ptr(table), _lib.ptr(hist), N, _lib.NRK_DTYPE_BF16, _lib.ptr(U), _lib.ptr(wk), _lib.ptr(w2), 0.0, B,
-            L, d, A, _lib.ptr(pooled), _lib.ptr(alpha), _lib.stream(dev)), "din_attn_fwd")
-        torch.cuda.synchronize()
-        outs.append((pooled, alpha))
-    (p0, a0), (p1, a1) = outs
-    assert torch.isfinite(p1).all() and torch.isfinite(a1).all()
-    assert (a0 - a1).abs().max().item() < 1e-5
-    assert (p0 - p1).abs().max().item() < 1e-5 * max(1.0, p0.abs().max().item())
+    pooled = torch.full((B, d), float("nan"), device=dev)
+    alpha = torch.full((B, L), float("nan"), device=dev)
+    _lib.check(L_.nrk_din_attn_fwd(
+        _lib.ptr(table), _lib.ptr(hist), N, _lib.NRK_DTYPE_BF16, _lib.ptr(U), _lib.ptr(wk), _lib.ptr(w2), 0.0, B,
+        L, d, A, _lib.ptr(pooled), _lib.ptr(alpha), _lib.stream(dev)), "din_attn_fwd")
+    torch.cuda.synchronize()
+    K = torch.where(hist[..., None] >= 0, table[hist.clamp_min(0).long()].double(), 0.0)
+    z = U.double()[:, None, :] + K @ wk.double().t()
+    a_ref = torch.softmax(z.clamp_min(0) @ w2.double(), dim=1)
+    p_ref = (a_ref[..., None] * K).sum(1)
+    assert torch.isfinite(pooled).all() and torch.isfinite(alpha).all()
+    assert (alpha.double() - a_ref).abs().max().item() < 1e-5
+    assert (pooled.double() - p_ref).abs().max().item() < 1e-5 * max(1.0, p_ref.abs().max().item())
 
 
 def test_fused_train_step_generic_path_matches_eager(gpu):
@@ -453,7 +455,7 @@ def _eval_batches(table32, n_users, L, C, seed, dev):
     return out
 
 
-LR_FIT = 2e-3  # at 5e-3 the two runs' rounding differences grew to 1e-2 in the third epoch's val loss
+LR_FIT = 1.62e-3  # the reference's lr (DIN.py:230)
 
 
 @pytest.mark.parametrize("sched", ["plateau", "step"])
@@ -463,13 +465,23 @@ def test_fit_epoch_driver_matches_eager_main_loop(gpu, tmp_path, sched):
     same scheduler, batch order and evaluate(); the last partial batch (12
     rows) is trained on by both, as the reference's DataLoader keeps it.
 
+    This is a SELF-comparison of the epoch driver, not a parity test: both
+    sides are this package (the fused graphed step vs its own eager torch loop
+    over the autograd attention kernels).  Parity of the step itself is pinned
+    against the fp64 oracle and the reference's fixtures in
+    tests/test_din_bf16_oracle.py and test_train_grads_and_two_adam_steps.
+
     Checked exactly: the lr of every epoch equals what a torch scheduler fed
     fit's own validation losses produces (StepLR(gamma 0.5) forces a change
     every epoch), and the best-NDCG checkpoint (weights_only=True) reproduces
-    the best epoch's NDCG.  Per-epoch train / val losses vs the eager loop:
-    1e-3 abs (the two runs use different bf16 attention kernels and head
-    reductions, so rounding differs; one-step numerics are pinned tightly in
-    test_fused_train_step_matches_eager and tests/test_din_bf16_oracle.py)."""
+    the best epoch's NDCG.  Per-epoch train / val losses vs the eager loop at
+    the reference's lr 1.62e-3: 1e-3 abs.  Why not tighter: the two runs use
+    different attention kernels and head reductions, so each step's gradients
+    differ by f32 rounding (~1e-6 relative), and Adam's sign-normalised steps
+    turn those differences in near-zero gradient entries into parameter
+    differences of up to lr per step; over 3 epochs x 18 steps the val loss
+    moves by a few 1e-4 (a run at lr 5e-3 drifted to 1e-2, which says the
+    comparison measures trajectory divergence, not an error of either side)."""
     from newsrecommend_amd.din import DIN, evaluate, fit
 
     dev, table, hist, tgt, lab, ma, mb = _setup_fused(0.0, d=64, L=20)
@@ -588,3 +600,31 @@ def test_fused_step_dpooled_in_backward_matches_head_bwd0(gpu, B, monkeypatch):
         ref = pb.grad
         assert torch.allclose(pa.grad, ref, atol=1e-7 + 1e-4 * ref.abs().max().item(), rtol=1e-4), \
             (n, (pa.grad - ref).abs().max().item())
+
+
+def test_fused_graph_k_norm_partials_multi_step(gpu, monkeypatch):
+    """the gradient reduction's squared-norm partials
+    (nrk_clip_adam_partials, fuse_dp without a grad hook) over K > 1 graphed
+    steps with clipping ACTIVE (max_norm 0.05), against the same trainer with
+    NRK_DIN_FUSE_DP=0 (head bwd0 + nrk_din_attn_bwd_params + the norm read by
+    nrk_clip_adam from the whole gradient): every step's loss, and after each
+    K-step launch the stored (clipped) gradients, whose norm must equal
+    max_norm.  Two launches of K = 4 steps, dropout on."""
+    from newsrecommend_amd.din import FusedTrainStep
+
+    dev, table, hist, tgt, lab, ma, mb = _setup_fused(0.36, d=128, L=50)
+    K, B, clip = 4, 512, 0.05
+    ta = FusedTrainStep(ma, table, hist, tgt, lab, B, lr=1e-4, weight_decay=1e-4, clip=clip, steps_per_graph=K)
+    monkeypatch.setenv("NRK_DIN_FUSE_DP", "0")
+    tb = FusedTrainStep(mb, table, hist, tgt, lab, B, lr=1e-4, weight_decay=1e-4, clip=clip, steps_per_graph=K)
+    assert ta.norm_part is not None and tb.norm_part is None
+    perm = torch.randperm(hist.shape[0], device=dev)
+    for r in range(2):
+        sl = perm[r * K * B:(r + 1) * K * B].view(K, B)
+        la, lb = ta.step_many(sl).clone(), tb.step_many(sl).clone()
+        assert (la - lb).abs().max().item() < 1e-5, (r, la.flatten(), lb.flatten())
+        ga = torch.cat([p.grad.reshape(-1) for p in ma.parameters()])
+        gb = torch.cat([p.grad.reshape(-1) for p in mb.parameters()])
+        assert abs(ga.norm().item() - clip) < 1e-5 * clip, (r, ga.norm().item())  # clipping active, norm right
+        assert abs(gb.norm().item() - clip) < 1e-5 * clip, (r, gb.norm().item())
+        assert (ga - gb).abs().max().item() < 1e-7 + 1e-3 * gb.abs().max().item(), (r, (ga - gb).abs().max().item())

@@ -1,10 +1,13 @@
 """World-2 run of the product's multi-GPU code on the GPU box (one card, two
 ranks on cuda:0, gloo): ShardedIndexFlat / ShardedIndexIVFFlat equal one index
 over the whole corpus, and FusedTrainStep's data-parallel gradient hook
-produces the rank-mean gradient with replicas staying identical.  The RCCL
-branch (all_gather_into_tensor / all_reduce on device buffers) is the
-driver's 8-GPU scaling run; here gloo carries host copies of the same
-buffers.  The ranks run as child processes of torch.distributed.run."""
+produces the rank-mean gradient with replicas staying identical (gloo carries
+host copies of the device buffers).  The RCCL branches of dist.py
+(all_gather_into_tensor / all_reduce / all_to_all on device buffers, and the
+all_reduce captured inside the DIN step's HIP graph) run here too, at world 1
+over the "nccl" backend (test_rccl_branch_world1, tests/rccl_world1_worker.py).
+What no test here covers is RCCL across several GPUs (the driver's 8-GPU
+scaling run).  The ranks run as child processes of torch.distributed.run."""
 import json
 import os
 import socket

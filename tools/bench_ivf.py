@@ -71,7 +71,7 @@ for combo in itertools.product(*grid):
     flops = 2.0 * a.d * float((sizes[pr]).sum())
     cnt_l = np.bincount(pr[pr >= 0].ravel(), minlength=a.nlist)
     # phase B rows per work item: waves x 32 x (2 query tiles per wave, 1 at d > 128)
-    wq = (8 if os.environ.get("NRK_IVF_COLLECT_WAVES", "4") == "8" else 4) * 32 * (2 if a.d <= 128 else 1)
+    wq = 4 * 32 * (2 if a.d <= 128 else 1)
     padded = 2.0 * a.d * float((np.ceil(cnt_l / wq) * wq * sizes).sum())
     print(f"{combo}: stages ms group {st[0]:.4f} screen {st[1]:.4f} merge {st[2]:.4f} fallback {st[3]:.4f}  "
           f"ivf wall {wall * 1e3:.3f} ms, full (with coarse) {full * 1e3:.3f} ms = {a.nq / full:,.0f} QPS; "
