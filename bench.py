@@ -471,16 +471,21 @@ def bench_e2e(args, rank, world, dev):
     barrier(world)
     el = max_over_ranks(time.perf_counter() - t0, world, dev)
     # stage split (rank-local, outside the timed region)
+    from newsrecommend_amd.din import KernelTimer
+
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     for _ in range(3):
         index.search_device_own(profiles, kr)
     torch.cuda.synchronize()
     t2 = time.perf_counter()
-    for _ in range(3):
-        rerank(model, table, hist[ulo:uhi], cand)
-    torch.cuda.synchronize()
+    with KernelTimer() as kt:
+        for _ in range(3):
+            rerank(model, table, hist[ulo:uhi], cand)
+        torch.cuda.synchronize()
     t3 = time.perf_counter()
+    rr = _rerank_roofline(kt.mean_ms("rerank"), hist[ulo:uhi], cand, d, 128, L,
+                          f"rerank:e2e,users={uhi - ulo},C={kr + 1},d={d},gpus={world}")
     out = {
         "metric": "end-to-end users/s (retrieve top-200 + DIN re-rank + NDCG@5)", "value": U * args.steps / el,
         "unit": "users/s", "ms_per_step": el / args.steps * 1e3,
@@ -490,6 +495,9 @@ def bench_e2e(args, rank, world, dev):
                                    f"user-shard{world} re-rank") if world > 1 else "single GPU"},
         "stages_ms": {"retrieve": (t2 - t1) / 3 * 1e3, "rerank": (t3 - t2) / 3 * 1e3},
         "rerank_samples_per_step": int((uhi - ulo) * (kr + 1)),
+        "rerank_kernel_ms": kt.mean_ms("rerank"), "rerank_path": __import__(
+            "newsrecommend_amd.pipeline", fromlist=["rerank"]).rerank.path, "rerank_roofline": rr["hbm"],
+        "rerank_valu": rr["valu"], "table_dtype": "bf16 (the corpus rows rounded once; fp32 corpora: DESIGN.md Parity)",
         "ndcg_at_5_mean_rank0": float(nd.mean().item()),
         "fallback_queries": int(index.local.last_fallback.item()),
         "exact_scan_queries": int(index.local.last_exact_scan.item()),
@@ -511,6 +519,33 @@ def bench_e2e(args, rank, world, dev):
     del index, table
     torch.cuda.empty_cache()
     return out
+
+
+def _rerank_roofline(ms, hist, cand, d, A, L, key, n_samples=None):
+    """Roofline of the fused re-rank launch (nrk_din_rerank): ALGORITHMIC bytes
+    = per candidate its bf16 row (2d), id and logit (8 B), per user its L ids
+    and nv history rows (2d each); VALU work = 2 lane-ops (add, |.|-fma) per
+    (candidate, scored row, attention unit), scored rows = nv + 1 padding row
+    when nv < L, against the 78.6 T lane-op/s of the fp32 vector peak
+    (157.3 TFLOP/s counting an fma as 2)."""
+    nv = (hist >= 0).sum(1).double()
+    nr = nv + (nv < L).double()
+    if cand is not None:
+        per_user = torch.full_like(nv, float(cand.shape[1]))
+        n_samples = float(cand.shape[1] * cand.shape[0])
+        ops = float((per_user * nr).sum()) * A * 2
+    else:
+        ops = n_samples * float(nr.mean()) * A * 2
+    byt = n_samples * (2 * d + 8) + float((4 * L + 2 * d * nv).sum())
+    sec = ms * 1e-3
+    gbs = byt / sec / 1e9
+    return {"hbm": {"bound": "hbm", "binding": "valu (the scoring; see valu)", "kernel": f"din_rerank_kernel<{d}, {A}, 32>", "achieved": gbs,
+                    "peak": HBM_GBS, "unit": "GB/s", "frac": gbs / HBM_GBS, "traffic": _pmc_traffic(key),
+                    "algorithmic": f"{byt:.4g} B per launch ({2 * d + 8} B per candidate + the users' ids and "
+                                   f"history rows), {ms:.3f} ms (HIP events)"},
+            "valu": {"achieved": ops / sec / 1e12, "peak": 78.6, "unit": "T lane-ops/s",
+                     "frac": ops / sec / 1e12 / 78.6,
+                     "algorithmic": f"{ops:.4g} lane-ops (2 per candidate x scored row x unit)"}}
 
 
 def bench_retrieval_flow(args, rank, world, dev):
@@ -571,6 +606,11 @@ def bench_retrieval_flow(args, rank, world, dev):
     res = stage()
     barrier(world)
     el = max_over_ranks(time.perf_counter() - t0, world, dev)
+    from newsrecommend_amd.din import KernelTimer
+
+    with KernelTimer() as kt:  # the fused launch alone, outside the timed region
+        stage()
+        torch.cuda.synchronize()
     sizes = torch.diff(cluster_off)
     _, Iu = centroid_index.search_device(profiles[lo:hi], 1)
     cand_per_user = sizes[Iu[:, 0]].double()
@@ -581,6 +621,10 @@ def bench_retrieval_flow(args, rank, world, dev):
            "cluster_size_min_mean_max": [int(sizes.min()), float(sizes.double().mean()), int(sizes.max())],
            "candidates_per_user_mean": float(cand_per_user.mean()),
            "rerank_samples_per_s": float(cand_per_user.sum()) * world / el,
+           "rerank_kernel_ms": kt.mean_ms("rerank"),
+           "rerank_roofline": _rerank_roofline(kt.mean_ms("rerank"), hist[lo:hi], None, d, 128, L,
+                                               f"rerank:flow,users={hi - lo},gpus={world}",
+                                               n_samples=float(cand_per_user.sum()) + (hi - lo))["hbm"],
            "rerank_path": __import__("newsrecommend_amd.pipeline", fromlist=["rerank"]).rerank.path,
            "ndcg_at_5_mean_rank0": float(res["ndcg"].mean()), "loss_mean_rank0": float(res["loss"].mean())}
     del xb, table, index, centroid_index
@@ -676,7 +720,10 @@ def bench_din(args, rank, world, dev):
     perm = torch.randperm(rows, device=dev)
     nbatch = rows // B
     fused = not args.din_eager
-    graphed = fused and world == 1
+    # the data-parallel step is graphed too when the gradient all_reduce is RCCL
+    # (captured inside the graph: tests/rccl_world1_worker.py); gloo
+    # rehearsals carry host copies, which a graph cannot capture
+    graphed = fused and (world == 1 or BACKEND == "nccl")
     opt = torch.optim.Adam(model.parameters(), lr=1.62e-3, weight_decay=8.96e-5)
     if fused:
         from newsrecommend_amd.din import FusedTrainStep
@@ -767,8 +814,9 @@ def bench_din(args, rank, world, dev):
         "config": {"workload": "configs[2]: DIN train bf16, 5M synthetic click rows, seq_len=50, emb_dim=128",
                    "rows": rows, "items": n_items, "batch": B, "attn_units": A, "fc_units": F,
                    "parallelism": f"dp{world}",
-                   "step": (f"fused head/optimizer kernels, one hip graph per {DIN_STEPS_PER_GRAPH} steps" if graphed else
-                            "fused head/optimizer kernels + RCCL grad all_reduce") if fused else "eager torch"},
+                   "step": ((f"fused head/optimizer kernels, one hip graph per {DIN_STEPS_PER_GRAPH} steps"
+                             + (" (RCCL grad all_reduce captured in the graph)" if world > 1 else "")) if graphed else
+                            "fused head/optimizer kernels + gloo grad all_reduce") if fused else "eager torch"},
         "final_loss": float(loss.reshape(-1)[0].item()),
         "kernels_ms": {"attn_fwd": fwd_ms, "attn_bwd (8-wave + reduce)" if fused else "attn_bwd+reduce": bwd_ms},
         "roofline_step": {"bound": "hbm", "achieved": step_gbs, "peak": HBM_GBS, "unit": "GB/s",

@@ -198,36 +198,42 @@ int nrk_din_batch(const int64_t* idx, int32_t B, const int32_t* hist_all, const 
 int nrk_din_batch_u(const float* q, int32_t B, int32_t d, const float* W1, const float* b1, int32_t A,
                     float* U, void* W1k_bf16, void* stream);
 
-/* DIN attention for re-ranking (DIN.py:166-173: every candidate of a user
- * attends over the same history): pooled [nU*C][d] f32 for candidates whose
- * query rows give Uc [nU*C][ldu] f32 (first A columns = q W1[:, :d]^T + b1,
- * e.g. from nrk_din_item_proj), users' history ids hist [nU][L] int32 (-1 or
- * >= n_table = zero row, DIN.py:108 padding), table [N][d] bf16, W1k [A][d]
- * bf16 = W1[:, d:], w2 [A].  P = K W1k^T is formed once per user; padding
- * slots share one logit.  d in {64, 128, 256}, L <= 64, A in {32,64,96,128}. */
-int nrk_din_rerank_attn(const void* table, int64_t n_table, int32_t dtype, const int32_t* hist,
-                        int32_t nU, int32_t L, const float* Uc, int32_t ldu, int32_t C, int32_t d,
-                        const void* W1k_bf16, const float* w2, int32_t A, float* pooled, void* stream);
-
-/* Query-side projections of re-rank candidates, gathered from the item table:
- * out [n][NO] f32 = table[ids[i]] W^T + bias (ids outside [0, n_table): zero
- * row).  W [NO][d] f32 enters as W_hi = bf16(W), W_lo = bf16(W - W_hi)
- * ([NO][d] bf16 each).  Replaces the q gather + torch.addmm of the attention
- * query half (DIN.py:96-104) and of the head's first layer (DIN.py:200-204).
- * d in {64, 128, 256}, NO in 128..256 step 32 (pad W with zero rows). */
-int nrk_din_item_proj(const void* table, int64_t n_table, int32_t dtype, const int32_t* ids, int64_t n,
-                      int32_t d, const void* W_hi, const void* W_lo, const float* bias, int32_t NO,
-                      float* out, void* stream);
-
-/* Eval-mode DIN head on re-rank candidates (DIN.py:200-204, BatchNorms folded
- * into the Linears by the caller): logit[i] = h3 . relu(H2 relu(Q1[i] +
- * H1p pooled[i] + c1) + c2) + c3, -inf where cand[i] < 0.  pooled [n][d] f32
- * (nrk_din_rerank_attn), Q1 [n][ldq] f32 (query half, no bias), H1p [F][d] as
- * bf16 hi + lo, c1 [F], H2 [F/2][F], c2 [F/2], h3 [F/2].  F = 32. */
-int nrk_din_rerank_head(const float* pooled, int64_t n, int32_t d, const float* Q1, int32_t ldq,
-                        const int32_t* cand, const void* H1p_hi, const void* H1p_lo, const float* c1,
-                        int32_t F, const float* H2, const float* c2, const float* h3, float c3,
-                        float* logit, void* stream);
+/* DIN evaluate() for re-ranking, fused (DIN.py:155-189 minus the loss / NDCG
+ * bookkeeping; Retrieval.py:28-34 -> finialize_retrieval.py -> DIN.py): the
+ * eval-mode logits of every candidate of every user, each candidate attending
+ * over its user's history (`his.expand(C, -1, -1)`, DIN.py:166-173), in ONE
+ * launch that writes only the logits.
+ *   table [N][d] bf16 item embeddings; hist [nU][L] int32 history rows (-1 or
+ *   >= n_table = a zero padding slot: DIN.py:84-86, 108 softmaxes over all L);
+ *   user u's candidates: cand[cand_off[u] .. cand_off[u] + cand_len[u]) int32
+ *   rows, then extra[u] when extra != NULL (the appended ground truth of
+ *   finialize_retrieval.py:11-12; < 0 = a padded slot); rows outside [0, N)
+ *   get logit -inf.  Logits of user u: out[out_off[u] + c], c < cand_len[u]
+ *   (+ 1 with extra).  Candidate lists may be shared (the flow passes every
+ *   user of a cluster the same offset).
+ *   params: the model with its three eval-mode BatchNorms folded into the
+ *   Linears after them and every weight split into bf16 hi + lo
+ *   (newsrecommend_amd.pipeline.rerank_params).
+ * d in {64, 128, 256}, A and F in {32, 64, 96, 128}, L <= 64.  ws: >= 256 B
+ * (nrk_din_rerank_workspace), reset by the call (graph-capturable). */
+typedef struct nrk_din_rerank_params_s {
+  const void *W1q_hi, *W1q_lo;  /* bf16 [A][d]: W1[:, :d] (attention query half) */
+  const void *W1k_hi, *W1k_lo;  /* bf16 [A][d]: W1[:, d:] (key half) */
+  const float* b1;              /* [A] */
+  const float* w2;              /* [A] (b2 cancels in the softmax) */
+  const void *H1q_hi, *H1q_lo;  /* bf16 [F][d]: fc.1 with BN0 folded, query half */
+  const void *H1p_hi, *H1p_lo;  /* bf16 [F][d]: pooled half */
+  const float* c1;              /* [F] */
+  const void *H2_hi, *H2_lo;    /* bf16 [F/2][F]: fc.5 with BN1 folded */
+  const float* c2;              /* [F/2] */
+  const float* h3;              /* [F/2]: fc.9 with BN2 folded */
+  float c3;
+} nrk_din_rerank_params;
+int nrk_din_rerank_workspace(size_t* ws_bytes);
+int nrk_din_rerank(const void* table, int64_t n_table, int32_t dtype, const int32_t* hist, int32_t nU, int32_t L,
+                   const int32_t* cand, const int64_t* cand_off, const int32_t* cand_len, const int32_t* extra,
+                   const int64_t* out_off, float* out, int32_t d, int32_t A, int32_t F,
+                   const nrk_din_rerank_params* params, void* ws, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------ inverted lists --
  * faiss Clustering / IndexIVFFlat building blocks (Retrieval.py:11-23).

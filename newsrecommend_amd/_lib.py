@@ -67,15 +67,22 @@ SIGNATURES = {
     "nrk_din_batch_u": (ctypes.c_int, [c_p, c_i32, c_i32, c_p, c_p, c_i32, c_p, c_p, c_p]),
     "nrk_din_batch": (ctypes.c_int, [c_p, c_i32, c_p, c_p, c_p, c_i64, c_i32, c_p, c_i64, c_i32, c_i32, c_p, c_p,
                                      c_i32, c_p, c_p, c_p, c_p, c_p, c_p]),
-    "nrk_din_rerank_attn": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_i32, c_i32, c_p, c_i32, c_i32, c_i32, c_p, c_p,
-                                           c_i32, c_p, c_p]),
-    "nrk_din_item_proj": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_i64, c_i32, c_p, c_p, c_p, c_i32, c_p, c_p]),
-    "nrk_din_rerank_head": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_i32, c_p, c_p, c_p, c_p, c_i32, c_p, c_p, c_p,
-                                           c_f32, c_p, c_p]),
+    "nrk_din_rerank_workspace": (ctypes.c_int, [ctypes.POINTER(c_size)]),
+    "nrk_din_rerank": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_i32, c_i32,
+                                      c_i32, c_p, c_p, c_size, c_p]),
     "nrk_gather_rows": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_i64, c_i32, c_p, c_p]),
     "nrk_train_samples": (ctypes.c_int, [c_p, c_i64, c_p, c_i64, c_i32, c_p, c_i64, c_p, c_p, c_p, c_p]),
     "nrk_triplet_samples": (ctypes.c_int, [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p]),
 }
+
+
+
+class RerankParams(ctypes.Structure):
+    """nrk_din_rerank_params (include/nrk.h): device pointers of the folded,
+    hi/lo-split eval model (pipeline.rerank_params)."""
+    _fields_ = [(n, c_p) for n in ("W1q_hi", "W1q_lo", "W1k_hi", "W1k_lo", "b1", "w2", "H1q_hi", "H1q_lo", "H1p_hi",
+                                   "H1p_lo", "c1", "H2_hi", "H2_lo", "c2", "h3")] + [("c3", c_f32)]
+
 
 _lib = None
 

@@ -206,20 +206,21 @@ __device__ __forceinline__ int pow2ceil(int n) {
 // that good, so the fallback only has to collect those.
 struct FbState {
   int* list;        // [nq] queries, in slot order
-  int* count;       // [0] = slots used, [1] = overflow count
-  int slots;        // slots with candidate storage
-  double* thr_g;    // [slots]
-  int64_t* thr_i;   // [slots]
+  int* count;       // [0] = entries pushed, [1] = overflow count (fallback_select)
+  int slots;        // slots with candidate storage (n, the tiled fallback's candidate lists)
+  int tslots;       // slots with a stored threshold (>= slots)
+  double* thr_g;    // [tslots]
+  int64_t* thr_i;   // [tslots]
   int* n;           // [slots] candidates seen (may exceed cap)
   int force;        // testing: certify nothing
   __device__ void push(int qi, double g, int64_t i) const {
     const int s = atomicAdd(count, 1);
     list[s] = qi;
-    if (s < slots) {
+    if (s < tslots) {
       thr_g[s] = g;
       thr_i[s] = i;
-      n[s] = 0;
     }
+    if (s < slots) n[s] = 0;
   }
 };
 
@@ -901,7 +902,7 @@ __global__ __launch_bounds__(256) void small_select_wave_kernel(const double* __
 // with exact_score, and keeps the items at least as good as the slot's
 // threshold.  Cost = slots x nb x d fp64 FMA, spread over every CU.
 constexpr int FB_TR = 64;
-constexpr int FB_SLOTS_MAX = 16384;  // fallback / collect slots per search (uncertified queries beyond them: exact_topk)
+constexpr int FB_SLOTS_MAX = 16384;  // collect slots per round / tiled-fallback slots per search
 
 __global__ __launch_bounds__(256) void fallback_scan_kernel(const float* __restrict__ xq,
                                                             const float* __restrict__ xb, int64_t nb, int d,
@@ -1331,33 +1332,35 @@ __global__ __launch_bounds__(256) void collect_rescore_kernel(
 // collect_rescore ranks the candidates exactly.  Only a buffer overflow (more
 // than `cap` items within the bound) goes on to the tiled fp64 fallback.
 //
-// Collect storage is indexed by slot s (the merge's fallback order; the first
-// fb.slots uncertified queries, which are also the ones with a stored e_k).
-// One block: turns the merge's fallback list into the one-list work table
+// Collect storage is indexed by slot s: round r of the pass takes the merge's
+// fallback entries [r S, r S + S) (S = FB_SLOTS_MAX; every entry carries the
+// merge's e_k), so any number of uncertified queries is collected in
+// ceil(nq / S) rounds over the same fixed storage (a search of N x 4096
+// queries against one corpus shard leaves more than S uncertified at L2).
+// One block: turns this round's entries into the one-list work table
 // (list_off, seg_off, work_off, slot_pair = s), the per-slot thresholds and
-// the gathered bf16 query rows, saves the slot -> query map for
-// collect_rescore, and empties
-// the fallback list, which the overflowing queries refill.  Entries past the
-// storage (nq > 4096 only) stay in the fallback list, moved to its front,
-// with threshold -inf (they were pushed without one).
+// the gathered bf16 query rows, and saves the slot -> query map for
+// collect_rescore.  Queries whose candidates overflow the collect buffer go to
+// the tiled fallback's own list (collect_rescore pushes them there).
 __global__ __launch_bounds__(1024) void flat_collect_plan_kernel(
     FbState fb, int64_t nq, int64_t nb, int wq, int ch, const double* __restrict__ qmeta,
-    const float* __restrict__ stats, int dp, int l2, int cap, int force_overflow, int64_t* __restrict__ list_off,
-    int* __restrict__ seg_off, int* __restrict__ work_off, int* __restrict__ slot_pair, float* __restrict__ thr,
-    double* __restrict__ lb_g, int64_t* __restrict__ lb_i, int* __restrict__ cand_cnt, int* __restrict__ clist,
-    int* __restrict__ ccount, const uint16_t* __restrict__ qh, uint16_t* __restrict__ qc) {
+    const float* __restrict__ stats, int dp, int l2, int cap, int force_overflow, int round, int S,
+    int64_t* __restrict__ list_off, int* __restrict__ seg_off, int* __restrict__ work_off, int* __restrict__ slot_pair,
+    float* __restrict__ thr, double* __restrict__ lb_g, int64_t* __restrict__ lb_i, int* __restrict__ cand_cnt,
+    int* __restrict__ clist, int* __restrict__ ccount, const uint16_t* __restrict__ qh, uint16_t* __restrict__ qc) {
   const int t = threadIdx.x, nt = blockDim.x;
   const int n = (int)min((int64_t)fb.count[0], nq);
-  const int nc = n < fb.slots ? n : fb.slots;  // collected slots
+  const int lo = round * S;
+  const int nc = n - lo <= 0 ? 0 : (n - lo < S ? n - lo : S);  // this round's slots
   const int rows = (nc + wq - 1) / wq * wq;
   for (int s = t; s < rows; s += nt) slot_pair[s] = s < nc ? s : -1;
   for (int s = t; s < nc; s += nt) {
-    const int q = fb.list[s];
+    const int q = fb.list[lo + s];
     clist[s] = q;
-    const bool has = fb.thr_i[s] >= 0;  // the merge rescored >= k candidates
-    thr[s] = has ? collect_threshold(fb.thr_g[s], qmeta + 4 * q, stats, dp, l2) : INFINITY;
-    lb_g[s] = has ? fb.thr_g[s] : -INFINITY;
-    lb_i[s] = has ? fb.thr_i[s] : -1;
+    const bool has = fb.thr_i[lo + s] >= 0;  // the merge rescored >= k candidates
+    thr[s] = has ? collect_threshold(fb.thr_g[lo + s], qmeta + 4 * q, stats, dp, l2) : INFINITY;
+    lb_g[s] = has ? fb.thr_g[lo + s] : -INFINITY;
+    lb_i[s] = has ? fb.thr_i[lo + s] : -1;
     cand_cnt[s] = (has && !force_overflow) ? 0 : cap + 1;
   }
   if (t == 0) {
@@ -1372,31 +1375,13 @@ __global__ __launch_bounds__(1024) void flat_collect_plan_kernel(
   }
   // the collected slots' bf16 query rows (padding rows zero): one wave per row
   for (int row = t >> 6; row < rows; row += nt >> 6) {
-    const int64_t q = row < nc ? fb.list[row] : -1;
+    const int64_t q = row < nc ? fb.list[lo + row] : -1;
     for (int j = (t & 63) * 4; j < dp; j += 256) {
       uint2 v = make_uint2(0u, 0u);
       if (q >= 0) v = *reinterpret_cast<const uint2*>(qh + q * dp + j);
       *reinterpret_cast<uint2*>(qc + (int64_t)row * dp + j) = v;
     }
   }
-  __syncthreads();  // every thread has read fb.count and the collected part of fb.list
-  // the rest (s >= slots >= 1024 > nt): move to the front in rounds of nt;
-  // each round reads above everything written so far
-  for (int base = 0; base < n - nc; base += nt) {
-    const int src = nc + base + t;
-    const int q = src < n ? fb.list[src] : -1;
-    __syncthreads();
-    if (src < n) {
-      fb.list[base + t] = q;
-      if (base + t < fb.slots) {
-        fb.thr_g[base + t] = -INFINITY;
-        fb.thr_i[base + t] = -1;
-        fb.n[base + t] = 0;
-      }
-    }
-    __syncthreads();
-  }
-  if (t == 0) fb.count[0] = n - nc;
 }
 
 // ================================================================== plan ==
@@ -1411,7 +1396,7 @@ struct FlatPlan {
   int fb_slots, fb_cap;     // tiled fallback: slots with candidate storage, candidates per slot
   int64_t nq_pad, chunk, chunk_pre;
   size_t off_qh, off_qmeta, off_ps, off_pi, off_pt, off_fbl, off_fbc, off_tau, off_pre, total;
-  size_t off_fbt, off_fbi, off_fbn, off_fcg, off_fci, off_ovl;
+  size_t off_fbt, off_fbi, off_fbn, off_fcg, off_fci, off_ovl, off_tfl, off_tft, off_tfi;
   // collect pass for uncertified queries (flat_collect_plan_kernel)
   int cwq, cch, ccap, cgrid;
   int64_t crows;
@@ -1585,27 +1570,32 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
   p.off_pi = take((size_t)nq * p.U * 4);
   p.off_pt = take((size_t)nq * p.nch * 2 * 4);
   p.off_fbl = take((size_t)nq * 4);
-  // fallback storage: candidates at least as good as the merge's k-th; the cap
-  // leaves room for 2k + 64 (ties and near-ties), overflow goes to exact_topk.
-  // A slot for every query up to FB_SLOTS_MAX (16 K): a corpus shard searched
-  // by N x 4096 queries (weak scaling) leaves more than 4096 of them uncertified
-  // at L2, and the queries beyond the slots took the block-per-query exact scan
-  // (2.3 s for 574 queries over a 2.5M-row shard at world 4).  Each slot holds
+  // Uncertified queries are collected in rounds of FB_SLOTS_MAX (16 K) slots,
+  // as many rounds as nq needs (a corpus shard searched by N x 4096 queries
+  // leaves more than 4096 of them uncertified at L2; queries beyond a fixed
+  // slot budget used to take the block-per-query exact scan: 2.3 s for 574
+  // queries over a 2.5M-row shard at world 4).  The tiled fp64 fallback then
+  // takes the (rare) queries whose collect buffer overflowed, with storage for
+  // candidates at least as good as the merge's k-th; its cap leaves room for
+  // 2k + 64 (ties and near-ties), overflow goes to exact_topk.  Each slot holds
   // fb_cap x 16 B of fallback candidates and ccap x 4 B of collect positions
   // (16 KB at k <= 224), so the cap bounds this part of the workspace at 256 MB
-  // (it was 1 GB at 64 K slots, almost all of it idle)
   p.fb_slots = (int)(nq < FB_SLOTS_MAX ? nq : FB_SLOTS_MAX);
   p.fb_cap = host_pow2ceil(2 * k + 64);
   if (p.fb_cap < 512) p.fb_cap = 512;
   p.fb_cap = test_hook("NRK_FB_CAP", p.fb_cap);
   if (p.fb_cap < 1) p.fb_cap = 1;
   if (p.fb_cap > 8192) p.fb_cap = 8192;  // select kernel sorts cap x 16 B in LDS
-  p.off_fbt = take((size_t)p.fb_slots * 8);
-  p.off_fbi = take((size_t)p.fb_slots * 8);
+  p.off_fbt = take((size_t)nq * 8);  // the merge's e_k of every uncertified query
+  p.off_fbi = take((size_t)nq * 8);
   p.off_fbn = take((size_t)p.fb_slots * 4);
   p.off_fcg = take((size_t)p.fb_slots * p.fb_cap * 8);
   p.off_fci = take((size_t)p.fb_slots * p.fb_cap * 8);
   p.off_ovl = take((size_t)nq * 4);
+  // the tiled fallback's own list (queries whose collect buffer overflowed)
+  p.off_tfl = take((size_t)nq * 4);
+  p.off_tft = take((size_t)p.fb_slots * 8);
+  p.off_tfi = take((size_t)p.fb_slots * 8);
   // collect pass: one query tile per wave (128 queries per work item), 4096-row
   // chunks (each chunk's query tiles run back to back on one XCD), storage for
   // the fb_slots uncertified queries that carry an e_k
@@ -1816,14 +1806,24 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
   int* pi = reinterpret_cast<int*>(w + p.off_pi);
   float* pt = reinterpret_cast<float*>(w + p.off_pt);
   int* fbl = reinterpret_cast<int*>(w + p.off_fbl);
-  FbState fb;
+  FbState fb;  // the merge's uncertified queries (collect pass, in rounds)
   fb.list = fbl;
   fb.count = fbc;
-  fb.slots = p.fb_slots;
+  fb.slots = 0;
+  fb.tslots = (int)nq;
   fb.thr_g = reinterpret_cast<double*>(w + p.off_fbt);
   fb.thr_i = reinterpret_cast<int64_t*>(w + p.off_fbi);
-  fb.n = reinterpret_cast<int*>(w + p.off_fbn);
+  fb.n = nullptr;
   fb.force = test_hook("NRK_FORCE_FALLBACK", 0);
+  FbState fbt;  // the tiled fp64 fallback (collect buffer overflow)
+  fbt.list = reinterpret_cast<int*>(w + p.off_tfl);
+  fbt.count = fbc + 2;
+  fbt.slots = p.fb_slots;
+  fbt.tslots = p.fb_slots;
+  fbt.thr_g = reinterpret_cast<double*>(w + p.off_tft);
+  fbt.thr_i = reinterpret_cast<int64_t*>(w + p.off_tfi);
+  fbt.n = reinterpret_cast<int*>(w + p.off_fbn);
+  fbt.force = 0;
   double* fcg = reinterpret_cast<double*>(w + p.off_fcg);
   int64_t* fci = reinterpret_cast<int64_t*>(w + p.off_fci);
   int* ovl = reinterpret_cast<int*>(w + p.off_ovl);
@@ -1880,33 +1880,36 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
     int* cpos = reinterpret_cast<int*>(w + p.off_cpos);
     int* clist = reinterpret_cast<int*>(w + p.off_clist);
     int* ccount = reinterpret_cast<int*>(w + p.off_ccount);
-    hipLaunchKernelGGL(flat_collect_plan_kernel, dim3(1), dim3(1024), 0, st, fb, nq, nb, p.cwq, p.cch, qmeta, stats,
-                       p.dp, l2, p.ccap, fb.force >= 2 ? 1 : 0, clo, cseg, cwork, csp, cthr, clbg, clbi, ccnt, clist,
-                       ccount, qh, cqi);
-    NRK_CHECK_LAUNCH("flat_collect_plan_kernel");
     screen_fn fc = pick_screen(p.dp, 1, p.M, l2 != 0, 3);
     if (!fc) return fail(NRK_EUNSUPPORTED, "knn_flat: no collect kernel for dp=%d", p.dp);
     IvfScreen isc{cwork, clo, cseg, csp, 1, p.cch, (int)cdiv(nb, (int64_t)p.cch), cthr, ccnt, cpos, p.ccap, 1};
-    hipLaunchKernelGGL(fc, dim3((unsigned)p.cgrid), dim3(4 * 64), 0, st, cqi, xb_bf16, xb_meta, (int64_t)p.fb_slots, nb,
-                       0, 0, 0, 1, nullptr, nullptr, nullptr, nullptr, isc);
-    NRK_CHECK_LAUNCH("screen_kernel (flat collect)");
     const size_t smem = (size_t)host_pow2ceil(p.ccap) * 16 + (size_t)d * 4;
-    hipLaunchKernelGGL(collect_rescore_kernel, dim3((unsigned)p.fb_slots), dim3(256), smem, st, ccnt, cpos, p.ccap,
-                       nullptr, xq, xb, d, k, l2, clbg, clbi, D, I, S, id_offset, fb, clist, ccount);
-    NRK_CHECK_LAUNCH("collect_rescore_kernel (flat)");
+    const int rounds = (int)cdiv(nq, (int64_t)FB_SLOTS_MAX);
+    for (int r = 0; r < rounds; ++r) {  // each round exits at once when it has no queries
+      hipLaunchKernelGGL(flat_collect_plan_kernel, dim3(1), dim3(1024), 0, st, fb, nq, nb, p.cwq, p.cch, qmeta, stats,
+                         p.dp, l2, p.ccap, fb.force >= 2 ? 1 : 0, r, FB_SLOTS_MAX, clo, cseg, cwork, csp, cthr, clbg,
+                         clbi, ccnt, clist, ccount, qh, cqi);
+      NRK_CHECK_LAUNCH("flat_collect_plan_kernel");
+      hipLaunchKernelGGL(fc, dim3((unsigned)p.cgrid), dim3(4 * 64), 0, st, cqi, xb_bf16, xb_meta, (int64_t)p.fb_slots,
+                         nb, 0, 0, 0, 1, nullptr, nullptr, nullptr, nullptr, isc);
+      NRK_CHECK_LAUNCH("screen_kernel (flat collect)");
+      hipLaunchKernelGGL(collect_rescore_kernel, dim3((unsigned)p.fb_slots), dim3(256), smem, st, ccnt, cpos, p.ccap,
+                         nullptr, xq, xb, d, k, l2, clbg, clbi, D, I, S, id_offset, fbt, clist, ccount);
+      NRK_CHECK_LAUNCH("collect_rescore_kernel (flat)");
+    }
   }
   {
     const int64_t ntiles = cdiv(nb, (int64_t)FB_TR);
     const int grid = (int)(ntiles < 2048 ? ntiles : 2048);
     hipLaunchKernelGGL(fallback_scan_kernel, dim3(grid), dim3(256), (size_t)FB_TR * (d + 1) * 4, st, xq, xb, nb, d,
-                       l2, fb, fcg, fci, p.fb_cap, IvfFb{});
+                       l2, fbt, fcg, fci, p.fb_cap, IvfFb{});
     NRK_CHECK_LAUNCH("fallback_scan_kernel");
-    hipLaunchKernelGGL(fallback_select_kernel, dim3(256), dim3(256), (size_t)host_pow2ceil(p.fb_cap) * 16, st, fb, fcg, fci,
-                       p.fb_cap, k, l2, D, I, S, id_offset, ovl);
+    hipLaunchKernelGGL(fallback_select_kernel, dim3(256), dim3(256), (size_t)host_pow2ceil(p.fb_cap) * 16, st, fbt, fcg,
+                       fci, p.fb_cap, k, l2, D, I, S, id_offset, ovl);
     NRK_CHECK_LAUNCH("fallback_select_kernel");
   }
-  int rc = exact_launch(xq, nq, xb, nb, d, k, l2, ovl, fbc + 1, 256, D, I, S, id_offset, st, IvfFb{}, n_fallback,
-                        reinterpret_cast<const int*>(w + p.off_ccount + 4), fbc);
+  int rc = exact_launch(xq, nq, xb, nb, d, k, l2, ovl, fbt.count + 1, 256, D, I, S, id_offset, st, IvfFb{}, n_fallback,
+                        reinterpret_cast<const int*>(w + p.off_ccount + 4), fbt.count);
   if (rc != NRK_OK) return rc;
   mark(4);
   return NRK_OK;
@@ -2134,6 +2137,7 @@ extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe,
   fb.list = reinterpret_cast<int*>(w + p.off_fbl);
   fb.count = fbc;
   fb.slots = p.fb_slots;
+  fb.tslots = p.fb_slots;
   fb.thr_g = reinterpret_cast<double*>(w + p.off_fbt);
   fb.thr_i = reinterpret_cast<int64_t*>(w + p.off_fbi);
   fb.n = reinterpret_cast<int*>(w + p.off_fbn);

@@ -55,13 +55,14 @@ def _pad_last(t: torch.Tensor, width: int) -> torch.Tensor:
 
 
 class KernelTimer:
-    """Bench hook: while active, brackets each attention kernel launch with
+    """Bench hook: while active, brackets each kernel launch that marks itself
+    (the attention kernels: "fwd" / "bwd"; the fused re-rank: "rerank") with
     torch.cuda.Event pairs on the launch stream (the current stream)."""
 
     active = None
 
     def __init__(self):
-        self.fwd, self.bwd = [], []
+        self.ev = {}
 
     def __enter__(self):
         KernelTimer.active = self
@@ -86,10 +87,10 @@ class KernelTimer:
             return
         end = torch.cuda.Event(enable_timing=True)
         end.record()
-        (t.fwd if kind == "fwd" else t.bwd).append((start, end))
+        t.ev.setdefault(kind, []).append((start, end))
 
     def mean_ms(self, kind, skip=0):
-        ev = (self.fwd if kind == "fwd" else self.bwd)[skip:]
+        ev = self.ev.get(kind, [])[skip:]
         return sum(a.elapsed_time(b) for a, b in ev) / max(len(ev), 1)
 
 

@@ -21,12 +21,13 @@ stage is a batch over users, with ids instead of embeddings:
 """
 from __future__ import annotations
 
+import ctypes
 import warnings
 
 import numpy as np
 import torch
 
-RERANK_SHARED_MAX_L = 64  # nrk_din_rerank_attn holds the history image of one user in LDS
+RERANK_MAX_L = 64  # nrk_din_rerank holds one user's history rows (and their projections) in LDS
 
 
 def cluster_candidates(centroid_index, cluster_lists, profiles: np.ndarray, uids) -> dict:
@@ -83,83 +84,94 @@ def _split_bf16(w: torch.Tensor):
     return hi.contiguous(), (w - hi.float()).to(torch.bfloat16).contiguous()
 
 
-def _rerank_shared(model, table, hist_rows, cand_rows, batch_samples):
-    """Shared-history path, three HIP kernels per batch of users:
-      nrk_din_item_proj    [U | Q1] = q [W1q ; H1q]^T + [b1 ; 0] gathered from
-                           the bf16 table (the attention query half and the
-                           head's first-layer query half in one pass),
-      nrk_din_rerank_attn  P = K W1k^T once per user, per-candidate scores,
-                           softmax over the L slots, pooled = alpha K,
-      nrk_din_rerank_head  the eval-mode head (BatchNorms folded into the
-                           Linears) -> logits, -inf on padded candidates.
-    Heads the fused kernel does not cover (F != 32, BatchNorm without running
-    statistics) run as torch ops on the gathered rows."""
-    from . import _lib
-    from .din import gather_rows
+_PARAMS_CACHE: dict = {}
 
-    U, C = cand_rows.shape
-    L = hist_rows.shape[1]
-    d = table.shape[1]
-    dev = table.device
-    W1, b1 = model.attn.attn[0].weight, model.attn.attn[0].bias
-    A = W1.shape[0]
-    W1k = W1[:, d:].to(torch.bfloat16).contiguous()
-    w2 = model.attn.attn[2].weight.reshape(-1).contiguous()
+
+def rerank_params(model, d: int):
+    """The eval model as nrk_din_rerank takes it (include/nrk.h
+    nrk_din_rerank_params): W1 = [W1q | W1k] (DIN.py:99), w2, b1; the head with
+    its three BatchNorms folded into the Linears after them (_fold_eval_head);
+    every weight the kernel feeds to a bf16 MFMA split into hi + lo.  Returns
+    (params struct, A, F, tensors kept alive) or None when the head has no
+    running statistics.  Cached per model until any parameter or buffer
+    changes (torch's version counters)."""
+    from . import _lib
+
+    tens = list(model.parameters()) + list(model.buffers())
+    key = (id(model), tuple(t._version for t in tens), tuple(t.data_ptr() for t in tens))
+    hit = _PARAMS_CACHE.get(id(model))
+    if hit is not None and hit[0] == key:
+        return hit[1]
     head = _fold_eval_head(model.fc)
-    fused = head is not None and head[0][0].shape[0] == 32
-    if fused:
-        (H1, c1), (H2, c2), (H3, c3) = head
-        F = H1.shape[0]
-        Wcat = torch.cat([W1[:, :d], H1[:, :d]], 0)
-        bcat = torch.cat([b1, torch.zeros(F, device=dev)]).contiguous()
-    else:
-        Wcat, bcat = W1[:, :d], b1.contiguous()
-        if head is not None:
-            (H1, c1), (H2, c2), (H3, c3) = head
-            H1q, H1p = H1[:, :d].t(), H1[:, d:].t()
-    NO = max(128, -(-Wcat.shape[0] // 32) * 32)  # nrk_din_item_proj: 128..256 outputs, zero rows pad
-    Wpad = torch.zeros((NO, d), device=dev)
-    Wpad[:Wcat.shape[0]] = Wcat
-    bpad = torch.zeros(NO, device=dev)
-    bpad[:bcat.shape[0]] = bcat
-    W_hi, W_lo = _split_bf16(Wpad)
-    if fused:
-        Hp_hi, Hp_lo = _split_bf16(H1[:, d:].contiguous())
-        H2c, c2c, h3c = H2.contiguous(), c2.contiguous(), H3.reshape(-1).contiguous()
-        c3v = float(c3.reshape(-1)[0])
-    lib = _lib.load()
-    st = _lib.stream(dev)
-    out = torch.empty((U, C), dtype=torch.float32, device=dev)
-    ub = max(1, batch_samples // max(C, 1))
-    for lo in range(0, U, ub):
-        hi = min(U, lo + ub)
-        n = (hi - lo) * C
-        cr = cand_rows[lo:hi].reshape(-1).to(torch.int32).contiguous()
-        proj = torch.empty((n, NO), dtype=torch.float32, device=dev)
-        _lib.check(lib.nrk_din_item_proj(_lib.ptr(table), table.shape[0], _lib.NRK_DTYPE_BF16, _lib.ptr(cr), n, d,
-                                         _lib.ptr(W_hi), _lib.ptr(W_lo), _lib.ptr(bpad), NO, _lib.ptr(proj), st),
-                   "din_item_proj")
-        pooled = torch.empty((n, d), dtype=torch.float32, device=dev)
-        hr = hist_rows[lo:hi].to(torch.int32).contiguous()
-        _lib.check(lib.nrk_din_rerank_attn(
-            _lib.ptr(table), table.shape[0], _lib.NRK_DTYPE_BF16, _lib.ptr(hr), hi - lo, L, _lib.ptr(proj), NO, C, d,
-            _lib.ptr(W1k), _lib.ptr(w2), A, _lib.ptr(pooled), st), "din_rerank_attn")
-        if fused:
-            lg = torch.empty(n, dtype=torch.float32, device=dev)
-            _lib.check(lib.nrk_din_rerank_head(
-                _lib.ptr(pooled), n, d, _lib.ptr(proj) + 4 * A, NO, _lib.ptr(cr), _lib.ptr(Hp_hi), _lib.ptr(Hp_lo),
-                _lib.ptr(c1), F, _lib.ptr(H2c), _lib.ptr(c2c), _lib.ptr(h3c), c3v, _lib.ptr(lg), st),
-                "din_rerank_head")
-            out[lo:hi] = lg.view(hi - lo, C)
-            continue
-        q = gather_rows(table, cr)
-        if head is None:
-            lg = model.fc(torch.cat([q, pooled], dim=1)).view(hi - lo, C)
-        else:
-            h1 = torch.addmm(c1, q, H1q).addmm_(pooled, H1p).relu_()
-            lg = torch.addmm(c3, torch.addmm(c2, h1, H2.t()).relu_(), H3.t()).view(hi - lo, C)
-        out[lo:hi] = torch.where(cand_rows[lo:hi] >= 0, lg, torch.full_like(lg, -float("inf")))
+    if head is None:
+        return None
+    W1, b1 = model.attn.attn[0].weight, model.attn.attn[0].bias
+    w2 = model.attn.attn[2].weight.reshape(-1).contiguous().float()
+    (H1, c1), (H2, c2), (H3, c3) = head
+    keep = {}
+    for name, t in (("W1q", W1[:, :d]), ("W1k", W1[:, d:]), ("H1q", H1[:, :d]), ("H1p", H1[:, d:]), ("H2", H2)):
+        keep[name + "_hi"], keep[name + "_lo"] = _split_bf16(t.detach().float().contiguous())
+    keep["b1"] = b1.detach().float().contiguous()
+    keep["w2"] = w2.detach()
+    keep["c1"] = c1.detach().float().contiguous()
+    keep["c2"] = c2.detach().float().contiguous()
+    keep["h3"] = H3.detach().reshape(-1).float().contiguous()
+    prm = _lib.RerankParams(**{k: v.data_ptr() for k, v in keep.items()}, c3=float(c3.reshape(-1)[0]))
+    out = (prm, W1.shape[0], H1.shape[0], keep)
+    _PARAMS_CACHE[id(model)] = (key, out)
     return out
+
+
+def rerank_ragged(model, table: torch.Tensor, hist_rows: torch.Tensor, cand: torch.Tensor, cand_off: torch.Tensor,
+                  cand_len: torch.Tensor, extra: torch.Tensor | None, out_off: torch.Tensor, n_out: int,
+                  prm=None) -> torch.Tensor:
+    """nrk_din_rerank: one launch for all users.  User u scores
+    cand[cand_off[u] : cand_off[u] + cand_len[u]] (+ extra[u] when given, -1 =
+    a padded slot) against its history hist_rows[u] and writes
+    out[out_off[u] + c]; rows outside the table get -inf.  Returns out (n_out,)
+    f32 (entries not covered by any user stay uninitialised)."""
+    from . import _lib
+
+    dev = table.device
+    U, L = hist_rows.shape
+    d = table.shape[1]
+    if prm is None:
+        prm = rerank_params(model, d)
+    p, A, F, _keep = prm
+    out = torch.empty(n_out, dtype=torch.float32, device=dev)
+    if U == 0:
+        return out
+    lib = _lib.load()
+    sz = _lib.c_size(0)
+    _lib.check(lib.nrk_din_rerank_workspace(sz), "din_rerank_workspace")
+    ws = torch.empty(sz.value, dtype=torch.uint8, device=dev)
+    h = hist_rows.to(torch.int32).contiguous()
+    c = cand.to(torch.int32).contiguous()
+    co, cl, oo = cand_off.to(torch.int64).contiguous(), cand_len.to(torch.int32).contiguous(), \
+        out_off.to(torch.int64).contiguous()
+    ex = extra.to(torch.int32).contiguous() if extra is not None else None
+    from .din import KernelTimer
+
+    t0 = KernelTimer.mark("rerank")
+    _lib.check(lib.nrk_din_rerank(_lib.ptr(table), table.shape[0], _lib.NRK_DTYPE_BF16, _lib.ptr(h), U, L, _lib.ptr(c),
+                                  _lib.ptr(co), _lib.ptr(cl), _lib.ptr(ex), _lib.ptr(oo), _lib.ptr(out), d, A, F,
+                                  ctypes.byref(p), _lib.ptr(ws), ws.numel(), _lib.stream(dev)), "din_rerank")
+    KernelTimer.push("rerank", t0)
+    return out
+
+
+def fused_ok(model, table: torch.Tensor, L: int):
+    """Why the fused re-rank kernel cannot run this model / table (empty: it can)."""
+    W1 = model.attn.attn[0].weight
+    A, F = W1.shape[0], model.fc[1].weight.shape[0]
+    d = table.shape[1]
+    return [w for w, bad in (("table is not bf16", table.dtype != torch.bfloat16),
+                             (f"emb_dim {d} not in (64, 128, 256)", d not in (64, 128, 256)),
+                             (f"history length {L} > {RERANK_MAX_L}", L > RERANK_MAX_L),
+                             (f"attn_units {A} not in (32, 64, 96, 128)", A not in (32, 64, 96, 128)),
+                             (f"fc_units {F} not in (32, 64, 96, 128)", F not in (32, 64, 96, 128)),
+                             ("model emb_dim != table width", W1.shape[1] != 2 * d),
+                             ("BatchNorm without running statistics", _fold_eval_head(model.fc) is None)) if bad]
 
 
 @torch.no_grad()
@@ -168,25 +180,26 @@ def rerank(model, table: torch.Tensor, hist_rows: torch.Tensor, cand_rows: torch
     """DIN logits (U, C) for candidate rows (U, C) (-1 = padding -> -inf) of
     users with history rows (U, L) (-1 = padding), all rows of `table` on the
     device.  Eval-mode BatchNorm is row-independent, so one forward over many
-    users equals the reference's per-user forwards.  With a bf16 table
-    (d in {64, 128, 256}, L <= 64) the attention runs shared per user
-    (nrk_din_rerank_attn); otherwise every candidate is a DIN sample."""
+    users equals the reference's per-user forwards.  With a bf16 table,
+    d in {64, 128, 256}, L <= 64, A and F in {32, 64, 96, 128} the whole
+    evaluate() forward is one fused kernel (nrk_din_rerank); otherwise every
+    candidate is a DIN sample (model.forward_ids, C x the attention work)."""
     model.eval()
     U, C = cand_rows.shape
     L = hist_rows.shape[1]
-    why = [w for w, bad in (("shared=False", not shared), ("table is not bf16", table.dtype != torch.bfloat16),
-                            (f"emb_dim {table.shape[1]} not in (64, 128, 256)", table.shape[1] not in (64, 128, 256)),
-                            (f"history length {L} > {RERANK_SHARED_MAX_L}", L > RERANK_SHARED_MAX_L),
-                            ("model emb_dim != table width", model.attn.attn[0].weight.shape[1] != 2 * table.shape[1]))
-           if bad]
+    why = (["shared=False"] if not shared else []) + fused_ok(model, table, L)
     # which path ran, for callers and benchmarks (the per-candidate one costs C x the attention work)
-    rerank.path = "shared" if not why else "per-candidate: " + ", ".join(why)
+    rerank.path = "fused" if not why else "per-candidate: " + ", ".join(why)
+    dev = table.device
     if not why:
-        return _rerank_shared(model, table, hist_rows, cand_rows, batch_samples)
+        off = torch.arange(U, device=dev, dtype=torch.int64) * C
+        out = rerank_ragged(model, table, hist_rows, cand_rows.reshape(-1), off,
+                            torch.full((U,), C, dtype=torch.int32, device=dev), None, off, U * C)
+        return out.view(U, C)
     if shared:
-        warnings.warn(f"rerank: {rerank.path} -> per-candidate DIN forward (C x the attention work of the shared "
+        warnings.warn(f"rerank: {rerank.path} -> per-candidate DIN forward (C x the attention work of the fused "
                       f"path)", stacklevel=2)
-    out = torch.empty((U, C), dtype=torch.float32, device=table.device)
+    out = torch.empty((U, C), dtype=torch.float32, device=dev)
     ub = max(1, batch_samples // max(C, 1))
     for lo in range(0, U, ub):
         hi = min(U, lo + ub)
@@ -200,6 +213,13 @@ def rerank(model, table: torch.Tensor, hist_rows: torch.Tensor, cand_rows: torch
 rerank.path = None
 
 
+def _seg_sum(x: torch.Tensor, start: torch.Tensor, end: torch.Tensor) -> torch.Tensor:
+    """Sums of x over the segments [start, end) (cumulative-sum differences)."""
+    c = torch.zeros(x.numel() + 1, dtype=x.dtype, device=x.device)
+    torch.cumsum(x, 0, out=c[1:])
+    return c[end] - c[start]
+
+
 @torch.no_grad()
 def rerank_clusters(model, table: torch.Tensor, hist_rows: torch.Tensor, user_cluster: torch.Tensor,
                     cluster_off: torch.Tensor, cluster_rows: torch.Tensor, last_rows: torch.Tensor | None = None,
@@ -208,62 +228,100 @@ def rerank_clusters(model, table: torch.Tensor, hist_rows: torch.Tensor, user_cl
     user's candidates are the WHOLE cluster its profile is nearest to
     (cluster_candidates), so all users of cluster c share one ragged list,
     rows cluster_rows[cluster_off[c]:cluster_off[c+1]] (corpus row order).
-    Users are grouped by cluster and each group is re-ranked as a padding-free
-    (n_users_c, C_c) batch (rerank, the shared-history kernels).
+    Users are grouped by cluster and ALL of them are scored by one fused
+    launch (nrk_din_rerank: each user's offset points at its cluster's list).
 
     last_rows (U,) -- the row of each user's last click -- gives
     EvalDataset's labels (one-hot at the FIRST candidate equal to it, none when
     absent; DIN.py:27-31), the per-user BCE (DIN.py:176-177) and NDCG@k
     (DIN.py:181-189, ndcg_at_k's tie rule).  append_missing: the ground truth
     (the last click) is appended to a user's list when the cluster lacks it
-    (finialize_retrieval.py:11-12): one extra column per group, -1 (padding,
-    excluded from the loss) where the cluster holds it.  Returns a dict:
-    `logits` list of (n_users_c, C_c [+1]) per cluster, `users` list of the
-    user indices of each group, and with last_rows `loss` (U,) f64 and
-    `ndcg` (U,) f64."""
+    (finialize_retrieval.py:11-12): one extra column per user, -1 (padding,
+    excluded from the loss) where the cluster holds it; a user whose cluster
+    is empty then scores the ground truth alone.  A user left with no
+    candidate at all gets loss and NDCG NaN (not 0), so means over users do
+    not silently count it.  Returns a dict: `logits` list of
+    (n_users_c, C_c [+1]) per non-empty group, `users` the user indices of
+    each group, and with last_rows `loss` (U,) f64 and `ndcg` (U,) f64."""
     dev = table.device
-    U = hist_rows.shape[0]
+    U, L = hist_rows.shape
     uc = user_cluster.to(dev).long()
     off = cluster_off.to(dev).long()
     rows = cluster_rows.to(dev).to(torch.int32)
+    nl = off.numel() - 1
+    why = fused_ok(model, table, L)
+    if why:
+        raise ValueError("rerank_clusters: the fused re-rank cannot run this model / table: " + ", ".join(why))
+    model.eval()
     order = torch.sort(uc, stable=True).indices
-    bounds = torch.searchsorted(uc[order], torch.arange(off.numel(), device=dev))
-    bh = bounds.cpu().tolist()  # one small host read: the group boundaries
-    oh = off.cpu().tolist()
+    ucs = uc[order]
+    sizes = (off[1:] - off[:-1])
+    clen = sizes[ucs]  # (U,) candidates of each user (in group order)
+    coff = off[ucs]
+    last = last_rows.to(dev).long()[order] if last_rows is not None else None
+    pos_in = None
+    if last is not None:
+        # position of the last click inside its user's cluster list (-1: absent),
+        # by a sorted search over (cluster, row) keys
+        n_tab = table.shape[0]
+        member_cl = torch.repeat_interleave(torch.arange(nl, device=dev), sizes)
+        keys = member_cl * (n_tab + 1) + rows.long()
+        skeys, sidx = torch.sort(keys)
+        q = ucs * (n_tab + 1) + last.clamp(0, n_tab)
+        if skeys.numel():
+            at = torch.searchsorted(skeys, q).clamp_max(skeys.numel() - 1)
+            found = (skeys[at] == q) & (last >= 0)
+            pos_in = torch.where(found, sidx[at] - coff, torch.full_like(last, -1))
+        else:
+            pos_in = torch.full_like(last, -1)
+    extra = None
+    if last is not None and append_missing:
+        extra = torch.where(pos_in >= 0, torch.full_like(last, -1), last).to(torch.int32)
+    width = clen + (1 if extra is not None else 0)
+    oo = torch.zeros(U + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(width, 0, out=oo[1:])
+    n_out = int(oo[-1].item())
+    flat = rerank_ragged(model, table, hist_rows[order], rows, coff, clen, extra, oo[:-1], n_out)
+    rerank.path = "fused"
     out = {"logits": [], "users": []}
-    if last_rows is not None:
-        loss = torch.zeros(U, dtype=torch.float64, device=dev)
-        ndcg = torch.zeros(U, dtype=torch.float64, device=dev)
-        last = last_rows.to(dev).to(torch.int32)
-    for c in range(off.numel() - 1):
+    cnt = torch.bincount(ucs, minlength=nl)
+    bh = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), torch.cumsum(cnt, 0)]).cpu().tolist()
+    wh = (sizes + (1 if extra is not None else 0)).cpu().tolist()
+    oh = oo.cpu().tolist()
+    for c in range(nl):
         lo, hi = bh[c], bh[c + 1]
-        if hi <= lo or oh[c + 1] <= oh[c]:
-            continue
-        us = order[lo:hi]
-        cand = rows[oh[c]:oh[c + 1]]
-        C = cand.numel()
-        cu = cand[None, :].expand(hi - lo, C)
-        if last_rows is not None and append_missing:
-            lu = last[us]
-            extra = torch.where((cu == lu[:, None]).any(1), torch.full_like(lu, -1), lu)
-            cu = torch.cat([cu, extra[:, None]], 1)
-        lg = rerank(model, table, hist_rows[us], cu, batch_samples=batch_samples)
-        out["logits"].append(lg)
-        out["users"].append(us)
-        if last_rows is not None:
-            hit = (cu == last[us][:, None]) & (cu >= 0)
-            first = torch.where(hit.any(1), hit.to(torch.int8).argmax(1), torch.full_like(us, -1))
-            lab = torch.zeros(cu.shape, dtype=torch.bool, device=dev)
-            has = first >= 0
-            lab[has.nonzero().squeeze(1), first[has]] = True
-            valid = cu >= 0
-            per = torch.nn.functional.binary_cross_entropy_with_logits(lg.clamp_min(-1e30), lab.float(),
-                                                                       reduction="none")
-            per = torch.where(valid, per.double(), torch.zeros_like(per, dtype=torch.float64))
-            loss[us] = per.sum(1) / valid.sum(1).double()
-            ndcg[us] = ndcg_at_k(lg, lab, k)
-    if last_rows is not None:
-        out["loss"], out["ndcg"] = loss, ndcg
+        if hi > lo and wh[c] > 0:
+            out["logits"].append(flat[oh[lo]:oh[hi]].view(hi - lo, wh[c]))
+            out["users"].append(order[lo:hi])
+    if last is not None:
+        # labels: one-hot at the first occurrence of the last click (its cluster
+        # position, else the appended column), BCE over the valid candidates
+        # (DIN.py:176-177), NDCG@k with ndcg_at_k's rule, all as segment sums
+        has_pos = pos_in >= 0
+        pcol = torch.where(has_pos, pos_in, clen if extra is not None else torch.full_like(clen, -1))
+        if extra is not None:
+            has_pos = has_pos | (extra >= 0)
+        pidx = oo[:-1] + pcol.clamp_min(0)
+        seg = torch.repeat_interleave(torch.arange(U, device=dev), width)
+        x = flat.double()
+        valid = torch.isfinite(x)
+        y = torch.zeros_like(x)
+        y[pidx[has_pos]] = 1.0
+        per = torch.where(valid, x.clamp_min(0) - x * y + torch.log1p(torch.exp(-x.abs())), torch.zeros_like(x))
+        nval = _seg_sum(valid.double(), oo[:-1], oo[1:])
+        loss = _seg_sum(per, oo[:-1], oo[1:]) / nval
+        pr = torch.sigmoid(flat)
+        pp = pr[pidx]
+        col = torch.arange(n_out, device=dev) - oo[:-1][seg]
+        before = (pr > pp[seg]) | ((pr == pp[seg]) & (col < pcol[seg]))
+        rank = _seg_sum(before.long(), oo[:-1], oo[1:]) + 1
+        nd = torch.where(has_pos & (rank <= k), 1.0 / torch.log2(rank.double() + 1.0), torch.zeros_like(loss))
+        nd = torch.where(nval > 0, nd, torch.full_like(nd, float("nan")))
+        loss_u = torch.empty(U, dtype=torch.float64, device=dev)
+        ndcg_u = torch.empty(U, dtype=torch.float64, device=dev)
+        loss_u[order] = loss
+        ndcg_u[order] = nd
+        out["loss"], out["ndcg"] = loss_u, ndcg_u
     return out
 
 

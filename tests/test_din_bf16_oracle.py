@@ -6,15 +6,19 @@ tests/test_oracle_din.py) and against the reference's evaluate() fixture.
     L = 50, bf16 table, B = 512, dropout 0): loss, every clipped gradient, the
     BatchNorm running statistics and the parameters after two clip + Adam steps
     (DIN.py:143-151).
-  * nrk_din_rerank_attn (the shared-history re-rank configs[4] runs) at
-    d = 256, L = 50, C = 201: logits and NDCG@5 (DIN.py:155-193).
+  * nrk_din_rerank (the fused evaluate() forward configs[4] and the
+    Retrieval.py flow run) at d = 256, L = 50, C = 201: logits and NDCG@5
+    (DIN.py:155-193).
 
-Two oracles per check:
-  "emulated" — the oracle fed exactly the kernel's inputs: the bf16 table
-      (upcast, exact) AND W1[:, d:] rounded to bf16 the way the kernels round
-      it.  What remains is fp32 accumulation order, so tolerances are tight.
-  "reference" — the oracle with the model's f32 W1 (the reference's exact
-      arithmetic).  The gap adds the bf16 rounding of W1k (relative 2^-9).
+Oracles:
+  train: "emulated" — the oracle fed exactly the kernel's inputs: the bf16
+      table (upcast, exact) AND W1[:, d:] rounded to bf16 the way the train
+      step rounds it.  What remains is fp32 accumulation order, so tolerances
+      are tight.  "reference" — the oracle with the model's f32 W1.
+  re-rank: the oracle with the model's f32 weights on the same bf16 table
+      (the reference's arithmetic: the fused kernel feeds every f32 weight to
+      its MFMAs as bf16 hi + lo, 16 mantissa bits, so there is no separate
+      "emulated" oracle).
 Tolerances (written here and in DESIGN.md "Parity"):
   train, emulated (each of 2 steps checked from the kernel's state before
       it): loss 2e-5 abs; each clipped gradient tensor max-abs error
@@ -23,9 +27,11 @@ Tolerances (written here and in DESIGN.md "Parity"):
       gradient error of 0 (Adam's sign-normalised step: bound 2 lr);
       BN running stats 1e-5 abs.
   train, reference: loss 2e-3 abs.
-  re-rank, emulated: logits 1e-3 abs;  reference: 2e-2 abs.  NDCG@5 per user
-      equal wherever the positive's logit is more than 2x the tolerance away
-      from every other candidate's logit (rank well defined under the bound).
+  re-rank: logits 1e-4 abs (north_star's DIN tolerance) against the
+      reference; NDCG@5 per user equal for every user whose positive is more
+      than 2x the MEASURED logit error away from every other candidate's
+      logit, and the number of users that margin exempts is printed and
+      asserted (0 on the c5 fixture and the random case).
 """
 import os
 
@@ -160,18 +166,21 @@ def _rerank_oracle(p, T, hist_u, cand_u):
     return lo.reshape(-1)
 
 
-def _rank_ambiguous(ref_logits_u, lab_u, tol):
-    """True when the positive's logit lies within 2 tol of another candidate's
-    (its rank is then not determined under the stated tolerance)."""
+def _margin(ref_logits_u, lab_u):
+    """Distance of the positive's reference logit to the nearest other
+    candidate's (inf without a positive): below twice the kernel's error the
+    rank of the positive is not determined by the error bound."""
     pos = np.flatnonzero(lab_u == 1)
     if pos.size == 0:
-        return False
+        return np.inf
     others = np.delete(ref_logits_u, pos[0])
-    return bool(np.abs(others - ref_logits_u[pos[0]]).min(initial=np.inf) <= 2 * tol)
+    return float(np.abs(others - ref_logits_u[pos[0]]).min(initial=np.inf))
 
 
-def test_rerank_shared_vs_oracle_c5_shape(gpu):
-    """nrk_din_rerank_attn at configs[4]'s shape (d 256, L 50, C 201) vs the oracle."""
+def test_rerank_fused_vs_oracle_c5_shape(gpu):
+    """nrk_din_rerank at configs[4]'s shape (d 256, L 50, C 201, A 128, F 32)
+    vs the fp64 oracle with the model's f32 weights: logits <= 1e-4, NDCG@5
+    per user exact."""
     from newsrecommend_amd.din import DIN
     from newsrecommend_amd.pipeline import ndcg_at_k, rerank
     from oracle import din_oracle as o
@@ -184,8 +193,10 @@ def test_rerank_shared_vs_oracle_c5_shape(gpu):
     lens = torch.randint(1, L + 1, (U,), generator=g, device=dev)
     lens[0], lens[1] = 1, L
     hist = torch.where(torch.arange(L, device=dev)[None] < lens[:, None], hist, torch.full_like(hist, -1))
+    hist[2] = -1  # an empty history: every slot is padding
     cand = torch.randint(0, N, (U, C), generator=g, device=dev, dtype=torch.int32)
     cand[::5, -1] = -1  # users without an appended ground truth: one padded slot
+    cand[3, 7] = N + 3  # a row outside the table: padded too
     gt_col = torch.randint(0, C - 1, (U,), generator=g, device=dev)
     labels = torch.zeros((U, C), dtype=torch.bool, device=dev)
     labels[torch.arange(U, device=dev), gt_col] = True
@@ -198,32 +209,36 @@ def test_rerank_shared_vs_oracle_c5_shape(gpu):
             bn.weight.uniform_(0.5, 1.5)
             bn.bias.uniform_(-0.1, 0.1)
     logits = rerank(model, table, hist, cand)
+    assert rerank.path == "fused", rerank.path
     nd = ndcg_at_k(logits, labels, 5).cpu().numpy()
     T = table.float().cpu().numpy().astype(np.float64)
     H, Cn, Lg, Lb = hist.cpu().numpy(), cand.cpu().numpy(), logits.cpu().numpy(), labels.cpu().numpy()
-    p_emu, p_ref = _params_f64(model, True), _params_f64(model, False)
-    worst_emu = worst_ref = 0.0
+    p_ref = _params_f64(model, False)
+    worst, refs = 0.0, []
     for u in range(U):
-        valid = Cn[u] >= 0
+        valid = (Cn[u] >= 0) & (Cn[u] < N)
         assert np.isneginf(Lg[u][~valid]).all()
-        got = Lg[u][valid]
-        emu = _rerank_oracle(p_emu, T, H[u], Cn[u])
-        ref = _rerank_oracle(p_ref, T, H[u], Cn[u])
-        worst_emu = max(worst_emu, np.abs(got - emu).max())
-        worst_ref = max(worst_ref, np.abs(got - ref).max())
-        lab_u = Lb[u][valid].astype(np.int64)
+        ref = _rerank_oracle(p_ref, T, H[u], np.where(valid, Cn[u], -1))
+        worst = max(worst, float(np.abs(Lg[u][valid] - ref).max()))
+        refs.append((ref, Lb[u][valid].astype(np.int64)))
+    print(f"fused re-rank logits max abs err vs the fp64 reference: {worst:.3g}")
+    assert worst < 1e-4, worst
+    exempt = 0
+    for u, (ref, lab_u) in enumerate(refs):
         nd_ref = o.ndcg_single(1 / (1 + np.exp(-ref)), lab_u, 5)
-        assert nd[u] == nd_ref or _rank_ambiguous(ref, lab_u, 2e-2), (u, nd[u], nd_ref)
-    print(f"rerank logits max abs err: emulated {worst_emu:.3g}, reference {worst_ref:.3g}")
-    assert worst_emu < 1e-3, worst_emu
-    assert worst_ref < 2e-2, worst_ref
+        if _margin(ref, lab_u) <= 2 * worst:
+            exempt += 1
+            continue
+        assert nd[u] == nd_ref, (u, nd[u], nd_ref)
+    print(f"NDCG@5 equal for all users; {exempt} exempted (positive within 2 x {worst:.2g} of another logit)")
+    assert exempt == 0
 
 
 def test_rerank_matches_reference_evaluate_fixture_c5(gpu):
     """The reference's own evaluate() at configs[4]'s re-rank shape (fixture
-    din_rerank_c5: d 256, L 50, 201 candidates, made by DIN.py): the shared
-    bf16 re-rank's logits and NDCG@5, and the fp32 generic evaluate() path's
-    loss and NDCG, against the reference's numbers."""
+    din_rerank_c5: d 256, L 50, 201 candidates, made by DIN.py): the fused
+    re-rank's logits (<= 1e-4) and every user's NDCG@5, and the fp32 generic
+    evaluate() path's loss and NDCG, against the reference's numbers."""
     from newsrecommend_amd.din import DIN, evaluate
     from newsrecommend_amd.pipeline import ndcg_at_k, rerank
 
@@ -239,14 +254,14 @@ def test_rerank_matches_reference_evaluate_fixture_c5(gpu):
     model.load_state_dict({k[4:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("sd::")})
     model = model.to(dev).eval()
     table32 = torch.from_numpy(z["table"]).to(dev)
-    # (1) bf16 shared-history re-rank (the configs[4] path); the table is bf16-exact
+    # (1) the fused re-rank (the configs[4] path); the table is bf16-exact
     logits = rerank(model, table32.to(torch.bfloat16), hist, cand).cpu().numpy()
+    assert rerank.path == "fused", rerank.path
     err = np.abs(logits - z["ev_logits"]).max()
-    print(f"fixture c5: shared re-rank logits max abs err {err:.3g}")
-    assert err < 2e-2, err
+    print(f"fixture c5: fused re-rank logits max abs err {err:.3g}")
+    assert err < 1e-4, err
     nd = ndcg_at_k(torch.from_numpy(logits).to(dev), torch.from_numpy(lab).to(dev) > 0, 5).cpu().numpy()
-    for u in range(len(nd)):
-        assert nd[u] == z["ev_ndcg_user"][u] or _rank_ambiguous(z["ev_logits"][u], lab[u], 2e-2), u
+    np.testing.assert_array_equal(nd, z["ev_ndcg_user"])  # every user (smallest margin 6.6e-4 >> 2 x err)
     # (2) the fp32 generic evaluate() (every candidate its own DIN sample)
     hist_emb = torch.where(hist[..., None] >= 0, table32[hist.clamp_min(0).long()], 0.0)
     batches = []

@@ -55,12 +55,12 @@ def test_screen_partial_chunk_tiles(gpu, metric, d, k):
     _check(xq, xb, k, metric, gpu)
 
 
-@pytest.mark.parametrize("form", ["0", "2"])
+@pytest.mark.parametrize("form", ["0", "1"])
 @pytest.mark.parametrize("d,n", [(128, 60_001), (128, 70_003), (256, 60_001), (256, 70_003)])
 def test_screen_main_pass_forms(gpu, monkeypatch, form, d, n):
     """The inner-product main pass runs on the 16x16x32 kernel (screen16.h) by
-    default at k <= 8 for d 128 / 256; the 32x32x16 kernel (NRK_SCREEN16=0) and
-    the alternate 16x16x32 schedule (=2) give the oracle's results too, with and
+    default at k <= 8 for d 128 / 256 (=1); the 32x32x16 kernel (NRK_SCREEN16=0,
+    the one every other form runs) gives the oracle's results too, with and
     without partial last tiles."""
     monkeypatch.setenv("NRK_SCREEN16", form)
     xq, xb = _mixture(n, 300, d, seed=d + n % 7)
@@ -222,6 +222,20 @@ def test_forced_fallback_paths(gpu, monkeypatch, force, cap):
             idx = _check(xq, xb, k, metric, gpu)
             assert int(idx.last_fallback.item()) == 200
             assert int(idx.last_exact_scan.item()) == (200 if force == "2" else 0)
+
+
+@pytest.mark.parametrize("metric", [ko.METRIC_IP, ko.METRIC_L2])
+def test_collect_rounds_beyond_the_slot_budget(gpu, monkeypatch, metric):
+    """more uncertified queries than collect slots (20,000
+    > FB_SLOTS_MAX = 16,384, every query uncertified by NRK_FORCE_FALLBACK=1, as
+    an 8-GPU shard searched by 8 x 4096 queries can leave them at L2): the
+    collect pass runs in two rounds over the same storage and answers every
+    query -- results equal the oracle and NO query takes the fp64 scan."""
+    monkeypatch.setenv("NRK_FORCE_FALLBACK", "1")
+    xq, xb = _mixture(30_000, 20_000, 64, seed=21)
+    idx = _check(xq, xb, 5, metric, gpu)
+    assert int(idx.last_fallback.item()) == 20_000
+    assert int(idx.last_exact_scan.item()) == 0
 
 
 @pytest.mark.parametrize("metric", [ko.METRIC_IP, ko.METRIC_L2])

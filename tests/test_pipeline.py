@@ -120,13 +120,40 @@ def test_retrieve_and_rerank_end_to_end(gpu):
     assert nd.shape == (U,) and top.shape == (U, 5)
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("d,L,C", [(256, 50, 201), (64, 20, 37), (128, 64, 70)])
-def test_rerank_shared_history_matches_per_candidate(d, L, C):
-    """nrk_din_rerank_attn (P = K W1k^T once per user) == every candidate as
-    its own DIN sample (the generic attention kernel), eval mode, bf16 table;
-    padded histories and padded candidates included."""
+def _din_model(d, A, F, dev, seed=0):
     from newsrecommend_amd.din import DIN
+
+    torch.manual_seed(seed)
+    model = DIN(d, A, F, 0.0).to(dev).eval()
+    with torch.no_grad():  # non-trivial BN statistics and affines
+        for bn in (model.fc[0], model.fc[4], model.fc[8]):
+            bn.running_mean.uniform_(-0.2, 0.2)
+            bn.running_var.uniform_(0.5, 1.5)
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.1, 0.1)
+    return model
+
+
+def _oracle_logits(model, T, hist_u, cand_u):
+    """fp64 DIN eval forward (oracle/din_oracle.py) of one user's candidates."""
+    from oracle import din_oracle as o
+
+    p = {k: v.detach().cpu().numpy().astype(np.float64) for k, v in model.state_dict().items()
+         if "num_batches" not in k}
+    keys = np.where(hist_u[:, None] >= 0, T[np.maximum(hist_u, 0)], 0.0)
+    lo, _, _, _ = o.din_forward(p, T[cand_u], np.broadcast_to(keys, (len(cand_u),) + keys.shape), train=False)
+    return lo.reshape(-1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d,L,C,A,F", [(256, 50, 201, 128, 32), (64, 20, 37, 32, 64), (128, 64, 70, 96, 128),
+                                       (256, 64, 130, 64, 96), (128, 33, 64, 128, 32)])
+def test_rerank_fused_vs_oracle_and_per_candidate(d, L, C, A, F):
+    """nrk_din_rerank over the reference's hyper-parameter space (Optuna
+    DIN.py:203-204: attn_units and fc_units 32..128 step 32) against the fp64
+    oracle (<= 1e-4 of the logit scale) and against every candidate as its own
+    DIN sample (model.forward_ids: the same logits up to that path's bf16 W1k,
+    2e-3); padded histories (an empty one included) and padded candidates."""
     from newsrecommend_amd.pipeline import rerank
 
     dev = torch.device("cuda")
@@ -136,89 +163,65 @@ def test_rerank_shared_history_matches_per_candidate(d, L, C):
     hist = torch.randint(0, N, (U, L), generator=g, device=dev, dtype=torch.int32)
     lens = torch.randint(1, L + 1, (U,), generator=g, device=dev)
     hist = torch.where(torch.arange(L, device=dev)[None] < lens[:, None], hist, torch.full_like(hist, -1))
+    hist[1] = -1
     cand = torch.randint(0, N, (U, C), generator=g, device=dev, dtype=torch.int32)
     cand[:, -3:] = -1
-    torch.manual_seed(0)
-    model = DIN(d, 128, 32, 0.0).to(dev).eval()
-    with torch.no_grad():  # non-trivial BN statistics
-        for bn in (model.fc[0], model.fc[4], model.fc[8]):
-            bn.running_mean.uniform_(-0.2, 0.2)
-            bn.running_var.uniform_(0.5, 1.5)
-    a = rerank(model, table, hist, cand, shared=True)
+    model = _din_model(d, A, F, dev)
+    a = rerank(model, table, hist, cand)
+    assert rerank.path == "fused", rerank.path
     b = rerank(model, table, hist, cand, shared=False)
     fin = torch.isfinite(b)
     assert torch.equal(fin, torch.isfinite(a))
-    err = (a[fin] - b[fin]).abs().max().item()
-    assert err < 2e-3 * max(1.0, b[fin].abs().max().item()), err
+    scale = max(1.0, b[fin].abs().max().item())
+    assert (a[fin] - b[fin]).abs().max().item() < 2e-3 * scale
+    T = table.float().cpu().numpy().astype(np.float64)
+    H, Cn, A_ = hist.cpu().numpy(), cand.cpu().numpy(), a.cpu().numpy()
+    worst = 0.0
+    for u in range(0, U, 3):
+        v = Cn[u] >= 0
+        worst = max(worst, float(np.abs(A_[u][v] - _oracle_logits(model, T, H[u], Cn[u][v])).max()))
+    print(f"fused re-rank d={d} A={A} F={F}: max abs err vs fp64 {worst:.3g}")
+    assert worst < 1e-4 * scale, worst
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("d,NO,n", [(256, 160, 1000), (128, 128, 77), (64, 256, 33)])
-def test_item_proj_matches_fp64(d, NO, n):
-    """nrk_din_item_proj (gathered bf16 rows x W^T + bias, W as bf16 hi + lo)
-    vs fp64 on the same rows; invalid ids give the bias."""
-    from newsrecommend_amd import _lib
-    from newsrecommend_amd.pipeline import _split_bf16
+def test_rerank_ragged_shared_lists_extra_and_gaps():
+    """nrk_din_rerank's ragged form (the flow's): users sharing one candidate
+    list (same offset), lists of 0, 1, 63, 64, 65 and 300 candidates, an
+    appended extra candidate (-1 = a padded slot, a row past the table = -inf),
+    duplicated candidates, out_off with gaps between users; every logit equals
+    the rectangular rerank() of the same list, bit for bit, on two runs."""
+    from newsrecommend_amd.pipeline import rerank, rerank_ragged
 
     dev = torch.device("cuda")
-    g = torch.Generator(device=dev).manual_seed(7)
-    N = 3000
-    table = torch.randn((N, d), generator=g, device=dev).to(torch.bfloat16)
-    ids = torch.randint(0, N, (n,), generator=g, device=dev, dtype=torch.int32)
-    ids[::7] = -1
-    ids[3::11] = N + 5
-    W = torch.randn((NO, d), generator=g, device=dev) * 0.1
-    b = torch.randn(NO, generator=g, device=dev)
-    hi, lo = _split_bf16(W)
-    out = torch.empty((n, NO), device=dev)
-    _lib.check(_lib.load().nrk_din_item_proj(_lib.ptr(table), N, _lib.NRK_DTYPE_BF16, _lib.ptr(ids), n, d,
-                                             _lib.ptr(hi), _lib.ptr(lo), _lib.ptr(b), NO, _lib.ptr(out),
-                                             _lib.stream(dev)), "item_proj")
-    ok = (ids >= 0) & (ids < N)
-    q = torch.where(ok[:, None], table[ids.clamp(0, N - 1).long()].double(), 0.0)
-    ref = q @ W.double().t() + b.double()
-    bound = (q.abs() @ W.double().abs().t()).max().item() * 2.0 ** -15 + 1e-6
-    err = (out.double() - ref).abs().max().item()
-    assert err <= bound, (err, bound)
-    assert torch.equal(out[~ok], b.expand(int((~ok).sum()), NO))
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("d", [256, 64])
-def test_rerank_head_matches_fp64(d):
-    """nrk_din_rerank_head (pooled H1p on MFMA with hi/lo splits, two small
-    layers per lane) vs the fp64 composition; -inf on padded candidates."""
-    from newsrecommend_amd import _lib
-    from newsrecommend_amd.pipeline import _split_bf16
-
-    dev = torch.device("cuda")
-    g = torch.Generator(device=dev).manual_seed(9)
-    n, F, ldq = 301, 32, 160
-    pooled = torch.randn((n, d), generator=g, device=dev)
-    Q = torch.randn((n, ldq), generator=g, device=dev)
-    cand = torch.randint(0, 100, (n,), generator=g, device=dev, dtype=torch.int32)
-    cand[::9] = -1
-    H1p = torch.randn((F, d), generator=g, device=dev) * 0.1
-    c1 = torch.randn(F, generator=g, device=dev) * 0.1
-    H2 = torch.randn((F // 2, F), generator=g, device=dev) * 0.3
-    c2 = torch.randn(F // 2, generator=g, device=dev) * 0.1
-    h3 = torch.randn(F // 2, generator=g, device=dev) * 0.3
-    c3 = 0.25
-    hi, lo = _split_bf16(H1p)
-    lg = torch.empty(n, device=dev)
-    off = 128  # Q1 = columns 128..159 of each Q row
-    _lib.check(_lib.load().nrk_din_rerank_head(_lib.ptr(pooled), n, d, _lib.ptr(Q) + 4 * off, ldq, _lib.ptr(cand),
-                                               _lib.ptr(hi), _lib.ptr(lo), _lib.ptr(c1), F, _lib.ptr(H2),
-                                               _lib.ptr(c2), _lib.ptr(h3), c3, _lib.ptr(lg), _lib.stream(dev)),
-               "rerank_head")
-    p64 = pooled.double()
-    h1 = (Q[:, off:off + F].double() + p64 @ H1p.double().t() + c1.double()).relu()
-    h2 = (h1 @ H2.double().t() + c2.double()).relu()
-    ref = h2 @ h3.double() + c3
-    valid = cand >= 0
-    assert torch.isneginf(lg[~valid]).all()
-    err = (lg[valid].double() - ref[valid]).abs().max().item()
-    assert err < 1e-4 * max(1.0, ref.abs().max().item()), err
+    g = torch.Generator(device=dev).manual_seed(11)
+    d, L, N = 128, 40, 3000
+    table = (torch.randn((N, d), generator=g, device=dev) * 0.5).to(torch.bfloat16)
+    model = _din_model(d, 128, 32, dev, seed=3)
+    pool = torch.randint(0, N, (600,), generator=g, device=dev, dtype=torch.int32)
+    pool[10] = pool[11]  # a duplicate
+    lists = [(0, 0), (5, 1), (20, 63), (20, 64), (100, 65), (200, 300), (20, 64), (0, 0)]  # (offset, length)
+    extra = torch.tensor([7, -1, 12, N + 4, -1, 99, 5, -1], dtype=torch.int32, device=dev)
+    U = len(lists)
+    hist = torch.randint(0, N, (U, L), generator=g, device=dev, dtype=torch.int32)
+    hist[:, 30:] = -1
+    hist[3] = -1
+    co = torch.tensor([o for o, _ in lists], dtype=torch.int64, device=dev)
+    cl = torch.tensor([n for _, n in lists], dtype=torch.int32, device=dev)
+    width = cl.long() + 1
+    oo = torch.cumsum(width + 3, 0) - (width + 3)  # gaps of 3 between users
+    n_out = int((oo[-1] + width[-1]).item()) + 5
+    out = rerank_ragged(model, table, hist, pool, co, cl, extra, oo, n_out)
+    got = rerank_ragged(model, table, hist, pool, co, cl, extra, oo, n_out)
+    for u, (o, n) in enumerate(lists):
+        lst = torch.cat([pool[o:o + n], extra[u:u + 1]])
+        ref = rerank(model, table, hist[u:u + 1], lst[None])[0]
+        seg = got[oo[u]:oo[u] + n + 1]
+        assert torch.equal(seg, ref), u
+        assert torch.equal(out[oo[u]:oo[u] + n + 1], ref), u
+        if extra[u] < 0 or extra[u] >= N:
+            assert torch.isneginf(seg[-1])
+    assert torch.equal(got[0:1], rerank(model, table, hist[:1], extra[:1, None])[0])  # list of 0 + extra
 
 
 def test_top_and_ndcg_equal_stable_sort_and_segment_ndcg():

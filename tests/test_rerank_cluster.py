@@ -20,7 +20,7 @@ import pytest
 import torch
 
 from tests.conftest import GOLDEN
-from tests.test_din_bf16_oracle import _params_f64, _rank_ambiguous, _rerank_oracle
+from tests.test_din_bf16_oracle import _margin, _params_f64, _rerank_oracle
 
 pytestmark = pytest.mark.gpu
 
@@ -55,7 +55,7 @@ def test_rerank_whole_cluster_vs_reference_evaluate(gpu):
     hist = torch.from_numpy(z["ev_hist_rows"]).to(dev)
     assert hist.shape[1] == L == 64
     logits = rerank(model, table, hist, torch.from_numpy(cand).to(dev))
-    assert rerank.path == "shared", rerank.path
+    assert rerank.path == "fused", rerank.path
     lg = logits.cpu().numpy()
     lab_flat, ref_flat = z["ev_lab"], z["ev_logits"]
     seg = np.concatenate([[0], np.cumsum(cl)])
@@ -71,20 +71,30 @@ def test_rerank_whole_cluster_vs_reference_evaluate(gpu):
         losses.append(np.mean(np.maximum(x, 0) - x * y + np.log1p(np.exp(-np.abs(x)))))
     print(f"whole-cluster re-rank: logits max abs err vs evaluate() {worst:.3g}, "
           f"mean BCE {np.mean(losses):.6f} vs {float(z['ev_loss']):.6f}")
-    assert worst < 2e-2, worst
-    assert abs(float(np.mean(losses)) - float(z["ev_loss"])) < 1e-2
+    assert worst < 1e-4, worst
+    assert abs(float(np.mean(losses)) - float(z["ev_loss"])) < 1e-5
     nd = ndcg_at_k(logits, torch.from_numpy(labels).to(dev), 5).cpu().numpy()
+    exempt = []
     for u in range(U):
         ref = ref_flat[seg[u]:seg[u + 1]]
         lab_u = lab_flat[seg[u]:seg[u + 1]].astype(np.int64)
-        assert nd[u] == z["ev_ndcg_user"][u] or _rank_ambiguous(ref, lab_u, 2e-2), (u, nd[u], z["ev_ndcg_user"][u])
+        if _margin(ref, lab_u) <= 2 * worst:
+            exempt.append(u)
+            continue
+        assert nd[u] == z["ev_ndcg_user"][u], (u, nd[u], z["ev_ndcg_user"][u])
+    # the fixture holds ONE user whose positive is 6.8e-6 from another logit
+    # (below the reference's own f32 rounding of these sums); every other
+    # margin is >= 1.5e-4
+    print(f"NDCG@5 equal for {U - len(exempt)} of {U} users; exempted {exempt} "
+          f"(margins {[round(_margin(ref_flat[seg[u]:seg[u + 1]], lab_flat[seg[u]:seg[u + 1]]), 9) for u in exempt]})")
+    assert len(exempt) <= 1
 
 
 def test_rerank_whole_cluster_vs_oracle_and_grouped(gpu):
-    """The same users through pipeline.rerank_clusters (users grouped by
-    cluster, no padding): logits bit-identical to the padded batch, 1e-3 of
-    the emulated fp64 oracle on every 37th candidate, per-user BCE and NDCG
-    equal to the padded path's."""
+    """The same users through pipeline.rerank_clusters (ONE fused launch, every
+    user pointing at its cluster's shared list, no padding): logits
+    bit-identical to the padded batch, 1e-4 of the fp64 oracle on every 37th
+    candidate, per-user BCE and NDCG equal to the padded path's."""
     from newsrecommend_amd.pipeline import ndcg_at_k, rerank, rerank_clusters
 
     dev = torch.device("cuda")
@@ -106,17 +116,17 @@ def test_rerank_whole_cluster_vs_oracle_and_grouped(gpu):
     res = rerank_clusters(model, table, hist, torch.from_numpy(uc).to(dev), torch.from_numpy(off).to(dev),
                           torch.from_numpy(rows_np).to(dev), torch.from_numpy(last).to(dev), k=5)
     T = table.float().cpu().numpy().astype(np.float64)
-    p_emu = _params_f64(model, True)
+    p_ref = _params_f64(model, False)
     worst = 0.0
     for lg, us in zip(res["logits"], res["users"]):
         lg, us = lg.cpu().numpy(), us.cpu().numpy()
         for i, u in enumerate(us):
             assert np.array_equal(lg[i], padded[u, :cl[u]]), u  # grouping changes nothing
             sub = np.arange(0, cl[u], 37)
-            emu = _rerank_oracle(p_emu, T, z["ev_hist_rows"][u], cand[u, sub])
-            worst = max(worst, float(np.abs(lg[i, sub] - emu).max()))
-    print(f"whole-cluster re-rank vs emulated oracle: {worst:.3g}")
-    assert worst < 1e-3, worst
+            ref = _rerank_oracle(p_ref, T, z["ev_hist_rows"][u], cand[u, sub])
+            worst = max(worst, float(np.abs(lg[i, sub] - ref).max()))
+    print(f"whole-cluster re-rank vs the fp64 oracle: {worst:.3g}")
+    assert worst < 1e-4, worst
     labels = np.zeros((U, Cmax), bool)
     for u in range(U):
         labels[u, :cl[u]] = z["ev_lab"][seg[u]:seg[u + 1]] == 1
@@ -126,6 +136,43 @@ def test_rerank_whole_cluster_vs_oracle_and_grouped(gpu):
     for u in range(U):
         x, y = padded[u, :cl[u]].astype(np.float64), labels[u, :cl[u]].astype(np.float64)
         assert abs(loss[u] - np.mean(np.maximum(x, 0) - x * y + np.log1p(np.exp(-np.abs(x))))) < 1e-6
+
+
+def test_rerank_clusters_append_missing_and_empty_cluster(gpu):
+    """append_missing scores the ground truth of users whose
+    nearest cluster lacks it -- including a user whose cluster is EMPTY (the
+    ground truth alone: loss and NDCG of that one candidate, NDCG 1) -- and a
+    user with no candidate at all (empty cluster, no append) gets NaN loss /
+    NDCG instead of a silent 0.  Every logit equals the per-user fused
+    rerank() of the same list (bit for bit)."""
+    from newsrecommend_amd.pipeline import rerank, rerank_clusters
+
+    dev = torch.device("cuda")
+    z, table, model, off_np, L = _fixture(dev)
+    rows_np = z["cluster_rows"]
+    # clusters: the fixture's three, then an empty one
+    off = torch.from_numpy(np.concatenate([off_np, [off_np[-1]]])).to(dev)
+    hist = torch.from_numpy(z["ev_hist_rows"]).to(dev)
+    U = hist.shape[0]
+    uc = torch.from_numpy(z["user_cluster"].astype(np.int64)).to(dev)
+    uc[0] = 3  # user 0's nearest cluster is the empty one
+    last = torch.from_numpy(rows_np[[0, 5, off_np[1] + 2] * (U // 3) + [7] * (U % 3)][:U].astype(np.int64)).to(dev)
+    rows = torch.from_numpy(rows_np).to(dev)
+    res = rerank_clusters(model, table, hist, uc, off, rows, last, k=5, append_missing=True)
+    nd, loss = res["ndcg"].cpu().numpy(), res["loss"].cpu().numpy()
+    assert nd[0] == 1.0 and np.isfinite(loss[0])  # the ground truth alone ranks first
+    for lg, us in zip(res["logits"], res["users"]):
+        for i, u in enumerate(us.cpu().tolist()):
+            c = int(uc[u])
+            lst = rows[off[c]:off[c + 1]]
+            hit = bool((lst == last[u]).any())
+            cand = torch.cat([lst, torch.tensor([-1 if hit else int(last[u])], device=dev)]).to(torch.int32)
+            ref = rerank(model, table, hist[u:u + 1], cand[None])[0]
+            assert torch.equal(lg[i], ref), u
+    assert np.isfinite(loss).all() and np.isfinite(nd).all()
+    res2 = rerank_clusters(model, table, hist, uc, off, rows, last, k=5, append_missing=False)
+    assert np.isnan(res2["loss"][0].item()) and np.isnan(res2["ndcg"][0].item())
+    assert np.isfinite(res2["loss"][1:].cpu().numpy()).all()
 
 
 def test_cluster_candidates_batched(gpu):
