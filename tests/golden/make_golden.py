@@ -239,17 +239,19 @@ def din_dataset_fixture(name, seed):
         )
 
 
-def din_rerank_fixture(name, seed, d=256, L=50, n_users=24, n_cand=201, n_items=1200):
+def din_rerank_fixture(name, seed, d=256, L=50, n_users=24, n_cand=201, n_items=1200, bf16_exact=True):
     """configs[4]'s re-rank shape through the reference's own EvalDataset +
     evaluate() (DIN.py:21-57,155-193): d = 256, L = 50, 201 candidates per
     user, DIN(256, 128, 32, 0.36) in eval mode with non-trivial BN statistics.
-    The item table is rounded to bf16-representable values so the same numbers
-    feed the reference's fp32 forward and the bf16-table GPU path."""
+    bf16_exact: the item table is rounded to bf16-representable values so the
+    same numbers feed the reference's fp32 forward and the bf16-table GPU path;
+    otherwise it is a plain fp32 table, as embedding_generate.py produces (the
+    bf16-table path then sees each embedding rounded once)."""
     with tempfile.TemporaryDirectory() as wd:
         rng = np.random.default_rng(seed)
         ids = rng.choice(np.arange(1000, 1000 + 10 * n_items), size=n_items, replace=False)
         table = torch.from_numpy(rng.standard_normal((n_items, d)).astype(np.float32) * 0.5)
-        table = table.to(torch.bfloat16).float().numpy()
+        table = table.to(torch.bfloat16).float().numpy() if bf16_exact else table.numpy()
         emb = {int(a): table[i] for i, a in enumerate(ids)}
         test_clicks, test_recs = {}, {}
         for u in range(n_users):
@@ -477,6 +479,9 @@ def main():
     if sys.argv[1:] == ["din_rerank_cluster"]:  # regenerate only the whole-cluster re-rank fixture
         din_rerank_cluster_fixture("din_rerank_cluster", seed=19)
         return
+    if sys.argv[1:] == ["din_rerank_f32"]:  # regenerate only the fp32-table re-rank fixture
+        din_rerank_fixture("din_rerank_f32", seed=20, n_users=16, bf16_exact=False)
+        return
     din_forward_fixture("din_fwd_c1", d=64, A=32, F=32, B=64, L=20, n_items=300, seed=11)
     din_forward_fixture("din_fwd_c3", d=128, A=128, F=32, B=96, L=50, n_items=600, seed=12)
     din_train_fixture("din_train_c1", d=64, A=32, F=32, B=48, L=20, n_items=300, seed=13)
@@ -486,6 +491,7 @@ def main():
     din_rerank_fixture("din_rerank_c5", seed=17)
     embedding_train_fixture("embedding_train", seed=18)
     din_rerank_cluster_fixture("din_rerank_cluster", seed=19)
+    din_rerank_fixture("din_rerank_f32", seed=20, n_users=16, bf16_exact=False)
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))

@@ -273,3 +273,53 @@ def test_rerank_matches_reference_evaluate_fixture_c5(gpu):
     loss, ndcg = evaluate(model, batches, torch.nn.BCEWithLogitsLoss(), dev, 5)
     assert abs(loss - float(z["ev_loss"])) < 1e-5, (loss, float(z["ev_loss"]))
     assert abs(ndcg - float(z["ev_ndcg"])) < 1e-9, (ndcg, float(z["ev_ndcg"]))
+
+
+def test_rerank_fp32_table_fixture_bf16_effect(gpu):
+    """An fp32 item table as embedding_generate.py produces (fixture
+    din_rerank_f32, made by the reference's own evaluate(); NOT bf16-exact).
+    The fused re-rank consumes a bf16 table, so every embedding is rounded
+    once.  Asserted: (1) the kernel is exact on what it is given -- its logits
+    equal the fp64 oracle fed the bf16-ROUNDED table to <= 1e-4; (2) the
+    generic fp32 path (rerank on the fp32 table: every candidate its own DIN
+    sample) equals the reference's logits to <= 1e-4 and every NDCG.  Reported
+    (printed, and bounded loosely): the bf16 table's own effect on the logits
+    and how many users keep the reference's NDCG@5."""
+    from newsrecommend_amd.din import DIN
+    from newsrecommend_amd.pipeline import ndcg_at_k, rerank
+
+    z = np.load(os.path.join(GOLDEN, "din_rerank_f32.npz"))
+    dev = torch.device("cuda")
+    d, L = int(z["d"]), int(z["L"])
+    row = {int(a): i for i, a in enumerate(z["item_ids"])}
+    to_rows = np.vectorize(lambda a: row.get(int(a), -1))
+    hist = torch.from_numpy(to_rows(z["ev_hist"]).astype(np.int32)).to(dev)
+    cand = torch.from_numpy(to_rows(z["ev_cand"]).astype(np.int32)).to(dev)
+    lab = torch.from_numpy(z["ev_lab"]).to(dev) > 0
+    model = DIN(d, int(z["A"]), int(z["F"]), 0.36)
+    model.load_state_dict({k[4:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("sd::")})
+    model = model.to(dev).eval()
+    t32 = torch.from_numpy(z["table"]).to(dev)
+    assert not torch.equal(t32, t32.to(torch.bfloat16).float())  # really not bf16-exact
+    lg_bf = rerank(model, t32.to(torch.bfloat16), hist, cand)
+    assert rerank.path == "fused"
+    lg_32 = rerank(model, t32, hist, cand)
+    assert rerank.path.startswith("per-candidate")
+    ref = z["ev_logits"]
+    err32 = float(np.abs(lg_32.cpu().numpy() - ref).max())
+    assert err32 < 1e-4, err32
+    np.testing.assert_array_equal(ndcg_at_k(lg_32, lab, 5).cpu().numpy(), z["ev_ndcg_user"])
+    # (1) exactness on the rounded table
+    Tb = t32.to(torch.bfloat16).float().cpu().numpy().astype(np.float64)
+    p_ref = _params_f64(model, False)
+    H, Cn, Lg = hist.cpu().numpy(), cand.cpu().numpy(), lg_bf.cpu().numpy()
+    worst = max(float(np.abs(Lg[u] - _rerank_oracle(p_ref, Tb, H[u], Cn[u])).max()) for u in range(len(Cn)))
+    assert worst < 1e-4, worst
+    # the bf16 table's effect, reported
+    eff = float(np.abs(Lg - ref).max())
+    nd = ndcg_at_k(lg_bf, lab, 5).cpu().numpy()
+    same = int((nd == z["ev_ndcg_user"]).sum())
+    print(f"fp32-table fixture: fused (bf16 table) vs oracle on the rounded table {worst:.3g}; vs the reference's "
+          f"fp32 logits {eff:.3g}; NDCG@5 equal for {same} of {len(nd)} users; mean NDCG {nd.mean():.4f} vs "
+          f"{float(z['ev_ndcg']):.4f}; fp32 generic path vs reference {err32:.3g}")
+    assert eff < 5e-2
