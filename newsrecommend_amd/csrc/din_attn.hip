@@ -2580,40 +2580,45 @@ template <int D>
 __global__ __launch_bounds__(256) void din_u_kernel(const float* __restrict__ q, int B, const float* __restrict__ W1,
                                                     const float* __restrict__ b1, int A, float* __restrict__ U,
                                                     uint16_t* __restrict__ W1k_bf) {
-  constexpr int KS = D / 16;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 31, h = lane >> 5;
-  const int b0 = blockIdx.x * 32;
+  // U = q W1q^T + b1 for 16 samples per block on v_mfma_f32_16x16x32_bf16 (256
+  // blocks at B = 4096; the 32x32x16 form had 128): q is exact in bf16, W1q
+  // enters as hi + mid + lo bf16 parts (truncation: every product is the exact
+  // f32 product).  Wave w owns the 16-unit tiles w, w + 4, ...
+  constexpr int KS = D / 32;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l15 = lane & 15, l4 = lane >> 4;
+  const int b0 = blockIdx.x * 16;
   for (int64_t e = (int64_t)blockIdx.x * 256 + tid; e < (int64_t)A * D; e += (int64_t)gridDim.x * 256) {
     const int64_t n = e / D, k = e % D;
     W1k_bf[e] = f32_to_bf16_rne(W1[n * 2 * D + D + k]);
   }
-  const int b = b0 + r;
+  const int b = b0 + l15;
   bf16x8 qf[KS];
 #pragma unroll
-  for (int s2 = 0; s2 < KS; ++s2) {
+  for (int s = 0; s < KS; ++s) {
     float4 lo4 = make_float4(0.f, 0.f, 0.f, 0.f), hi4 = lo4;
     if (b < B) {
-      lo4 = *reinterpret_cast<const float4*>(q + (int64_t)b * D + 16 * s2 + 8 * h);
-      hi4 = *reinterpret_cast<const float4*>(q + (int64_t)b * D + 16 * s2 + 8 * h + 4);
+      lo4 = *reinterpret_cast<const float4*>(q + (int64_t)b * D + 32 * s + 8 * l4);
+      hi4 = *reinterpret_cast<const float4*>(q + (int64_t)b * D + 32 * s + 8 * l4 + 4);
     }
-    qf[s2][0] = (short)f32_to_bf16_rne(lo4.x); qf[s2][1] = (short)f32_to_bf16_rne(lo4.y);
-    qf[s2][2] = (short)f32_to_bf16_rne(lo4.z); qf[s2][3] = (short)f32_to_bf16_rne(lo4.w);
-    qf[s2][4] = (short)f32_to_bf16_rne(hi4.x); qf[s2][5] = (short)f32_to_bf16_rne(hi4.y);
-    qf[s2][6] = (short)f32_to_bf16_rne(hi4.z); qf[s2][7] = (short)f32_to_bf16_rne(hi4.w);
+    qf[s][0] = (short)f32_to_bf16_rne(lo4.x); qf[s][1] = (short)f32_to_bf16_rne(lo4.y);
+    qf[s][2] = (short)f32_to_bf16_rne(lo4.z); qf[s][3] = (short)f32_to_bf16_rne(lo4.w);
+    qf[s][4] = (short)f32_to_bf16_rne(hi4.x); qf[s][5] = (short)f32_to_bf16_rne(hi4.y);
+    qf[s][6] = (short)f32_to_bf16_rne(hi4.z); qf[s][7] = (short)f32_to_bf16_rne(hi4.w);
   }
-  for (int ws = w; ws < A / 32; ws += 4) {
-    float bv[16];  // b1 of this lane's output units, loaded ahead of the MFMA chain
+  for (int ut = w; ut < A / 16; ut += 4) {
+    const int u = 16 * ut + l15;
+    const float bv = b1[u];
+    const float* wrow = W1 + (int64_t)u * 2 * D + 8 * l4;
+    float4 wv0[KS], wv1[KS];
 #pragma unroll
-    for (int g = 0; g < 16; ++g) bv[g] = b1[32 * ws + acc_row(g, h)];
-    f32x16 acc;
+    for (int s = 0; s < KS; ++s) {  // every load of the tile in flight at once
+      wv0[s] = *reinterpret_cast<const float4*>(wrow + 32 * s);
+      wv1[s] = *reinterpret_cast<const float4*>(wrow + 32 * s + 4);
+    }
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int g = 0; g < 16; ++g) acc[g] = 0.f;
-    const float* wrow = W1 + (int64_t)(32 * ws + r) * 2 * D;
-#pragma unroll
-    for (int s2 = 0; s2 < KS; ++s2) {
-      const float4 w0 = *reinterpret_cast<const float4*>(wrow + 16 * s2 + 8 * h);
-      const float4 w1 = *reinterpret_cast<const float4*>(wrow + 16 * s2 + 8 * h + 4);
-      const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+    for (int s = 0; s < KS; ++s) {
+      const float wv[8] = {wv0[s].x, wv0[s].y, wv0[s].z, wv0[s].w, wv1[s].x, wv1[s].y, wv1[s].z, wv1[s].w};
       bf16x8 fh, fm, fl;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -2623,13 +2628,14 @@ __global__ __launch_bounds__(256) void din_u_kernel(const float* __restrict__ q,
         fm[j] = m1;
         fl[j] = l1;
       }
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fl, qf[s2], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fm, qf[s2], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fh, qf[s2], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[s], fl, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[s], fm, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[s], fh, acc, 0, 0, 0);
     }
-    if (b < B) {
 #pragma unroll
-      for (int g = 0; g < 16; ++g) U[(int64_t)b * A + 32 * ws + acc_row(g, h)] = acc[g] + bv[g];
+    for (int i = 0; i < 4; ++i) {
+      const int bb = b0 + 4 * l4 + i;
+      if (bb < B) U[(int64_t)bb * A + u] = acc[i] + bv;
     }
   }
 }
@@ -3081,7 +3087,7 @@ extern "C" int nrk_din_batch_u(const float* q, int32_t B, int32_t d, const float
   NRK_CHECK_ARG(B >= 0, "din_batch_u: bad B=%d", B);
   if (B == 0) return NRK_OK;
   NRK_CHECK_ARG(q && W1 && b1 && U && W1k_bf16, "din_batch_u: null pointer");
-  const unsigned grid = (unsigned)cdiv(B, 32);
+  const unsigned grid = (unsigned)cdiv(B, 16);
   hipStream_t st = (hipStream_t)stream;
   uint16_t* wk = static_cast<uint16_t*>(W1k_bf16);
   if (d == 256) hipLaunchKernelGGL(din_u_kernel<256>, dim3(grid), dim3(256), 0, st, q, B, W1, b1, A, U, wk);

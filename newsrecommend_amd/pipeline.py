@@ -116,7 +116,7 @@ def rerank_params(model, d: int):
     keep["c1"] = c1.detach().float().contiguous()
     keep["c2"] = c2.detach().float().contiguous()
     keep["h3"] = H3.detach().reshape(-1).float().contiguous()
-    prm = _lib.RerankParams(**{k: v.data_ptr() for k, v in keep.items()}, c3=float(c3.reshape(-1)[0]))
+    prm = _lib.RerankParams(**{k: v.data_ptr() for k, v in keep.items()}, c3=float(c3.detach().reshape(-1)[0]))
     out = (prm, W1.shape[0], H1.shape[0], keep)
     _PARAMS_CACHE[id(model)] = (key, out)
     return out
@@ -301,7 +301,7 @@ def rerank_clusters(model, table: torch.Tensor, hist_rows: torch.Tensor, user_cl
         pcol = torch.where(has_pos, pos_in, clen if extra is not None else torch.full_like(clen, -1))
         if extra is not None:
             has_pos = has_pos | (extra >= 0)
-        pidx = oo[:-1] + pcol.clamp_min(0)
+        pidx = (oo[:-1] + pcol.clamp_min(0)).clamp(0, max(n_out - 1, 0))  # an empty list's index stays in range
         seg = torch.repeat_interleave(torch.arange(U, device=dev), width)
         x = flat.double()
         valid = torch.isfinite(x)
@@ -311,7 +311,7 @@ def rerank_clusters(model, table: torch.Tensor, hist_rows: torch.Tensor, user_cl
         nval = _seg_sum(valid.double(), oo[:-1], oo[1:])
         loss = _seg_sum(per, oo[:-1], oo[1:]) / nval
         pr = torch.sigmoid(flat)
-        pp = pr[pidx]
+        pp = pr[pidx] if n_out else torch.zeros(U, device=dev)
         col = torch.arange(n_out, device=dev) - oo[:-1][seg]
         before = (pr > pp[seg]) | ((pr == pp[seg]) & (col < pcol[seg]))
         rank = _seg_sum(before.long(), oo[:-1], oo[1:]) + 1
