@@ -101,8 +101,10 @@ struct Geo {
 
 template <int D, int A, int F>
 struct Lds {  // byte offsets
-  int p, hsp, rt, q, us, ms, lgp, total;
-  __host__ __device__ constexpr Lds() : p(0), hsp(0), rt(0), q(0), us(0), ms(0), lgp(0), total(0) {
+  int p, hsp, rt, q, us, ms, lgp, cst, h2, total;
+  bool h2l;  // H2 hi / lo resident in LDS (when it fits)
+  __host__ __device__ constexpr Lds()
+      : p(0), hsp(0), rt(0), q(0), us(0), ms(0), lgp(0), cst(0), h2(0), total(0), h2l(false) {
     using G = Geo<D, A>;
     p = 0;                                     // P' [LP][PRS] f32
     hsp = p + LP * G::PRS * 4;                 // SP / 2 [LP] f32
@@ -113,9 +115,22 @@ struct Lds {  // byte offsets
     const int ub = CH * G::PRS * 4 > CH * (F + 4) * 4 ? CH * G::PRS * 4 : CH * (F + 4) * 4;
     ms = us + ub;                              // {m, sum} of the two row groups [2][2][CH] f32
     lgp = ms + 4 * CH * 4;                     // partial logits [F/32][CH] f32 (F/2 units in 16-unit tiles)
-    total = lgp + (F / 32 > 0 ? F / 32 : 1) * CH * 4 + 16;
+    cst = lgp + (F / 32 > 0 ? F / 32 : 1) * CH * 4;  // c1 [F], c2 [F/2], h3 [F/2] f32; candidate valid [CH] i32
+    h2 = cst + 2 * F * 4 + CH * 4 + A * 4;     // (+ w2 [A] f32);  H2 hi, lo [F/2][F] bf16 (if it fits)
+    const int h2b = 2 * (F / 2) * F * 2;
+    h2l = h2 + h2b + 16 <= 160 * 1024;
+    total = (h2l ? h2 + h2b : h2) + 16;
   }
 };
+
+// A uniform pointer the compiler cannot see through: loads from it stay where
+// they are written instead of being hoisted out of the user / chunk loops (loop-
+// invariant fragment loads would otherwise pin their registers kernel-wide).
+template <class T>
+__device__ __forceinline__ const T* pinned(const T* p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
 
 __device__ __forceinline__ void split_bf16(float x, short& hi, short& lo) {
   const __bf16 h = (__bf16)x;
@@ -140,10 +155,50 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
   float* H1s = reinterpret_cast<float*>(smem + lo_.us);
   float* MS = reinterpret_cast<float*>(smem + lo_.ms);  // [g][{m, sum}][CH]
   float* LGP = reinterpret_cast<float*>(smem + lo_.lgp);
+  float* c1s = reinterpret_cast<float*>(smem + lo_.cst);
+  float* c2s = c1s + F;
+  float* h3s = c2s + F2;
+  int* cval = reinterpret_cast<int*>(h3s + F2);
+  float* w2s = reinterpret_cast<float*>(cval + CH);
+  uint16_t* H2h = reinterpret_cast<uint16_t*>(smem + lo_.h2);
+  uint16_t* H2l = H2h + F2 * F;
   int* qslot = reinterpret_cast<int*>(smem + lo_.total - 16);
 
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int l15 = lane & 15, l4 = lane >> 4;
+  // Lane-dependent indices are re-derived at the top of every user and chunk
+  // from a thread id the compiler cannot see through (refresh): otherwise it
+  // hoists dozens of per-thread LDS / global addresses to the kernel entry and
+  // spills them, and every reload then waits behind the in-flight row gathers
+  // (vmcnt counts in order).  Wave-uniform indices live in SGPRs.
+  int tid = threadIdx.x;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int lane, l15, l4, sj, pl, cq;
+  auto refresh = [&]() __attribute__((always_inline)) {
+    asm volatile("" : "+v"(tid));
+    lane = tid & 63;
+    l15 = lane & 15;
+    l4 = lane >> 4;
+    // scoring lane: candidate pair q = 4 pl + (w & 3) -> candidates 2q, 2q + 1;
+    // unit slice sj = lane & 7 (units sj SL .. sj SL + SL - 1); row group grp = w >> 2
+    sj = lane & 7;
+    pl = lane >> 3;
+    cq = 2 * (4 * pl + (w & 3));
+  };
+  refresh();
+  const int grp = w >> 2;
+
+  // ---- the head's constants -> LDS (published by the first barrier) ---------
+  for (int i = tid; i < F; i += NT) c1s[i] = a.c1[i];
+  for (int i = tid; i < A; i += NT) w2s[i] = a.w2[i];
+  for (int i = tid; i < F2; i += NT) {
+    c2s[i] = a.c2[i];
+    h3s[i] = a.h3[i];
+  }
+  if constexpr (lo_.h2l) {
+    for (int i = tid; i < F2 * F / 8; i += NT) {
+      reinterpret_cast<uint4*>(H2h)[i] = reinterpret_cast<const uint4*>(a.H2_hi)[i];
+      reinterpret_cast<uint4*>(H2l)[i] = reinterpret_cast<const uint4*>(a.H2_lo)[i];
+    }
+  }
 
   // ---- resident: this wave's 16-unit tile of W1q^T (B operand, hi + lo) --
   // projection tiles: unit tile ut, candidate tiles [ct0, ct0 + nct)
@@ -163,23 +218,38 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
     b1u = a.b1[u];
     w2u = a.w2[u];
   }
-  // ---- scoring lane: candidate pair q = 4 pl + (w & 3) -> candidates 2q, 2q + 1;
-  // unit slice j = lane & 7 (units j SL .. j SL + SL - 1); row group g = w >> 2
-  const int sj = lane & 7, pl = lane >> 3, grp = w >> 2;
-  const int cq = 2 * (4 * pl + (w & 3));
   float sgn[SL];
 #pragma unroll
   for (int i = 0; i < SL; ++i) sgn[i] = a.w2[sj * SL + i] >= 0.f ? 1.f : -1.f;
 
-  // ---- staging registers: the next work item's 64 rows (history or candidates)
+  // ---- staging: the next work item's 64 rows (history or candidates) go
+  // through registers.  Ids are read well before the rows they name (a
+  // dependent load pair would otherwise expose two memory latencies per
+  // chunk): sidn = the row ids this thread stages next.
   uint4 stg[NE];
-  auto stage_rows = [&](auto idfn) __attribute__((always_inline)) {
+  int sidn[NE];
+  unsigned svalid = 0;  // bit k: stg[k] holds a valid candidate row
+  // candidate ci of user u_ (the appended extra at ci == len), -1 = padded slot
+  auto cand_id = [&](int u_, int64_t off, int len, int ci) -> int {
+    int id = -1;
+    if (ci < len) id = a.cand[off + ci];
+    else if (ci == len && a.extra) id = a.extra[u_];
+    return id >= 0 && id < a.n_table ? id : -1;
+  };
+  auto load_cids = [&](int u_, int64_t off, int len, int c0_) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < NE; ++k) sidn[k] = cand_id(u_, off, len, c0_ + (tid + NT * k) / CPR);
+  };
+  auto issue_rows = [&]() __attribute__((always_inline)) {
+    svalid = 0;
 #pragma unroll
     for (int k = 0; k < NE; ++k) {
-      const int e = tid + NT * k, row = e / CPR, cc = e % CPR;
-      const int64_t id = idfn(row);
+      const int cc = (tid + NT * k) % CPR;
       stg[k] = make_uint4(0, 0, 0, 0);
-      if (id >= 0) stg[k] = *reinterpret_cast<const uint4*>(a.table + id * D + cc * 8);
+      if (sidn[k] >= 0) {
+        stg[k] = *reinterpret_cast<const uint4*>(a.table + (int64_t)sidn[k] * D + cc * 8);
+        svalid |= 1u << k;
+      }
     }
   };
   auto store_rows = [&]() __attribute__((always_inline)) {
@@ -189,30 +259,36 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
       *reinterpret_cast<uint4*>(img + img_off<D>(row, cc)) = stg[k];
     }
   };
-  // history of user u: valid mask of the first L slots (wave-uniform), rows compacted
-  auto stage_hist = [&](int u, uint64_t& vm) __attribute__((always_inline)) {
-    const int id = lane < a.L ? a.hist[(int64_t)u * a.L + lane] : -1;
-    vm = __ballot(lane < a.L && id >= 0 && id < a.n_table);
-    const int nv = __popcll(vm);
-    stage_rows([&](int row) -> int64_t {
-      const int src = __shfl(id, row < nv ? nth_set_bit(vm, row) : 0, 64);
-      return row < nv ? (int64_t)src : (int64_t)-1;
-    });
+  auto store_valid = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+      const int e = tid + NT * k;
+      if (e % CPR == 0) cval[e / CPR] = (svalid >> k) & 1;
+    }
   };
-  auto cand_id = [&](int u, int64_t off, int len, int ci) -> int64_t {
-    int id = -1;
-    if (ci < len) id = a.cand[off + ci];
-    else if (ci == len && a.extra) id = a.extra[u];
-    return id >= 0 && id < a.n_table ? (int64_t)id : (int64_t)-1;
+  // history of a user (hid: lane's slot id): valid mask of the first L slots
+  // (wave-uniform), rows compacted to the front
+  auto load_hid = [&](int u_) -> int { return lane < a.L ? a.hist[(int64_t)u_ * a.L + lane] : -1; };
+  auto issue_hist = [&](int hid, uint64_t& vm_) __attribute__((always_inline)) {
+    vm_ = __ballot(lane < a.L && hid >= 0 && hid < a.n_table);
+    const int nv_ = __popcll(vm_);
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+      const int e = tid + NT * k, row = e / CPR, cc = e % CPR;
+      const int src = __shfl(hid, row < nv_ ? nth_set_bit(vm_, row) : 0, 64);
+      stg[k] = make_uint4(0, 0, 0, 0);
+      if (row < nv_) stg[k] = *reinterpret_cast<const uint4*>(a.table + (int64_t)src * D + cc * 8);
+    }
   };
 
   if (tid == 0) qslot[0] = atomicAdd(a.queue, 1);
   __syncthreads();
   int u = qslot[0];
   uint64_t vm = 0;
-  if (u < a.nU) stage_hist(u, vm);
+  if (u < a.nU) issue_hist(load_hid(u), vm);
 
   while (u < a.nU) {
+    refresh();
     const int nv = __popcll(vm), npad = a.L - nv, nr = nv + (npad > 0 ? 1 : 0);
     const int nrp = (nr + 31) & ~31;  // rows of the softmax-weight MFMA (K multiple of 32)
     const int64_t coff = a.cand_off[u];
@@ -224,33 +300,76 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
     store_rows();     // history rows -> image
     if (tid == 0) qslot[1] = atomicAdd(a.queue, 1);  // the next user (read after chunk 0's first barrier)
     __syncthreads();
-    if (nchunk > 0) stage_rows([&](int row) { return cand_id(u, coff, clen, row); });
+    if (nchunk > 0) load_cids(u, coff, clen, 0);  // chunk 0's ids (its rows are issued after [P | R])
 
     // ---- [P | R] = K [W1k ; H1p]^T for the 16-row tiles below nrp ----------
     {
       const int nrt = nrp / 16, ntile = (NUT + NFT) * nrt;
-      for (int t = w; t < ntile; t += 8) {
-        const int uti = t / nrt, rt = t % nrt;  // consecutive tiles of a wave share unit tiles where possible
+      // the B fragments of tile t (W1k or H1p rows, hi + lo), loaded one tile ahead
+      auto frag_src = [&](int t, const uint16_t*& bh, const uint16_t*& bl) __attribute__((always_inline)) {
+        const int uti = t / nrt;
         const bool isP = uti < NUT;
         const int urow = isP ? 16 * uti + l15 : 16 * (uti - NUT) + l15;
-        const uint16_t* bh = (isP ? a.W1k_hi : a.H1p_hi) + (int64_t)urow * D + 8 * l4;
-        const uint16_t* bl = (isP ? a.W1k_lo : a.H1p_lo) + (int64_t)urow * D + 8 * l4;
-        bf16x8 fh[KSD], fl[KSD];
+        bh = (isP ? pinned(a.W1k_hi) : pinned(a.H1p_hi)) + (int64_t)urow * D + 8 * l4;
+        bl = (isP ? pinned(a.W1k_lo) : pinned(a.H1p_lo)) + (int64_t)urow * D + 8 * l4;
+      };
+      bf16x8 fh[KSD], fl[KSD];
+      if (w < ntile) {
+        const uint16_t *bh, *bl;
+        frag_src(w, bh, bl);
 #pragma unroll
         for (int s = 0; s < KSD; ++s) {
           fh[s] = *reinterpret_cast<const bf16x8*>(bh + 32 * s);
           fl[s] = *reinterpret_cast<const bf16x8*>(bl + 32 * s);
         }
+      }
+      for (int t = w; t < ntile; t += 8) {
+        const int uti = t / nrt, rt = t % nrt;  // consecutive tiles of a wave share unit tiles where possible
+        const bool isP = uti < NUT;
+        const int urow = isP ? 16 * uti + l15 : 16 * (uti - NUT) + l15;
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (KSD <= 4) {  // double-buffered: the next tile's fragments load under these MFMAs
+          bf16x8 nh[KSD], nl[KSD];
+          if (t + 8 < ntile) {
+            const uint16_t *bh, *bl;
+            frag_src(t + 8, bh, bl);
 #pragma unroll
-        for (int s = 0; s < KSD; ++s) {
-          const bf16x8 af = *reinterpret_cast<const bf16x8*>(img + img_off<D>(16 * rt + l15, 4 * s + l4));
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, fl[s], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, fh[s], acc, 0, 0, 0);
+            for (int s = 0; s < KSD; ++s) {
+              nh[s] = *reinterpret_cast<const bf16x8*>(bh + 32 * s);
+              nl[s] = *reinterpret_cast<const bf16x8*>(bl + 32 * s);
+            }
+          }
+#pragma unroll
+          for (int s = 0; s < KSD; ++s) {
+            const bf16x8 af = *reinterpret_cast<const bf16x8*>(img + img_off<D>(16 * rt + l15, 4 * s + l4));
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, fl[s], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, fh[s], acc, 0, 0, 0);
+          }
+#pragma unroll
+          for (int s = 0; s < KSD; ++s) {
+            fh[s] = nh[s];
+            fl[s] = nl[s];
+          }
+        } else {  // d = 256: no registers to spare for a second tile
+          if (t != w) {
+            const uint16_t *bh, *bl;
+            frag_src(t, bh, bl);
+#pragma unroll
+            for (int s = 0; s < KSD; ++s) {
+              fh[s] = *reinterpret_cast<const bf16x8*>(bh + 32 * s);
+              fl[s] = *reinterpret_cast<const bf16x8*>(bl + 32 * s);
+            }
+          }
+#pragma unroll
+          for (int s = 0; s < KSD; ++s) {
+            const bf16x8 af = *reinterpret_cast<const bf16x8*>(img + img_off<D>(16 * rt + l15, 4 * s + l4));
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, fl[s], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, fh[s], acc, 0, 0, 0);
+          }
         }
         const int r0 = 16 * rt + 4 * l4;
         if (isP) {
-          const float wv = a.w2[urow];
+          const float wv = w2s[urow];
           const int col = (urow / SL) * SLP + urow % SL;
 #pragma unroll
           for (int i = 0; i < 4; ++i) Pp[(r0 + i) * PRS + col] = wv * acc[i];
@@ -266,6 +385,7 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
         }
       }
     }
+    if (nchunk > 0) issue_rows();  // chunk 0's rows
     __syncthreads();
     {  // SP / 2 per row: thread = (row, slice)
       const int r = tid >> 3, j = tid & 7;
@@ -283,14 +403,30 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
     for (int ch = 0; ch < nchunk; ++ch) {
       const int c0 = ch * CH, nc = ctot - c0 < CH ? ctot - c0 : CH;
       __syncthreads();  // previous chunk done with S / h1 / partial logits; SP published
+      refresh();
       store_rows();     // candidate rows -> image
+      store_valid();
       __syncthreads();
       if (ch == 0) un = qslot[1];
-      // the next work item's rows: the next chunk, or the next user's history
-      if (ch + 1 < nchunk) {
-        stage_rows([&](int row) { return cand_id(u, coff, clen, c0 + CH + row); });
-      } else if (un < a.nU) {
-        stage_hist(un, vm);
+      // the next work item: the next chunk, or the next user's history.  Its
+      // ids are read now, its rows once Q1 is issued (registers, kept in flight
+      // across the scoring)
+      const bool nxt_c = ch + 1 < nchunk, nxt_h = !nxt_c && un < a.nU;
+      int hid = -1;
+      if (nxt_c) load_cids(u, coff, clen, c0 + CH);
+      else if (nxt_h) hid = load_hid(un);
+      // Q1 tiles of this wave: candidate tile qct = w & 3, F tiles ft = (w >> 2) + 2 i;
+      // the first tile's H1q fragments are read before the projection
+      const int qct = w & 3;
+      bf16x8 q1h[KSD], q1l[KSD];
+      {
+        const int64_t fo = (int64_t)(16 * (w >> 2) + l15) * D + 8 * l4;
+        const uint16_t *qh = pinned(a.H1q_hi), *ql = pinned(a.H1q_lo);
+#pragma unroll
+        for (int s = 0; s < KSD; ++s) {
+          q1h[s] = *reinterpret_cast<const bf16x8*>(qh + fo + 32 * s);
+          q1l[s] = *reinterpret_cast<const bf16x8*>(ql + fo + 32 * s);
+        }
       }
       // ---- 1. U' = w2 (W1q q + b1) -> Us;  Q1 = H1q q tiles -> registers ----
       if (proj_on) {
@@ -307,26 +443,28 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
           for (int i = 0; i < 4; ++i) Us[(16 * ct + 4 * l4 + i) * PRS + col] = w2u * (acc[i] + b1u);
         }
       }
-      // Q1 tiles of this wave: candidate tile ct = w & 3, F tiles ft = (w >> 2) + 2 i
       f32x4 q1[NQT];
-      const int qct = w & 3;
 #pragma unroll
       for (int i = 0; i < NQT; ++i) {
         q1[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const int ft = (w >> 2) + 2 * i;
-        {
-          const uint16_t* bh = a.H1q_hi + (int64_t)(16 * ft + l15) * D + 8 * l4;
-          const uint16_t* bl = a.H1q_lo + (int64_t)(16 * ft + l15) * D + 8 * l4;
+        if (i > 0) {  // F > 32: later tiles' fragments are read here
+          const int64_t fo = (int64_t)(16 * ((w >> 2) + 2 * i) + l15) * D + 8 * l4;
+          const uint16_t *qh = pinned(a.H1q_hi), *ql = pinned(a.H1q_lo);
 #pragma unroll
           for (int s = 0; s < KSD; ++s) {
-            const bf16x8 af = *reinterpret_cast<const bf16x8*>(img + img_off<D>(16 * qct + l15, 4 * s + l4));
-            const bf16x8 fh = *reinterpret_cast<const bf16x8*>(bh + 32 * s);
-            const bf16x8 fl = *reinterpret_cast<const bf16x8*>(bl + 32 * s);
-            q1[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, fl, q1[i], 0, 0, 0);
-            q1[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, fh, q1[i], 0, 0, 0);
+            q1h[s] = *reinterpret_cast<const bf16x8*>(qh + fo + 32 * s);
+            q1l[s] = *reinterpret_cast<const bf16x8*>(ql + fo + 32 * s);
           }
         }
+#pragma unroll
+        for (int s = 0; s < KSD; ++s) {
+          const bf16x8 af = *reinterpret_cast<const bf16x8*>(img + img_off<D>(16 * qct + l15, 4 * s + l4));
+          q1[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, q1l[s], q1[i], 0, 0, 0);
+          q1[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, q1h[s], q1[i], 0, 0, 0);
+        }
       }
+      if (nxt_c) issue_rows();
+      else if (nxt_h) issue_hist(hid, vm);
       __syncthreads();  // U' published; the image is dead (S takes its place)
 
       // ---- 2. scoring: rows r = grp, grp + 2, ... -------------------------
@@ -451,7 +589,7 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
                 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(eh[ks], rh, acc, 0, 0, 0);
               }
             }
-            const float cb = a.c1[f];
+            const float cb = c1s[f];
 #pragma unroll
             for (int k = 0; k < 4; ++k) H1s[(16 * qct + 4 * l4 + k) * (F + 4) + f] = fmaxf(acc[k] / den[k] + cb, 0.f);
           }
@@ -478,13 +616,15 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
               hh[jj] = h;
               hl[jj] = l;
             }
-            const bf16x8 bh = *reinterpret_cast<const bf16x8*>(a.H2_hi + (int64_t)v * F + 32 * ks + 8 * l4);
-            const bf16x8 bl = *reinterpret_cast<const bf16x8*>(a.H2_lo + (int64_t)v * F + 32 * ks + 8 * l4);
+            const uint16_t* h2h = lo_.h2l ? H2h : pinned(a.H2_hi);
+            const uint16_t* h2l = lo_.h2l ? H2l : pinned(a.H2_lo);
+            const bf16x8 bh = *reinterpret_cast<const bf16x8*>(h2h + v * F + 32 * ks + 8 * l4);
+            const bf16x8 bl = *reinterpret_cast<const bf16x8*>(h2l + v * F + 32 * ks + 8 * l4);
             acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hl, bh, acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hh, bl, acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hh, bh, acc, 0, 0, 0);
           }
-          const float cv = a.c2[v], hv = a.h3[v];
+          const float cv = c2s[v], hv = h3s[v];
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
             const float z = row_sum16(hv * fmaxf(acc[k] + cv, 0.f));
@@ -498,13 +638,12 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
       if (tid < nc) {
         float lg = a.c3;
         for (int t2 = 0; t2 < F2 / 16; ++t2) lg += LGP[t2 * CH + tid];
-        const bool ok = cand_id(u, coff, clen, c0 + tid) >= 0;
-        a.out[ooff + c0 + tid] = ok ? lg : -INFINITY;
+        a.out[ooff + c0 + tid] = cval[tid] ? lg : -INFINITY;
       }
     }
     if (nchunk == 0) {  // nothing to score: the next user's history still has to be staged
       un = qslot[1];
-      if (un < a.nU) stage_hist(un, vm);
+      if (un < a.nU) issue_hist(load_hid(un), vm);
     }
     u = un;
   }

@@ -223,15 +223,19 @@ def test_rerank_fused_vs_oracle_c5_shape(gpu):
         refs.append((ref, Lb[u][valid].astype(np.int64)))
     print(f"fused re-rank logits max abs err vs the fp64 reference: {worst:.3g}")
     assert worst < 1e-4, worst
-    exempt = 0
+    # every user's NDCG@5 is compared; a difference is only admissible where the
+    # positive lies within 2 x the measured logit error of another candidate
+    near, differ = 0, 0
     for u, (ref, lab_u) in enumerate(refs):
         nd_ref = o.ndcg_single(1 / (1 + np.exp(-ref)), lab_u, 5)
-        if _margin(ref, lab_u) <= 2 * worst:
-            exempt += 1
-            continue
-        assert nd[u] == nd_ref, (u, nd[u], nd_ref)
-    print(f"NDCG@5 equal for all users; {exempt} exempted (positive within 2 x {worst:.2g} of another logit)")
-    assert exempt == 0
+        close = _margin(ref, lab_u) <= 2 * worst
+        near += close
+        if nd[u] != nd_ref:
+            differ += 1
+            assert close, (u, nd[u], nd_ref, _margin(ref, lab_u))
+    print(f"NDCG@5: {differ} of {U} users differ from the fp64 reference; {near} users have the positive within "
+          f"2 x {worst:.2g} of another logit")
+    assert differ == 0
 
 
 def test_rerank_matches_reference_evaluate_fixture_c5(gpu):
