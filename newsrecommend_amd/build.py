@@ -24,6 +24,9 @@ ARCH = "gfx950"
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"]
 SOURCES = ["nrk_common.cpp", "click_log.cpp", "knn_flat.hip", "din_attn.hip", "ivf_build.hip", "din_head.hip", "din_rerank.hip",
            "screen_dp32.hip", "screen_dp64.hip", "screen_dp128.hip", "screen_dp256.hip"]
+# din_rerank: no NaN inputs (finite weights and table rows; padded candidates are
+# written as -inf, never computed), so max / min need no IEEE canonicalisation
+FILE_FLAGS = {"din_rerank.hip": ["-fno-honor-nans", "-mno-amdgpu-ieee"]}
 
 
 def _run(cmd):
@@ -52,7 +55,7 @@ def build_lib(force: bool = False) -> str:
         objs.append(obj)
         if force or not _newer(obj, [src, *headers]):
             lang = ["-x", "hip"] if s.endswith(".hip") else []
-            jobs.append([HIPCC, *HIP_FLAGS, *lang, "-c", src, "-o", obj])
+            jobs.append([HIPCC, *HIP_FLAGS, *FILE_FLAGS.get(s, []), *lang, "-c", src, "-o", obj])
     with cf.ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
         list(ex.map(_run, jobs))
     if jobs or not _newer(LIB, objs):

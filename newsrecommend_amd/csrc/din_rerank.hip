@@ -123,13 +123,15 @@ struct Lds {  // byte offsets
   }
 };
 
-// A uniform pointer the compiler cannot see through: loads from it stay where
-// they are written instead of being hoisted out of the user / chunk loops (loop-
-// invariant fragment loads would otherwise pin their registers kernel-wide).
+// A pointer offset by an opaque zero: loads from it stay where they are written
+// instead of being hoisted out of the user / chunk loops (loop-invariant fragment
+// loads would otherwise pin their registers kernel-wide).  The base keeps its
+// global address space (hiding the pointer itself would turn them into flat loads).
 template <class T>
 __device__ __forceinline__ const T* pinned(const T* p) {
-  asm volatile("" : "+s"(p));
-  return p;
+  int z = 0;
+  asm volatile("" : "+s"(z));
+  return p + z;
 }
 
 __device__ __forceinline__ void split_bf16(float x, short& hi, short& lo) {
@@ -314,7 +316,7 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
         bl = (isP ? pinned(a.W1k_lo) : pinned(a.H1p_lo)) + (int64_t)urow * D + 8 * l4;
       };
       bf16x8 fh[KSD], fl[KSD];
-      if (w < ntile) {
+      if (KSD <= 4 && w < ntile) {
         const uint16_t *bh, *bl;
         frag_src(w, bh, bl);
 #pragma unroll
@@ -351,7 +353,7 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
             fl[s] = nl[s];
           }
         } else {  // d = 256: no registers to spare for a second tile
-          if (t != w) {
+          {
             const uint16_t *bh, *bl;
             frag_src(t, bh, bl);
 #pragma unroll
@@ -486,16 +488,19 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
       hsu1 = 0.5f * oct_sum(hsu1);
       float m0 = -INFINITY, m1 = -INFINITY;
       const bool pair_on = cq < nc;  // wave-uniform per lane group; whole waves skip when empty
-      if (__ballot(pair_on) != 0) {
-        for (int r = grp; r < nr; r += 2) {
+      if (__ballot(pair_on) != 0 && grp < nr) {
+        // a row's P' slice and SP / 2, read one row ahead (two register sets)
+        float pa[SL], pb[SL], ha, hb;
+        auto load_p = [&](float(&p)[SL], float& h, int r) __attribute__((always_inline)) {
+          h = hSP[r];
           const float* pr = Pp + r * PRS + sj * SLP;
-          float p[SL];
 #pragma unroll
           for (int i = 0; i < SL; i += 4) {
             const float4 x = *reinterpret_cast<const float4*>(pr + i);
             p[i] = x.x; p[i + 1] = x.y; p[i + 2] = x.z; p[i + 3] = x.w;
           }
-          const float hsp = hSP[r];
+        };
+        auto score = [&](const float(&p)[SL], float h, int r) __attribute__((always_inline)) {
           float a0 = 0.f, a1 = 0.f;
 #pragma unroll
           for (int i = 0; i < SL; ++i) {
@@ -504,13 +509,22 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
           }
           a0 = oct_sum(a0);
           a1 = oct_sum(a1);
-          const float s0 = fmaf(0.5f, a0, hsu0 + hsp), s1 = fmaf(0.5f, a1, hsu1 + hsp);
+          const float s0 = fmaf(0.5f, a0, hsu0 + h), s1 = fmaf(0.5f, a1, hsu1 + h);
           m0 = fmaxf(m0, s0);
           m1 = fmaxf(m1, s1);
           if (sj == 0) {
             S[cq * SST + r] = s0;
             S[(cq + 1) * SST + r] = s1;
           }
+        };
+        load_p(pa, ha, grp);
+        for (int r = grp; r < nr; r += 4) {
+          const bool more = r + 2 < nr;
+          if (more) load_p(pb, hb, r + 2);
+          score(pa, ha, r);
+          if (!more) break;
+          if (r + 4 < nr) load_p(pa, ha, r + 4);
+          score(pb, hb, r + 2);
         }
       }
       // softmax weights of this group's rows: e = exp(s - m_g) (lane sj: every 8th row)

@@ -82,7 +82,9 @@ __device__ inline float wave_max(float v) {
 // Cross-lane sums on the VALU (DPP row ops and the CDNA4 half-row / half-wave
 // swaps) instead of ds_bpermute (an LDS round trip, ~100 cycles, per step):
 // every lane of the group receives the group's sum, in a fixed order.
-#define NRK_DPP(v, ctrl) __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), (ctrl), 0xf, 0xf, false))
+// (bound_ctrl set: every pattern used below is a full permutation, so it changes
+// nothing but lets the compiler fold the move into the consuming v_add / v_max)
+#define NRK_DPP(v, ctrl) __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), (ctrl), 0xf, 0xf, true))
 // sum over each quad (lanes 4k..4k+3)
 __device__ __forceinline__ float quad_sum(float v) {
   v += NRK_DPP(v, 0xB1);  // quad_perm [1,0,3,2]
