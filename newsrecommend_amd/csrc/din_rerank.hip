@@ -101,10 +101,11 @@ struct Geo {
 
 template <int D, int A, int F>
 struct Lds {  // byte offsets
-  int p, hsp, rt, q, us, ms, lgp, cst, h2, total;
+  int p, hsp, rt, q, us, ms, lgp, cst, h2, sx, total;
   bool h2l;  // H2 hi / lo resident in LDS (when it fits)
+  bool ssep;  // S in a region of its own (when it fits), not over the image
   __host__ __device__ constexpr Lds()
-      : p(0), hsp(0), rt(0), q(0), us(0), ms(0), lgp(0), cst(0), h2(0), total(0), h2l(false) {
+      : p(0), hsp(0), rt(0), q(0), us(0), ms(0), lgp(0), cst(0), h2(0), sx(0), total(0), h2l(false), ssep(false) {
     using G = Geo<D, A>;
     p = 0;                                     // P' [LP][PRS] f32
     hsp = p + LP * G::PRS * 4;                 // SP / 2 [LP] f32
@@ -115,11 +116,14 @@ struct Lds {  // byte offsets
     const int ub = CH * G::PRS * 4 > CH * (F + 4) * 4 ? CH * G::PRS * 4 : CH * (F + 4) * 4;
     ms = us + ub;                              // {m, sum} of the two row groups [2][2][CH] f32
     lgp = ms + 4 * CH * 4;                     // partial logits [F/32][CH] f32 (F/2 units in 16-unit tiles)
-    cst = lgp + (F / 32 > 0 ? F / 32 : 1) * CH * 4;  // c1 [F], c2 [F/2], h3 [F/2] f32; candidate valid [CH] i32
-    h2 = cst + 2 * F * 4 + CH * 4 + A * 4;     // (+ w2 [A] f32);  H2 hi, lo [F/2][F] bf16 (if it fits)
+    cst = lgp + (F / 32 > 0 ? F / 32 : 1) * CH * 4;  // c1 [F], c2 [F/2], h3 [F/2] f32; candidate valid [2][CH] i32
+    h2 = cst + 2 * F * 4 + 2 * CH * 4 + A * 4;  // (+ w2 [A] f32);  H2 hi, lo [F/2][F] bf16 (if it fits)
     const int h2b = 2 * (F / 2) * F * 2;
     h2l = h2 + h2b + 16 <= 160 * 1024;
-    total = (h2l ? h2 + h2b : h2) + 16;
+    int end = h2l ? h2 + h2b : h2;
+    ssep = end + CH * SST * 4 + 16 <= 160 * 1024;
+    sx = ssep ? end : q;                       // S [CH][SST] f32
+    total = (ssep ? end + CH * SST * 4 : end) + 16;
   }
 };
 
@@ -152,7 +156,7 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
   uint16_t* Rth = reinterpret_cast<uint16_t*>(smem + lo_.rt);
   uint16_t* Rtl = Rth + F * LP;
   unsigned char* img = smem + lo_.q;
-  float* S = reinterpret_cast<float*>(smem + lo_.q);
+  float* S = reinterpret_cast<float*>(smem + lo_.sx);
   float* Us = reinterpret_cast<float*>(smem + lo_.us);
   float* H1s = reinterpret_cast<float*>(smem + lo_.us);
   float* MS = reinterpret_cast<float*>(smem + lo_.ms);  // [g][{m, sum}][CH]
@@ -161,7 +165,7 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
   float* c2s = c1s + F;
   float* h3s = c2s + F2;
   int* cval = reinterpret_cast<int*>(h3s + F2);
-  float* w2s = reinterpret_cast<float*>(cval + CH);
+  float* w2s = reinterpret_cast<float*>(cval + 2 * CH);
   uint16_t* H2h = reinterpret_cast<uint16_t*>(smem + lo_.h2);
   uint16_t* H2l = H2h + F2 * F;
   int* qslot = reinterpret_cast<int*>(smem + lo_.total - 16);
@@ -261,11 +265,11 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
       *reinterpret_cast<uint4*>(img + img_off<D>(row, cc)) = stg[k];
     }
   };
-  auto store_valid = [&]() __attribute__((always_inline)) {
+  auto store_valid = [&](int* cv) __attribute__((always_inline)) {
 #pragma unroll
     for (int k = 0; k < NE; ++k) {
       const int e = tid + NT * k;
-      if (e % CPR == 0) cval[e / CPR] = (svalid >> k) & 1;
+      if (e % CPR == 0) cv[e / CPR] = (svalid >> k) & 1;
     }
   };
   // history of a user (hid: lane's slot id): valid mask of the first L slots
@@ -404,10 +408,13 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
     int un = a.nU;
     for (int ch = 0; ch < nchunk; ++ch) {
       const int c0 = ch * CH, nc = ctot - c0 < CH ? ctot - c0 : CH;
-      __syncthreads();  // previous chunk done with S / h1 / partial logits; SP published
+      int* cvb = cval + (ch & 1) * CH;  // validity of this chunk's candidates (double-buffered)
+      // With S apart from the image, the previous chunk's head (which reads S,
+      // h1 and the other validity buffer) may still run while the rows land.
+      if (!lo_.ssep || ch == 0) __syncthreads();  // (ch == 0: SP published)
       refresh();
       store_rows();     // candidate rows -> image
-      store_valid();
+      store_valid(cvb);
       __syncthreads();
       if (ch == 0) un = qslot[1];
       // the next work item: the next chunk, or the next user's history.  Its
@@ -642,17 +649,23 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
             const float z = row_sum16(hv * fmaxf(acc[k] + cv, 0.f));
-            if (l15 == 0) LGP[t2 * CH + 16 * ct + 4 * l4 + k] = z;
+            const int cc = 16 * ct + 4 * l4 + k;
+            if constexpr (F2 == 16) {  // one unit tile: the logit is complete here
+              if (l15 == 0 && cc < nc) a.out[ooff + c0 + cc] = cvb[cc] ? a.c3 + z : -INFINITY;
+            } else {
+              if (l15 == 0) LGP[t2 * CH + cc] = z;
+            }
           }
         }
       }
-      __syncthreads();  // partial logits published
-
-      // ---- 5. logits -------------------------------------------------------
-      if (tid < nc) {
-        float lg = a.c3;
-        for (int t2 = 0; t2 < F2 / 16; ++t2) lg += LGP[t2 * CH + tid];
-        a.out[ooff + c0 + tid] = cval[tid] ? lg : -INFINITY;
+      if constexpr (F2 > 16) {
+        __syncthreads();  // partial logits published
+        // ---- 5. logits -----------------------------------------------------
+        if (tid < nc) {
+          float lg = a.c3;
+          for (int t2 = 0; t2 < F2 / 16; ++t2) lg += LGP[t2 * CH + tid];
+          a.out[ooff + c0 + tid] = cvb[tid] ? lg : -INFINITY;
+        }
       }
     }
     if (nchunk == 0) {  // nothing to score: the next user's history still has to be staged
