@@ -114,8 +114,8 @@ struct Lds {  // byte offsets
     const int qb = CH * D * 2 > CH * SST * 4 ? CH * D * 2 : CH * SST * 4;
     us = q + qb;                               // U' [CH][PRS] f32;  h1 [CH][F + 4] f32 later
     const int ub = CH * G::PRS * 4 > CH * (F + 4) * 4 ? CH * G::PRS * 4 : CH * (F + 4) * 4;
-    ms = us + ub;                              // {m, sum} of the two row groups [2][2][CH] f32
-    lgp = ms + 4 * CH * 4;                     // partial logits [F/32][CH] f32 (F/2 units in 16-unit tiles)
+    ms = us + ub;                              // {m, sum} of up to 8 row groups [8][2][CH] f32
+    lgp = ms + 16 * CH * 4;                    // partial logits [F/32][CH] f32 (F/2 units in 16-unit tiles)
     cst = lgp + (F / 32 > 0 ? F / 32 : 1) * CH * 4;  // c1 [F], c2 [F/2], h3 [F/2] f32; candidate valid [2][CH] i32
     h2 = cst + 2 * F * 4 + 2 * CH * 4 + A * 4;  // (+ w2 [A] f32);  H2 hi, lo [F/2][F] bf16 (if it fits)
     const int h2b = 2 * (F / 2) * F * 2;
@@ -177,20 +177,18 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
   // (vmcnt counts in order).  Wave-uniform indices live in SGPRs.
   int tid = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  int lane, l15, l4, sj, pl, cq;
+  int lane, l15, l4, sj, pl;
   auto refresh = [&]() __attribute__((always_inline)) {
     asm volatile("" : "+v"(tid));
     lane = tid & 63;
     l15 = lane & 15;
     l4 = lane >> 4;
-    // scoring lane: candidate pair q = 4 pl + (w & 3) -> candidates 2q, 2q + 1;
-    // unit slice sj = lane & 7 (units sj SL .. sj SL + SL - 1); row group grp = w >> 2
+    // scoring lane: pair slot pl (two candidates), unit slice sj = lane & 7
+    // (units sj SL .. sj SL + SL - 1)
     sj = lane & 7;
     pl = lane >> 3;
-    cq = 2 * (4 * pl + (w & 3));
   };
   refresh();
-  const int grp = w >> 2;
 
   // ---- the head's constants -> LDS (published by the first barrier) ---------
   for (int i = tid; i < F; i += NT) c1s[i] = a.c1[i];
@@ -476,7 +474,13 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
       else if (nxt_h) issue_hist(hid, vm);
       __syncthreads();  // U' published; the image is dead (S takes its place)
 
-      // ---- 2. scoring: rows r = grp, grp + 2, ... -------------------------
+      // ---- 2. scoring: G row groups; group grp takes rows grp, grp + G, ...
+      // and its 64 / G candidates (8 / G waves x 8 pairs).  G = 2 for full
+      // chunks; a short chunk spreads its few candidates' rows over more waves.
+      const int G = nc <= 16 ? 8 : (nc <= 32 ? 4 : 2);
+      const int wpg = 8 / G;
+      const int grp = w / wpg;  // wave-uniform
+      const int cq = 2 * (wpg * pl + w % wpg);
       float u0[SL], u1[SL];
 #pragma unroll
       for (int i = 0; i < SL; i += 4) {
@@ -525,19 +529,19 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
           }
         };
         load_p(pa, ha, grp);
-        for (int r = grp; r < nr; r += 4) {
-          const bool more = r + 2 < nr;
-          if (more) load_p(pb, hb, r + 2);
+        for (int r = grp; r < nr; r += 2 * G) {
+          const bool more = r + G < nr;
+          if (more) load_p(pb, hb, r + G);
           score(pa, ha, r);
           if (!more) break;
-          if (r + 4 < nr) load_p(pa, ha, r + 4);
-          score(pb, hb, r + 2);
+          if (r + 2 * G < nr) load_p(pa, ha, r + 2 * G);
+          score(pb, hb, r + G);
         }
       }
       // softmax weights of this group's rows: e = exp(s - m_g) (lane sj: every 8th row)
       {
         float sum0 = 0.f, sum1 = 0.f;
-        for (int r = grp + 2 * sj; r < nrp; r += 16) {
+        for (int r = grp + G * sj; r < nrp; r += 8 * G) {
           float e0 = 0.f, e1 = 0.f;
           if (r < nr) {
             e0 = __expf(S[cq * SST + r] - m0);
@@ -562,17 +566,24 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
 
       // ---- 3. h1 = relu(Q1 + (e R) / sum e + c1) ----------------------------
       {
-        // A operand: candidate ca = 16 qct + l15, rows 32 ks + 8 l4 + jj scaled by exp(m_g - m)
+        // A operand: candidate ca = 16 qct + l15, rows 32 ks + 8 l4 + jj (group
+        // jj mod G) scaled by exp(m_g - m)
         const int ca = 16 * qct + l15;
-        const float ma0 = MS[0 * CH + ca], ma1 = MS[2 * CH + ca], mm = fmaxf(ma0, ma1);
-        const float sc0 = __expf(ma0 - mm), sc1 = __expf(ma1 - mm);
+        float mm = -INFINITY;
+        for (int g = 0; g < G; ++g) mm = fmaxf(mm, MS[2 * g * CH + ca]);
+        float sc8[8];
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) sc8[jj] = __expf(MS[2 * (jj & (G - 1)) * CH + ca] - mm);
         // C tile rows: candidates 16 qct + 4 l4 + i
         float den[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int cc = 16 * qct + 4 * l4 + i;
-          const float x0 = MS[0 * CH + cc], x1 = MS[2 * CH + cc], xm = fmaxf(x0, x1);
-          den[i] = MS[1 * CH + cc] * __expf(x0 - xm) + MS[3 * CH + cc] * __expf(x1 - xm);
+          float xm = -INFINITY;
+          for (int g = 0; g < G; ++g) xm = fmaxf(xm, MS[2 * g * CH + cc]);
+          float dn = 0.f;
+          for (int g = 0; g < G; ++g) dn += MS[(2 * g + 1) * CH + cc] * __expf(MS[2 * g * CH + cc] - xm);
+          den[i] = dn;
         }
         const int nks = nrp / 32;
         bf16x8 eh[2], el[2];
@@ -581,8 +592,8 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
           if (ks < nks) {
             const float4 x0 = *reinterpret_cast<const float4*>(S + ca * SST + 32 * ks + 8 * l4);
             const float4 x1 = *reinterpret_cast<const float4*>(S + ca * SST + 32 * ks + 8 * l4 + 4);
-            const float xv[8] = {x0.x * sc0, x0.y * sc1, x0.z * sc0, x0.w * sc1,
-                                 x1.x * sc0, x1.y * sc1, x1.z * sc0, x1.w * sc1};
+            const float xv[8] = {x0.x * sc8[0], x0.y * sc8[1], x0.z * sc8[2], x0.w * sc8[3],
+                                 x1.x * sc8[4], x1.y * sc8[5], x1.z * sc8[6], x1.w * sc8[7]};
 #pragma unroll
             for (int jj = 0; jj < 8; ++jj) {
               short h, l;
