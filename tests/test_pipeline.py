@@ -146,14 +146,16 @@ def _oracle_logits(model, T, hist_u, cand_u):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("d,L,C,A,F", [(256, 50, 201, 128, 32), (64, 20, 37, 32, 64), (128, 64, 70, 96, 128),
-                                       (256, 64, 130, 64, 96), (128, 33, 64, 128, 32)])
+@pytest.mark.parametrize("d,L,C,A,F", [(256, 50, 201, 128, 32), (64, 20, 90, 32, 64), (128, 64, 70, 96, 128),
+                                       (256, 64, 130, 64, 96), (128, 33, 37, 128, 32)])
 def test_rerank_fused_vs_oracle_and_per_candidate(d, L, C, A, F):
     """nrk_din_rerank over the reference's hyper-parameter space (Optuna
     DIN.py:203-204: attn_units and fc_units 32..128 step 32) against the fp64
     oracle (<= 1e-4 of the logit scale) and against every candidate as its own
     DIN sample (model.forward_ids: the same logits up to that path's bf16 W1k,
-    2e-3); padded histories (an empty one included) and padded candidates."""
+    2e-3); padded histories (an empty one included) and padded candidates.
+    Chunks of 64 candidates and tails of 37 / 26 / 9 / 6 / 2 cover the kernel's
+    2, 4 and 8 row-group forms."""
     from newsrecommend_amd.pipeline import rerank
 
     dev = torch.device("cuda")
