@@ -307,69 +307,37 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
     if (nchunk > 0) load_cids(u, coff, clen, 0);  // chunk 0's ids (its rows are issued after [P | R])
 
     // ---- [P | R] = K [W1k ; H1p]^T for the 16-row tiles below nrp ----------
+    // Tile t = (unit tile t / nrt, row tile t % nrt); wave w takes the
+    // contiguous range [w ntile / 8, (w + 1) ntile / 8), so it reads the B
+    // fragments (hi + lo, from L2) of at most two or three unit tiles.
     {
       const int nrt = nrp / 16, ntile = (NUT + NFT) * nrt;
-      // the B fragments of tile t (W1k or H1p rows, hi + lo), loaded one tile ahead
-      auto frag_src = [&](int t, const uint16_t*& bh, const uint16_t*& bl) __attribute__((always_inline)) {
-        const int uti = t / nrt;
+      const int t0 = (w * ntile) >> 3, t1 = ((w + 1) * ntile) >> 3;
+      auto load_frags = [&](int uti, bf16x8(&fh)[KSD], bf16x8(&fl)[KSD]) __attribute__((always_inline)) {
         const bool isP = uti < NUT;
         const int urow = isP ? 16 * uti + l15 : 16 * (uti - NUT) + l15;
-        bh = (isP ? pinned(a.W1k_hi) : pinned(a.H1p_hi)) + (int64_t)urow * D + 8 * l4;
-        bl = (isP ? pinned(a.W1k_lo) : pinned(a.H1p_lo)) + (int64_t)urow * D + 8 * l4;
-      };
-      bf16x8 fh[KSD], fl[KSD];
-      if (KSD <= 4 && w < ntile) {
-        const uint16_t *bh, *bl;
-        frag_src(w, bh, bl);
+        const uint16_t* bh = (isP ? pinned(a.W1k_hi) : pinned(a.H1p_hi)) + (int64_t)urow * D + 8 * l4;
+        const uint16_t* bl = (isP ? pinned(a.W1k_lo) : pinned(a.H1p_lo)) + (int64_t)urow * D + 8 * l4;
 #pragma unroll
         for (int s = 0; s < KSD; ++s) {
           fh[s] = *reinterpret_cast<const bf16x8*>(bh + 32 * s);
           fl[s] = *reinterpret_cast<const bf16x8*>(bl + 32 * s);
         }
-      }
-      for (int t = w; t < ntile; t += 8) {
-        const int uti = t / nrt, rt = t % nrt;  // consecutive tiles of a wave share unit tiles where possible
+      };
+      for (int uti = t0 / nrt; uti * nrt < t1; ++uti) {
         const bool isP = uti < NUT;
         const int urow = isP ? 16 * uti + l15 : 16 * (uti - NUT) + l15;
+        bf16x8 fh[KSD], fl[KSD];
+        load_frags(uti, fh, fl);
+        const int rb = t0 > uti * nrt ? t0 - uti * nrt : 0;
+        const int re = t1 < (uti + 1) * nrt ? t1 - uti * nrt : nrt;
+        for (int rt = rb; rt < re; ++rt) {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-        if constexpr (KSD <= 4) {  // double-buffered: the next tile's fragments load under these MFMAs
-          bf16x8 nh[KSD], nl[KSD];
-          if (t + 8 < ntile) {
-            const uint16_t *bh, *bl;
-            frag_src(t + 8, bh, bl);
 #pragma unroll
-            for (int s = 0; s < KSD; ++s) {
-              nh[s] = *reinterpret_cast<const bf16x8*>(bh + 32 * s);
-              nl[s] = *reinterpret_cast<const bf16x8*>(bl + 32 * s);
-            }
-          }
-#pragma unroll
-          for (int s = 0; s < KSD; ++s) {
-            const bf16x8 af = *reinterpret_cast<const bf16x8*>(img + img_off<D>(16 * rt + l15, 4 * s + l4));
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, fl[s], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, fh[s], acc, 0, 0, 0);
-          }
-#pragma unroll
-          for (int s = 0; s < KSD; ++s) {
-            fh[s] = nh[s];
-            fl[s] = nl[s];
-          }
-        } else {  // d = 256: no registers to spare for a second tile
-          {
-            const uint16_t *bh, *bl;
-            frag_src(t, bh, bl);
-#pragma unroll
-            for (int s = 0; s < KSD; ++s) {
-              fh[s] = *reinterpret_cast<const bf16x8*>(bh + 32 * s);
-              fl[s] = *reinterpret_cast<const bf16x8*>(bl + 32 * s);
-            }
-          }
-#pragma unroll
-          for (int s = 0; s < KSD; ++s) {
-            const bf16x8 af = *reinterpret_cast<const bf16x8*>(img + img_off<D>(16 * rt + l15, 4 * s + l4));
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, fl[s], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, fh[s], acc, 0, 0, 0);
-          }
+        for (int s = 0; s < KSD; ++s) {
+          const bf16x8 af = *reinterpret_cast<const bf16x8*>(img + img_off<D>(16 * rt + l15, 4 * s + l4));
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, fl[s], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, fh[s], acc, 0, 0, 0);
         }
         const int r0 = 16 * rt + 4 * l4;
         if (isP) {
@@ -386,6 +354,7 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
               make_uint2((uint16_t)h[0] | ((uint32_t)(uint16_t)h[1] << 16), (uint16_t)h[2] | ((uint32_t)(uint16_t)h[3] << 16));
           *reinterpret_cast<uint2*>(Rtl + f * LP + r0) =
               make_uint2((uint16_t)l[0] | ((uint32_t)(uint16_t)l[1] << 16), (uint16_t)l[2] | ((uint32_t)(uint16_t)l[3] << 16));
+        }
         }
       }
     }
