@@ -114,8 +114,8 @@ struct Lds {  // byte offsets
     const int qb = CH * D * 2 > CH * SST * 4 ? CH * D * 2 : CH * SST * 4;
     us = q + qb;                               // U' [CH][PRS] f32;  h1 [CH][F + 4] f32 later
     const int ub = CH * G::PRS * 4 > CH * (F + 4) * 4 ? CH * G::PRS * 4 : CH * (F + 4) * 4;
-    ms = us + ub;                              // {m, sum} of up to 8 row groups [8][2][CH] f32
-    lgp = ms + 16 * CH * 4;                    // partial logits [F/32][CH] f32 (F/2 units in 16-unit tiles)
+    ms = us + ub;                              // {m, sum} of the two row groups [2][2][CH] f32
+    lgp = ms + 4 * CH * 4;                     // partial logits [F/32][CH] f32 (F/2 units in 16-unit tiles)
     cst = lgp + (F / 32 > 0 ? F / 32 : 1) * CH * 4;  // c1 [F], c2 [F/2], h3 [F/2] f32; candidate valid [2][CH] i32
     h2 = cst + 2 * F * 4 + 2 * CH * 4 + A * 4;  // (+ w2 [A] f32);  H2 hi, lo [F/2][F] bf16 (if it fits)
     const int h2b = 2 * (F / 2) * F * 2;
@@ -230,7 +230,10 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
   // through registers.  Ids are read well before the rows they name (a
   // dependent load pair would otherwise expose two memory latencies per
   // chunk): sidn = the row ids this thread stages next.
-  uint4 stg[NE];
+  // (non-temporal gathers: the rows are used once, and keeping them out of L2
+  // keeps the H1q / W1k / H1p fragments every chunk and user re-reads there)
+  bf16x8 stg[NE];
+  const bf16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
   int sidn[NE];
   unsigned svalid = 0;  // bit k: stg[k] holds a valid candidate row
   // candidate ci of user u_ (the appended extra at ci == len), -1 = padded slot
@@ -249,9 +252,9 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
 #pragma unroll
     for (int k = 0; k < NE; ++k) {
       const int cc = (tid + NT * k) % CPR;
-      stg[k] = make_uint4(0, 0, 0, 0);
+      stg[k] = z8;
       if (sidn[k] >= 0) {
-        stg[k] = *reinterpret_cast<const uint4*>(a.table + (int64_t)sidn[k] * D + cc * 8);
+        stg[k] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(a.table + (int64_t)sidn[k] * D + cc * 8));
         svalid |= 1u << k;
       }
     }
@@ -260,7 +263,7 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
 #pragma unroll
     for (int k = 0; k < NE; ++k) {
       const int e = tid + NT * k, row = e / CPR, cc = e % CPR;
-      *reinterpret_cast<uint4*>(img + img_off<D>(row, cc)) = stg[k];
+      *reinterpret_cast<bf16x8*>(img + img_off<D>(row, cc)) = stg[k];
     }
   };
   auto store_valid = [&](int* cv) __attribute__((always_inline)) {
@@ -280,8 +283,8 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
     for (int k = 0; k < NE; ++k) {
       const int e = tid + NT * k, row = e / CPR, cc = e % CPR;
       const int src = __shfl(hid, row < nv_ ? nth_set_bit(vm_, row) : 0, 64);
-      stg[k] = make_uint4(0, 0, 0, 0);
-      if (row < nv_) stg[k] = *reinterpret_cast<const uint4*>(a.table + (int64_t)src * D + cc * 8);
+      stg[k] = z8;
+      if (row < nv_) stg[k] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(a.table + (int64_t)src * D + cc * 8));
     }
   };
 
@@ -443,11 +446,13 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
       else if (nxt_h) issue_hist(hid, vm);
       __syncthreads();  // U' published; the image is dead (S takes its place)
 
-      // ---- 2. scoring: G row groups; group grp takes rows grp, grp + G, ...
-      // and its 64 / G candidates (8 / G waves x 8 pairs).  G = 2 for full
-      // chunks; a short chunk spreads its few candidates' rows over more waves.
-      const int G = nc <= 16 ? 8 : (nc <= 32 ? 4 : 2);
-      const int wpg = 8 / G;
+      // ---- 2. scoring: G = 2 row groups; group grp (waves 4 grp .. 4 grp + 3)
+      // takes rows grp, grp + 2, ... of all 64 candidates.  (Spreading a short
+      // chunk over more groups would change the softmax's summation order with
+      // the list's padding: the padded and ragged forms of a list must agree
+      // bit for bit.)
+      constexpr int G = 2;
+      constexpr int wpg = 8 / G;
       const int grp = w / wpg;  // wave-uniform
       const int cq = 2 * (wpg * pl + w % wpg);
       float u0[SL], u1[SL];

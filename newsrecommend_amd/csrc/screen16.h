@@ -39,10 +39,13 @@ __device__ __forceinline__ void list_insert_tie(float (&ls)[N], int (&li)[N], fl
   }
 }
 
-// PREF: the next sub-tile's A fragments are read during the current chain (2 x DP / 32
-// fragments live); PREF = false reads each K step's two fragments just before its
-// MFMAs (2 live), for the M = 16 lists that would not fit beside the prefetch
-template <int DP, int QT, int M, int WAVES, int TIL, bool SCHED = true, bool PREF = true>
+// PD: A-fragment prefetch depth in K steps.  Each K step's two fragments are read
+// PD steps before their MFMAs, into a ring of 2 PD registers sets: PD = DP / 32
+// reads the whole next sub-tile during the current chain; a shallower ring
+// (the M = 16 lists, which would not fit beside a full prefetch) reads the
+// current sub-tile's later steps during its own chain, so the tile being
+// consumed is never the refill target: three LDS buffers instead of two.
+template <int DP, int QT, int M, int WAVES, int TIL, bool SCHED = true, int PD = DP / 32>
 __global__ __launch_bounds__(WAVES * 64, 2) void screen16_kernel(
     const uint16_t* __restrict__ qh, const uint16_t* __restrict__ xbh, const float* __restrict__ xmeta, int64_t nq,
     int64_t nb, int64_t chunk, int nch, int nqt, int tstride, float* __restrict__ part_s, int* __restrict__ part_i,
@@ -62,7 +65,9 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_kernel(
   constexpr int NQ2 = 2 * QT;   // 16-query half-tiles per wave
   constexpr int WQ = WAVES * 32 * QT;
   constexpr int BUF = TI * DP;
-  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BUF];
+  static_assert(PD >= 1 && PD <= KS2, "prefetch depth");
+  constexpr int NBUF = PD == KS2 ? 2 : 3;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[NBUF * BUF];
 
   const int nblk = gridDim.x, b = blockIdx.x;
   const int xg = b & 7, jj = b >> 3, q8 = nblk >> 3, r8 = nblk & 7;
@@ -119,7 +124,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_kernel(
   f32x4 accA[NQ2][2], accB[NQ2][2];
   int64_t baseA = -1, baseB = -1;
   int nvA = 0, nvB = 0;
-  bf16x8 af[2][PREF ? KS2 : 1];
+  bf16x8 af[2][PD];
   auto mask_rows = [&](f32x4 (&pa)[NQ2][2], int nv) __attribute__((always_inline)) {
 #pragma unroll
     for (int t = 0; t < NQ2; ++t)
@@ -175,17 +180,15 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_kernel(
     const f32x4 zero = {};
 #pragma unroll
     for (int s = 0; s < KS2; ++s) {
-      if constexpr (!PREF) {
-        af[0][0] = afrag(cur_tl, 32 * st + q16, s);
-        af[1][0] = afrag(cur_tl, 32 * st + 16 + q16, s);
-      }
 #pragma unroll
       for (int ih = 0; ih < 2; ++ih) {
 #pragma unroll
         for (int t = 0; t < NQ2; ++t)
-          cur[t][ih] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ih][PREF ? s : 0], qf[t][s],
+          cur[t][ih] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ih][s % PD], qf[t][s],
                                                              s == 0 ? zero : cur[t][ih], 0, 0, 0);
-        if constexpr (PREF) af[ih][s] = afrag(next_tl, nrow + 16 * ih, s);
+        // refill the slot with the fragment PD steps ahead: this sub-tile's, or the next one's
+        if (s + PD < KS2) af[ih][s % PD] = afrag(cur_tl, 32 * st + 16 * ih + q16, s + PD);
+        else af[ih][s % PD] = afrag(next_tl, nrow + 16 * ih, s + PD - KS2);
       }
     }
     float m2[NQ2][2], m[NQ2];
@@ -211,6 +214,8 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_kernel(
   };
   auto tile_d = [&](int it, auto buf_c) __attribute__((always_inline)) {
     constexpr int buf = decltype(buf_c)::value;
+    constexpr int nbuf = (buf + 1) % NBUF;  // tile it + 1
+    constexpr int rbuf = (buf + 2) % NBUF;  // refilled with tile it + 2
     const uint16_t* tl = lds + buf * BUF;
     const int64_t i0 = ibeg + (int64_t)it * TI;
     const int nvalid = (int)((iend - i0) < TI ? (iend - i0) : TI);
@@ -219,33 +224,30 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_kernel(
       sub_tile(std::integral_constant<int, 1>{}, i0, nvalid, tl, tl);
       sub_tile(std::integral_constant<int, 2>{}, i0, nvalid, tl, tl);
     }
-    if constexpr (PREF) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();  // tile it+1 landed; every wave is done with buffer buf
-      if (it + 2 < ntiles) issue_tile(it + 2, buf_c);
-      sub_tile(std::integral_constant<int, NSUB - 1>{}, i0, nvalid, lds + (buf ^ 1) * BUF, tl);
-    } else {  // the last sub-tile still reads buf: refill it only after
-      sub_tile(std::integral_constant<int, NSUB - 1>{}, i0, nvalid, tl, tl);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();  // tile it+1 landed; every wave is done with buffer buf
-      if (it + 2 < ntiles) issue_tile(it + 2, buf_c);
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // tile it+1 landed; every wave is done with rbuf: with two buffers the last
+    // sub-tile's fragments are all in registers already (PD = K steps), with
+    // three rbuf held tile it-1, which every wave has finished
+    __syncthreads();
+    if (it + 2 < ntiles) issue_tile(it + 2, std::integral_constant<int, rbuf>{});
+    sub_tile(std::integral_constant<int, NSUB - 1>{}, i0, nvalid, lds + nbuf * BUF, tl);
   };
   if (ntiles > 0) {
     issue_tile(0, std::integral_constant<int, 0>{});
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // tile 0 landed
     if (ntiles > 1) issue_tile(1, std::integral_constant<int, 1>{});
-    if constexpr (PREF) {
 #pragma unroll
-      for (int ih = 0; ih < 2; ++ih)
+    for (int ih = 0; ih < 2; ++ih)
 #pragma unroll
-        for (int s = 0; s < KS2; ++s) af[ih][s] = afrag(lds, 16 * ih + q16, s);
-    }
+      for (int s = 0; s < PD; ++s) af[ih][s] = afrag(lds, 16 * ih + q16, s);
   }
-  for (int it = 0; it < ntiles; it += 2) {
+  for (int it = 0; it < ntiles; it += NBUF) {
     tile_d(it, std::integral_constant<int, 0>{});
     if (it + 1 < ntiles) tile_d(it + 1, std::integral_constant<int, 1>{});
+    if constexpr (NBUF == 3) {
+      if (it + 2 < ntiles) tile_d(it + 2, std::integral_constant<int, 2 % NBUF>{});
+    }
   }
   if (baseB >= 0) {  // the last sub-tile's epilogue
     if (nvB < 32) mask_rows(accB, nvB);
