@@ -488,9 +488,13 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
         auto score = [&](const float(&p)[SL], float h, int r) __attribute__((always_inline)) {
           float a0 = 0.f, a1 = 0.f;
 #pragma unroll
-          for (int i = 0; i < SL; ++i) {
-            a0 = fmaf(fabsf(u0[i] + p[i]), sgn[i], a0);
-            a1 = fmaf(fabsf(u1[i] + p[i]), sgn[i], a1);
+          for (int i = 0; i < SL; i += 2) {  // two units per packed add
+            const f32x2 pv = {p[i], p[i + 1]};
+            const f32x2 y0 = f32x2{u0[i], u0[i + 1]} + pv, y1 = f32x2{u1[i], u1[i + 1]} + pv;
+            a0 = fmaf(fabsf(y0.x), sgn[i], a0);
+            a1 = fmaf(fabsf(y1.x), sgn[i], a1);
+            a0 = fmaf(fabsf(y0.y), sgn[i + 1], a0);
+            a1 = fmaf(fabsf(y1.y), sgn[i + 1], a1);
           }
           a0 = oct_sum(a0);
           a1 = oct_sum(a1);

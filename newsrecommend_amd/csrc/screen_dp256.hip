@@ -6,11 +6,14 @@ namespace nrk {
 NRK_SCREEN_DP(256)
 
 // 16x16x32 main pass at DP = 256 (8 waves, 64-item tiles, sched_group_barrier
-// interleave), M = 4 only (N1): 15.69 ms vs 15.82 for the 32x32x16 kernel (10M x
-// 256, k = 5; the compiler's own schedule 15.97).  M = 16 (k = 200) keeps the
-// 32x32x16 kernel: the 16x16x32 form spills 32 VGPRs there (34.8 vs 16.7 ms), and
-// reading the A fragments per K step instead (228 VGPRs) ran 17.40 vs 15.87 ms.
+// interleave).  M = 4 (N1): 15.69 ms vs 15.82 for the 32x32x16 kernel (10M x 256,
+// k = 5; the compiler's own schedule 15.97).  M = 16 (k = 200): the full next-
+// sub-tile prefetch spills 32 VGPRs beside the lists (34.8 vs 16.7 ms) and no
+// prefetch exposes the LDS latency (17.40 vs 15.87 ms); a 2-step fragment ring
+// over three LDS buffers fits (2 spills, outside the chain): 15.89 vs 16.41 ms
+// for the 32x32x16 kernel (4-step ring 16.19), same ids (profiles/r04_k200_ring_ab.log).
 screen_fn pick_screen16_dp256_w8(int M) {
+  if (M == 16) return screen16_kernel<256, 1, 16, 8, 64, true, 2>;
   return M == 4 ? screen16_kernel<256, 1, 4, 8, 64, true> : nullptr;
 }
 

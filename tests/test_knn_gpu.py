@@ -56,15 +56,17 @@ def test_screen_partial_chunk_tiles(gpu, metric, d, k):
 
 
 @pytest.mark.parametrize("form", ["0", "1"])
-@pytest.mark.parametrize("d,n", [(128, 60_001), (128, 70_003), (256, 60_001), (256, 70_003)])
-def test_screen_main_pass_forms(gpu, monkeypatch, form, d, n):
+@pytest.mark.parametrize("d,n,k", [(128, 60_001, 5), (128, 70_003, 5), (256, 60_001, 5), (256, 70_003, 5),
+                                   (256, 60_001, 200), (256, 70_003, 200)])
+def test_screen_main_pass_forms(gpu, monkeypatch, form, d, n, k):
     """The inner-product main pass runs on the 16x16x32 kernel (screen16.h) by
-    default at k <= 8 for d 128 / 256 (=1); the 32x32x16 kernel (NRK_SCREEN16=0,
-    the one every other form runs) gives the oracle's results too, with and
-    without partial last tiles."""
+    default at k <= 8 for d 128 / 256 and at k = 200 for d 256 (its 2-step
+    fragment ring over three LDS buffers) (=1); the 32x32x16 kernel
+    (NRK_SCREEN16=0, the one every other form runs) gives the oracle's results
+    too, with and without partial last tiles."""
     monkeypatch.setenv("NRK_SCREEN16", form)
     xq, xb = _mixture(n, 300, d, seed=d + n % 7)
-    _check(xq, xb, 5, ko.METRIC_IP, gpu)
+    _check(xq, xb, k, ko.METRIC_IP, gpu)
 
 
 @pytest.mark.parametrize("metric", [ko.METRIC_IP, ko.METRIC_L2])
@@ -107,12 +109,13 @@ def test_duplicates_and_ties_take_lower_id(gpu):
 
 
 @pytest.mark.parametrize("metric", [ko.METRIC_IP, ko.METRIC_L2])
-def test_k200_tied_block_at_the_selection_cut(gpu, metric):
+@pytest.mark.parametrize("d", [64, 256])
+def test_k200_tied_block_at_the_selection_cut(gpu, metric, d):
     """k = 200 (the merge SELECTS its 400 rescoring candidates by score keys):
     900 exact copies of one row spread over the corpus tie at the cut, so the
     tie rule (ascending id) decides which copies are rescored; results equal
-    the oracle's."""
-    xq, xb = _mixture(60_001, 64, 64, seed=11)
+    the oracle's (d 256: the 16x16x32 main pass's lane lists)."""
+    xq, xb = _mixture(60_001, 64, d, seed=11)
     rng = np.random.default_rng(5)
     dup = np.sort(rng.choice(np.arange(1, 60_001), 900, replace=False))
     xb[dup] = xb[0]
