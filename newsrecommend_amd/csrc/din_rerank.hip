@@ -92,8 +92,16 @@ __device__ __forceinline__ int img_off(int row, int chunk) {  // byte offset of 
 template <int D, int A>
 struct Geo {
   static constexpr int SL = A / 8;                 // units per scoring lane
-  static constexpr int SLP = SL == 16 ? 20 : SL;   // slice stride (floats): conflict-free b128 reads of 8 slices
-  static constexpr int PRS = 8 * SLP;              // P' / U' row stride (floats)
+  static constexpr int PRS = A;                    // P' / U' row stride (floats): 8 slices of SL units
+  // physical float4 of the i4-th float4 of slice sj: at SL = 16 the slices sj and
+  // sj + 4 (256 B apart, same banks) store their float4s rotated by two, so the
+  // eight slices' b128 reads of a row stay conflict-free without padding
+  __device__ static int pos4(int sj, int i4) { return SL == 16 ? (i4 + 2 * (sj >> 2)) & 3 : i4; }
+  // float offset of attention unit n within a P' / U' row
+  __device__ static int col(int n) {
+    const int sj = n / SL, w = n % SL;
+    return sj * SL + 4 * pos4(sj, w >> 2) + (w & 3);
+  }
   static constexpr int NE = LP * (D / 8) / NT;     // staged 16-B chunks per thread
   static constexpr int KSD = D / 32;               // k-steps over d
   static constexpr int NUT = A / 16;               // 16-unit tiles of U / P
@@ -101,18 +109,20 @@ struct Geo {
 
 template <int D, int A, int F>
 struct Lds {  // byte offsets
-  int p, hsp, rt, q, us, ms, lgp, cst, h2, sx, total;
-  bool h2l;  // H2 hi / lo resident in LDS (when it fits)
+  int p, hsp, rt, q, us, ms, lgp, cst, h2, sx, h1q, total;
+  bool h2l;   // H2 hi / lo resident in LDS (when it fits)
   bool ssep;  // S in a region of its own (when it fits), not over the image
+  bool h1l;   // H1q hi / lo resident in LDS (when it fits; else read from L2 per chunk)
   __host__ __device__ constexpr Lds()
-      : p(0), hsp(0), rt(0), q(0), us(0), ms(0), lgp(0), cst(0), h2(0), sx(0), total(0), h2l(false), ssep(false) {
+      : p(0), hsp(0), rt(0), q(0), us(0), ms(0), lgp(0), cst(0), h2(0), sx(0), h1q(0), total(0), h2l(false),
+        ssep(false), h1l(false) {
     using G = Geo<D, A>;
-    p = 0;                                     // P' [LP][PRS] f32
+    p = 0;                                     // P' [LP][A] f32
     hsp = p + LP * G::PRS * 4;                 // SP / 2 [LP] f32
     rt = hsp + LP * 4;                         // R^T hi, lo [F][LP] bf16
     q = rt + 2 * F * LP * 2;                   // candidate / history image [64][D] bf16;  S [CH][SST] f32 later
     const int qb = CH * D * 2 > CH * SST * 4 ? CH * D * 2 : CH * SST * 4;
-    us = q + qb;                               // U' [CH][PRS] f32;  h1 [CH][F + 4] f32 later
+    us = q + qb;                               // U' [CH][A] f32;  h1 [CH][F + 4] f32 later
     const int ub = CH * G::PRS * 4 > CH * (F + 4) * 4 ? CH * G::PRS * 4 : CH * (F + 4) * 4;
     ms = us + ub;                              // {m, sum} of the two row groups [2][2][CH] f32
     lgp = ms + 4 * CH * 4;                     // partial logits [F/32][CH] f32 (F/2 units in 16-unit tiles)
@@ -123,7 +133,10 @@ struct Lds {  // byte offsets
     int end = h2l ? h2 + h2b : h2;
     ssep = end + CH * SST * 4 + 16 <= 160 * 1024;
     sx = ssep ? end : q;                       // S [CH][SST] f32
-    total = (ssep ? end + CH * SST * 4 : end) + 16;
+    if (ssep) end += CH * SST * 4;
+    h1q = end;                                 // H1q hi, lo [F][D] bf16 (image swizzle), if it fits
+    h1l = end + 2 * F * D * 2 + 16 <= 160 * 1024;
+    total = (h1l ? end + 2 * F * D * 2 : end) + 16;
   }
 };
 
@@ -147,7 +160,7 @@ __device__ __forceinline__ void split_bf16(float x, short& hi, short& lo) {
 template <int D, int A, int F>
 __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
   using G = Geo<D, A>;
-  constexpr int SL = G::SL, SLP = G::SLP, PRS = G::PRS, NE = G::NE, KSD = G::KSD, NUT = G::NUT;
+  constexpr int SL = G::SL, PRS = G::PRS, NE = G::NE, KSD = G::KSD, NUT = G::NUT;
   constexpr int CPR = D / 8, F2 = F / 2, NFT = F / 16, NQT = F / 32;  // Q1 tiles per wave
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr Lds<D, A, F> lo_{};
@@ -168,6 +181,8 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
   float* w2s = reinterpret_cast<float*>(cval + 2 * CH);
   uint16_t* H2h = reinterpret_cast<uint16_t*>(smem + lo_.h2);
   uint16_t* H2l = H2h + F2 * F;
+  unsigned char* H1qh = smem + lo_.h1q;  // H1q hi rows, then lo rows (img_off layout, row stride 2 D bytes)
+  unsigned char* H1ql = H1qh + F * D * 2;
   int* qslot = reinterpret_cast<int*>(smem + lo_.total - 16);
 
   // Lane-dependent indices are re-derived at the top of every user and chunk
@@ -196,6 +211,13 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
   for (int i = tid; i < F2; i += NT) {
     c2s[i] = a.c2[i];
     h3s[i] = a.h3[i];
+  }
+  if constexpr (lo_.h1l) {
+    for (int i = tid; i < F * CPR; i += NT) {
+      const int f = i / CPR, c = i % CPR;
+      *reinterpret_cast<bf16x8*>(H1qh + img_off<D>(f, c)) = *reinterpret_cast<const bf16x8*>(a.H1q_hi + (int64_t)f * D + 8 * c);
+      *reinterpret_cast<bf16x8*>(H1ql + img_off<D>(f, c)) = *reinterpret_cast<const bf16x8*>(a.H1q_lo + (int64_t)f * D + 8 * c);
+    }
   }
   if constexpr (lo_.h2l) {
     for (int i = tid; i < F2 * F / 8; i += NT) {
@@ -345,7 +367,7 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
         const int r0 = 16 * rt + 4 * l4;
         if (isP) {
           const float wv = w2s[urow];
-          const int col = (urow / SL) * SLP + urow % SL;
+          const int col = G::col(urow);
 #pragma unroll
           for (int i = 0; i < 4; ++i) Pp[(r0 + i) * PRS + col] = wv * acc[i];
         } else {
@@ -368,7 +390,7 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
       float sp = 0.f;
       if (r < nr) {
 #pragma unroll
-        for (int i = 0; i < SL; ++i) sp += Pp[r * PRS + j * SLP + i];
+        for (int i = 0; i < SL; ++i) sp += Pp[r * PRS + j * SL + i];
       }
       sp = oct_sum(sp);
       if (j == 0) hSP[r] = 0.5f * sp;
@@ -395,10 +417,11 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
       if (nxt_c) load_cids(u, coff, clen, c0 + CH);
       else if (nxt_h) hid = load_hid(un);
       // Q1 tiles of this wave: candidate tile qct = w & 3, F tiles ft = (w >> 2) + 2 i;
-      // the first tile's H1q fragments are read before the projection
+      // H1q fragments from LDS, or (when it does not fit) from L2, the first
+      // tile's read before the projection
       const int qct = w & 3;
       bf16x8 q1h[KSD], q1l[KSD];
-      {
+      if constexpr (!lo_.h1l) {
         const int64_t fo = (int64_t)(16 * (w >> 2) + l15) * D + 8 * l4;
         const uint16_t *qh = pinned(a.H1q_hi), *ql = pinned(a.H1q_lo);
 #pragma unroll
@@ -417,7 +440,7 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
             acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wql[s], acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wqh[s], acc, 0, 0, 0);
           }
-          const int un_ = 16 * ut + l15, col = (un_ / SL) * SLP + un_ % SL;
+          const int col = G::col(16 * ut + l15);
 #pragma unroll
           for (int i = 0; i < 4; ++i) Us[(16 * ct + 4 * l4 + i) * PRS + col] = w2u * (acc[i] + b1u);
         }
@@ -426,7 +449,14 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
 #pragma unroll
       for (int i = 0; i < NQT; ++i) {
         q1[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (i > 0) {  // F > 32: later tiles' fragments are read here
+        if constexpr (lo_.h1l) {
+          const int f = 16 * ((w >> 2) + 2 * i) + l15;
+#pragma unroll
+          for (int s = 0; s < KSD; ++s) {
+            q1h[s] = *reinterpret_cast<const bf16x8*>(H1qh + img_off<D>(f, 4 * s + l4));
+            q1l[s] = *reinterpret_cast<const bf16x8*>(H1ql + img_off<D>(f, 4 * s + l4));
+          }
+        } else if (i > 0) {  // F > 32: later tiles' fragments are read here
           const int64_t fo = (int64_t)(16 * ((w >> 2) + 2 * i) + l15) * D + 8 * l4;
           const uint16_t *qh = pinned(a.H1q_hi), *ql = pinned(a.H1q_lo);
 #pragma unroll
@@ -458,8 +488,9 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
       float u0[SL], u1[SL];
 #pragma unroll
       for (int i = 0; i < SL; i += 4) {
-        const float4 x0 = *reinterpret_cast<const float4*>(Us + cq * PRS + sj * SLP + i);
-        const float4 x1 = *reinterpret_cast<const float4*>(Us + (cq + 1) * PRS + sj * SLP + i);
+        const int o = sj * SL + 4 * G::pos4(sj, i >> 2);
+        const float4 x0 = *reinterpret_cast<const float4*>(Us + cq * PRS + o);
+        const float4 x1 = *reinterpret_cast<const float4*>(Us + (cq + 1) * PRS + o);
         u0[i] = x0.x; u0[i + 1] = x0.y; u0[i + 2] = x0.z; u0[i + 3] = x0.w;
         u1[i] = x1.x; u1[i + 1] = x1.y; u1[i + 2] = x1.z; u1[i + 3] = x1.w;
       }
@@ -478,10 +509,10 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
         float pa[SL], pb[SL], ha, hb;
         auto load_p = [&](float(&p)[SL], float& h, int r) __attribute__((always_inline)) {
           h = hSP[r];
-          const float* pr = Pp + r * PRS + sj * SLP;
+          const float* pr = Pp + r * PRS + sj * SL;
 #pragma unroll
           for (int i = 0; i < SL; i += 4) {
-            const float4 x = *reinterpret_cast<const float4*>(pr + i);
+            const float4 x = *reinterpret_cast<const float4*>(pr + 4 * G::pos4(sj, i >> 2));
             p[i] = x.x; p[i + 1] = x.y; p[i + 2] = x.z; p[i + 3] = x.w;
           }
         };
