@@ -432,7 +432,7 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
       }
       // ---- 1. U' = w2 (W1q q + b1) -> Us;  Q1 = H1q q tiles -> registers ----
       if (proj_on) {
-        for (int ct = ct0; ct < ct0 + nct; ++ct) {
+        for (int ct = ct0; ct < ct0 + nct && 16 * ct < nc; ++ct) {  // (empty tiles of a short chunk skipped)
           f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int s = 0; s < KSD; ++s) {
@@ -465,46 +465,52 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
             q1l[s] = *reinterpret_cast<const bf16x8*>(ql + fo + 32 * s);
           }
         }
+        if (16 * qct < nc) {
 #pragma unroll
-        for (int s = 0; s < KSD; ++s) {
-          const bf16x8 af = *reinterpret_cast<const bf16x8*>(img + img_off<D>(16 * qct + l15, 4 * s + l4));
-          q1[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, q1l[s], q1[i], 0, 0, 0);
-          q1[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, q1h[s], q1[i], 0, 0, 0);
+          for (int s = 0; s < KSD; ++s) {
+            const bf16x8 af = *reinterpret_cast<const bf16x8*>(img + img_off<D>(16 * qct + l15, 4 * s + l4));
+            q1[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, q1l[s], q1[i], 0, 0, 0);
+            q1[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, q1h[s], q1[i], 0, 0, 0);
+          }
         }
       }
       if (nxt_c) issue_rows();
       else if (nxt_h) issue_hist(hid, vm);
       __syncthreads();  // U' published; the image is dead (S takes its place)
 
-      // ---- 2. scoring: G = 2 row groups; group grp (waves 4 grp .. 4 grp + 3)
-      // takes rows grp, grp + 2, ... of all 64 candidates.  (Spreading a short
-      // chunk over more groups would change the softmax's summation order with
-      // the list's padding: the padded and ragged forms of a list must agree
-      // bit for bit.)
+      // ---- 2. scoring.  Softmax groups: rows grp, grp + 2, ... (grp = w >> 2); in
+      // the exp phase below, lane (pl, sj) of wave w takes the candidate pair cq
+      // and the rows grp + 2 sj + 16 k.  A full chunk scores the same way (each
+      // wave writes the S rows its own exp phase reads).  A chunk of at most 32
+      // candidates spreads its rows over 4 or 8 stripes of waves instead and
+      // combines the stripes' maxima through LDS; the max is exact and the
+      // scores and the exp / sum order are those of the full layout, so the
+      // padded and ragged forms of a list still agree bit for bit.
       constexpr int G = 2;
-      constexpr int wpg = 8 / G;
-      const int grp = w / wpg;  // wave-uniform
-      const int cq = 2 * (wpg * pl + w % wpg);
-      float u0[SL], u1[SL];
-#pragma unroll
-      for (int i = 0; i < SL; i += 4) {
-        const int o = sj * SL + 4 * G::pos4(sj, i >> 2);
-        const float4 x0 = *reinterpret_cast<const float4*>(Us + cq * PRS + o);
-        const float4 x1 = *reinterpret_cast<const float4*>(Us + (cq + 1) * PRS + o);
-        u0[i] = x0.x; u0[i + 1] = x0.y; u0[i + 2] = x0.z; u0[i + 3] = x0.w;
-        u1[i] = x1.x; u1[i + 1] = x1.y; u1[i + 2] = x1.z; u1[i + 3] = x1.w;
-      }
-      float hsu0 = 0.f, hsu1 = 0.f;
-#pragma unroll
-      for (int i = 0; i < SL; ++i) {
-        hsu0 += u0[i];
-        hsu1 += u1[i];
-      }
-      hsu0 = 0.5f * oct_sum(hsu0);
-      hsu1 = 0.5f * oct_sum(hsu1);
+      const int grp = w >> 2;  // wave-uniform
+      const int cq = 2 * (4 * pl + (w & 3));
+      const bool spread = nc <= 32;  // uniform
       float m0 = -INFINITY, m1 = -INFINITY;
-      const bool pair_on = cq < nc;  // wave-uniform per lane group; whole waves skip when empty
-      if (__ballot(pair_on) != 0 && grp < nr) {
+      // this lane's candidate pair (cx, cx + 1) over rows r0, r0 + rs, ...
+      auto score_rows = [&](int cx, int r0, int rs) __attribute__((always_inline)) {
+        float u0[SL], u1[SL];
+#pragma unroll
+        for (int i = 0; i < SL; i += 4) {
+          const int o = sj * SL + 4 * G::pos4(sj, i >> 2);
+          const float4 x0 = *reinterpret_cast<const float4*>(Us + cx * PRS + o);
+          const float4 x1 = *reinterpret_cast<const float4*>(Us + (cx + 1) * PRS + o);
+          u0[i] = x0.x; u0[i + 1] = x0.y; u0[i + 2] = x0.z; u0[i + 3] = x0.w;
+          u1[i] = x1.x; u1[i + 1] = x1.y; u1[i + 2] = x1.z; u1[i + 3] = x1.w;
+        }
+        float hsu0 = 0.f, hsu1 = 0.f;
+#pragma unroll
+        for (int i = 0; i < SL; ++i) {
+          hsu0 += u0[i];
+          hsu1 += u1[i];
+        }
+        hsu0 = 0.5f * oct_sum(hsu0);
+        hsu1 = 0.5f * oct_sum(hsu1);
+        if (__ballot(cx < nc) == 0 || r0 >= nr) return;  // whole waves skip empty pairs
         // a row's P' slice and SP / 2, read one row ahead (two register sets)
         float pa[SL], pb[SL], ha, hb;
         auto load_p = [&](float(&p)[SL], float& h, int r) __attribute__((always_inline)) {
@@ -533,22 +539,44 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
           m0 = fmaxf(m0, s0);
           m1 = fmaxf(m1, s1);
           if (sj == 0) {
-            S[cq * SST + r] = s0;
-            S[(cq + 1) * SST + r] = s1;
+            S[cx * SST + r] = s0;
+            S[(cx + 1) * SST + r] = s1;
           }
         };
-        load_p(pa, ha, grp);
-        for (int r = grp; r < nr; r += 2 * G) {
-          const bool more = r + G < nr;
-          if (more) load_p(pb, hb, r + G);
+        load_p(pa, ha, r0);
+        for (int r = r0; r < nr; r += 2 * rs) {
+          const bool more = r + rs < nr;
+          if (more) load_p(pb, hb, r + rs);
           score(pa, ha, r);
           if (!more) break;
-          if (r + 2 * G < nr) load_p(pa, ha, r + 2 * G);
-          score(pb, hb, r + G);
+          if (r + 2 * rs < nr) load_p(pa, ha, r + 2 * rs);
+          score(pb, hb, r + rs);
+        }
+      };
+      if (!spread) {
+        score_rows(cq, grp, G);
+      } else {
+        // stripes of rows: 8 (one wave each, 8 pairs = 16 candidates) or 4 (wave
+        // pairs, two sets of 8 pairs); their maxima in the S rows of candidates
+        // 32.. (beyond any spread chunk's candidates)
+        const int nst = nc <= 16 ? 8 : 4;
+        const int stripe = nc <= 16 ? w : (w >> 1);
+        const int cs = 2 * (8 * (nc <= 16 ? 0 : (w & 1)) + pl);
+        float* MX = S + 32 * SST;  // [stripe][CH]
+        score_rows(cs, stripe, nst);
+        if (sj == 0) {
+          MX[stripe * CH + cs] = m0;
+          MX[stripe * CH + cs + 1] = m1;
+        }
+        __syncthreads();  // the stripes' scores and maxima published
+        m0 = m1 = -INFINITY;
+        for (int st = grp; st < nst; st += 2) {  // the stripes holding this group's rows
+          m0 = fmaxf(m0, MX[st * CH + cq]);
+          m1 = fmaxf(m1, MX[st * CH + cq + 1]);
         }
       }
       // softmax weights of this group's rows: e = exp(s - m_g) (lane sj: every 8th row)
-      {
+      if (!spread || cq < 32) {
         float sum0 = 0.f, sum1 = 0.f;
         for (int r = grp + G * sj; r < nrp; r += 8 * G) {
           float e0 = 0.f, e1 = 0.f;
@@ -574,25 +602,19 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
       __syncthreads();  // S (softmax weights), MS published; U' dead (h1 takes its place)
 
       // ---- 3. h1 = relu(Q1 + (e R) / sum e + c1) ----------------------------
-      {
+      if (16 * qct < nc) {
         // A operand: candidate ca = 16 qct + l15, rows 32 ks + 8 l4 + jj (group
-        // jj mod G) scaled by exp(m_g - m)
+        // jj mod 2) scaled by exp(m_g - m)
         const int ca = 16 * qct + l15;
-        float mm = -INFINITY;
-        for (int g = 0; g < G; ++g) mm = fmaxf(mm, MS[2 * g * CH + ca]);
-        float sc8[8];
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) sc8[jj] = __expf(MS[2 * (jj & (G - 1)) * CH + ca] - mm);
+        const float ma0 = MS[0 * CH + ca], ma1 = MS[2 * CH + ca], mm = fmaxf(ma0, ma1);
+        const float sc0 = __expf(ma0 - mm), sc1 = __expf(ma1 - mm);
         // C tile rows: candidates 16 qct + 4 l4 + i
         float den[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int cc = 16 * qct + 4 * l4 + i;
-          float xm = -INFINITY;
-          for (int g = 0; g < G; ++g) xm = fmaxf(xm, MS[2 * g * CH + cc]);
-          float dn = 0.f;
-          for (int g = 0; g < G; ++g) dn += MS[(2 * g + 1) * CH + cc] * __expf(MS[2 * g * CH + cc] - xm);
-          den[i] = dn;
+          const float x0 = MS[0 * CH + cc], x1 = MS[2 * CH + cc], xm = fmaxf(x0, x1);
+          den[i] = MS[1 * CH + cc] * __expf(x0 - xm) + MS[3 * CH + cc] * __expf(x1 - xm);
         }
         const int nks = nrp / 32;
         bf16x8 eh[2], el[2];
@@ -601,8 +623,8 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
           if (ks < nks) {
             const float4 x0 = *reinterpret_cast<const float4*>(S + ca * SST + 32 * ks + 8 * l4);
             const float4 x1 = *reinterpret_cast<const float4*>(S + ca * SST + 32 * ks + 8 * l4 + 4);
-            const float xv[8] = {x0.x * sc8[0], x0.y * sc8[1], x0.z * sc8[2], x0.w * sc8[3],
-                                 x1.x * sc8[4], x1.y * sc8[5], x1.z * sc8[6], x1.w * sc8[7]};
+            const float xv[8] = {x0.x * sc0, x0.y * sc1, x0.z * sc0, x0.w * sc1,
+                                 x1.x * sc0, x1.y * sc1, x1.z * sc0, x1.w * sc1};
 #pragma unroll
             for (int jj = 0; jj < 8; ++jj) {
               short h, l;
@@ -643,6 +665,7 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
         const int nt2 = 4 * (F2 / 16);
         for (int t = w; t < nt2; t += 8) {
           const int ct = t & 3, t2 = t >> 2;
+          if (16 * ct >= nc) continue;  // an empty tile of a short chunk
           const int ca = 16 * ct + l15, v = 16 * t2 + l15;
           f32x4 acc = {0.f, 0.f, 0.f, 0.f};
           for (int ks = 0; ks < F / 32; ++ks) {
