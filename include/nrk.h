@@ -234,6 +234,25 @@ int nrk_din_rerank(const void* table, int64_t n_table, int32_t dtype, const int3
                    const int32_t* cand, const int64_t* cand_off, const int32_t* cand_len, const int32_t* extra,
                    const int64_t* out_off, float* out, int32_t d, int32_t A, int32_t F,
                    const nrk_din_rerank_params* params, void* ws, size_t ws_bytes, void* stream);
+/* Shared candidate lists (the flow: every user of a cluster scores the same
+ * list).  The candidate half of the attention MLP and of the head's first
+ * Linear depends on the item alone, so such a list is projected once:
+ *   out [n][A + F] f32 = [ U'(rows[i]) = w2 . (W1q q + b1) in the kernel's
+ *   slice order (A) | Q1(rows[i]) = H1q q (F) ], q = table[rows[i]] (a zero row
+ *   when rows[i] is outside [0, N)),
+ * with the MFMA sequence nrk_din_rerank applies per candidate, and
+ * nrk_din_rerank_projected then stages those instead of the rows:
+ * cand_proj [.][A + F] parallel to cand, extra_proj [nU][A + F] (extra's
+ * projections; required when extra != NULL).  cand / extra still decide which
+ * candidates are valid.  Logits are bit-identical to nrk_din_rerank's. */
+int nrk_din_rerank_project(const void* table, int64_t n_table, int32_t dtype, const int32_t* rows, int64_t n,
+                           int32_t d, int32_t A, int32_t F, const nrk_din_rerank_params* params, float* out,
+                           void* stream);
+int nrk_din_rerank_projected(const void* table, int64_t n_table, int32_t dtype, const int32_t* hist, int32_t nU,
+                             int32_t L, const int32_t* cand, const int64_t* cand_off, const int32_t* cand_len,
+                             const int32_t* extra, const int64_t* out_off, float* out, int32_t d, int32_t A,
+                             int32_t F, const nrk_din_rerank_params* params, const float* cand_proj,
+                             const float* extra_proj, void* ws, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------ inverted lists --
  * faiss Clustering / IndexIVFFlat building blocks (Retrieval.py:11-23).

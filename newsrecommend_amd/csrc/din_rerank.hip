@@ -77,6 +77,10 @@ struct RerankArgs {
   float c3;
   int F;
   int* queue;  // user counter, zero at launch
+  // projected candidates (PROJ): [U' (A) | Q1 (F)] f32 per candidate, cproj
+  // parallel to cand, xproj [nU] for the extras (nrk_din_rerank_project)
+  const float* cproj;
+  const float* xproj;
 };
 
 // LDS image of 64 rows of D bf16: 16-B chunks XOR-swizzled by row, so the
@@ -107,7 +111,7 @@ struct Geo {
   static constexpr int NUT = A / 16;               // 16-unit tiles of U / P
 };
 
-template <int D, int A, int F>
+template <int D, int A, int F, bool PROJ>
 struct Lds {  // byte offsets
   int p, hsp, rt, q, us, ms, lgp, cst, h2, sx, h1q, total;
   bool h2l;   // H2 hi / lo resident in LDS (when it fits)
@@ -121,7 +125,9 @@ struct Lds {  // byte offsets
     hsp = p + LP * G::PRS * 4;                 // SP / 2 [LP] f32
     rt = hsp + LP * 4;                         // R^T hi, lo [F][LP] bf16
     q = rt + 2 * F * LP * 2;                   // candidate / history image [64][D] bf16;  S [CH][SST] f32 later
-    const int qb = CH * D * 2 > CH * SST * 4 ? CH * D * 2 : CH * SST * 4;
+                                               // (PROJ: history image, then the chunk's Q1 [CH][F] f32)
+    int qb = CH * D * 2 > CH * SST * 4 ? CH * D * 2 : CH * SST * 4;
+    if (PROJ && CH * F * 4 > qb) qb = CH * F * 4;
     us = q + qb;                               // U' [CH][A] f32;  h1 [CH][F + 4] f32 later
     const int ub = CH * G::PRS * 4 > CH * (F + 4) * 4 ? CH * G::PRS * 4 : CH * (F + 4) * 4;
     ms = us + ub;                              // {m, sum} of the two row groups [2][2][CH] f32
@@ -130,12 +136,13 @@ struct Lds {  // byte offsets
     h2 = cst + 2 * F * 4 + 2 * CH * 4 + A * 4;  // (+ w2 [A] f32);  H2 hi, lo [F/2][F] bf16 (if it fits)
     const int h2b = 2 * (F / 2) * F * 2;
     h2l = h2 + h2b + 16 <= 160 * 1024;
+    if (PROJ && h2 + h2b + CH * SST * 4 + 16 > 160 * 1024) h2l = false;  // PROJ needs S apart: H2 from L2
     int end = h2l ? h2 + h2b : h2;
     ssep = end + CH * SST * 4 + 16 <= 160 * 1024;
     sx = ssep ? end : q;                       // S [CH][SST] f32
     if (ssep) end += CH * SST * 4;
     h1q = end;                                 // H1q hi, lo [F][D] bf16 (image swizzle), if it fits
-    h1l = end + 2 * F * D * 2 + 16 <= 160 * 1024;
+    h1l = !PROJ && end + 2 * F * D * 2 + 16 <= 160 * 1024;
     total = (h1l ? end + 2 * F * D * 2 : end) + 16;
   }
 };
@@ -157,13 +164,14 @@ __device__ __forceinline__ void split_bf16(float x, short& hi, short& lo) {
   lo = __builtin_bit_cast(short, (__bf16)(x - (float)h));
 }
 
-template <int D, int A, int F>
+template <int D, int A, int F, bool PROJ>
 __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
   using G = Geo<D, A>;
   constexpr int SL = G::SL, PRS = G::PRS, NE = G::NE, KSD = G::KSD, NUT = G::NUT;
   constexpr int CPR = D / 8, F2 = F / 2, NFT = F / 16, NQT = F / 32;  // Q1 tiles per wave
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr Lds<D, A, F> lo_{};
+  constexpr Lds<D, A, F, PROJ> lo_{};
+  static_assert(!PROJ || lo_.ssep, "din_rerank: the projected form keeps S apart from the image");
   float* Pp = reinterpret_cast<float*>(smem + lo_.p);
   float* hSP = reinterpret_cast<float*>(smem + lo_.hsp);
   uint16_t* Rth = reinterpret_cast<uint16_t*>(smem + lo_.rt);
@@ -234,7 +242,7 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
   const int nct = 4 / GP, ct0 = pg * nct;
   bf16x8 wqh[KSD], wql[KSD];
   float b1u = 0.f, w2u = 0.f;
-  {
+  if constexpr (!PROJ) {
     const int u = 16 * ut + l15;
 #pragma unroll
     for (int s = 0; s < KSD; ++s) {
@@ -309,6 +317,37 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
       if (row < nv_) stg[k] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(a.table + (int64_t)src * D + cc * 8));
     }
   };
+  // PROJ: a chunk's projected candidates, CPX float4s each ([U' | Q1]: to the
+  // U' rows and the Q1 rows of LDS), and the validity of candidate tid (< CH)
+  constexpr int CPX = (A + F) / 4, NEP = (CH * CPX + NT - 1) / NT;
+  float4 stp[PROJ ? NEP : 1];
+  int vid = -1;
+  float* Q1s = reinterpret_cast<float*>(smem + lo_.q);  // [CH][F] (PROJ)
+  auto load_proj = [&](int u_, int64_t off, int len, int c0_) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < NEP; ++k) {
+      const int e = tid + NT * k, cand = e / CPX, part = e % CPX, ci = c0_ + cand;
+      const float* src = nullptr;
+      if (e < CH * CPX) {
+        if (ci < len) src = a.cproj + (off + ci) * (A + F);
+        else if (ci == len && a.xproj) src = a.xproj + (int64_t)u_ * (A + F);
+      }
+      stp[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (src) stp[k] = *reinterpret_cast<const float4*>(src + 4 * part);
+    }
+    vid = tid < CH ? cand_id(u_, off, len, c0_ + tid) : -1;
+  };
+  auto store_proj = [&](int* cv) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < NEP; ++k) {
+      const int e = tid + NT * k, cand = e / CPX, part = e % CPX;
+      if (e < CH * CPX) {
+        if (part < A / 4) *reinterpret_cast<float4*>(Us + cand * PRS + 4 * part) = stp[k];
+        else *reinterpret_cast<float4*>(Q1s + cand * F + 4 * (part - A / 4)) = stp[k];
+      }
+    }
+    if (tid < CH) cv[tid] = vid >= 0;
+  };
 
   if (tid == 0) qslot[0] = atomicAdd(a.queue, 1);
   __syncthreads();
@@ -329,7 +368,10 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
     store_rows();     // history rows -> image
     if (tid == 0) qslot[1] = atomicAdd(a.queue, 1);  // the next user (read after chunk 0's first barrier)
     __syncthreads();
-    if (nchunk > 0) load_cids(u, coff, clen, 0);  // chunk 0's ids (its rows are issued after [P | R])
+    if (nchunk > 0) {
+      if constexpr (PROJ) load_proj(u, coff, clen, 0);  // chunk 0's projections (in flight during [P | R])
+      else load_cids(u, coff, clen, 0);  // chunk 0's ids (its rows are issued after [P | R])
+    }
 
     // ---- [P | R] = K [W1k ; H1p]^T for the 16-row tiles below nrp ----------
     // Tile t = (unit tile t / nrt, row tile t % nrt); wave w takes the
@@ -383,7 +425,9 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
         }
       }
     }
-    if (nchunk > 0) issue_rows();  // chunk 0's rows
+    if constexpr (!PROJ) {
+      if (nchunk > 0) issue_rows();  // chunk 0's rows
+    }
     __syncthreads();
     {  // SP / 2 per row: thread = (row, slice)
       const int r = tid >> 3, j = tid & 7;
@@ -403,25 +447,34 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
       int* cvb = cval + (ch & 1) * CH;  // validity of this chunk's candidates (double-buffered)
       // With S apart from the image, the previous chunk's head (which reads S,
       // h1 and the other validity buffer) may still run while the rows land.
-      if (!lo_.ssep || ch == 0) __syncthreads();  // (ch == 0: SP published)
+      // (PROJ: the store below writes U' over the previous chunk's h1)
+      if (!lo_.ssep || ch == 0 || PROJ) __syncthreads();  // (ch == 0: SP published)
       refresh();
-      store_rows();     // candidate rows -> image
-      store_valid(cvb);
+      if constexpr (PROJ) {
+        store_proj(cvb);  // projected candidates -> U' rows, Q1 rows
+      } else {
+        store_rows();     // candidate rows -> image
+        store_valid(cvb);
+      }
       __syncthreads();
       if (ch == 0) un = qslot[1];
       // the next work item: the next chunk, or the next user's history.  Its
       // ids are read now, its rows once Q1 is issued (registers, kept in flight
-      // across the scoring)
+      // across the scoring; PROJ: the projections are read now)
       const bool nxt_c = ch + 1 < nchunk, nxt_h = !nxt_c && un < a.nU;
       int hid = -1;
-      if (nxt_c) load_cids(u, coff, clen, c0 + CH);
-      else if (nxt_h) hid = load_hid(un);
+      if constexpr (PROJ) {
+        if (nxt_c) load_proj(u, coff, clen, c0 + CH);
+      } else {
+        if (nxt_c) load_cids(u, coff, clen, c0 + CH);
+      }
+      if (nxt_h) hid = load_hid(un);
       // Q1 tiles of this wave: candidate tile qct = w & 3, F tiles ft = (w >> 2) + 2 i;
       // H1q fragments from LDS, or (when it does not fit) from L2, the first
       // tile's read before the projection
       const int qct = w & 3;
       bf16x8 q1h[KSD], q1l[KSD];
-      if constexpr (!lo_.h1l) {
+      if constexpr (!lo_.h1l && !PROJ) {
         const int64_t fo = (int64_t)(16 * (w >> 2) + l15) * D + 8 * l4;
         const uint16_t *qh = pinned(a.H1q_hi), *ql = pinned(a.H1q_lo);
 #pragma unroll
@@ -431,7 +484,8 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
         }
       }
       // ---- 1. U' = w2 (W1q q + b1) -> Us;  Q1 = H1q q tiles -> registers ----
-      if (proj_on) {
+      // (PROJ: both were staged)
+      if (proj_on && !PROJ) {
         for (int ct = ct0; ct < ct0 + nct && 16 * ct < nc; ++ct) {  // (empty tiles of a short chunk skipped)
           f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -449,6 +503,7 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
 #pragma unroll
       for (int i = 0; i < NQT; ++i) {
         q1[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (PROJ) continue;  // (Q1 staged)
         if constexpr (lo_.h1l) {
           const int f = 16 * ((w >> 2) + 2 * i) + l15;
 #pragma unroll
@@ -474,9 +529,13 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
           }
         }
       }
-      if (nxt_c) issue_rows();
-      else if (nxt_h) issue_hist(hid, vm);
-      __syncthreads();  // U' published; the image is dead (S takes its place)
+      if constexpr (PROJ) {
+        if (nxt_h) issue_hist(hid, vm);  // (U', Q1 were published by the barrier above)
+      } else {
+        if (nxt_c) issue_rows();
+        else if (nxt_h) issue_hist(hid, vm);
+        __syncthreads();  // U' published; the image is dead (S takes its place)
+      }
 
       // ---- 2. scoring.  Softmax groups: rows grp, grp + 2, ... (grp = w >> 2); in
       // the exp phase below, lane (pl, sj) of wave w takes the candidate pair cq
@@ -640,7 +699,10 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
           {
             f32x4 acc;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) acc[k] = q1[i][k] * den[k];
+            for (int k = 0; k < 4; ++k) {
+              const float qv = PROJ ? Q1s[(16 * qct + 4 * l4 + k) * F + 16 * ft + l15] : q1[i][k];
+              acc[k] = qv * den[k];
+            }
             const int f = 16 * ft + l15;
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
@@ -719,33 +781,121 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
   }
 }
 
-template <int D, int A, int F>
+template <int D, int A, int F, bool PROJ>
 int launch(const RerankArgs& a, hipStream_t st) {
-  constexpr Lds<D, A, F> l{};
+  constexpr Lds<D, A, F, PROJ> l{};
   static_assert(l.total <= 160 * 1024, "din_rerank: LDS");
   int grid = a.nU < 256 ? a.nU : 256;
-  hipLaunchKernelGGL((din_rerank_kernel<D, A, F>), dim3(grid), dim3(NT), (size_t)l.total, st, a);
+  hipLaunchKernelGGL((din_rerank_kernel<D, A, F, PROJ>), dim3(grid), dim3(NT), (size_t)l.total, st, a);
   NRK_CHECK_LAUNCH("din_rerank_kernel");
   return NRK_OK;
 }
 
-template <int D, int A>
+// ---- item projections for shared candidate lists (nrk_din_rerank_project):
+// phase 1 of the main kernel for a list of rows, with its MFMA order, so a
+// projected candidate scores bit for bit as one staged from its row.  64 rows
+// per 256-thread block; wave w takes the unit tiles w, w + 4, ... of
+// [W1q ; H1q] (fragments from L2) over the block's four candidate tiles.
+struct ProjArgs {
+  const uint16_t* table;
+  int64_t n_table;
+  const int32_t* rows;
+  int64_t n;
+  const uint16_t *W1q_hi, *W1q_lo, *H1q_hi, *H1q_lo;
+  const float *b1, *w2;
+  float* out;  // [n][A + F]: U' in the kernel's slice order, then Q1
+};
+
+template <int D, int A, int F>
+__global__ __launch_bounds__(256) void din_rerank_project_kernel(ProjArgs a) {
+  using G = Geo<D, A>;
+  constexpr int CPR = D / 8, KSD = D / 32, NUT = A / 16, NFT = F / 16;
+  __shared__ __attribute__((aligned(16))) unsigned char img[CH * D * 2];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l15 = lane & 15, l4 = lane >> 4;
+  const int64_t r0 = (int64_t)blockIdx.x * CH;
+  for (int e = tid; e < CH * CPR; e += 256) {
+    const int row = e / CPR, cc = e % CPR;
+    const int id = r0 + row < a.n ? a.rows[r0 + row] : -1;
+    bf16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (id >= 0 && id < a.n_table) v = *reinterpret_cast<const bf16x8*>(a.table + (int64_t)id * D + 8 * cc);
+    *reinterpret_cast<bf16x8*>(img + img_off<D>(row, cc)) = v;
+  }
+  __syncthreads();
+  for (int t = w; t < NUT + NFT; t += 4) {
+    const bool isU = t < NUT;
+    const int urow = isU ? 16 * t + l15 : 16 * (t - NUT) + l15;
+    const uint16_t* bh = (isU ? a.W1q_hi : a.H1q_hi) + (int64_t)urow * D + 8 * l4;
+    const uint16_t* bl = (isU ? a.W1q_lo : a.H1q_lo) + (int64_t)urow * D + 8 * l4;
+    bf16x8 fh[KSD], fl[KSD];
+#pragma unroll
+    for (int s = 0; s < KSD; ++s) {
+      fh[s] = *reinterpret_cast<const bf16x8*>(bh + 32 * s);
+      fl[s] = *reinterpret_cast<const bf16x8*>(bl + 32 * s);
+    }
+    const float b1u = isU ? a.b1[urow] : 0.f, w2u = isU ? a.w2[urow] : 0.f;
+    const int oc = isU ? G::col(urow) : A + urow;
+    for (int ct = 0; ct < 4; ++ct) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KSD; ++s) {
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(img + img_off<D>(16 * ct + l15, 4 * s + l4));
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, fl[s], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, fh[s], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t row = r0 + 16 * ct + 4 * l4 + i;
+        if (row < a.n) a.out[row * (A + F) + oc] = isU ? w2u * (acc[i] + b1u) : acc[i];
+      }
+    }
+  }
+}
+
+template <int D, int A, bool PROJ>
 int launch_f(const RerankArgs& a, hipStream_t st) {
   switch (a.F) {
-    case 32: return launch<D, A, 32>(a, st);
-    case 64: return launch<D, A, 64>(a, st);
-    case 96: return launch<D, A, 96>(a, st);
-    default: return launch<D, A, 128>(a, st);
+    case 32: return launch<D, A, 32, PROJ>(a, st);
+    case 64: return launch<D, A, 64, PROJ>(a, st);
+    case 96: return launch<D, A, 96, PROJ>(a, st);
+    default: return launch<D, A, 128, PROJ>(a, st);
+  }
+}
+
+template <int D, bool PROJ>
+int launch_a(int A, const RerankArgs& a, hipStream_t st) {
+  switch (A) {
+    case 32: return launch_f<D, 32, PROJ>(a, st);
+    case 64: return launch_f<D, 64, PROJ>(a, st);
+    case 96: return launch_f<D, 96, PROJ>(a, st);
+    default: return launch_f<D, 128, PROJ>(a, st);
+  }
+}
+
+template <int D, int A, int F>
+int launch_proj(const ProjArgs& a, hipStream_t st) {
+  const int64_t grid = (a.n + CH - 1) / CH;
+  hipLaunchKernelGGL((din_rerank_project_kernel<D, A, F>), dim3((unsigned)grid), dim3(256), 0, st, a);
+  NRK_CHECK_LAUNCH("din_rerank_project_kernel");
+  return NRK_OK;
+}
+
+template <int D, int A>
+int launch_proj_f(int F, const ProjArgs& a, hipStream_t st) {
+  switch (F) {
+    case 32: return launch_proj<D, A, 32>(a, st);
+    case 64: return launch_proj<D, A, 64>(a, st);
+    case 96: return launch_proj<D, A, 96>(a, st);
+    default: return launch_proj<D, A, 128>(a, st);
   }
 }
 
 template <int D>
-int launch_a(int A, const RerankArgs& a, hipStream_t st) {
+int launch_proj_a(int A, int F, const ProjArgs& a, hipStream_t st) {
   switch (A) {
-    case 32: return launch_f<D, 32>(a, st);
-    case 64: return launch_f<D, 64>(a, st);
-    case 96: return launch_f<D, 96>(a, st);
-    default: return launch_f<D, 128>(a, st);
+    case 32: return launch_proj_f<D, 32>(F, a, st);
+    case 64: return launch_proj_f<D, 64>(F, a, st);
+    case 96: return launch_proj_f<D, 96>(F, a, st);
+    default: return launch_proj_f<D, 128>(F, a, st);
   }
 }
 
@@ -760,10 +910,11 @@ extern "C" int nrk_din_rerank_workspace(size_t* ws_bytes) {
   return NRK_OK;
 }
 
-extern "C" int nrk_din_rerank(const void* table, int64_t n_table, int32_t dtype, const int32_t* hist, int32_t nU,
-                              int32_t L, const int32_t* cand, const int64_t* cand_off, const int32_t* cand_len,
-                              const int32_t* extra, const int64_t* out_off, float* out, int32_t d, int32_t A, int32_t F,
-                              const nrk_din_rerank_params* p, void* ws, size_t ws_bytes, void* stream) {
+static int rerank_impl(const void* table, int64_t n_table, int32_t dtype, const int32_t* hist, int32_t nU,
+                       int32_t L, const int32_t* cand, const int64_t* cand_off, const int32_t* cand_len,
+                       const int32_t* extra, const int64_t* out_off, float* out, int32_t d, int32_t A, int32_t F,
+                       const nrk_din_rerank_params* p, const float* cand_proj, const float* extra_proj, void* ws,
+                       size_t ws_bytes, void* stream) {
   NRK_CHECK_ARG(dtype == NRK_DTYPE_BF16, "din_rerank: the table must be bf16");
   NRK_CHECK_ARG(d == 64 || d == 128 || d == 256, "din_rerank: emb_dim %d unsupported (64, 128, 256)", d);
   NRK_CHECK_ARG(A >= 32 && A <= 128 && A % 32 == 0, "din_rerank: attn_units %d unsupported (32..128 step 32)", A);
@@ -775,6 +926,7 @@ extern "C" int nrk_din_rerank(const void* table, int64_t n_table, int32_t dtype,
   NRK_CHECK_ARG(p->W1q_hi && p->W1q_lo && p->W1k_hi && p->W1k_lo && p->b1 && p->w2 && p->H1q_hi && p->H1q_lo &&
                     p->H1p_hi && p->H1p_lo && p->c1 && p->H2_hi && p->H2_lo && p->c2 && p->h3,
                 "din_rerank: null parameter pointer");
+  NRK_CHECK_ARG(!extra || !cand_proj || extra_proj, "din_rerank_projected: extra without extra_proj");
   if (ws_bytes < 256) return fail(NRK_EWORKSPACE, "din_rerank: workspace %zu < 256", ws_bytes);
   hipStream_t st = (hipStream_t)stream;
   if (hipMemsetAsync(ws, 0, 4, st) != hipSuccess) return fail(NRK_ELAUNCH, "din_rerank: memset failed");
@@ -808,7 +960,62 @@ extern "C" int nrk_din_rerank(const void* table, int64_t n_table, int32_t dtype,
   a.c3 = p->c3;
   a.F = F;
   a.queue = static_cast<int*>(ws);
-  if (d == 256) return rr::launch_a<256>(A, a, st);
-  if (d == 128) return rr::launch_a<128>(A, a, st);
-  return rr::launch_a<64>(A, a, st);
+  a.cproj = cand_proj;
+  a.xproj = extra_proj;
+  if (cand_proj) {
+    if (d == 256) return rr::launch_a<256, true>(A, a, st);
+    if (d == 128) return rr::launch_a<128, true>(A, a, st);
+    return rr::launch_a<64, true>(A, a, st);
+  }
+  if (d == 256) return rr::launch_a<256, false>(A, a, st);
+  if (d == 128) return rr::launch_a<128, false>(A, a, st);
+  return rr::launch_a<64, false>(A, a, st);
+}
+
+extern "C" int nrk_din_rerank(const void* table, int64_t n_table, int32_t dtype, const int32_t* hist, int32_t nU,
+                              int32_t L, const int32_t* cand, const int64_t* cand_off, const int32_t* cand_len,
+                              const int32_t* extra, const int64_t* out_off, float* out, int32_t d, int32_t A, int32_t F,
+                              const nrk_din_rerank_params* p, void* ws, size_t ws_bytes, void* stream) {
+  return rerank_impl(table, n_table, dtype, hist, nU, L, cand, cand_off, cand_len, extra, out_off, out, d, A, F, p,
+                     nullptr, nullptr, ws, ws_bytes, stream);
+}
+
+extern "C" int nrk_din_rerank_projected(const void* table, int64_t n_table, int32_t dtype, const int32_t* hist,
+                                        int32_t nU, int32_t L, const int32_t* cand, const int64_t* cand_off,
+                                        const int32_t* cand_len, const int32_t* extra, const int64_t* out_off,
+                                        float* out, int32_t d, int32_t A, int32_t F, const nrk_din_rerank_params* p,
+                                        const float* cand_proj, const float* extra_proj, void* ws, size_t ws_bytes,
+                                        void* stream) {
+  NRK_CHECK_ARG(cand_proj, "din_rerank_projected: null cand_proj");
+  return rerank_impl(table, n_table, dtype, hist, nU, L, cand, cand_off, cand_len, extra, out_off, out, d, A, F, p,
+                     cand_proj, extra_proj, ws, ws_bytes, stream);
+}
+
+extern "C" int nrk_din_rerank_project(const void* table, int64_t n_table, int32_t dtype, const int32_t* rows, int64_t n,
+                                      int32_t d, int32_t A, int32_t F, const nrk_din_rerank_params* p, float* out,
+                                      void* stream) {
+  NRK_CHECK_ARG(dtype == NRK_DTYPE_BF16, "din_rerank_project: the table must be bf16");
+  NRK_CHECK_ARG(d == 64 || d == 128 || d == 256, "din_rerank_project: emb_dim %d unsupported (64, 128, 256)", d);
+  NRK_CHECK_ARG(A >= 32 && A <= 128 && A % 32 == 0, "din_rerank_project: attn_units %d unsupported", A);
+  NRK_CHECK_ARG(F >= 32 && F <= 128 && F % 32 == 0, "din_rerank_project: fc_units %d unsupported", F);
+  NRK_CHECK_ARG(n >= 0, "din_rerank_project: bad row count");
+  if (n == 0) return NRK_OK;
+  NRK_CHECK_ARG(table && rows && p && out && p->W1q_hi && p->W1q_lo && p->H1q_hi && p->H1q_lo && p->b1 && p->w2,
+                "din_rerank_project: null pointer");
+  rr::ProjArgs a;
+  a.table = static_cast<const uint16_t*>(table);
+  a.n_table = n_table;
+  a.rows = rows;
+  a.n = n;
+  a.W1q_hi = static_cast<const uint16_t*>(p->W1q_hi);
+  a.W1q_lo = static_cast<const uint16_t*>(p->W1q_lo);
+  a.H1q_hi = static_cast<const uint16_t*>(p->H1q_hi);
+  a.H1q_lo = static_cast<const uint16_t*>(p->H1q_lo);
+  a.b1 = p->b1;
+  a.w2 = p->w2;
+  a.out = out;
+  hipStream_t st = (hipStream_t)stream;
+  if (d == 256) return rr::launch_proj_a<256>(A, F, a, st);
+  if (d == 128) return rr::launch_proj_a<128>(A, F, a, st);
+  return rr::launch_proj_a<64>(A, F, a, st);
 }

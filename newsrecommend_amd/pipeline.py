@@ -122,14 +122,35 @@ def rerank_params(model, d: int):
     return out
 
 
+def rerank_project(model, table: torch.Tensor, rows: torch.Tensor, prm=None) -> torch.Tensor:
+    """nrk_din_rerank_project: the candidate-only part of the re-rank for each
+    row, [U' (A) | Q1 (F)] f32, with the arithmetic nrk_din_rerank applies per
+    candidate (a shared list is projected once instead of once per user)."""
+    from . import _lib
+
+    d = table.shape[1]
+    if prm is None:
+        prm = rerank_params(model, d)
+    p, A, F, _keep = prm
+    r = rows.to(torch.int32).contiguous()
+    out = torch.empty((r.numel(), A + F), dtype=torch.float32, device=table.device)
+    _lib.check(_lib.load().nrk_din_rerank_project(_lib.ptr(table), table.shape[0], _lib.NRK_DTYPE_BF16, _lib.ptr(r),
+                                                  r.numel(), d, A, F, ctypes.byref(p), _lib.ptr(out),
+                                                  _lib.stream(table.device)), "din_rerank_project")
+    return out
+
+
 def rerank_ragged(model, table: torch.Tensor, hist_rows: torch.Tensor, cand: torch.Tensor, cand_off: torch.Tensor,
                   cand_len: torch.Tensor, extra: torch.Tensor | None, out_off: torch.Tensor, n_out: int,
-                  prm=None) -> torch.Tensor:
+                  prm=None, shared: bool = False) -> torch.Tensor:
     """nrk_din_rerank: one launch for all users.  User u scores
     cand[cand_off[u] : cand_off[u] + cand_len[u]] (+ extra[u] when given, -1 =
     a padded slot) against its history hist_rows[u] and writes
     out[out_off[u] + c]; rows outside the table get -inf.  Returns out (n_out,)
-    f32 (entries not covered by any user stay uninitialised)."""
+    f32 (entries not covered by any user stay uninitialised).  shared: the
+    lists are shared by many users (the flow's clusters): cand and extra are
+    projected once (rerank_project) and nrk_din_rerank_projected scores the
+    projections; the logits are bit-identical either way."""
     from . import _lib
 
     dev = table.device
@@ -152,10 +173,19 @@ def rerank_ragged(model, table: torch.Tensor, hist_rows: torch.Tensor, cand: tor
     ex = extra.to(torch.int32).contiguous() if extra is not None else None
     from .din import KernelTimer
 
-    t0 = KernelTimer.mark("rerank")
-    _lib.check(lib.nrk_din_rerank(_lib.ptr(table), table.shape[0], _lib.NRK_DTYPE_BF16, _lib.ptr(h), U, L, _lib.ptr(c),
-                                  _lib.ptr(co), _lib.ptr(cl), _lib.ptr(ex), _lib.ptr(oo), _lib.ptr(out), d, A, F,
-                                  ctypes.byref(p), _lib.ptr(ws), ws.numel(), _lib.stream(dev)), "din_rerank")
+    t0 = KernelTimer.mark("rerank")  # (the projections included)
+    if shared:
+        cp = rerank_project(model, table, c, prm)
+        xp = rerank_project(model, table, ex, prm) if ex is not None else None
+        _lib.check(lib.nrk_din_rerank_projected(_lib.ptr(table), table.shape[0], _lib.NRK_DTYPE_BF16, _lib.ptr(h), U, L,
+                                                _lib.ptr(c), _lib.ptr(co), _lib.ptr(cl), _lib.ptr(ex), _lib.ptr(oo),
+                                                _lib.ptr(out), d, A, F, ctypes.byref(p), _lib.ptr(cp), _lib.ptr(xp),
+                                                _lib.ptr(ws), ws.numel(), _lib.stream(dev)), "din_rerank_projected")
+    else:
+        _lib.check(lib.nrk_din_rerank(_lib.ptr(table), table.shape[0], _lib.NRK_DTYPE_BF16, _lib.ptr(h), U, L,
+                                      _lib.ptr(c), _lib.ptr(co), _lib.ptr(cl), _lib.ptr(ex), _lib.ptr(oo),
+                                      _lib.ptr(out), d, A, F, ctypes.byref(p), _lib.ptr(ws), ws.numel(),
+                                      _lib.stream(dev)), "din_rerank")
     KernelTimer.push("rerank", t0)
     return out
 
@@ -281,7 +311,7 @@ def rerank_clusters(model, table: torch.Tensor, hist_rows: torch.Tensor, user_cl
     oo = torch.zeros(U + 1, dtype=torch.int64, device=dev)
     torch.cumsum(width, 0, out=oo[1:])
     n_out = int(oo[-1].item())
-    flat = rerank_ragged(model, table, hist_rows[order], rows, coff, clen, extra, oo[:-1], n_out)
+    flat = rerank_ragged(model, table, hist_rows[order], rows, coff, clen, extra, oo[:-1], n_out, shared=True)
     rerank.path = "fused"
     out = {"logits": [], "users": []}
     cnt = torch.bincount(ucs, minlength=nl)

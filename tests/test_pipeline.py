@@ -192,7 +192,8 @@ def test_rerank_ragged_shared_lists_extra_and_gaps():
     list (same offset), lists of 0, 1, 63, 64, 65 and 300 candidates, an
     appended extra candidate (-1 = a padded slot, a row past the table = -inf),
     duplicated candidates, out_off with gaps between users; every logit equals
-    the rectangular rerank() of the same list, bit for bit, on two runs."""
+    the rectangular rerank() of the same list, bit for bit, staged from the rows
+    and from the lists' projections (nrk_din_rerank_projected)."""
     from newsrecommend_amd.pipeline import rerank, rerank_ragged
 
     dev = torch.device("cuda")
@@ -214,7 +215,7 @@ def test_rerank_ragged_shared_lists_extra_and_gaps():
     oo = torch.cumsum(width + 3, 0) - (width + 3)  # gaps of 3 between users
     n_out = int((oo[-1] + width[-1]).item()) + 5
     out = rerank_ragged(model, table, hist, pool, co, cl, extra, oo, n_out)
-    got = rerank_ragged(model, table, hist, pool, co, cl, extra, oo, n_out)
+    got = rerank_ragged(model, table, hist, pool, co, cl, extra, oo, n_out, shared=True)  # projected lists
     for u, (o, n) in enumerate(lists):
         lst = torch.cat([pool[o:o + n], extra[u:u + 1]])
         ref = rerank(model, table, hist[u:u + 1], lst[None])[0]
