@@ -253,6 +253,14 @@ int nrk_din_rerank_projected(const void* table, int64_t n_table, int32_t dtype, 
                              const int32_t* extra, const int64_t* out_off, float* out, int32_t d, int32_t A,
                              int32_t F, const nrk_din_rerank_params* params, const float* cand_proj,
                              const float* extra_proj, void* ws, size_t ws_bytes, void* stream);
+/* evaluate()'s per-user tail over re-rank logits (DIN.py:176-189): user u's
+ * logits are [seg_off[u], seg_off[u+1]); pos[u] the index of its positive
+ * (-1: none); prob = sigmoid(logits) as the caller computes it.  Writes the f64
+ * BCE-with-logits sum over the finite logits (label 1 at pos[u]), their count,
+ * and before[u] = #{j : prob_j > prob_pos or (prob_j == prob_pos and j < pos)}
+ * (NDCG rank - 1, the stable-sort tie rule).  One block per user. */
+int nrk_rerank_user_stats(const float* logits, const float* prob, const int64_t* seg_off, const int64_t* pos,
+                          int32_t nU, double* loss_sum, int64_t* nval, int64_t* before, void* stream);
 
 /* ------------------------------------------------------ inverted lists --
  * faiss Clustering / IndexIVFFlat building blocks (Retrieval.py:11-23).

@@ -899,6 +899,54 @@ int launch_proj_a(int A, int F, const ProjArgs& a, hipStream_t st) {
   }
 }
 
+// ---- the evaluate() tail per user (DIN.py:176-189 as pipeline.rerank_clusters
+// states it), over the logits of user u = [seg[u], seg[u + 1]): the BCE sum
+// over the valid (finite) candidates in f64 (label 1 at pos[u], -1 = none),
+// their count, and #{j : p_j > p_pos or (p_j == p_pos and j < pos)} for the
+// NDCG rank, p = the sigmoid probabilities the caller computed.  One block per
+// user, fixed-order reductions.
+__global__ __launch_bounds__(256) void user_stats_kernel(const float* __restrict__ logits, const float* __restrict__ prob,
+                                                         const int64_t* __restrict__ seg, const int64_t* __restrict__ pos,
+                                                         double* __restrict__ loss_sum, int64_t* __restrict__ nval,
+                                                         int64_t* __restrict__ before) {
+  const int u = blockIdx.x, tid = threadIdx.x;
+  const int64_t lo = seg[u], hi = seg[u + 1], ps = pos[u];
+  const float pp = ps >= 0 ? prob[ps] : 0.f;
+  double ls = 0.0;
+  int64_t nv = 0, nb = 0;
+  for (int64_t i = lo + tid; i < hi; i += 256) {
+    const float x = logits[i];
+    if (isfinite(x)) {
+      const double xd = x;
+      ls += (xd > 0.0 ? xd : 0.0) - (i == ps ? xd : 0.0) + log1p(exp(-fabs(xd)));
+      ++nv;
+    }
+    if (ps >= 0) {
+      const float p = prob[i];
+      nb += (p > pp || (p == pp && i < ps)) ? 1 : 0;
+    }
+  }
+  __shared__ double sl[256];
+  __shared__ int64_t sv[256], sb[256];
+  sl[tid] = ls;
+  sv[tid] = nv;
+  sb[tid] = nb;
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if (tid < h) {
+      sl[tid] += sl[tid + h];
+      sv[tid] += sv[tid + h];
+      sb[tid] += sb[tid + h];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    loss_sum[u] = sl[0];
+    nval[u] = sv[0];
+    before[u] = sb[0];
+  }
+}
+
 }  // namespace rr
 }  // namespace nrk
 
@@ -1018,4 +1066,15 @@ extern "C" int nrk_din_rerank_project(const void* table, int64_t n_table, int32_
   if (d == 256) return rr::launch_proj_a<256>(A, F, a, st);
   if (d == 128) return rr::launch_proj_a<128>(A, F, a, st);
   return rr::launch_proj_a<64>(A, F, a, st);
+}
+
+extern "C" int nrk_rerank_user_stats(const float* logits, const float* prob, const int64_t* seg_off, const int64_t* pos,
+                                     int32_t nU, double* loss_sum, int64_t* nval, int64_t* before, void* stream) {
+  NRK_CHECK_ARG(nU >= 0, "rerank_user_stats: bad user count %d", nU);
+  if (nU == 0) return NRK_OK;
+  NRK_CHECK_ARG(logits && prob && seg_off && pos && loss_sum && nval && before, "rerank_user_stats: null pointer");
+  hipLaunchKernelGGL(rr::user_stats_kernel, dim3(nU), dim3(256), 0, (hipStream_t)stream, logits, prob, seg_off, pos,
+                     loss_sum, nval, before);
+  NRK_CHECK_LAUNCH("user_stats_kernel");
+  return NRK_OK;
 }

@@ -243,13 +243,6 @@ def rerank(model, table: torch.Tensor, hist_rows: torch.Tensor, cand_rows: torch
 rerank.path = None
 
 
-def _seg_sum(x: torch.Tensor, start: torch.Tensor, end: torch.Tensor) -> torch.Tensor:
-    """Sums of x over the segments [start, end) (cumulative-sum differences)."""
-    c = torch.zeros(x.numel() + 1, dtype=x.dtype, device=x.device)
-    torch.cumsum(x, 0, out=c[1:])
-    return c[end] - c[start]
-
-
 @torch.no_grad()
 def rerank_clusters(model, table: torch.Tensor, hist_rows: torch.Tensor, user_cluster: torch.Tensor,
                     cluster_off: torch.Tensor, cluster_rows: torch.Tensor, last_rows: torch.Tensor | None = None,
@@ -331,20 +324,21 @@ def rerank_clusters(model, table: torch.Tensor, hist_rows: torch.Tensor, user_cl
         pcol = torch.where(has_pos, pos_in, clen if extra is not None else torch.full_like(clen, -1))
         if extra is not None:
             has_pos = has_pos | (extra >= 0)
-        pidx = (oo[:-1] + pcol.clamp_min(0)).clamp(0, max(n_out - 1, 0))  # an empty list's index stays in range
-        seg = torch.repeat_interleave(torch.arange(U, device=dev), width)
-        x = flat.double()
-        valid = torch.isfinite(x)
-        y = torch.zeros_like(x)
-        y[pidx[has_pos]] = 1.0
-        per = torch.where(valid, x.clamp_min(0) - x * y + torch.log1p(torch.exp(-x.abs())), torch.zeros_like(x))
-        nval = _seg_sum(valid.double(), oo[:-1], oo[1:])
-        loss = _seg_sum(per, oo[:-1], oo[1:]) / nval
+        # one block per user (nrk_rerank_user_stats): the BCE sum over the
+        # finite logits in f64, their count, and the candidates ranked before
+        # the positive by the sigmoid probabilities (stable-sort ties)
+        from . import _lib
+
+        pos = torch.where(has_pos, oo[:-1] + pcol.clamp_min(0), torch.full_like(pcol, -1)).to(torch.int64).contiguous()
         pr = torch.sigmoid(flat)
-        pp = pr[pidx] if n_out else torch.zeros(U, device=dev)
-        col = torch.arange(n_out, device=dev) - oo[:-1][seg]
-        before = (pr > pp[seg]) | ((pr == pp[seg]) & (col < pcol[seg]))
-        rank = _seg_sum(before.long(), oo[:-1], oo[1:]) + 1
+        loss_sum = torch.empty(U, dtype=torch.float64, device=dev)
+        nval = torch.empty(U, dtype=torch.int64, device=dev)
+        before = torch.empty(U, dtype=torch.int64, device=dev)
+        _lib.check(_lib.load().nrk_rerank_user_stats(_lib.ptr(flat), _lib.ptr(pr), _lib.ptr(oo), _lib.ptr(pos), U,
+                                                     _lib.ptr(loss_sum), _lib.ptr(nval), _lib.ptr(before),
+                                                     _lib.stream(dev)), "rerank_user_stats")
+        loss = loss_sum / nval.double()
+        rank = before + 1
         nd = torch.where(has_pos & (rank <= k), 1.0 / torch.log2(rank.double() + 1.0), torch.zeros_like(loss))
         nd = torch.where(nval > 0, nd, torch.full_like(nd, float("nan")))
         loss_u = torch.empty(U, dtype=torch.float64, device=dev)
