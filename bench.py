@@ -521,13 +521,15 @@ def bench_e2e(args, rank, world, dev):
     return out
 
 
-def _rerank_roofline(ms, hist, cand, d, A, L, key, n_samples=None):
+def _rerank_roofline(ms, hist, cand, d, A, L, key, n_samples=None, proj=None):
     """Roofline of the fused re-rank launch (nrk_din_rerank): ALGORITHMIC bytes
     = per candidate its bf16 row (2d), id and logit (8 B), per user its L ids
     and nv history rows (2d each); VALU work = 2 lane-ops (add, |.|-fma) per
     (candidate, scored row, attention unit), scored rows = nv + 1 padding row
     when nv < L, against the 78.6 T lane-op/s of the fp32 vector peak
-    (157.3 TFLOP/s counting an fma as 2)."""
+    (157.3 TFLOP/s counting an fma as 2).  proj = (F, list items): shared lists
+    projected once (nrk_din_rerank_project: each item's bf16 row in, A + F f32
+    out) and scored from the projections (4 (A + F) + 8 B per candidate)."""
     nv = (hist >= 0).sum(1).double()
     nr = nv + (nv < L).double()
     if cand is not None:
@@ -536,13 +538,19 @@ def _rerank_roofline(ms, hist, cand, d, A, L, key, n_samples=None):
         ops = float((per_user * nr).sum()) * A * 2
     else:
         ops = n_samples * float(nr.mean()) * A * 2
-    byt = n_samples * (2 * d + 8) + float((4 * L + 2 * d * nv).sum())
+    per_c = 2 * d + 8 if proj is None else 4 * (A + proj[0]) + 8
+    byt = n_samples * per_c + float((4 * L + 2 * d * nv).sum())
+    kern = f"din_rerank_kernel<{d}, {A}, 32>"
+    if proj is not None:
+        byt += proj[1] * (2 * d + 4 + 4 * (A + proj[0]))
+        kern = f"din_rerank_project_kernel<{d}, {A}, 32> + " + kern + " (projected shared lists)"
     sec = ms * 1e-3
     gbs = byt / sec / 1e9
-    return {"hbm": {"bound": "hbm", "binding": "valu (the scoring; see valu)", "kernel": f"din_rerank_kernel<{d}, {A}, 32>", "achieved": gbs,
+    return {"hbm": {"bound": "hbm", "binding": "valu (the scoring; see valu)", "kernel": kern, "achieved": gbs,
                     "peak": HBM_GBS, "unit": "GB/s", "frac": gbs / HBM_GBS, "traffic": _pmc_traffic(key),
-                    "algorithmic": f"{byt:.4g} B per launch ({2 * d + 8} B per candidate + the users' ids and "
-                                   f"history rows), {ms:.3f} ms (HIP events)"},
+                    "algorithmic": f"{byt:.4g} B per launch ({per_c} B per candidate + the users' ids and history "
+                                   f"rows{' + the list projections' if proj is not None else ''}), {ms:.3f} ms "
+                                   f"(HIP events)"},
             "valu": {"achieved": ops / sec / 1e12, "peak": 78.6, "unit": "T lane-ops/s",
                      "frac": ops / sec / 1e12 / 78.6,
                      "algorithmic": f"{ops:.4g} lane-ops (2 per candidate x scored row x unit)"}}
@@ -624,7 +632,8 @@ def bench_retrieval_flow(args, rank, world, dev):
            "rerank_kernel_ms": kt.mean_ms("rerank"),
            "rerank_roofline": _rerank_roofline(kt.mean_ms("rerank"), hist[lo:hi], None, d, 128, L,
                                                f"rerank:flow,users={hi - lo},gpus={world}",
-                                               n_samples=float(cand_per_user.sum()) + (hi - lo))["hbm"],
+                                               n_samples=float(cand_per_user.sum()) + (hi - lo),
+                                               proj=(32, int(xb.shape[0]) + (hi - lo)))["hbm"],
            "rerank_path": __import__("newsrecommend_amd.pipeline", fromlist=["rerank"]).rerank.path,
            "ndcg_at_5_mean_rank0": float(res["ndcg"].mean()), "loss_mean_rank0": float(res["loss"].mean())}
     del xb, table, index, centroid_index
