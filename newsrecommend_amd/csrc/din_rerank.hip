@@ -266,16 +266,23 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
   const bf16x8 z8 = {0, 0, 0, 0, 0, 0, 0, 0};
   int sidn[NE];
   unsigned svalid = 0;  // bit k: stg[k] holds a valid candidate row
-  // candidate ci of user u_ (the appended extra at ci == len), -1 = padded slot
-  auto cand_id = [&](int u_, int64_t off, int len, int ci) -> int {
+  // the stored id of candidate ci of user u_ (the appended extra at ci == len;
+  // -1 past the list): a load whose value is only tested where it is used
+  // (valid_id), so issuing it never waits for it
+  auto cand_raw = [&](int u_, int64_t off, int len, int ci) -> int {
     int id = -1;
     if (ci < len) id = a.cand[off + ci];
     else if (ci == len && a.extra) id = a.extra[u_];
-    return id >= 0 && id < a.n_table ? id : -1;
+    return id;
+  };
+  auto valid_id = [&](int id) -> bool { return id >= 0 && id < a.n_table; };
+  auto cand_id = [&](int u_, int64_t off, int len, int ci) -> int {
+    const int id = cand_raw(u_, off, len, ci);
+    return valid_id(id) ? id : -1;
   };
   auto load_cids = [&](int u_, int64_t off, int len, int c0_) __attribute__((always_inline)) {
 #pragma unroll
-    for (int k = 0; k < NE; ++k) sidn[k] = cand_id(u_, off, len, c0_ + (tid + NT * k) / CPR);
+    for (int k = 0; k < NE; ++k) sidn[k] = cand_raw(u_, off, len, c0_ + (tid + NT * k) / CPR);
   };
   auto issue_rows = [&]() __attribute__((always_inline)) {
     svalid = 0;
@@ -283,7 +290,7 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
     for (int k = 0; k < NE; ++k) {
       const int cc = (tid + NT * k) % CPR;
       stg[k] = z8;
-      if (sidn[k] >= 0) {
+      if (valid_id(sidn[k])) {
         stg[k] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(a.table + (int64_t)sidn[k] * D + cc * 8));
         svalid |= 1u << k;
       }
@@ -335,7 +342,7 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
       stp[k] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (src) stp[k] = *reinterpret_cast<const float4*>(src + 4 * part);
     }
-    vid = tid < CH ? cand_id(u_, off, len, c0_ + tid) : -1;
+    vid = tid < CH ? cand_raw(u_, off, len, c0_ + tid) : -1;
   };
   auto store_proj = [&](int* cv) __attribute__((always_inline)) {
 #pragma unroll
@@ -346,7 +353,7 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
         else *reinterpret_cast<float4*>(Q1s + cand * F + 4 * (part - A / 4)) = stp[k];
       }
     }
-    if (tid < CH) cv[tid] = vid >= 0;
+    if (tid < CH) cv[tid] = valid_id(vid);
   };
 
   if (tid == 0) qslot[0] = atomicAdd(a.queue, 1);
@@ -675,6 +682,9 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
           const float x0 = MS[0 * CH + cc], x1 = MS[2 * CH + cc], xm = fmaxf(x0, x1);
           den[i] = MS[1 * CH + cc] * __expf(x0 - xm) + MS[3 * CH + cc] * __expf(x1 - xm);
         }
+        float rden[4];  // (a hardware reciprocal per candidate row instead of IEEE divisions)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rden[i] = __builtin_amdgcn_rcpf(den[i]);  // v_rcp_f32, 1 ulp
         const int nks = nrp / 32;
         bf16x8 eh[2], el[2];
 #pragma unroll
@@ -716,7 +726,7 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
             }
             const float cb = c1s[f];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) H1s[(16 * qct + 4 * l4 + k) * (F + 4) + f] = fmaxf(acc[k] / den[k] + cb, 0.f);
+            for (int k = 0; k < 4; ++k) H1s[(16 * qct + 4 * l4 + k) * (F + 4) + f] = fmaxf(acc[k] * rden[k] + cb, 0.f);
           }
         }
       }
