@@ -520,8 +520,6 @@ class FusedTrainStep:
             self.hist_b, self.q_b, self.y_b = self.hist_k[0], self.q_k[0], self.y_k[0]
             self.U_b = torch.empty((B, A), dtype=torch.float32, device=dev)
             self.W1k_b = torch.empty((A, d), dtype=torch.bfloat16, device=dev)
-        self._gather_stream = torch.cuda.Stream(dev) if self.fast and self.K > 1 else None
-        self._gather_join = None
         self.graph = self.graph_k = None
         if graph:
             snap = [t.detach().clone() for t in (self.P, self.M, self.V, self.step_t)]
@@ -604,29 +602,11 @@ class FusedTrainStep:
         W1, b1 = m.attn.attn[0].weight, m.attn.attn[0].bias
         w2 = m.attn.attn[2].weight
         self.hist_b, self.q_b, self.y_b = self.hist_k[k], self.q_k[k], self.y_k[k]
-
-        def gather(k0, n, stream):
+        if gather_n > 0:
             _lib.check(L_.nrk_din_batch(
-                _lib.ptr(self.idx_ring[k0]), n * B, _lib.ptr(self.hist_all), _lib.ptr(self.tgt_all),
+                _lib.ptr(self.idx_ring[k]), gather_n * B, _lib.ptr(self.hist_all), _lib.ptr(self.tgt_all),
                 _lib.ptr(self.lab_all), self.hist_all.shape[0], L, _lib.ptr(self.table), N, dt, d, None, None, A,
-                _lib.ptr(self.hist_k[k0]), _lib.ptr(self.q_k[k0]), _lib.ptr(self.y_k[k0]), None, None, stream),
-                "din_batch")
-        if gather_n > 1:
-            # step k's rows now; the following steps' on a side stream, under
-            # step k's kernels (they read nothing a step writes), joined before
-            # step k + 1
-            gather(k, 1, st)
-            main = torch.cuda.current_stream(self.table.device)
-            side = self._gather_stream
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                gather(k + 1, gather_n - 1, _lib.stream(self.table.device))
-            self._gather_join = (k + 1, side)
-        elif gather_n == 1:
-            gather(k, 1, st)
-        if self._gather_join is not None and self._gather_join[0] == k:
-            torch.cuda.current_stream(self.table.device).wait_stream(self._gather_join[1])
-            self._gather_join = None
+                _lib.ptr(self.hist_b), _lib.ptr(self.q_b), _lib.ptr(self.y_b), None, None, st), "din_batch")
         _lib.check(L_.nrk_din_batch_u(_lib.ptr(self.q_b), B, d, _lib.ptr(W1), _lib.ptr(b1), A, _lib.ptr(self.U_b),
                                       _lib.ptr(self.W1k_b), st), "din_batch_u")
         t0 = KernelTimer.mark("fwd")
