@@ -276,7 +276,7 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
     return id;
   };
   auto valid_id = [&](int id) -> bool { return id >= 0 && id < a.n_table; };
-  auto cand_id = [&](int u_, int64_t off, int len, int ci) -> int {
+  [[maybe_unused]] auto cand_id = [&](int u_, int64_t off, int len, int ci) -> int {
     const int id = cand_raw(u_, off, len, ci);
     return valid_id(id) ? id : -1;
   };
