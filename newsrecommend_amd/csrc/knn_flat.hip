@@ -2188,6 +2188,8 @@ extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe,
   if (n > 0) {
     // ---- phase B: collect every probed item at or above e_k - B_q
     screen_fn fbk = pick_screen(p.dp, p.qt, p.M, l2 != 0, 3);
+    // the 16x16x32 collect where built (NRK_SCREEN16=0: the 32x32x16 one; a test hook)
+    if (p.dp == 128 && p.qt == 2 && p.wavesB == 4 && test_hook("NRK_SCREEN16", 1)) fbk = pick_collect16_dp128(l2 != 0);
     if (!fbk) return fail(NRK_EUNSUPPORTED, "ivf_search: no collect kernel for dp=%d", p.dp);
     IvfScreen isb{work, list_off, seg, sp, nlist, p.chB, p.cmaxB, thr, ccnt, cpos, p.cap, nprobe};
     hipLaunchKernelGGL(fbk, dim3((unsigned)p.ubB), dim3(p.wavesB * 64), 0, st, qi, xbh_ivf, meta_ivf, nq, n, 0, 0, 0, 1,

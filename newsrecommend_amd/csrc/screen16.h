@@ -283,6 +283,312 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_kernel(
   }
 }
 
+// IVF collect (screen.h MODE 3) on v_mfma_f32_16x16x32_bf16: MODE 3's work items
+// (a list chunk x a tile of the list's probing queries, a persistent grid over the
+// device work table) and its LDS candidate staging, in screen16's layout with the
+// deferred epilogue.  A wave runs the MFMAs of its 16-query half-tiles up to the
+// last one holding a real probing query: list segments are padded to the work
+// item's rows, and the padding a wave still computes is now < 16 rows instead of
+// < 32.  L2: scores 2 ip - |x|^2, the rows' norms staged with each tile.
+template <int DP, int QT, int WAVES, int TIL, bool L2, int PD = DP / 32>
+__global__ __launch_bounds__(WAVES * 64, 2) void screen16_collect_kernel(
+    const uint16_t* __restrict__ qh, const uint16_t* __restrict__ xbh, const float* __restrict__ xmeta, int64_t nq,
+    int64_t nb, int64_t chunk, int nch, int nqt, int tstride, float* __restrict__ part_s, int* __restrict__ part_i,
+    float* __restrict__ part_t, const float* __restrict__ tau_q, IvfScreen iv) {
+  (void)nq;
+  (void)nb;
+  (void)chunk;
+  (void)nch;
+  (void)nqt;
+  (void)tstride;
+  (void)part_s;
+  (void)part_i;
+  (void)part_t;
+  (void)tau_q;
+  constexpr int CPR = DP / 8;
+  constexpr int TI = TIL;
+  constexpr int NSUB = TI / 32;
+  static_assert(NSUB % 2 == 0, "sub-tiles alternate between two accumulator sets");
+  constexpr int TCH = TI * CPR;
+  constexpr int NT = WAVES * 64;
+  constexpr int GPT = TCH / NT;
+  static_assert(TCH % NT == 0, "tile must split evenly over the workgroup");
+  constexpr int KS2 = DP / 32;
+  constexpr int NQ2 = 2 * QT;
+  constexpr int WQ = WAVES * 32 * QT;
+  static_assert(WQ <= 1024, "collect rows: 10 bits");
+  constexpr int BUF = TI * DP;  // uint16 per buffer
+  static_assert(PD >= 1 && PD <= KS2, "prefetch depth");
+  constexpr int NBUF = PD == KS2 ? 2 : 3;
+  typedef CollectLds<WQ> CL;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[NBUF * BUF];
+  // L2: the tiles' row norms in a ring of three (tile it in slot it % 3): a
+  // sub-tile's norms are read at its deferred epilogue, which for a tile's last
+  // sub-tile runs in the next tile, after its rows' buffer was refilled
+  __shared__ __attribute__((aligned(16))) float nrm[L2 ? 3 * TI : 4];
+  __shared__ CL cl;
+
+  const int nblk = gridDim.x, b = blockIdx.x;
+  const int xg = b & 7, jj = b >> 3, q8 = nblk >> 3, r8 = nblk & 7;
+  const int logical0 = (xg < r8 ? xg * (q8 + 1) : r8 * (q8 + 1) + (xg - r8) * q8) + jj;
+  const int total = iv.work_off[iv.nlist];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int q16 = lane & 15, g = lane >> 4;
+  for (int logical = logical0; logical < total; logical += nblk) {
+    if (logical != logical0) __syncthreads();  // the previous item is done with the LDS buffers and staging
+    int lo = 0, hi = iv.nlist;  // largest l with work_off[l] <= logical (empty lists own no items)
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (iv.work_off[mid] <= logical) lo = mid;
+      else hi = mid;
+    }
+    const int64_t lb = iv.list_off[lo], le = iv.list_off[lo + 1];
+    const int nchl = (int)cdiv(le - lb, (int64_t)iv.ch);
+    const int local = logical - iv.work_off[lo];
+    const int nqtl = (iv.work_off[lo + 1] - iv.work_off[lo]) / nchl;
+    const int c = local / nqtl, qt = local - c * nqtl;  // query tile innermost (the chunk stays in L2)
+    const int64_t ibeg = lb + (int64_t)c * iv.ch;
+    const int64_t iend = ibeg + iv.ch < le ? ibeg + iv.ch : le;
+    const int64_t seg0 = iv.seg_off[lo];
+
+    bf16x8 qf[NQ2][KS2];
+    float cthr[NQ2];  // collect threshold of the lane's query (+inf: padding row)
+    // (Wave-major rows: a wave's half-tiles share each A fragment.  Spreading a
+    // partly filled item's rows over all waves measured slower, 2.99 -> 3.10 ms.)
+    int nact = 0;     // half-tiles up to the last one holding a real row (padding is a suffix)
+#pragma unroll
+    for (int t = 0; t < NQ2; ++t) {
+      const int row = w * QT * 32 + 16 * t + q16;
+      const int64_t gr = seg0 + (int64_t)qt * WQ + row;
+      const bf16x8* src = reinterpret_cast<const bf16x8*>(qh + gr * DP + 8 * g);
+#pragma unroll
+      for (int s = 0; s < KS2; ++s) qf[t][s] = src[4 * s];
+      const int pair = iv.slot_pair[gr];
+      const int qy = pair >= 0 ? pair / iv.nprobe : -1;
+      cthr[t] = pair >= 0 ? iv.thr_q[qy] : INFINITY;
+      if (g == 0) {
+        cl.qid[row] = qy;
+        cl.qcnt[row] = 0;
+      }
+      if (__any(pair >= 0)) nact = t + 1;
+    }
+    nact = __builtin_amdgcn_readfirstlane(nact);
+    if (tid == 0) cl.n = 0;  // ordered before any append by the first tile's barrier
+
+    const int64_t cnt = iend - ibeg > 0 ? iend - ibeg : 0;
+    const BufRsrc xrs = make_rsrc(xbh + ibeg * DP, (int)(cnt * DP * 2));
+    const BufRsrc nrs = make_rsrc(xmeta + 2 * ibeg, (int)(cnt * 8));
+    const int ntiles = (int)cdiv(cnt, (int64_t)TI);
+    // a thread's rows of a tile are NT / CPR apart, a multiple of the swizzle's
+    // 16-row period: one vector offset, the rest in the scalar offset
+    static_assert((NT / CPR) % 16 == 0, "staging rows per pass: a multiple of the swizzle period");
+    const int voff = (tid / CPR) * DP * 2 + 16 * ((tid % CPR) ^ swz<CPR>(tid / CPR));
+    auto issue_tile = [&](int it, auto buf_c) {
+      constexpr int buf = decltype(buf_c)::value;
+      const int soff = it * TI * DP * 2;
+#pragma unroll
+      for (int u = 0; u < GPT; ++u)
+        buffer_load_lds16(xrs, lds + buf * BUF + (u * NT + w * 64) * 8, voff, soff + u * (NT / CPR) * DP * 2);
+      if constexpr (L2) {
+        if (w == 0) {
+          float* ns = nrm + (it % 3) * TI;
+#pragma unroll
+          for (int u = 0; u < TI / 64; ++u) buffer_load_lds4(nrs, ns + 64 * u, lane * 8, it * TI * 8 + 512 * u);
+        }
+      }
+    };
+    auto afrag = [&](const uint16_t* tl, int row, int s) {
+      return *reinterpret_cast<const bf16x8*>(tl + row * DP + 8 * ((4 * s + g) ^ swz<CPR>(row)));
+    };
+    // staged append of one candidate (position pos) of half-tile t's query
+    auto append = [&](int t, int pos) __attribute__((always_inline)) {
+      const int e = atomicAdd(&cl.n, 1);
+      if (e < CL::CAP) {
+        const int row = w * QT * 32 + 16 * t + q16;
+        const int rank = atomicAdd(&cl.qcnt[row], 1);
+        cl.ent[e] = make_int2(row | (rank << 10), pos);
+      } else {
+        const int qy = cl.qid[w * QT * 32 + 16 * t + q16];
+        if (__builtin_nontemporal_load(&iv.cand_cnt[qy]) <= iv.cap) {
+          // staging full: append directly (stop once the query overflowed)
+          const int slot = atomicAdd(&iv.cand_cnt[qy], 1);
+          if (slot < iv.cap) iv.cand_pos[(int64_t)qy * iv.cap + slot] = pos;
+        }
+      }
+    };
+
+    // the tile pipeline for NA active half-tiles (NA = 0: staging and barriers only)
+    auto run = [&](auto na_c) __attribute__((always_inline)) {
+      constexpr int NA = decltype(na_c)::value;
+      f32x4 accA[NQ2][2], accB[NQ2][2];
+      int64_t baseA = -1, baseB = -1;
+      int nvA = 0, nvB = 0;
+      bf16x8 af[2][PD];
+      auto mask_rows = [&](f32x4 (&pa)[NQ2][2], int nv) __attribute__((always_inline)) {
+#pragma unroll
+        for (int t = 0; t < NA; ++t)
+#pragma unroll
+          for (int ih = 0; ih < 2; ++ih)
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+              if (16 * ih + 4 * g + v >= nv) pa[t][ih][v] = -INFINITY;
+      };
+      auto tree = [&](f32x4 (&pa)[NQ2][2], int64_t pbase, float (&m2)[NQ2][2], float (&m)[NQ2])
+          __attribute__((always_inline)) {
+        float n[2][4];  // L2: |x|^2 of the sub-tile's rows 16 ih + 4 g + v
+        if constexpr (L2) {
+          const int off = pbase >= 0 ? (int)(pbase - ibeg) : 0;  // (nothing pending: any slot)
+          const float* ln = nrm + ((off / TI) % 3) * TI + off % TI + 4 * g;
+#pragma unroll
+          for (int ih = 0; ih < 2; ++ih) {
+            const float4 x = *reinterpret_cast<const float4*>(ln + 16 * ih);
+            n[ih][0] = x.x;
+            n[ih][1] = x.y;
+            n[ih][2] = x.z;
+            n[ih][3] = x.w;
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < NA; ++t) {
+#pragma unroll
+          for (int ih = 0; ih < 2; ++ih) {
+            if constexpr (L2) {
+#pragma unroll
+              for (int v = 0; v < 4; ++v) pa[t][ih][v] = fmaf(2.f, pa[t][ih][v], -n[ih][v]);
+            }
+            m2[t][ih] = fmax_ieee(fmax_ieee(pa[t][ih][0], pa[t][ih][1]), fmax_ieee(pa[t][ih][2], pa[t][ih][3]));
+          }
+          m[t] = fmax_ieee(m2[t][0], m2[t][1]);
+        }
+      };
+      auto drain = [&](f32x4 (&pa)[NQ2][2], int64_t pbase, const float (&m2)[NQ2][2], const float (&m)[NQ2])
+          __attribute__((always_inline)) {
+        bool hit = false;
+#pragma unroll
+        for (int t = 0; t < NA; ++t) hit |= m[t] >= cthr[t];
+        if (!__any(hit)) return;
+#pragma unroll
+        for (int t = 0; t < NA; ++t) {
+          if (__any(m[t] >= cthr[t])) {
+#pragma unroll
+            for (int ih = 0; ih < 2; ++ih) {
+              if (__any(m2[t][ih] >= cthr[t])) {
+#pragma unroll
+                for (int v = 0; v < 4; ++v)
+                  if (pa[t][ih][v] >= cthr[t]) append(t, (int)(pbase + 16 * ih + 4 * g + v));
+              }
+            }
+          }
+        }
+      };
+      auto sub_tile = [&](auto st_c, int64_t i0, int nvalid, const uint16_t* next_tl, const uint16_t* cur_tl)
+          __attribute__((always_inline)) {
+        constexpr int st = decltype(st_c)::value;
+        constexpr int par = st & 1;
+        f32x4(&cur)[NQ2][2] = par ? accB : accA;
+        f32x4(&pend)[NQ2][2] = par ? accA : accB;
+        const int64_t pbase = par ? baseA : baseB;
+        const int pnv = par ? nvA : nvB;
+        if (pbase >= 0 && pnv < 32) mask_rows(pend, pnv);
+        const int nrow = (st + 1 < NSUB ? 32 * (st + 1) : 0) + q16;
+        const f32x4 zero = {};
+#pragma unroll
+        for (int s = 0; s < KS2; ++s) {
+#pragma unroll
+          for (int ih = 0; ih < 2; ++ih) {
+#pragma unroll
+            for (int t = 0; t < NA; ++t)
+              cur[t][ih] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ih][s % PD], qf[t][s],
+                                                                   s == 0 ? zero : cur[t][ih], 0, 0, 0);
+            if (s + PD < KS2) af[ih][s % PD] = afrag(cur_tl, 32 * st + 16 * ih + q16, s + PD);
+            else af[ih][s % PD] = afrag(next_tl, nrow + 16 * ih, s + PD - KS2);
+          }
+        }
+        float m2[NQ2][2], m[NQ2];
+        tree(pend, pbase, m2, m);
+#pragma unroll
+        for (int t = 0; t < NA; ++t) m[t] = pbase >= 0 ? m[t] : -INFINITY;  // nothing pending: drain is a no-op
+        drain(pend, pbase, m2, m);
+        if constexpr (par == 0) {
+          baseA = i0 + 32 * st;
+          nvA = nvalid - 32 * st;
+        } else {
+          baseB = i0 + 32 * st;
+          nvB = nvalid - 32 * st;
+        }
+      };
+      auto tile_d = [&](int it, auto buf_c) __attribute__((always_inline)) {
+        constexpr int buf = decltype(buf_c)::value;
+        constexpr int nbuf = (buf + 1) % NBUF;
+        constexpr int rbuf = (buf + 2) % NBUF;
+        const uint16_t* tl = lds + buf * BUF;
+        const int64_t i0 = ibeg + (int64_t)it * TI;
+        const int nvalid = (int)((iend - i0) < TI ? (iend - i0) : TI);
+        sub_tile(std::integral_constant<int, 0>{}, i0, nvalid, tl, tl);
+        if constexpr (NSUB == 4) {
+          sub_tile(std::integral_constant<int, 1>{}, i0, nvalid, tl, tl);
+          sub_tile(std::integral_constant<int, 2>{}, i0, nvalid, tl, tl);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // tile it+1 landed; every wave is done with rbuf and with norm slot (it + 2) % 3
+        // (tile it-1's last epilogue ran in this tile's first sub-tile)
+        __syncthreads();
+        if (it + 2 < ntiles) issue_tile(it + 2, std::integral_constant<int, rbuf>{});
+        sub_tile(std::integral_constant<int, NSUB - 1>{}, i0, nvalid, lds + nbuf * BUF, tl);
+      };
+      if (ntiles > 0) {
+        issue_tile(0, std::integral_constant<int, 0>{});
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // tile 0 landed
+        if (ntiles > 1) issue_tile(1, std::integral_constant<int, 1>{});
+#pragma unroll
+        for (int ih = 0; ih < 2; ++ih)
+#pragma unroll
+          for (int s = 0; s < PD; ++s) af[ih][s] = afrag(lds, 16 * ih + q16, s);
+      }
+      for (int it = 0; it < ntiles; it += NBUF) {
+        tile_d(it, std::integral_constant<int, 0>{});
+        if (it + 1 < ntiles) tile_d(it + 1, std::integral_constant<int, 1>{});
+        if constexpr (NBUF == 3) {
+          if (it + 2 < ntiles) tile_d(it + 2, std::integral_constant<int, 2 % NBUF>{});
+        }
+      }
+      if (baseB >= 0) {  // the last sub-tile's epilogue
+        if (nvB < 32) mask_rows(accB, nvB);
+        float m2[NQ2][2], m[NQ2];
+        tree(accB, baseB, m2, m);
+        drain(accB, baseB, m2, m);
+      }
+    };
+    if (nact == NQ2) run(std::integral_constant<int, NQ2>{});
+    else if (nact == 0) run(std::integral_constant<int, 0>{});
+    else if constexpr (NQ2 == 4) {
+      if (nact == 3) run(std::integral_constant<int, 3>{});
+      else if (nact == 2) run(std::integral_constant<int, 2>{});
+      else run(std::integral_constant<int, 1>{});
+    } else {
+      run(std::integral_constant<int, 1>{});
+    }
+
+    // flush the staged candidates: one global atomic per query row
+    __syncthreads();
+    for (int row = tid; row < WQ; row += NT) {
+      const int n_r = cl.qcnt[row];
+      cl.base[row] = n_r > 0 ? atomicAdd(&iv.cand_cnt[cl.qid[row]], n_r) : 0;
+    }
+    __syncthreads();
+    const int ne = cl.n < CL::CAP ? cl.n : CL::CAP;
+    for (int e = tid; e < ne; e += NT) {
+      const int2 en = cl.ent[e];
+      const int row = en.x & 1023, dst = cl.base[row] + (en.x >> 10);
+      if (dst < iv.cap) iv.cand_pos[(int64_t)cl.qid[row] * iv.cap + dst] = en.y;
+    }
+  }
+}
+
+// IVF collect on the 16x16x32 form for (DP, l2), or nullptr (screen.h's MODE 3)
+screen_fn pick_collect16_dp128(bool l2);
+
 // the 16x16x32 main pass for (DP, qt, M), or nullptr (no such form: use screen.h's)
 screen_fn pick_screen16_dp128(int qt, int M);
 screen_fn pick_screen16_dp256_w8(int M);

@@ -14,4 +14,11 @@ screen_fn pick_screen16_dp128(int qt, int M) {
   if (M != 4 || qt != 2) return nullptr;
   return screen16_kernel<128, 2, 4, 4, 128, false>;
 }
+
+// IVF collect (MODE 3), two query tiles per wave (256 probing queries per work
+// item, as the 32x32x16 form); L2 on 128-item tiles, inner product on 64-item
+// tiles (its 128-item form spills 8 VGPRs).
+screen_fn pick_collect16_dp128(bool l2) {
+  return l2 ? screen16_collect_kernel<128, 2, 4, 128, true> : screen16_collect_kernel<128, 2, 4, 64, false>;
+}
 }  // namespace nrk

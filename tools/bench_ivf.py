@@ -73,10 +73,14 @@ for combo in itertools.product(*grid):
     # phase B rows per work item: waves x 32 x (2 query tiles per wave, 1 at d > 128)
     wq = 4 * 32 * (2 if a.d <= 128 else 1)
     padded = 2.0 * a.d * float((np.ceil(cnt_l / wq) * wq * sizes).sum())
+    # MFMA work issued: waves skip query tiles past a list's last prober (32 rows
+    # for the 32x32x16 collect, 16 for the 16x16x32 one)
+    iss = {gq: 2.0 * a.d * float((np.ceil(cnt_l / gq) * gq * sizes).sum()) for gq in (16, 32)}
     print(f"{combo}: stages ms group {st[0]:.4f} screen {st[1]:.4f} merge {st[2]:.4f} fallback {st[3]:.4f}  "
           f"ivf wall {wall * 1e3:.3f} ms, full (with coarse) {full * 1e3:.3f} ms = {a.nq / full:,.0f} QPS; "
           f"screen {flops / st[1] / 1e9:.1f} TFLOP/s useful, {padded / st[1] / 1e9:.1f} incl. query-tile padding "
-          f"(useful {flops / 1e12:.2f} TF, padded {padded / 1e12:.2f} TF); fallback={int(ivf.last_fallback.item())}",
+          f"(useful {flops / 1e12:.2f} TF, padded {padded / 1e12:.2f} TF; issued at 32 / 16-query tiles "
+          f"{iss[32] / 1e12:.2f} / {iss[16] / 1e12:.2f} TF); fallback={int(ivf.last_fallback.item())}",
           flush=True)
 flat = nf.IndexFlat(a.d, metric)
 flat.add(xb)
