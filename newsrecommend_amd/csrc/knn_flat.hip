@@ -2010,7 +2010,7 @@ static IvfPlan make_ivf_plan(int64_t nq, int nprobe, int nlist, int64_t max_list
     off = align_up(off + bytes, 256);
     return o;
   };
-  p.off_fbc = take(16);
+  p.off_fbc = take(64);  // fallback counters [0, 16), collect work tickets [32, 64)
   p.off_cnt = take((size_t)nlist * 4);
   p.off_fill = take((size_t)nlist * 4);
   p.off_hist = take((size_t)GROUP_BLOCKS * nlist * 4);
@@ -2104,7 +2104,7 @@ extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe,
   NRK_CHECK_ARG(ws != nullptr, "ivf_search: null workspace");
   char* w = static_cast<char*>(ws);
   int* fbc = reinterpret_cast<int*>(w + p.off_fbc);
-  if (hipMemsetAsync(fbc, 0, 16, st) != hipSuccess) return fail(NRK_ELAUNCH, "ivf_search: memset failed");
+  if (hipMemsetAsync(fbc, 0, 64, st) != hipSuccess) return fail(NRK_ELAUNCH, "ivf_search: memset failed");
   if (n_fallback && hipMemsetAsync(n_fallback, 0, 8, st) != hipSuccess)
     return fail(NRK_ELAUNCH, "ivf_search: memset failed");
   if (nq == 0) return NRK_OK;
@@ -2191,7 +2191,7 @@ extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe,
     // the 16x16x32 collect where built (NRK_SCREEN16=0: the 32x32x16 one; a test hook)
     if (p.dp == 128 && p.qt == 2 && p.wavesB == 4 && test_hook("NRK_SCREEN16", 1)) fbk = pick_collect16_dp128(l2 != 0);
     if (!fbk) return fail(NRK_EUNSUPPORTED, "ivf_search: no collect kernel for dp=%d", p.dp);
-    IvfScreen isb{work, list_off, seg, sp, nlist, p.chB, p.cmaxB, thr, ccnt, cpos, p.cap, nprobe};
+    IvfScreen isb{work, list_off, seg, sp, nlist, p.chB, p.cmaxB, thr, ccnt, cpos, p.cap, nprobe, fbc + 8};
     hipLaunchKernelGGL(fbk, dim3((unsigned)p.ubB), dim3(p.wavesB * 64), 0, st, qi, xbh_ivf, meta_ivf, nq, n, 0, 0, 0, 1,
                        nullptr, nullptr, nullptr, nullptr, isb);
     NRK_CHECK_LAUNCH("screen_kernel (ivf collect)");

@@ -109,6 +109,8 @@ struct IvfScreen {
   int* cand_cnt;           // [nq]
   int* cand_pos;           // [nq][cap] list-major positions
   int cap, nprobe;
+  // screen16 collect: per-XCD work tickets (8 ints, zero at launch)
+  int* ticket;
 };
 
 // MODE 3 block-local candidate staging: hits are appended with LDS atomics and

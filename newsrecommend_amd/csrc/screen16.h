@@ -327,15 +327,28 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_collect_kernel(
   // sub-tile runs in the next tile, after its rows' buffer was refilled
   __shared__ __attribute__((aligned(16))) float nrm[L2 ? 3 * TI : 4];
   __shared__ CL cl;
+  __shared__ int next_item;
 
+  // Work items are split into 8 contiguous ranges, one per XCD (block b runs on
+  // XCD b mod 8), and each XCD's workgroups take its items in order from a
+  // ticket counter: the query tiles of a list chunk start together on one XCD
+  // (the chunk is read once into its L2), and items of uneven cost (partly
+  // filled query tiles, short list tails) balance dynamically.
   const int nblk = gridDim.x, b = blockIdx.x;
-  const int xg = b & 7, jj = b >> 3, q8 = nblk >> 3, r8 = nblk & 7;
-  const int logical0 = (xg < r8 ? xg * (q8 + 1) : r8 * (q8 + 1) + (xg - r8) * q8) + jj;
+  const int nx = nblk >= 8 ? 8 : 1, xg = b % nx;
   const int total = iv.work_off[iv.nlist];
+  const int per = total / nx, rem = total % nx;
+  const int xbeg = xg < rem ? xg * (per + 1) : rem * (per + 1) + (xg - rem) * per;
+  const int xend = xbeg + per + (xg < rem ? 1 : 0);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int q16 = lane & 15, g = lane >> 4;
-  for (int logical = logical0; logical < total; logical += nblk) {
-    if (logical != logical0) __syncthreads();  // the previous item is done with the LDS buffers and staging
+  if (tid == 0) next_item = xbeg + atomicAdd(&iv.ticket[xg], 1);
+  for (;;) {
+    __syncthreads();  // next_item published; the previous item is done with the LDS buffers and staging
+    const int logical = next_item;
+    if (logical >= xend) break;
+    int nxt = 0;  // the following item's ticket, fetched under this item's work
+    if (tid == 0) nxt = xbeg + atomicAdd(&iv.ticket[xg], 1);
     int lo = 0, hi = iv.nlist;  // largest l with work_off[l] <= logical (empty lists own no items)
     while (hi - lo > 1) {
       const int mid = (lo + hi) >> 1;
@@ -583,6 +596,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_collect_kernel(
       const int row = en.x & 1023, dst = cl.base[row] + (en.x >> 10);
       if (dst < iv.cap) iv.cand_pos[(int64_t)cl.qid[row] * iv.cap + dst] = en.y;
     }
+    if (tid == 0) next_item = nxt;  // (every thread read this item's index before its first barrier)
   }
 }
 

@@ -16,9 +16,10 @@ screen_fn pick_screen16_dp128(int qt, int M) {
 }
 
 // IVF collect (MODE 3), two query tiles per wave (256 probing queries per work
-// item, as the 32x32x16 form); L2 on 128-item tiles, inner product on 64-item
-// tiles (its 128-item form spills 8 VGPRs).
+// item, as the 32x32x16 form), 64-item tiles (L2 at configs[3]: 3.04 vs 3.10 ms
+// for 128-item tiles, profiles/r04_ivf_collect16_tiles_chunks.log; the inner
+// product's 128-item form spills).
 screen_fn pick_collect16_dp128(bool l2) {
-  return l2 ? screen16_collect_kernel<128, 2, 4, 128, true> : screen16_collect_kernel<128, 2, 4, 64, false>;
+  return l2 ? screen16_collect_kernel<128, 2, 4, 64, true> : screen16_collect_kernel<128, 2, 4, 64, false>;
 }
 }  // namespace nrk
