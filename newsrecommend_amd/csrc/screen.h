@@ -56,6 +56,45 @@ NRK_BUFFER_LOAD_LDS(16)
 NRK_BUFFER_LOAD_LDS(4)
 #undef NRK_BUFFER_LOAD_LDS
 
+// The same LDS DMA issued from inline assembly.  The compiler tracks a
+// builtin's LDS write and, not knowing which LDS addresses it covers, puts an
+// s_waitcnt vmcnt(0) before the next LDS read of ANY buffer, i.e. right after a
+// tile prefetch it waits for that prefetch to land.  Issued here, the write is
+// invisible to it: the kernel orders the tile's reads itself (an explicit
+// vmcnt wait for that tile's loads, then the workgroup barrier).  The compiler's
+// own vmcnt waits stay correct (they only count the loads it knows of, so
+// they are stricter than needed).
+typedef int __attribute__((ext_vector_type(4))) i32x4;
+__device__ __forceinline__ i32x4 dma_rsrc(const void* base, int bytes) {
+  const uint64_t a = (uint64_t)base;
+  i32x4 r;
+  r.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  r.y = __builtin_amdgcn_readfirstlane((int)((uint32_t)(a >> 32) & 0xffffu));  // stride 0
+  r.z = __builtin_amdgcn_readfirstlane(bytes);                                 // num_records
+  r.w = 0x00020000;
+  return r;
+}
+template <int SIZE>
+__device__ __forceinline__ void dma_lds(const i32x4& r, const void* lds_dst, int vo, int so) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const int la = __builtin_amdgcn_readfirstlane(
+      (int)(uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)lds_dst);
+  const int sof = __builtin_amdgcn_readfirstlane(so);
+  // s_nop 4: the VMEM instruction may read SGPRs a VALU (readfirstlane) just wrote
+  if constexpr (SIZE == 16)
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 4\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                 :: "s"(la), "v"(vo), "s"(r), "s"(sof) : "memory", "m0");
+  else
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 4\n\tbuffer_load_dword %1, %2, %3 offen lds"
+                 :: "s"(la), "v"(vo), "s"(r), "s"(sof) : "memory", "m0");
+#else
+  (void)r;
+  (void)lds_dst;
+  (void)vo;
+  (void)so;
+#endif
+}
+
 // Sorted (descending) insertion into a register list of N entries.  Ties keep
 // the resident entry first (it has the lower id: a lane scans ids upward).
 template <int N>

@@ -290,7 +290,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_kernel(
 // last one holding a real probing query: list segments are padded to the work
 // item's rows, and the padding a wave still computes is now < 16 rows instead of
 // < 32.  L2: scores 2 ip - |x|^2, the rows' norms staged with each tile.
-template <int DP, int QT, int WAVES, int TIL, bool L2, int PD = DP / 32>
+template <int DP, int QT, int WAVES, int TIL, bool L2, int NB = 2>
 __global__ __launch_bounds__(WAVES * 64, 2) void screen16_collect_kernel(
     const uint16_t* __restrict__ qh, const uint16_t* __restrict__ xbh, const float* __restrict__ xmeta, int64_t nq,
     int64_t nb, int64_t chunk, int nch, int nqt, int tstride, float* __restrict__ part_s, int* __restrict__ part_i,
@@ -318,14 +318,18 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_collect_kernel(
   constexpr int WQ = WAVES * 32 * QT;
   static_assert(WQ <= 1024, "collect rows: 10 bits");
   constexpr int BUF = TI * DP;  // uint16 per buffer
-  static_assert(PD >= 1 && PD <= KS2, "prefetch depth");
-  constexpr int NBUF = PD == KS2 ? 2 : 3;
+  // NB tile buffers: at tile it's barrier tile it + NB is issued into tile it's
+  // buffer (its last sub-tile's A fragments are all in registers), NB - 1 tiles
+  // ahead of its use
+  constexpr int PD = KS2;
+  static_assert(NB >= 2 && NB <= 4, "tile buffers");
+  constexpr int NSLOT = NB + 1;
   typedef CollectLds<WQ> CL;
-  __shared__ __attribute__((aligned(16))) uint16_t lds[NBUF * BUF];
-  // L2: the tiles' row norms in a ring of three (tile it in slot it % 3): a
+  __shared__ __attribute__((aligned(16))) uint16_t lds[NB * BUF];
+  // L2: the tiles' row norms in a ring of NB + 1 (tile it in slot it % (NB + 1)): a
   // sub-tile's norms are read at its deferred epilogue, which for a tile's last
   // sub-tile runs in the next tile, after its rows' buffer was refilled
-  __shared__ __attribute__((aligned(16))) float nrm[L2 ? 3 * TI : 4];
+  __shared__ __attribute__((aligned(16))) float nrm[L2 ? NSLOT * TI : 4];
   __shared__ CL cl;
   __shared__ int next_item;
 
@@ -340,7 +344,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_collect_kernel(
   const int per = total / nx, rem = total % nx;
   const int xbeg = xg < rem ? xg * (per + 1) : rem * (per + 1) + (xg - rem) * per;
   const int xend = xbeg + per + (xg < rem ? 1 : 0);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q16 = lane & 15, g = lane >> 4;
   if (tid == 0) next_item = xbeg + atomicAdd(&iv.ticket[xg], 1);
   for (;;) {
@@ -389,8 +393,8 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_collect_kernel(
     if (tid == 0) cl.n = 0;  // ordered before any append by the first tile's barrier
 
     const int64_t cnt = iend - ibeg > 0 ? iend - ibeg : 0;
-    const BufRsrc xrs = make_rsrc(xbh + ibeg * DP, (int)(cnt * DP * 2));
-    const BufRsrc nrs = make_rsrc(xmeta + 2 * ibeg, (int)(cnt * 8));
+    const i32x4 xrs = dma_rsrc(xbh + ibeg * DP, (int)(cnt * DP * 2));
+    const i32x4 nrs = dma_rsrc(xmeta + 2 * ibeg, (int)(cnt * 8));
     const int ntiles = (int)cdiv(cnt, (int64_t)TI);
     // a thread's rows of a tile are NT / CPR apart, a multiple of the swizzle's
     // 16-row period: one vector offset, the rest in the scalar offset
@@ -401,17 +405,34 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_collect_kernel(
       const int soff = it * TI * DP * 2;
 #pragma unroll
       for (int u = 0; u < GPT; ++u)
-        buffer_load_lds16(xrs, lds + buf * BUF + (u * NT + w * 64) * 8, voff, soff + u * (NT / CPR) * DP * 2);
+        dma_lds<16>(xrs, lds + buf * BUF + (u * NT + w * 64) * 8, voff, soff + u * (NT / CPR) * DP * 2);
       if constexpr (L2) {
         if (w == 0) {
-          float* ns = nrm + (it % 3) * TI;
+          float* ns = nrm + (it % NSLOT) * TI;
 #pragma unroll
-          for (int u = 0; u < TI / 64; ++u) buffer_load_lds4(nrs, ns + 64 * u, lane * 8, it * TI * 8 + 512 * u);
+          for (int u = 0; u < TI / 64; ++u) dma_lds<4>(nrs, ns + 64 * u, lane * 8, it * TI * 8 + 512 * u);
         }
       }
     };
     auto afrag = [&](const uint16_t* tl, int row, int s) {
       return *reinterpret_cast<const bf16x8*>(tl + row * DP + 8 * ((4 * s + g) ^ swz<CPR>(row)));
+    };
+    // wait until at most k tiles' DMA (the k issued last) are outstanding
+    auto wait_tiles = [&](int k) __attribute__((always_inline)) {
+      constexpr int LPT = GPT;                        // loads per tile and thread
+      constexpr int LPT0 = GPT + (L2 ? TI / 64 : 0);  // wave 0: + the norms
+      auto wc = [](auto n_c) {
+        constexpr int n = decltype(n_c)::value;  // vmcnt only (expcnt, lgkmcnt at their maxima)
+        __builtin_amdgcn_s_waitcnt((n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8));
+      };
+      if (k <= 0) wc(std::integral_constant<int, 0>{});
+      else if (NB < 3 || k == 1) {
+        if (w == 0) wc(std::integral_constant<int, LPT0>{});
+        else wc(std::integral_constant<int, LPT>{});
+      } else {
+        if (w == 0) wc(std::integral_constant<int, 2 * LPT0>{});
+        else wc(std::integral_constant<int, 2 * LPT>{});
+      }
     };
     // staged append of one candidate (position pos) of half-tile t's query
     auto append = [&](int t, int pos) __attribute__((always_inline)) {
@@ -451,7 +472,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_collect_kernel(
         float n[2][4];  // L2: |x|^2 of the sub-tile's rows 16 ih + 4 g + v
         if constexpr (L2) {
           const int off = pbase >= 0 ? (int)(pbase - ibeg) : 0;  // (nothing pending: any slot)
-          const float* ln = nrm + ((off / TI) % 3) * TI + off % TI + 4 * g;
+          const float* ln = nrm + ((off / TI) % NSLOT) * TI + off % TI + 4 * g;
 #pragma unroll
           for (int ih = 0; ih < 2; ++ih) {
             const float4 x = *reinterpret_cast<const float4*>(ln + 16 * ih);
@@ -532,8 +553,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_collect_kernel(
       };
       auto tile_d = [&](int it, auto buf_c) __attribute__((always_inline)) {
         constexpr int buf = decltype(buf_c)::value;
-        constexpr int nbuf = (buf + 1) % NBUF;
-        constexpr int rbuf = (buf + 2) % NBUF;
+        constexpr int nbuf = (buf + 1) % NB;
         const uint16_t* tl = lds + buf * BUF;
         const int64_t i0 = ibeg + (int64_t)it * TI;
         const int nvalid = (int)((iend - i0) < TI ? (iend - i0) : TI);
@@ -542,28 +562,38 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_collect_kernel(
           sub_tile(std::integral_constant<int, 1>{}, i0, nvalid, tl, tl);
           sub_tile(std::integral_constant<int, 2>{}, i0, nvalid, tl, tl);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        // tile it+1 landed; every wave is done with rbuf and with norm slot (it + 2) % 3
-        // (tile it-1's last epilogue ran in this tile's first sub-tile)
+        // tile it+1 landed (tiles up to it + NB - 1 were issued); every wave is done
+        // with this tile's rows and with norm slot (it + NB) % (NB + 1) (tile it-1's
+        // last epilogue ran in this tile's first sub-tile)
+        wait_tiles(ntiles - 2 - it < NB - 2 ? ntiles - 2 - it : NB - 2);
         __syncthreads();
-        if (it + 2 < ntiles) issue_tile(it + 2, std::integral_constant<int, rbuf>{});
+        if (it + NB < ntiles) issue_tile(it + NB, buf_c);
         sub_tile(std::integral_constant<int, NSUB - 1>{}, i0, nvalid, lds + nbuf * BUF, tl);
       };
       if (ntiles > 0) {
         issue_tile(0, std::integral_constant<int, 0>{});
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (ntiles > 1) issue_tile(1, std::integral_constant<int, 1 % NB>{});
+        if constexpr (NB >= 3) {
+          if (ntiles > 2) issue_tile(2, std::integral_constant<int, 2 % NB>{});
+        }
+        if constexpr (NB >= 4) {
+          if (ntiles > 3) issue_tile(3, std::integral_constant<int, 3 % NB>{});
+        }
+        wait_tiles(ntiles - 1 < NB - 1 ? ntiles - 1 : NB - 1);
         __syncthreads();  // tile 0 landed
-        if (ntiles > 1) issue_tile(1, std::integral_constant<int, 1>{});
 #pragma unroll
         for (int ih = 0; ih < 2; ++ih)
 #pragma unroll
           for (int s = 0; s < PD; ++s) af[ih][s] = afrag(lds, 16 * ih + q16, s);
       }
-      for (int it = 0; it < ntiles; it += NBUF) {
+      for (int it = 0; it < ntiles; it += NB) {
         tile_d(it, std::integral_constant<int, 0>{});
         if (it + 1 < ntiles) tile_d(it + 1, std::integral_constant<int, 1>{});
-        if constexpr (NBUF == 3) {
-          if (it + 2 < ntiles) tile_d(it + 2, std::integral_constant<int, 2 % NBUF>{});
+        if constexpr (NB >= 3) {
+          if (it + 2 < ntiles) tile_d(it + 2, std::integral_constant<int, 2 % NB>{});
+        }
+        if constexpr (NB >= 4) {
+          if (it + 3 < ntiles) tile_d(it + 3, std::integral_constant<int, 3 % NB>{});
         }
       }
       if (baseB >= 0) {  // the last sub-tile's epilogue

@@ -18,8 +18,9 @@ screen_fn pick_screen16_dp128(int qt, int M) {
 // IVF collect (MODE 3), two query tiles per wave (256 probing queries per work
 // item, as the 32x32x16 form), 64-item tiles (L2 at configs[3]: 3.04 vs 3.10 ms
 // for 128-item tiles, profiles/r04_ivf_collect16_tiles_chunks.log; the inner
-// product's 128-item form spills).
+// product's 128-item form spills), three tile buffers (with the DMA issued from
+// inline assembly: 2.70 ms vs 2.80 for two and four, r04_ivf_collect16_nb_ab.log).
 screen_fn pick_collect16_dp128(bool l2) {
-  return l2 ? screen16_collect_kernel<128, 2, 4, 64, true> : screen16_collect_kernel<128, 2, 4, 64, false>;
+  return l2 ? screen16_collect_kernel<128, 2, 4, 64, true, 3> : screen16_collect_kernel<128, 2, 4, 64, false, 3>;
 }
 }  // namespace nrk
