@@ -57,13 +57,15 @@ NRK_BUFFER_LOAD_LDS(4)
 #undef NRK_BUFFER_LOAD_LDS
 
 // The same LDS DMA issued from inline assembly.  The compiler tracks a
-// builtin's LDS write and, not knowing which LDS addresses it covers, puts an
-// s_waitcnt vmcnt(0) before the next LDS read of ANY buffer, i.e. right after a
-// tile prefetch it waits for that prefetch to land.  Issued here, the write is
-// invisible to it: the kernel orders the tile's reads itself (an explicit
-// vmcnt wait for that tile's loads, then the workgroup barrier).  The compiler's
-// own vmcnt waits stay correct (they only count the loads it knows of, so
-// they are stricter than needed).
+// builtin's LDS write; where it cannot tell an LDS read apart from it (the
+// screen16 collect kernel's dynamically indexed norm ring) it puts an s_waitcnt
+// vmcnt(0) before that read, i.e. right after a tile prefetch it waits for the
+// prefetch to land.  Issued here, the write is invisible to it: the kernel
+// orders the tile's reads itself (an explicit vmcnt wait for that tile's loads,
+// then the workgroup barrier).  The compiler's own vmcnt waits stay correct
+// (they only count the loads it knows of, so they are stricter than needed).
+// The flat screen kernels keep the builtin: no such waits there, and the asm
+// form measured slower (0.92 -> 1.32 ms at configs[1], profiles/r04_dma_asm_flat_ab.log).
 typedef int __attribute__((ext_vector_type(4))) i32x4;
 __device__ __forceinline__ i32x4 dma_rsrc(const void* base, int bytes) {
   const uint64_t a = (uint64_t)base;
