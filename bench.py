@@ -281,7 +281,7 @@ def bench_ivf(args, rank, world, dev):
                       "exact_rescore": float(st[2]), "fallback": float(st[3])},
         "fallback_queries": int(index.local.last_fallback.item()),
         "exact_scan_queries": int(index.local.last_exact_scan.item()),
-        "roofline": {"bound": "mfma", "kernel": "screen_kernel MODE 3 (IVF collect, bf16 v_mfma_f32_32x32x16)",
+        "roofline": {"bound": "mfma", "kernel": "screen16_collect_kernel<128, 2, 4, 64, true, 3> (IVF collect, bf16 v_mfma_f32_16x16x32)",
                      "achieved": achieved, "peak": BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / BF16_DENSE_TFLOPS,
                      "traffic": _pmc_traffic(f"ivf:nb={args.ivf_nb},d={d},nq={nq},k={k},nlist={nlist},"
