@@ -2166,7 +2166,9 @@ extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe,
     if (!fa) return fail(NRK_EUNSUPPORTED, "ivf_search: no screen kernel for dp=%d", p.dp);
     IvfScreen isa{work, list_off, seg, sp, nlist, p.chA, p.cmaxA, nullptr, nullptr, nullptr, 0, p.nA};
     hipLaunchKernelGGL(fa, dim3((unsigned)p.ubA), dim3(p.waves * 64), 0, st, qi, xbh_ivf, meta_ivf, nq, n, 0, 0, 0,
-                       2, nullptr, pa, pt, nullptr, isa);  // every other tile: seeds from half the rows (measured +3 %)
+                       3, nullptr, pa, pt, nullptr, isa);  // every third tile: seeds from a third of the rows
+    // (tile strides 2 / 3 / 4 / 6: search 3.49 / 3.46 / 3.48 / 3.50 ms, phase A falling and the
+    // exact rescore of the wider collect rising; profiles/r04_ivf_phaseA_stride_ab.log)
     NRK_CHECK_LAUNCH("screen_kernel (ivf phase A)");
     const int nva = 2 * p.nA * p.cmaxA;
     auto tsel = nva <= 64 ? tau_select_kernel<1> : nva <= 256 ? tau_select_kernel<4> : tau_select_kernel<16>;
