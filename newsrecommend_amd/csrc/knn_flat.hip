@@ -1425,6 +1425,10 @@ static int host_pow2ceil(int n) {
 //                         (the tiled fp64 fallback answers)
 //   NRK_FB_CAP=n          tiled-fallback candidates per slot (tiny: the
 //                         block-per-query exact kernel answers)
+//   NRK_SCREEN16=0        the 32x32x16 kernels for the flat inner-product main
+//                         pass and the IVF collect (test_knn_gpu.py
+//                         ::test_screen_main_pass_forms, test_ivf_gpu.py
+//                         ::test_ivf_collect_forms)
 static int test_hook(const char* name, int dflt) {
   const char* v = getenv(name);
   return v && *v ? atoi(v) : dflt;

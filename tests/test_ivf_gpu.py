@@ -93,6 +93,24 @@ def test_ivf_search_matches_oracle(gpu, metric, d, k, nprobe):
     assert ivf.max_list == int(np.bincount(assign, minlength=50).max())
 
 
+@pytest.mark.parametrize("metric", [ko.METRIC_IP, ko.METRIC_L2])
+@pytest.mark.parametrize("form", ["0", "1"])
+def test_ivf_collect_forms(gpu, monkeypatch, metric, form):
+    """Both phase-B collect kernels give the oracle's result: the 16x16x32
+    screen16_collect_kernel (d = 128, k <= 8; the default) and the 32x32x16
+    screen MODE 3 (NRK_SCREEN16=0, a test hook)."""
+    monkeypatch.setenv("NRK_SCREEN16", form)
+    xq, xb = _mixture(60_000, 700, 128, seed=77 + int(form))
+    ivf = _ivf(xb, 40, metric)
+    ivf.nprobe = 8
+    D, I = ivf.search(xq, 5)
+    cent = ivf.quantizer._xb[:40].cpu().numpy()
+    assign = ivf._assign.cpu().numpy()
+    Do, Io, _, _ = io.ivf_search(xq, xb, cent, assign, 8, 5, metric)
+    np.testing.assert_array_equal(I, Io)
+    np.testing.assert_array_equal(D, Do)
+
+
 def test_ivf_all_lists_equals_flat_and_list_ids(gpu):
     from newsrecommend_amd import faiss as nf
 
