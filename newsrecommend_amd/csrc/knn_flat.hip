@@ -1969,16 +1969,19 @@ static IvfPlan make_ivf_plan(int64_t nq, int nprobe, int nlist, int64_t max_list
   p.nq_pad = (int64_t)p.nqt * p.wq;
   const int64_t ml = max_list > 0 ? max_list : 1;
   const int64_t ch_gib = ((int64_t)1 << 30) / (p.dp * 2) / 64 * 64;  // buffer descriptor range
-  // phase A: the nA nearest lists per query in chunks of ~1024 items (2 lane
+  // phase A: the nA nearest lists per query in chunks of max_list / 128 items (2 lane
   // streams per chunk and query; more streams -> tighter seeds); tau_select
   // takes <= 1024 values per query
   p.nA = nprobe < 2 ? nprobe : 2;
-  // chunks scale with the lists (max_list / 128, in [64, 1024] rows): a
+  // chunks scale with the lists (max_list / 128, in [64, 4096] rows): a
   // corpus shard's short lists (the 8-GPU configs[3]: ~4K rows) otherwise
   // gave ~20 lane maxima per query, weak seeds, a low collect threshold and
   // ~3 % of the queries overflowing into the fp64 scan
+  // (capped at 4096 rows: at configs[3] (max list 213K) 1024-row chunks made ~5-tile
+  // items whose prologues dominated phase A; 0.49 -> 0.41 ms, the exact rescore +0.01
+  // ms; ml / 32 starved the seeds: profiles/r04_ivf_phaseA_chunks_ab.log)
   int64_t chA = (int64_t)align_up((size_t)(ml / 128 > 64 ? ml / 128 : 64), 64);
-  if (chA > 1024) chA = 1024;
+  if (chA > 4096) chA = 4096;
   const int64_t cmax_a = 512 / p.nA;
   if (cdiv(ml, chA) > cmax_a) chA = (int64_t)align_up((size_t)cdiv(ml, cmax_a), 64);
   if (chA > ch_gib) chA = ch_gib;
