@@ -1275,6 +1275,15 @@ __global__ __launch_bounds__(256) void ivf_seed_kernel(const int* __restrict__ s
 
 // IVF phase B: exact rescoring of every collected candidate, top-k.  Queries
 // whose buffer overflowed go to the fallback with threshold (e_k, id).
+constexpr int CR_CW = 16;   // collect_rescore: columns per staging step
+constexpr int CR_MIN = 64;  // ... staged from this many candidates
+// dynamic LDS of collect_rescore_kernel for a candidate capacity and dimension
+static size_t collect_rescore_smem(int cap, int d) {
+  size_t p = 1;
+  while (p < (size_t)cap) p <<= 1;
+  return p * 16 + (size_t)((d + 3) & ~3) * 4 + (size_t)256 * (CR_CW + 4) * 4;
+}
+
 __global__ __launch_bounds__(256) void collect_rescore_kernel(
     const int* __restrict__ cand_cnt, const int* __restrict__ cand_pos, int cap, const int64_t* __restrict__ pos2id,
     const float* __restrict__ xq, const float* __restrict__ xb, int d, int k, int l2,
@@ -1297,17 +1306,60 @@ __global__ __launch_bounds__(256) void collect_rescore_kernel(
   int64_t* id = reinterpret_cast<int64_t*>(g + P);
   float* qs = reinterpret_cast<float*>(id + P);
   for (int i = tid; i < d; i += 256) qs[i] = xq[(int64_t)qi * d + i];
-  __syncthreads();
+  const bool staged = (d & 3) == 0 && c >= CR_MIN;
   for (int i = tid; i < P; i += 256) {
     if (i < c) {
       const int pos = cand_pos[(int64_t)sl * cap + i];
-      const int64_t item = pos2id ? pos2id[pos] : (int64_t)pos;
-      const double sc = exact_score(qs, xb + item * d, d, l2 != 0);
-      g[i] = l2 ? -sc : sc;
-      id[i] = item;
+      id[i] = pos2id ? pos2id[pos] : (int64_t)pos;
     } else {
       g[i] = -INFINITY;
       id[i] = INT64_MAX;
+    }
+  }
+  __syncthreads();
+  if (staged) {
+    // lane = candidate row, fp64 in the oracle's serial order; the rows are
+    // staged through LDS CR_CW columns at a time by coalesced float4 loads
+    // (one lane per candidate row reading it 4 B at a time left every load
+    // instruction touching 256 different rows)
+    float* stg = qs + ((d + 3) & ~3);  // [256][CR_CW + 4]
+    for (int r0 = 0; r0 < c; r0 += 256) {
+      const int nr = c - r0 < 256 ? c - r0 : 256;
+      double acc = 0.0;
+      for (int c0 = 0; c0 < d; c0 += CR_CW) {
+        const int cw = d - c0 < CR_CW ? d - c0 : CR_CW;
+#pragma unroll
+        for (int t = 0; t < CR_CW / 4; ++t) {
+          const int e = tid + 256 * t, row = e / (CR_CW / 4), c4 = e % (CR_CW / 4);
+          if (row < nr && 4 * c4 < cw)
+            *reinterpret_cast<float4*>(stg + row * (CR_CW + 4) + 4 * c4) =
+                *reinterpret_cast<const float4*>(xb + id[r0 + row] * d + c0 + 4 * c4);
+        }
+        __syncthreads();
+        if (tid < nr) {
+          const float* xr = stg + tid * (CR_CW + 4);
+          for (int j = 0; j < cw; j += 4) {
+            const float4 v = *reinterpret_cast<const float4*>(xr + j);
+            const float xv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              if (l2) {
+                const double t = (double)qs[c0 + j + u] - (double)xv[u];
+                acc = fma(t, t, acc);
+              } else {
+                acc = fma((double)qs[c0 + j + u], (double)xv[u], acc);
+              }
+            }
+          }
+        }
+        __syncthreads();
+      }
+      if (tid < nr) g[r0 + tid] = l2 ? -acc : acc;
+    }
+  } else {
+    for (int i = tid; i < c; i += 256) {
+      const double sc = exact_score(qs, xb + id[i] * d, d, l2 != 0);
+      g[i] = l2 ? -sc : sc;
     }
   }
   __syncthreads();
@@ -1887,7 +1939,7 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
     screen_fn fc = pick_screen(p.dp, 1, p.M, l2 != 0, 3);
     if (!fc) return fail(NRK_EUNSUPPORTED, "knn_flat: no collect kernel for dp=%d", p.dp);
     IvfScreen isc{cwork, clo, cseg, csp, 1, p.cch, (int)cdiv(nb, (int64_t)p.cch), cthr, ccnt, cpos, p.ccap, 1};
-    const size_t smem = (size_t)host_pow2ceil(p.ccap) * 16 + (size_t)d * 4;
+    const size_t smem = collect_rescore_smem(p.ccap, d);
     const int rounds = (int)cdiv(nq, (int64_t)FB_SLOTS_MAX);
     for (int r = 0; r < rounds; ++r) {  // each round exits at once when it has no queries
       hipLaunchKernelGGL(flat_collect_plan_kernel, dim3(1), dim3(1024), 0, st, fb, nq, nb, p.cwq, p.cch, qmeta, stats,
@@ -2210,7 +2262,7 @@ extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe,
   {
     if (force_fb && n > 0 && hipMemsetAsync(ccnt, 0x7f, (size_t)nq * 4, st) != hipSuccess)  // testing: overflow all
       return fail(NRK_ELAUNCH, "ivf_search: memset failed");
-    const size_t smem = (size_t)host_pow2ceil(p.cap) * 16 + (size_t)d * 4;
+    const size_t smem = collect_rescore_smem(p.cap, d);
     hipLaunchKernelGGL(collect_rescore_kernel, dim3((unsigned)nq), dim3(256), smem, st, ccnt, cpos, p.cap, pos2id, xq,
                        xb, d, k, l2, lbg, lbi, D, I, S, id_offset, fb);
     NRK_CHECK_LAUNCH("collect_rescore_kernel");
