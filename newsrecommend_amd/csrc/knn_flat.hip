@@ -1212,7 +1212,10 @@ __device__ __forceinline__ float collect_threshold(double ek, const double* __re
   const double Xh = stats[0], Rr = stats[1], NX = stats[2];
   const double gam = (double)dp * 0x1p-22;
   const double bip = gam * nqh * Xh + nqh * Rr + nrq * Xh + nrq * Rr;
-  const double B = l2 ? 2.0 * bip + 0x1p-21 * (NX + nqh * Xh) : bip;
+  // L2: + dp 2^-23 NX for screens whose accumulators start at -|x|^2 / 2
+  // (screen16_collect_kernel): up to dp fp32 roundings of a running value that
+  // holds half the row norm, doubled with the score
+  const double B = l2 ? 2.0 * bip + 0x1p-21 * (NX + nqh * Xh) + (double)dp * 0x1p-23 * NX : bip;
   double t = (l2 ? qn2 + ek : ek) - B;
   t -= 1e-9 * (fabs(t) + fabs(ek) + qn2 + B);
   float f = (float)t;

@@ -289,7 +289,10 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_kernel(
 // deferred epilogue.  A wave runs the MFMAs of its 16-query half-tiles up to the
 // last one holding a real probing query: list segments are padded to the work
 // item's rows, and the padding a wave still computes is now < 16 rows instead of
-// < 32.  L2: scores 2 ip - |x|^2, the rows' norms staged with each tile.
+// < 32.  L2: the accumulators start at -|x|^2 / 2 (the rows' norms are staged
+// with each tile), so they end at s / 2 for the score s = 2 ip - |x|^2 and the
+// epilogue compares them with half the threshold (collect_threshold's bound
+// covers the roundings of the norm inside the MFMA chain).
 template <int DP, int QT, int WAVES, int TIL, bool L2, int NB = 2>
 __global__ __launch_bounds__(WAVES * 64, 2) void screen16_collect_kernel(
     const uint16_t* __restrict__ qh, const uint16_t* __restrict__ xbh, const float* __restrict__ xmeta, int64_t nq,
@@ -326,9 +329,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_collect_kernel(
   constexpr int NSLOT = NB + 1;
   typedef CollectLds<WQ> CL;
   __shared__ __attribute__((aligned(16))) uint16_t lds[NB * BUF];
-  // L2: the tiles' row norms in a ring of NB + 1 (tile it in slot it % (NB + 1)): a
-  // sub-tile's norms are read at its deferred epilogue, which for a tile's last
-  // sub-tile runs in the next tile, after its rows' buffer was refilled
+  // L2: the tiles' row norms in a ring of NB + 1 slots (tile it in slot it % (NB + 1))
   __shared__ __attribute__((aligned(16))) float nrm[L2 ? NSLOT * TI : 4];
   __shared__ CL cl;
   __shared__ int next_item;
@@ -382,7 +383,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_collect_kernel(
       for (int s = 0; s < KS2; ++s) qf[t][s] = src[4 * s];
       const int pair = iv.slot_pair[gr];
       const int qy = pair >= 0 ? pair / iv.nprobe : -1;
-      cthr[t] = pair >= 0 ? iv.thr_q[qy] : INFINITY;
+      cthr[t] = pair >= 0 ? (L2 ? 0.5f : 1.f) * iv.thr_q[qy] : INFINITY;  // (L2: scores held halved)
       if (g == 0) {
         cl.qid[row] = qy;
         cl.qcnt[row] = 0;
@@ -467,29 +468,20 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_collect_kernel(
             for (int v = 0; v < 4; ++v)
               if (16 * ih + 4 * g + v >= nv) pa[t][ih][v] = -INFINITY;
       };
-      auto tree = [&](f32x4 (&pa)[NQ2][2], int64_t pbase, float (&m2)[NQ2][2], float (&m)[NQ2])
-          __attribute__((always_inline)) {
-        float n[2][4];  // L2: |x|^2 of the sub-tile's rows 16 ih + 4 g + v
-        if constexpr (L2) {
-          const int off = pbase >= 0 ? (int)(pbase - ibeg) : 0;  // (nothing pending: any slot)
-          const float* ln = nrm + ((off / TI) % NSLOT) * TI + off % TI + 4 * g;
+      // L2: -|x|^2 / 2 of the next chain's rows 16 ih + 4 g + v (its accumulators' start)
+      f32x4 ninit[2];
+      auto load_ninit = [&](const float* ns, int row0) __attribute__((always_inline)) {
 #pragma unroll
-          for (int ih = 0; ih < 2; ++ih) {
-            const float4 x = *reinterpret_cast<const float4*>(ln + 16 * ih);
-            n[ih][0] = x.x;
-            n[ih][1] = x.y;
-            n[ih][2] = x.z;
-            n[ih][3] = x.w;
-          }
+        for (int ih = 0; ih < 2; ++ih) {
+          const float4 x = *reinterpret_cast<const float4*>(ns + row0 + 16 * ih + 4 * g);
+          ninit[ih] = f32x4{-0.5f * x.x, -0.5f * x.y, -0.5f * x.z, -0.5f * x.w};
         }
+      };
+      auto tree = [&](f32x4 (&pa)[NQ2][2], float (&m2)[NQ2][2], float (&m)[NQ2]) __attribute__((always_inline)) {
 #pragma unroll
         for (int t = 0; t < NA; ++t) {
 #pragma unroll
           for (int ih = 0; ih < 2; ++ih) {
-            if constexpr (L2) {
-#pragma unroll
-              for (int v = 0; v < 4; ++v) pa[t][ih][v] = fmaf(2.f, pa[t][ih][v], -n[ih][v]);
-            }
             m2[t][ih] = fmax_ieee(fmax_ieee(pa[t][ih][0], pa[t][ih][1]), fmax_ieee(pa[t][ih][2], pa[t][ih][3]));
           }
           m[t] = fmax_ieee(m2[t][0], m2[t][1]);
@@ -515,8 +507,8 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_collect_kernel(
           }
         }
       };
-      auto sub_tile = [&](auto st_c, int64_t i0, int nvalid, const uint16_t* next_tl, const uint16_t* cur_tl)
-          __attribute__((always_inline)) {
+      auto sub_tile = [&](auto st_c, int64_t i0, int nvalid, const uint16_t* next_tl, const uint16_t* cur_tl,
+                          const float* cur_ns, const float* next_ns) __attribute__((always_inline)) {
         constexpr int st = decltype(st_c)::value;
         constexpr int par = st & 1;
         f32x4(&cur)[NQ2][2] = par ? accB : accA;
@@ -533,13 +525,21 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_collect_kernel(
 #pragma unroll
             for (int t = 0; t < NA; ++t)
               cur[t][ih] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ih][s % PD], qf[t][s],
-                                                                   s == 0 ? zero : cur[t][ih], 0, 0, 0);
+                                                                   s == 0 ? (L2 ? ninit[ih] : zero) : cur[t][ih], 0, 0, 0);
             if (s + PD < KS2) af[ih][s % PD] = afrag(cur_tl, 32 * st + 16 * ih + q16, s + PD);
             else af[ih][s % PD] = afrag(next_tl, nrow + 16 * ih, s + PD - KS2);
           }
         }
+        // the next chain's norms: this tile's next sub-tile, or the next tile's first
+        // (landed: the last sub-tile runs after the tile barrier)
+        if constexpr (L2) {
+          if constexpr (st + 1 < NSUB) load_ninit(cur_ns, 32 * (st + 1));
+          else load_ninit(next_ns, 0);
+        }
+        (void)cur_ns;
+        (void)next_ns;
         float m2[NQ2][2], m[NQ2];
-        tree(pend, pbase, m2, m);
+        tree(pend, m2, m);
 #pragma unroll
         for (int t = 0; t < NA; ++t) m[t] = pbase >= 0 ? m[t] : -INFINITY;  // nothing pending: drain is a no-op
         drain(pend, pbase, m2, m);
@@ -557,18 +557,20 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_collect_kernel(
         const uint16_t* tl = lds + buf * BUF;
         const int64_t i0 = ibeg + (int64_t)it * TI;
         const int nvalid = (int)((iend - i0) < TI ? (iend - i0) : TI);
-        sub_tile(std::integral_constant<int, 0>{}, i0, nvalid, tl, tl);
+        const float* ns = nrm + (it % NSLOT) * TI;            // (L2 only)
+        const float* nns = nrm + ((it + 1) % NSLOT) * TI;
+        sub_tile(std::integral_constant<int, 0>{}, i0, nvalid, tl, tl, ns, nns);
         if constexpr (NSUB == 4) {
-          sub_tile(std::integral_constant<int, 1>{}, i0, nvalid, tl, tl);
-          sub_tile(std::integral_constant<int, 2>{}, i0, nvalid, tl, tl);
+          sub_tile(std::integral_constant<int, 1>{}, i0, nvalid, tl, tl, ns, nns);
+          sub_tile(std::integral_constant<int, 2>{}, i0, nvalid, tl, tl, ns, nns);
         }
         // tile it+1 landed (tiles up to it + NB - 1 were issued); every wave is done
         // with this tile's rows and with norm slot (it + NB) % (NB + 1) (tile it-1's
-        // last epilogue ran in this tile's first sub-tile)
+        // norms were last read before this tile)
         wait_tiles(ntiles - 2 - it < NB - 2 ? ntiles - 2 - it : NB - 2);
         __syncthreads();
         if (it + NB < ntiles) issue_tile(it + NB, buf_c);
-        sub_tile(std::integral_constant<int, NSUB - 1>{}, i0, nvalid, lds + nbuf * BUF, tl);
+        sub_tile(std::integral_constant<int, NSUB - 1>{}, i0, nvalid, lds + nbuf * BUF, tl, ns, nns);
       };
       if (ntiles > 0) {
         issue_tile(0, std::integral_constant<int, 0>{});
@@ -581,6 +583,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_collect_kernel(
         }
         wait_tiles(ntiles - 1 < NB - 1 ? ntiles - 1 : NB - 1);
         __syncthreads();  // tile 0 landed
+        if constexpr (L2) load_ninit(nrm, 0);
 #pragma unroll
         for (int ih = 0; ih < 2; ++ih)
 #pragma unroll
@@ -599,7 +602,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_collect_kernel(
       if (baseB >= 0) {  // the last sub-tile's epilogue
         if (nvB < 32) mask_rows(accB, nvB);
         float m2[NQ2][2], m[NQ2];
-        tree(accB, baseB, m2, m);
+        tree(accB, m2, m);
         drain(accB, baseB, m2, m);
       }
     };
