@@ -111,6 +111,26 @@ def test_ivf_collect_forms(gpu, monkeypatch, metric, form):
     np.testing.assert_array_equal(D, Do)
 
 
+@pytest.mark.parametrize("metric", [ko.METRIC_IP, ko.METRIC_L2])
+@pytest.mark.parametrize("force", ["0", "1"])
+def test_ivf_collect16_small_lists(gpu, monkeypatch, metric, force):
+    """The 16x16x32 collect (d = 128, k <= 8) on lists of a few dozen rows (one
+    partial 64-row tile per chunk), a few probing queries per list (work items
+    with 1-3 active half-tiles) and, with NRK_FORCE_FALLBACK=1, every query's
+    candidate buffer overflowed into the IVF-aware fallback."""
+    monkeypatch.setenv("NRK_FORCE_FALLBACK", force)
+    xq, xb = _mixture(3_000, 50, 128, seed=91, centers=16)
+    ivf = _ivf(xb, 40, metric)
+    ivf.nprobe = 3
+    D, I = ivf.search(xq, 5)
+    Do, Io, _, _ = io.ivf_search(xq, xb, ivf.quantizer._xb[:40].cpu().numpy(), ivf._assign.cpu().numpy(), 3, 5,
+                                 metric)
+    np.testing.assert_array_equal(I, Io)
+    np.testing.assert_array_equal(D, Do)
+    if force == "1":
+        assert int(ivf.last_fallback.item()) == 50
+
+
 def test_ivf_all_lists_equals_flat_and_list_ids(gpu):
     from newsrecommend_amd import faiss as nf
 
