@@ -437,7 +437,7 @@ def bench_e2e(args, rank, world, dev):
     xb = clustered_corpus(n, d, seed=1234, device=dev)
     index = ShardedIndexFlat(d, 0, device=dev)
     index.add_full(xb)
-    table = xb.to(torch.bfloat16)  # the DIN item table: the same embeddings, bf16 (full copy on every rank)
+    table = xb  # the DIN item table: the same fp32 embeddings (embedding_generate.py:119-122), on every rank
     n1 = bench_n1(args, rank, world, dev, index, xb) if not args.no_n1 else None
     del xb
     torch.cuda.empty_cache()
@@ -484,8 +484,9 @@ def bench_e2e(args, rank, world, dev):
             rerank(model, table, hist[ulo:uhi], cand)
         torch.cuda.synchronize()
     t3 = time.perf_counter()
-    rr = _rerank_roofline(kt.mean_ms("rerank"), hist[ulo:uhi], cand, d, 128, L,
-                          f"rerank:e2e,users={uhi - ulo},C={kr + 1},d={d},gpus={world}")
+    rr = _rerank_roofline(kt.mean_ms("rerank"), kt.mean_ms("rerank_project"), hist[ulo:uhi], d, 128, 32, L,
+                          f"rerank:e2e,users={uhi - ulo},C={kr + 1},d={d},gpus={world}", table.element_size(),
+                          n_samples=float(cand.shape[0] * cand.shape[1]), proj_rows=cand.numel())
     out = {
         "metric": "end-to-end users/s (retrieve top-200 + DIN re-rank + NDCG@5)", "value": U * args.steps / el,
         "unit": "users/s", "ms_per_step": el / args.steps * 1e3,
@@ -495,9 +496,10 @@ def bench_e2e(args, rank, world, dev):
                                    f"user-shard{world} re-rank") if world > 1 else "single GPU"},
         "stages_ms": {"retrieve": (t2 - t1) / 3 * 1e3, "rerank": (t3 - t2) / 3 * 1e3},
         "rerank_samples_per_step": int((uhi - ulo) * (kr + 1)),
-        "rerank_kernel_ms": kt.mean_ms("rerank"), "rerank_path": __import__(
-            "newsrecommend_amd.pipeline", fromlist=["rerank"]).rerank.path, "rerank_roofline": rr["hbm"],
-        "rerank_valu": rr["valu"], "table_dtype": "bf16 (the corpus rows rounded once; fp32 corpora: DESIGN.md Parity)",
+        "rerank_kernel_ms": kt.mean_ms("rerank"), "rerank_project_ms": kt.mean_ms("rerank_project"),
+        "rerank_path": __import__("newsrecommend_amd.pipeline", fromlist=["rerank"]).rerank.path,
+        "rerank_roofline": rr["hbm"], "rerank_valu": rr["valu"], "rerank_project_roofline": rr["proj"],
+        "table_dtype": str(table.dtype).replace("torch.", ""),
         "ndcg_at_5_mean_rank0": float(nd.mean().item()),
         "fallback_queries": int(index.local.last_fallback.item()),
         "exact_scan_queries": int(index.local.last_exact_scan.item()),
@@ -521,39 +523,41 @@ def bench_e2e(args, rank, world, dev):
     return out
 
 
-def _rerank_roofline(ms, hist, cand, d, A, L, key, n_samples=None, proj=None):
-    """Roofline of the fused re-rank launch (nrk_din_rerank): ALGORITHMIC bytes
-    = per candidate its bf16 row (2d), id and logit (8 B), per user its L ids
-    and nv history rows (2d each); VALU work = 2 lane-ops (add, |.|-fma) per
-    (candidate, scored row, attention unit), scored rows = nv + 1 padding row
-    when nv < L, against the 78.6 T lane-op/s of the fp32 vector peak
-    (157.3 TFLOP/s counting an fma as 2).  proj = (F, list items): shared lists
-    projected once (nrk_din_rerank_project: each item's bf16 row in, A + F f32
-    out) and scored from the projections (4 (A + F) + 8 B per candidate)."""
+def _rerank_roofline(ms, ms_proj, hist, d, A, F, L, key, es, n_samples, proj_rows):
+    """Rooflines of the re-rank (nrk_din_rerank_project(_hist) +
+    nrk_din_rerank_projected), ALGORITHMIC bytes:
+      main kernel: per scored candidate its projection [U' | Q1] (4 (A + F) B),
+        id and logit (8 B); per user its L ids and the projections of its nv
+        valid history rows;
+      projections: per projected candidate row its table row (es * d B), id
+        and projection out; per history slot its id and projection out, plus
+        the nv valid rows;
+    VALU work of the main kernel = 2 lane-ops (add, |.|-fma) per (candidate,
+    scored row, attention unit), scored rows = nv + 1 padding row when nv < L,
+    against the 78.6 T lane-op/s of the fp32 vector peak (157.3 TFLOP/s
+    counting an fma as 2).  es: table element size (4: the reference's f32)."""
     nv = (hist >= 0).sum(1).double()
     nr = nv + (nv < L).double()
-    if cand is not None:
-        per_user = torch.full_like(nv, float(cand.shape[1]))
-        n_samples = float(cand.shape[1] * cand.shape[0])
-        ops = float((per_user * nr).sum()) * A * 2
-    else:
-        ops = n_samples * float(nr.mean()) * A * 2
-    per_c = 2 * d + 8 if proj is None else 4 * (A + proj[0]) + 8
-    byt = n_samples * per_c + float((4 * L + 2 * d * nv).sum())
-    kern = f"din_rerank_kernel<{d}, {A}, 32>"
-    if proj is not None:
-        byt += proj[1] * (2 * d + 4 + 4 * (A + proj[0]))
-        kern = f"din_rerank_project_kernel<{d}, {A}, 32> + " + kern + " (projected shared lists)"
+    U = hist.shape[0]
+    ops = n_samples * float(nr.mean()) * A * 2
+    pw = 4 * (A + F)
+    byt = n_samples * (pw + 8) + float((4 * L + pw * nv).sum())
+    byt_p = proj_rows * (es * d + 4 + pw) + U * L * (4 + pw) + float(nv.sum()) * es * d
+    kern = f"din_rerank_kernel<.., {A}, {F}, PROJ> (projected)"
     sec = ms * 1e-3
     gbs = byt / sec / 1e9
+    gbs_p = byt_p / (ms_proj * 1e-3) / 1e9 if ms_proj > 0 else 0.0
     return {"hbm": {"bound": "hbm", "binding": "valu (the scoring; see valu)", "kernel": kern, "achieved": gbs,
                     "peak": HBM_GBS, "unit": "GB/s", "frac": gbs / HBM_GBS, "traffic": _pmc_traffic(key),
-                    "algorithmic": f"{byt:.4g} B per launch ({per_c} B per candidate + the users' ids and history "
-                                   f"rows{' + the list projections' if proj is not None else ''}), {ms:.3f} ms "
-                                   f"(HIP events)"},
+                    "algorithmic": f"{byt:.4g} B per launch ({pw + 8} B per candidate + the users' ids and history "
+                                   f"projections), {ms:.3f} ms (HIP events, the main kernel alone)"},
             "valu": {"achieved": ops / sec / 1e12, "peak": 78.6, "unit": "T lane-ops/s",
                      "frac": ops / sec / 1e12 / 78.6,
-                     "algorithmic": f"{ops:.4g} lane-ops (2 per candidate x scored row x unit)"}}
+                     "algorithmic": f"{ops:.4g} lane-ops (2 per candidate x scored row x unit)"},
+            "proj": {"bound": "hbm", "kernel": f"din_rerank_project_kernel<{d}, {es == 4}> (candidates + history)",
+                     "achieved": gbs_p, "peak": HBM_GBS, "unit": "GB/s", "frac": gbs_p / HBM_GBS,
+                     "algorithmic": f"{byt_p:.4g} B ({proj_rows} candidate rows + {U * L} history slots: "
+                                    f"{es * d} B row in, {pw} B out), {ms_proj:.3f} ms (HIP events)"}}
 
 
 def bench_retrieval_flow(args, rank, world, dev):
@@ -575,7 +579,7 @@ def bench_retrieval_flow(args, rank, world, dev):
     n, d, nlist, L = 364_047, 256, 300, 64
     U = args.flow_users
     xb = clustered_corpus(n, d, seed=1234, device=dev)
-    table = xb.to(torch.bfloat16)
+    table = xb  # the reference's fp32 article embeddings (embedding_generate.py:119-122)
     barrier(world)
     t0 = time.perf_counter()
     clustering = nf.Clustering(d, nlist)
@@ -616,7 +620,7 @@ def bench_retrieval_flow(args, rank, world, dev):
     el = max_over_ranks(time.perf_counter() - t0, world, dev)
     from newsrecommend_amd.din import KernelTimer
 
-    with KernelTimer() as kt:  # the fused launch alone, outside the timed region
+    with KernelTimer() as kt:  # the re-rank kernels, outside the timed region
         stage()
         torch.cuda.synchronize()
     sizes = torch.diff(cluster_off)
@@ -625,15 +629,16 @@ def bench_retrieval_flow(args, rank, world, dev):
     out = {"metric": "Retrieval.py -> evaluate() users/s (whole-cluster candidates)", "value": U / el,
            "unit": "users/s", "ms": el * 1e3, "build_s": build_s,
            "config": f"{n}x{d} corpus, Clustering(k={nlist}, niter=80) + IndexHNSWFlat(M=32) assignment, {U} users, "
-                     f"whole nearest cluster + GT appended, DIN(256, 128, 32), L={L}, bf16 table",
+                     f"whole nearest cluster + GT appended, DIN(256, 128, 32), L={L}, {table.dtype} table",
            "cluster_size_min_mean_max": [int(sizes.min()), float(sizes.double().mean()), int(sizes.max())],
            "candidates_per_user_mean": float(cand_per_user.mean()),
            "rerank_samples_per_s": float(cand_per_user.sum()) * world / el,
-           "rerank_kernel_ms": kt.mean_ms("rerank"),
-           "rerank_roofline": _rerank_roofline(kt.mean_ms("rerank"), hist[lo:hi], None, d, 128, L,
-                                               f"rerank:flow,users={hi - lo},gpus={world}",
-                                               n_samples=float(cand_per_user.sum()) + (hi - lo),
-                                               proj=(32, int(xb.shape[0]) + (hi - lo)))["hbm"],
+           "rerank_kernel_ms": kt.mean_ms("rerank"), "rerank_project_ms": kt.mean_ms("rerank_project"),
+           "table_dtype": str(table.dtype).replace("torch.", ""),
+           **{k_: v_ for k_, v_ in zip(("rerank_roofline", "rerank_valu", "rerank_project_roofline"), _rerank_roofline(
+               kt.mean_ms("rerank"), kt.mean_ms("rerank_project"), hist[lo:hi], d, 128, 32, L,
+               f"rerank:flow,users={hi - lo},gpus={world}", table.element_size(),
+               n_samples=float(cand_per_user.sum()) + (hi - lo), proj_rows=int(xb.shape[0]) + (hi - lo)).values())},
            "rerank_path": __import__("newsrecommend_amd.pipeline", fromlist=["rerank"]).rerank.path,
            "ndcg_at_5_mean_rank0": float(res["ndcg"].mean()), "loss_mean_rank0": float(res["loss"].mean())}
     del xb, table, index, centroid_index

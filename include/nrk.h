@@ -203,7 +203,7 @@ int nrk_din_batch_u(const float* q, int32_t B, int32_t d, const float* W1, const
  * eval-mode logits of every candidate of every user, each candidate attending
  * over its user's history (`his.expand(C, -1, -1)`, DIN.py:166-173), in ONE
  * launch that writes only the logits.
- *   table [N][d] bf16 item embeddings; hist [nU][L] int32 history rows (-1 or
+ *   table [N][d] bf16 item embeddings (f32: the projected form below); hist [nU][L] int32 history rows (-1 or
  *   >= n_table = a zero padding slot: DIN.py:84-86, 108 softmaxes over all L);
  *   user u's candidates: cand[cand_off[u] .. cand_off[u] + cand_len[u]) int32
  *   rows, then extra[u] when extra != NULL (the appended ground truth of
@@ -234,25 +234,35 @@ int nrk_din_rerank(const void* table, int64_t n_table, int32_t dtype, const int3
                    const int32_t* cand, const int64_t* cand_off, const int32_t* cand_len, const int32_t* extra,
                    const int64_t* out_off, float* out, int32_t d, int32_t A, int32_t F,
                    const nrk_din_rerank_params* params, void* ws, size_t ws_bytes, void* stream);
-/* Shared candidate lists (the flow: every user of a cluster scores the same
- * list).  The candidate half of the attention MLP and of the head's first
- * Linear depends on the item alone, so such a list is projected once:
- *   out [n][A + F] f32 = [ U'(rows[i]) = w2 . (W1q q + b1) in the kernel's
- *   slice order (A) | Q1(rows[i]) = H1q q (F) ], q = table[rows[i]] (a zero row
- *   when rows[i] is outside [0, N)),
- * with the MFMA sequence nrk_din_rerank applies per candidate, and
- * nrk_din_rerank_projected then stages those instead of the rows:
- * cand_proj [.][A + F] parallel to cand, extra_proj [nU][A + F] (extra's
- * projections; required when extra != NULL).  cand / extra still decide which
- * candidates are valid.  Logits are bit-identical to nrk_din_rerank's. */
+/* Projected form (shared candidate lists, and every f32 table).  The
+ * candidate half of the attention MLP and of the head's first Linear depends
+ * on the item alone, and the key half on the history row alone, so rows are
+ * projected once:
+ *   nrk_din_rerank_project: out [n][A + F] f32 = [ U'(q) = w2 . (W1q q + b1)
+ *   in the kernel's slice order (A) | Q1(q) = H1q q (F) ], q = table[rows[i]];
+ *   nrk_din_rerank_project_hist: out [n][A + F] f32 = [ P'(k) = w2 . (W1k k)
+ *   (slice order) | R(k) = H1p k ], k = table[rows[i]] (rows = hist [nU][L]
+ *   flattened, so out is per history slot);
+ * a zero row where rows[i] is outside [0, N).  table: bf16 (the MFMA sequence
+ * nrk_din_rerank applies, so logits stay bit-identical to its) or f32 (each
+ * element split into bf16 hi + lo, three products: the reference's fp32
+ * embeddings, embedding_generate.py:119-122 / DIN.py:45-56, to ~2^-16).
+ * nrk_din_rerank_projected then stages projections instead of rows and never
+ * reads the table (any dtype): cand_proj [.][A + F] parallel to cand,
+ * extra_proj [nU][A + F] (required when extra != NULL), hist_proj
+ * [nU * L][A + F] (required).  cand / extra / hist still decide validity. */
 int nrk_din_rerank_project(const void* table, int64_t n_table, int32_t dtype, const int32_t* rows, int64_t n,
                            int32_t d, int32_t A, int32_t F, const nrk_din_rerank_params* params, float* out,
                            void* stream);
+int nrk_din_rerank_project_hist(const void* table, int64_t n_table, int32_t dtype, const int32_t* rows, int64_t n,
+                                int32_t d, int32_t A, int32_t F, const nrk_din_rerank_params* params, float* out,
+                                void* stream);
 int nrk_din_rerank_projected(const void* table, int64_t n_table, int32_t dtype, const int32_t* hist, int32_t nU,
                              int32_t L, const int32_t* cand, const int64_t* cand_off, const int32_t* cand_len,
                              const int32_t* extra, const int64_t* out_off, float* out, int32_t d, int32_t A,
                              int32_t F, const nrk_din_rerank_params* params, const float* cand_proj,
-                             const float* extra_proj, void* ws, size_t ws_bytes, void* stream);
+                             const float* extra_proj, const float* hist_proj, void* ws, size_t ws_bytes,
+                             void* stream);
 /* evaluate()'s per-user tail over re-rank logits (DIN.py:176-189): user u's
  * logits are [seg_off[u], seg_off[u+1]); pos[u] the index of its positive
  * (-1: none); prob = sigmoid(logits) as the caller computes it.  Writes the f64
@@ -295,9 +305,11 @@ int nrk_kmeans_update(const float* x, int32_t d, const int64_t* list_off, const 
  *   list_off / pos2id / pos2list from nrk_group_by_list; max_list = largest list.
  * Result: the exact top-k (same order and ties as nrk_knn_flat) among the
  * items of the probed lists.  Outputs and stage_events as nrk_knn_flat
- * (stage 0 = query prepare + grouping by list); n_fallback[0] = n_fallback[1] =
- * queries whose collect buffer overflowed (or that had fewer than k seeds),
- * answered by the fp64 scan of their probed lists. */
+ * (stage 0 = query prepare + grouping by list); n_fallback[0] = queries whose
+ * collect buffer overflowed (or that had fewer than k seeds), answered by the
+ * tiled fp64 scan of their probed lists; n_fallback[1] = of those, the queries
+ * that scan's candidate buffer could not hold either, answered by the
+ * block-per-query fp64 scan (the slow path). */
 int nrk_ivf_search_workspace(int64_t nq, int32_t nprobe, int32_t nlist, int64_t max_list,
                              int32_t d, int32_t k, size_t* ws_bytes);
 int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe, int32_t nprobe,

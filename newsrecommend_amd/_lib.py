@@ -71,8 +71,9 @@ SIGNATURES = {
     "nrk_din_rerank": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_i32, c_i32,
                                       c_i32, c_p, c_p, c_size, c_p]),
     "nrk_din_rerank_project": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_i64, c_i32, c_i32, c_i32, c_p, c_p, c_p]),
+    "nrk_din_rerank_project_hist": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_i64, c_i32, c_i32, c_i32, c_p, c_p, c_p]),
     "nrk_din_rerank_projected": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p,
-                                                c_i32, c_i32, c_i32, c_p, c_p, c_p, c_p, c_size, c_p]),
+                                                c_i32, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_size, c_p]),
     "nrk_rerank_user_stats": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_i32, c_p, c_p, c_p, c_p]),
     "nrk_gather_rows": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_i64, c_i32, c_p, c_p]),
     "nrk_train_samples": (ctypes.c_int, [c_p, c_i64, c_p, c_i64, c_i32, c_p, c_i64, c_p, c_p, c_p, c_p]),

@@ -78,9 +78,13 @@ struct RerankArgs {
   int F;
   int* queue;  // user counter, zero at launch
   // projected candidates (PROJ): [U' (A) | Q1 (F)] f32 per candidate, cproj
-  // parallel to cand, xproj [nU] for the extras (nrk_din_rerank_project)
+  // parallel to cand, xproj [nU] for the extras (nrk_din_rerank_project), and
+  // the history projected per slot: hproj [nU][L] x [P' (A) | R (F)] f32
+  // (nrk_din_rerank_project_hist).  The PROJ kernel never reads the table, so
+  // it serves bf16 and f32 tables alike.
   const float* cproj;
   const float* xproj;
+  const float* hproj;
 };
 
 // LDS image of 64 rows of D bf16: 16-B chunks XOR-swizzled by row, so the
@@ -125,9 +129,8 @@ struct Lds {  // byte offsets
     hsp = p + LP * G::PRS * 4;                 // SP / 2 [LP] f32
     rt = hsp + LP * 4;                         // R^T hi, lo [F][LP] bf16
     q = rt + 2 * F * LP * 2;                   // candidate / history image [64][D] bf16;  S [CH][SST] f32 later
-                                               // (PROJ: history image, then the chunk's Q1 [CH][F] f32)
-    int qb = CH * D * 2 > CH * SST * 4 ? CH * D * 2 : CH * SST * 4;
-    if (PROJ && CH * F * 4 > qb) qb = CH * F * 4;
+                                               // (PROJ: the chunk's Q1 [CH][F] f32; there is no row image)
+    const int qb = PROJ ? CH * F * 4 : (CH * D * 2 > CH * SST * 4 ? CH * D * 2 : CH * SST * 4);
     us = q + qb;                               // U' [CH][A] f32;  h1 [CH][F + 4] f32 later
     const int ub = CH * G::PRS * 4 > CH * (F + 4) * 4 ? CH * G::PRS * 4 : CH * (F + 4) * 4;
     ms = us + ub;                              // {m, sum} of the two row groups [2][2][CH] f32
@@ -355,12 +358,53 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
     }
     if (tid < CH) cv[tid] = valid_id(vid);
   };
+  // PROJ: a user's history arrives projected ([P' | R] per slot, from hproj):
+  // the compacted valid slots' projections go through the same registers as a
+  // chunk's (the next user is staged only after the last chunk's were stored),
+  // rows from nv on are zero (the shared padding row and the MFMA's K padding)
+  static_assert(CH == LP, "din_rerank: a chunk and a history hold the same row count");
+  auto issue_hist_proj = [&](int u_, int hid, uint64_t& vm_) __attribute__((always_inline)) {
+    vm_ = __ballot(lane < a.L && hid >= 0 && hid < a.n_table);
+    const int nv_ = __popcll(vm_);
+#pragma unroll
+    for (int k = 0; k < NEP; ++k) {
+      const int e = tid + NT * k, row = e / CPX, part = e % CPX;
+      stp[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < LP * CPX && row < nv_)
+        stp[k] = *reinterpret_cast<const float4*>(a.hproj + ((int64_t)u_ * a.L + nth_set_bit(vm_, row)) * (A + F) +
+                                                  4 * part);
+    }
+  };
+  auto store_hist_proj = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < NEP; ++k) {
+      const int e = tid + NT * k, row = e / CPX, part = e % CPX;
+      if (e < LP * CPX) {
+        if (part < A / 4) {
+          *reinterpret_cast<float4*>(Pp + row * PRS + 4 * part) = stp[k];  // (already in the slice order)
+        } else {
+          const int f0 = 4 * (part - A / 4);
+          const float v[4] = {stp[k].x, stp[k].y, stp[k].z, stp[k].w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            short h, l;
+            split_bf16(v[j], h, l);
+            Rth[(f0 + j) * LP + row] = (uint16_t)h;
+            Rtl[(f0 + j) * LP + row] = (uint16_t)l;
+          }
+        }
+      }
+    }
+  };
 
   if (tid == 0) qslot[0] = atomicAdd(a.queue, 1);
   __syncthreads();
   int u = qslot[0];
   uint64_t vm = 0;
-  if (u < a.nU) issue_hist(load_hid(u), vm);
+  if (u < a.nU) {
+    if constexpr (PROJ) issue_hist_proj(u, load_hid(u), vm);
+    else issue_hist(load_hid(u), vm);
+  }
 
   while (u < a.nU) {
     refresh();
@@ -371,8 +415,9 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
     const int ctot = clen + (a.extra ? 1 : 0);
     const int nchunk = (ctot + CH - 1) / CH;
     const int64_t ooff = a.out_off[u];
-    __syncthreads();  // the previous user's last chunk is done with the image region
-    store_rows();     // history rows -> image
+    __syncthreads();  // the previous user's last chunk is done with the image region (PROJ: with P', R)
+    if constexpr (PROJ) store_hist_proj();  // [P' | R] -> LDS
+    else store_rows();                      // history rows -> image
     if (tid == 0) qslot[1] = atomicAdd(a.queue, 1);  // the next user (read after chunk 0's first barrier)
     __syncthreads();
     if (nchunk > 0) {
@@ -384,7 +429,8 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
     // Tile t = (unit tile t / nrt, row tile t % nrt); wave w takes the
     // contiguous range [w ntile / 8, (w + 1) ntile / 8), so it reads the B
     // fragments (hi + lo, from L2) of at most two or three unit tiles.
-    {
+    // (PROJ: staged above, with this MFMA sequence, by nrk_din_rerank_project_hist)
+    if constexpr (!PROJ) {
       const int nrt = nrp / 16, ntile = (NUT + NFT) * nrt;
       const int t0 = (w * ntile) >> 3, t1 = ((w + 1) * ntile) >> 3;
       auto load_frags = [&](int uti, bf16x8(&fh)[KSD], bf16x8(&fl)[KSD]) __attribute__((always_inline)) {
@@ -537,7 +583,7 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
         }
       }
       if constexpr (PROJ) {
-        if (nxt_h) issue_hist(hid, vm);  // (U', Q1 were published by the barrier above)
+        if (nxt_h) issue_hist_proj(un, hid, vm);  // (U', Q1 were published by the barrier above)
       } else {
         if (nxt_c) issue_rows();
         else if (nxt_h) issue_hist(hid, vm);
@@ -785,7 +831,10 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
     }
     if (nchunk == 0) {  // nothing to score: the next user's history still has to be staged
       un = qslot[1];
-      if (un < a.nU) issue_hist(load_hid(un), vm);
+      if (un < a.nU) {
+        if constexpr (PROJ) issue_hist_proj(un, load_hid(un), vm);
+        else issue_hist(load_hid(un), vm);
+      }
     }
     u = un;
   }
@@ -799,66 +848,6 @@ int launch(const RerankArgs& a, hipStream_t st) {
   hipLaunchKernelGGL((din_rerank_kernel<D, A, F, PROJ>), dim3(grid), dim3(NT), (size_t)l.total, st, a);
   NRK_CHECK_LAUNCH("din_rerank_kernel");
   return NRK_OK;
-}
-
-// ---- item projections for shared candidate lists (nrk_din_rerank_project):
-// phase 1 of the main kernel for a list of rows, with its MFMA order, so a
-// projected candidate scores bit for bit as one staged from its row.  64 rows
-// per 256-thread block; wave w takes the unit tiles w, w + 4, ... of
-// [W1q ; H1q] (fragments from L2) over the block's four candidate tiles.
-struct ProjArgs {
-  const uint16_t* table;
-  int64_t n_table;
-  const int32_t* rows;
-  int64_t n;
-  const uint16_t *W1q_hi, *W1q_lo, *H1q_hi, *H1q_lo;
-  const float *b1, *w2;
-  float* out;  // [n][A + F]: U' in the kernel's slice order, then Q1
-};
-
-template <int D, int A, int F>
-__global__ __launch_bounds__(256) void din_rerank_project_kernel(ProjArgs a) {
-  using G = Geo<D, A>;
-  constexpr int CPR = D / 8, KSD = D / 32, NUT = A / 16, NFT = F / 16;
-  __shared__ __attribute__((aligned(16))) unsigned char img[CH * D * 2];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l15 = lane & 15, l4 = lane >> 4;
-  const int64_t r0 = (int64_t)blockIdx.x * CH;
-  for (int e = tid; e < CH * CPR; e += 256) {
-    const int row = e / CPR, cc = e % CPR;
-    const int id = r0 + row < a.n ? a.rows[r0 + row] : -1;
-    bf16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (id >= 0 && id < a.n_table) v = *reinterpret_cast<const bf16x8*>(a.table + (int64_t)id * D + 8 * cc);
-    *reinterpret_cast<bf16x8*>(img + img_off<D>(row, cc)) = v;
-  }
-  __syncthreads();
-  for (int t = w; t < NUT + NFT; t += 4) {
-    const bool isU = t < NUT;
-    const int urow = isU ? 16 * t + l15 : 16 * (t - NUT) + l15;
-    const uint16_t* bh = (isU ? a.W1q_hi : a.H1q_hi) + (int64_t)urow * D + 8 * l4;
-    const uint16_t* bl = (isU ? a.W1q_lo : a.H1q_lo) + (int64_t)urow * D + 8 * l4;
-    bf16x8 fh[KSD], fl[KSD];
-#pragma unroll
-    for (int s = 0; s < KSD; ++s) {
-      fh[s] = *reinterpret_cast<const bf16x8*>(bh + 32 * s);
-      fl[s] = *reinterpret_cast<const bf16x8*>(bl + 32 * s);
-    }
-    const float b1u = isU ? a.b1[urow] : 0.f, w2u = isU ? a.w2[urow] : 0.f;
-    const int oc = isU ? G::col(urow) : A + urow;
-    for (int ct = 0; ct < 4; ++ct) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < KSD; ++s) {
-        const bf16x8 af = *reinterpret_cast<const bf16x8*>(img + img_off<D>(16 * ct + l15, 4 * s + l4));
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, fl[s], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, fh[s], acc, 0, 0, 0);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int64_t row = r0 + 16 * ct + 4 * l4 + i;
-        if (row < a.n) a.out[row * (A + F) + oc] = isU ? w2u * (acc[i] + b1u) : acc[i];
-      }
-    }
-  }
 }
 
 template <int D, int A, bool PROJ>
@@ -881,32 +870,147 @@ int launch_a(int A, const RerankArgs& a, hipStream_t st) {
   }
 }
 
-template <int D, int A, int F>
+// ---- row projections (nrk_din_rerank_project / _project_hist): the
+// row-only halves of the re-rank, so that the main kernel (PROJ) reads
+// projections instead of table rows.
+//   candidates: [U' = w2 . (W1q q + b1) (A, slice order) | Q1 = H1q q (F)]
+//   history slots: [P' = w2 . (W1k k) (A, slice order) | R = H1p k (F)]
+// For a bf16 table this is the main kernel's own MFMA sequence (acc += a.Wlo,
+// acc += a.Whi per k-step), so its logits stay bit-identical; an f32 table is
+// split per element into bf16 hi + lo (16 mantissa bits) and enters as
+// acc += lo.Whi, acc += hi.Wlo, acc += hi.Whi (the lo.lo product, 2^-16 of the
+// others, is the only term dropped).  64 rows per 256-thread block; wave w
+// takes the unit tiles w, w + 4, ... of [Wa ; Wb] (fragments from L2) over the
+// block's four 16-row tiles.
+struct ProjArgs {
+  const void* table;
+  int64_t n_table;
+  const int32_t* rows;
+  int64_t n;
+  const uint16_t *Wa_hi, *Wa_lo, *Wb_hi, *Wb_lo;  // [A][d], [F][d]
+  const float *b1, *w2;                           // b1: null for the history (P' has no bias)
+  int A, F;
+  float* out;  // [n][A + F]
+};
+
+// Geo<D, A>::col with A at run time
+__device__ __forceinline__ int slice_col(int n, int A) {
+  const int SL = A / 8, sj = n / SL, w = n % SL;
+  const int p4 = SL == 16 ? ((w >> 2) + 2 * (sj >> 2)) & 3 : (w >> 2);
+  return sj * SL + 4 * p4 + (w & 3);
+}
+
+template <int D, bool F32>
+__global__ __launch_bounds__(256) void din_rerank_project_kernel(ProjArgs a) {
+  constexpr int CPR = D / 8, KSD = D / 32;
+  extern __shared__ __attribute__((aligned(16))) unsigned char pimg[];  // hi image [CH][D] bf16 (+ lo image)
+  unsigned char* iml = pimg + CH * D * 2;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l15 = lane & 15, l4 = lane >> 4;
+  const int64_t r0 = (int64_t)blockIdx.x * CH;
+  // every id, then every row load in flight before the first is used (a
+  // load -> split -> store loop would expose one HBM latency per chunk)
+  constexpr int NPT = CH * CPR / 256;  // 16-B (bf16) / 32-B (f32) chunks per thread
+  int ids[NPT];
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    const int row = (tid + 256 * k) / CPR;
+    ids[k] = r0 + row < a.n ? a.rows[r0 + row] : -1;
+  }
+  if constexpr (F32) {
+    f32x4 x0[NPT], x1[NPT];
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      const int cc = (tid + 256 * k) % CPR;
+      x0[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+      x1[k] = x0[k];
+      if (ids[k] >= 0 && ids[k] < a.n_table) {
+        const f32x4* src = reinterpret_cast<const f32x4*>(static_cast<const float*>(a.table) + (int64_t)ids[k] * D + 8 * cc);
+        x0[k] = __builtin_nontemporal_load(src);
+        x1[k] = __builtin_nontemporal_load(src + 1);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      const int e = tid + 256 * k, row = e / CPR, cc = e % CPR;
+      const float xv[8] = {x0[k][0], x0[k][1], x0[k][2], x0[k][3], x1[k][0], x1[k][1], x1[k][2], x1[k][3]};
+      bf16x8 h, l;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        short hj, lj;
+        split_bf16(xv[j], hj, lj);
+        h[j] = hj;
+        l[j] = lj;
+      }
+      *reinterpret_cast<bf16x8*>(pimg + img_off<D>(row, cc)) = h;
+      *reinterpret_cast<bf16x8*>(iml + img_off<D>(row, cc)) = l;
+    }
+  } else {
+    bf16x8 v[NPT];
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      const int cc = (tid + 256 * k) % CPR;
+      v[k] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (ids[k] >= 0 && ids[k] < a.n_table)
+        v[k] = __builtin_nontemporal_load(
+            reinterpret_cast<const bf16x8*>(static_cast<const uint16_t*>(a.table) + (int64_t)ids[k] * D + 8 * cc));
+    }
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      const int e = tid + 256 * k, row = e / CPR, cc = e % CPR;
+      *reinterpret_cast<bf16x8*>(pimg + img_off<D>(row, cc)) = v[k];
+    }
+  }
+  __syncthreads();
+  const int NUT = a.A / 16, NFT = a.F / 16, AF = a.A + a.F;
+  for (int t = w; t < NUT + NFT; t += 4) {
+    const bool isA = t < NUT;
+    const int urow = isA ? 16 * t + l15 : 16 * (t - NUT) + l15;
+    const uint16_t* bh = (isA ? a.Wa_hi : a.Wb_hi) + (int64_t)urow * D + 8 * l4;
+    const uint16_t* bl = (isA ? a.Wa_lo : a.Wb_lo) + (int64_t)urow * D + 8 * l4;
+    bf16x8 fh[KSD], fl[KSD];
+#pragma unroll
+    for (int s = 0; s < KSD; ++s) {
+      fh[s] = *reinterpret_cast<const bf16x8*>(bh + 32 * s);
+      fl[s] = *reinterpret_cast<const bf16x8*>(bl + 32 * s);
+    }
+    const float b1u = isA && a.b1 ? a.b1[urow] : 0.f, w2u = isA ? a.w2[urow] : 0.f;
+    const int oc = isA ? slice_col(urow, a.A) : a.A + urow;
+#pragma unroll 1  // (unrolled, the compiler hoists all four tiles' A fragments: 1 wave per SIMD at d = 256)
+    for (int ct = 0; ct < 4; ++ct) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KSD; ++s) {
+        const int o = img_off<D>(16 * ct + l15, 4 * s + l4);
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(pimg + o);
+        if constexpr (F32) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(iml + o), fh[s], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, fl[s], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, fh[s], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t row = r0 + 16 * ct + 4 * l4 + i;
+        // (candidates: w2 (acc + b1), as the main kernel forms U'; history:
+        // w2 acc, as it forms P' -- b1u is 0 there)
+        if (row < a.n) a.out[row * AF + oc] = isA ? w2u * (a.b1 ? acc[i] + b1u : acc[i]) : acc[i];
+      }
+    }
+  }
+}
+
+template <int D, bool F32>
 int launch_proj(const ProjArgs& a, hipStream_t st) {
   const int64_t grid = (a.n + CH - 1) / CH;
-  hipLaunchKernelGGL((din_rerank_project_kernel<D, A, F>), dim3((unsigned)grid), dim3(256), 0, st, a);
+  const size_t lds = (size_t)CH * D * 2 * (F32 ? 2 : 1);
+  hipLaunchKernelGGL((din_rerank_project_kernel<D, F32>), dim3((unsigned)grid), dim3(256), lds, st, a);
   NRK_CHECK_LAUNCH("din_rerank_project_kernel");
   return NRK_OK;
 }
 
-template <int D, int A>
-int launch_proj_f(int F, const ProjArgs& a, hipStream_t st) {
-  switch (F) {
-    case 32: return launch_proj<D, A, 32>(a, st);
-    case 64: return launch_proj<D, A, 64>(a, st);
-    case 96: return launch_proj<D, A, 96>(a, st);
-    default: return launch_proj<D, A, 128>(a, st);
-  }
-}
-
-template <int D>
-int launch_proj_a(int A, int F, const ProjArgs& a, hipStream_t st) {
-  switch (A) {
-    case 32: return launch_proj_f<D, 32>(F, a, st);
-    case 64: return launch_proj_f<D, 64>(F, a, st);
-    case 96: return launch_proj_f<D, 96>(F, a, st);
-    default: return launch_proj_f<D, 128>(F, a, st);
-  }
+template <bool F32>
+int launch_proj_d(int d, const ProjArgs& a, hipStream_t st) {
+  if (d == 256) return launch_proj<256, F32>(a, st);
+  if (d == 128) return launch_proj<128, F32>(a, st);
+  return launch_proj<64, F32>(a, st);
 }
 
 // ---- the evaluate() tail per user (DIN.py:176-189 as pipeline.rerank_clusters
@@ -920,7 +1024,8 @@ __global__ __launch_bounds__(256) void user_stats_kernel(const float* __restrict
                                                          double* __restrict__ loss_sum, int64_t* __restrict__ nval,
                                                          int64_t* __restrict__ before) {
   const int u = blockIdx.x, tid = threadIdx.x;
-  const int64_t lo = seg[u], hi = seg[u + 1], ps = pos[u];
+  const int64_t lo = seg[u], hi = seg[u + 1];
+  const int64_t ps = pos[u] >= lo && pos[u] < hi ? pos[u] : -1;  // (a position outside the user's logits: none)
   const float pp = ps >= 0 ? prob[ps] : 0.f;
   double ls = 0.0;
   int64_t nv = 0, nb = 0;
@@ -971,9 +1076,11 @@ extern "C" int nrk_din_rerank_workspace(size_t* ws_bytes) {
 static int rerank_impl(const void* table, int64_t n_table, int32_t dtype, const int32_t* hist, int32_t nU,
                        int32_t L, const int32_t* cand, const int64_t* cand_off, const int32_t* cand_len,
                        const int32_t* extra, const int64_t* out_off, float* out, int32_t d, int32_t A, int32_t F,
-                       const nrk_din_rerank_params* p, const float* cand_proj, const float* extra_proj, void* ws,
-                       size_t ws_bytes, void* stream) {
-  NRK_CHECK_ARG(dtype == NRK_DTYPE_BF16, "din_rerank: the table must be bf16");
+                       const nrk_din_rerank_params* p, const float* cand_proj, const float* extra_proj,
+                       const float* hist_proj, void* ws, size_t ws_bytes, void* stream) {
+  // (the projected form never reads the table: any dtype)
+  NRK_CHECK_ARG(cand_proj || dtype == NRK_DTYPE_BF16, "din_rerank: the table must be bf16 (f32: the projected form)");
+  NRK_CHECK_ARG(dtype == NRK_DTYPE_BF16 || dtype == NRK_DTYPE_F32, "din_rerank: bad table dtype %d", dtype);
   NRK_CHECK_ARG(d == 64 || d == 128 || d == 256, "din_rerank: emb_dim %d unsupported (64, 128, 256)", d);
   NRK_CHECK_ARG(A >= 32 && A <= 128 && A % 32 == 0, "din_rerank: attn_units %d unsupported (32..128 step 32)", A);
   NRK_CHECK_ARG(F >= 32 && F <= 128 && F % 32 == 0, "din_rerank: fc_units %d unsupported (32..128 step 32)", F);
@@ -985,6 +1092,7 @@ static int rerank_impl(const void* table, int64_t n_table, int32_t dtype, const 
                     p->H1p_hi && p->H1p_lo && p->c1 && p->H2_hi && p->H2_lo && p->c2 && p->h3,
                 "din_rerank: null parameter pointer");
   NRK_CHECK_ARG(!extra || !cand_proj || extra_proj, "din_rerank_projected: extra without extra_proj");
+  NRK_CHECK_ARG(!cand_proj || hist_proj, "din_rerank_projected: null hist_proj");
   if (ws_bytes < 256) return fail(NRK_EWORKSPACE, "din_rerank: workspace %zu < 256", ws_bytes);
   hipStream_t st = (hipStream_t)stream;
   if (hipMemsetAsync(ws, 0, 4, st) != hipSuccess) return fail(NRK_ELAUNCH, "din_rerank: memset failed");
@@ -1020,11 +1128,8 @@ static int rerank_impl(const void* table, int64_t n_table, int32_t dtype, const 
   a.queue = static_cast<int*>(ws);
   a.cproj = cand_proj;
   a.xproj = extra_proj;
-  if (cand_proj) {
-    if (d == 256) return rr::launch_a<256, true>(A, a, st);
-    if (d == 128) return rr::launch_a<128, true>(A, a, st);
-    return rr::launch_a<64, true>(A, a, st);
-  }
+  a.hproj = hist_proj;
+  if (cand_proj) return rr::launch_a<64, true>(A, a, st);  // (the projected kernel does not depend on d)
   if (d == 256) return rr::launch_a<256, false>(A, a, st);
   if (d == 128) return rr::launch_a<128, false>(A, a, st);
   return rr::launch_a<64, false>(A, a, st);
@@ -1035,47 +1140,61 @@ extern "C" int nrk_din_rerank(const void* table, int64_t n_table, int32_t dtype,
                               const int32_t* extra, const int64_t* out_off, float* out, int32_t d, int32_t A, int32_t F,
                               const nrk_din_rerank_params* p, void* ws, size_t ws_bytes, void* stream) {
   return rerank_impl(table, n_table, dtype, hist, nU, L, cand, cand_off, cand_len, extra, out_off, out, d, A, F, p,
-                     nullptr, nullptr, ws, ws_bytes, stream);
+                     nullptr, nullptr, nullptr, ws, ws_bytes, stream);
 }
 
 extern "C" int nrk_din_rerank_projected(const void* table, int64_t n_table, int32_t dtype, const int32_t* hist,
                                         int32_t nU, int32_t L, const int32_t* cand, const int64_t* cand_off,
                                         const int32_t* cand_len, const int32_t* extra, const int64_t* out_off,
                                         float* out, int32_t d, int32_t A, int32_t F, const nrk_din_rerank_params* p,
-                                        const float* cand_proj, const float* extra_proj, void* ws, size_t ws_bytes,
-                                        void* stream) {
+                                        const float* cand_proj, const float* extra_proj, const float* hist_proj,
+                                        void* ws, size_t ws_bytes, void* stream) {
   NRK_CHECK_ARG(cand_proj, "din_rerank_projected: null cand_proj");
   return rerank_impl(table, n_table, dtype, hist, nU, L, cand, cand_off, cand_len, extra, out_off, out, d, A, F, p,
-                     cand_proj, extra_proj, ws, ws_bytes, stream);
+                     cand_proj, extra_proj, hist_proj, ws, ws_bytes, stream);
+}
+
+static int project_impl(const char* what, bool hist, const void* table, int64_t n_table, int32_t dtype,
+                        const int32_t* rows, int64_t n, int32_t d, int32_t A, int32_t F, const nrk_din_rerank_params* p,
+                        float* out, void* stream) {
+  NRK_CHECK_ARG(dtype == NRK_DTYPE_BF16 || dtype == NRK_DTYPE_F32, "%s: table dtype %d unsupported (bf16, f32)", what,
+                dtype);
+  NRK_CHECK_ARG(d == 64 || d == 128 || d == 256, "%s: emb_dim %d unsupported (64, 128, 256)", what, d);
+  NRK_CHECK_ARG(A >= 32 && A <= 128 && A % 32 == 0, "%s: attn_units %d unsupported", what, A);
+  NRK_CHECK_ARG(F >= 32 && F <= 128 && F % 32 == 0, "%s: fc_units %d unsupported", what, F);
+  NRK_CHECK_ARG(n >= 0, "%s: bad row count", what);
+  if (n == 0) return NRK_OK;
+  NRK_CHECK_ARG(n <= (int64_t)UINT32_MAX * rr::CH, "%s: %lld rows: too many for one launch", what, (long long)n);
+  NRK_CHECK_ARG(table && rows && p && out && p->w2, "%s: null pointer", what);
+  rr::ProjArgs a;
+  a.table = table;
+  a.n_table = n_table;
+  a.rows = rows;
+  a.n = n;
+  a.Wa_hi = static_cast<const uint16_t*>(hist ? p->W1k_hi : p->W1q_hi);
+  a.Wa_lo = static_cast<const uint16_t*>(hist ? p->W1k_lo : p->W1q_lo);
+  a.Wb_hi = static_cast<const uint16_t*>(hist ? p->H1p_hi : p->H1q_hi);
+  a.Wb_lo = static_cast<const uint16_t*>(hist ? p->H1p_lo : p->H1q_lo);
+  a.b1 = hist ? nullptr : p->b1;
+  a.w2 = p->w2;
+  a.A = A;
+  a.F = F;
+  a.out = out;
+  NRK_CHECK_ARG(a.Wa_hi && a.Wa_lo && a.Wb_hi && a.Wb_lo && (hist || a.b1), "%s: null parameter pointer", what);
+  hipStream_t st = (hipStream_t)stream;
+  return dtype == NRK_DTYPE_F32 ? rr::launch_proj_d<true>(d, a, st) : rr::launch_proj_d<false>(d, a, st);
 }
 
 extern "C" int nrk_din_rerank_project(const void* table, int64_t n_table, int32_t dtype, const int32_t* rows, int64_t n,
                                       int32_t d, int32_t A, int32_t F, const nrk_din_rerank_params* p, float* out,
                                       void* stream) {
-  NRK_CHECK_ARG(dtype == NRK_DTYPE_BF16, "din_rerank_project: the table must be bf16");
-  NRK_CHECK_ARG(d == 64 || d == 128 || d == 256, "din_rerank_project: emb_dim %d unsupported (64, 128, 256)", d);
-  NRK_CHECK_ARG(A >= 32 && A <= 128 && A % 32 == 0, "din_rerank_project: attn_units %d unsupported", A);
-  NRK_CHECK_ARG(F >= 32 && F <= 128 && F % 32 == 0, "din_rerank_project: fc_units %d unsupported", F);
-  NRK_CHECK_ARG(n >= 0, "din_rerank_project: bad row count");
-  if (n == 0) return NRK_OK;
-  NRK_CHECK_ARG(table && rows && p && out && p->W1q_hi && p->W1q_lo && p->H1q_hi && p->H1q_lo && p->b1 && p->w2,
-                "din_rerank_project: null pointer");
-  rr::ProjArgs a;
-  a.table = static_cast<const uint16_t*>(table);
-  a.n_table = n_table;
-  a.rows = rows;
-  a.n = n;
-  a.W1q_hi = static_cast<const uint16_t*>(p->W1q_hi);
-  a.W1q_lo = static_cast<const uint16_t*>(p->W1q_lo);
-  a.H1q_hi = static_cast<const uint16_t*>(p->H1q_hi);
-  a.H1q_lo = static_cast<const uint16_t*>(p->H1q_lo);
-  a.b1 = p->b1;
-  a.w2 = p->w2;
-  a.out = out;
-  hipStream_t st = (hipStream_t)stream;
-  if (d == 256) return rr::launch_proj_a<256>(A, F, a, st);
-  if (d == 128) return rr::launch_proj_a<128>(A, F, a, st);
-  return rr::launch_proj_a<64>(A, F, a, st);
+  return project_impl("din_rerank_project", false, table, n_table, dtype, rows, n, d, A, F, p, out, stream);
+}
+
+extern "C" int nrk_din_rerank_project_hist(const void* table, int64_t n_table, int32_t dtype, const int32_t* rows,
+                                           int64_t n, int32_t d, int32_t A, int32_t F, const nrk_din_rerank_params* p,
+                                           float* out, void* stream) {
+  return project_impl("din_rerank_project_hist", true, table, n_table, dtype, rows, n, d, A, F, p, out, stream);
 }
 
 extern "C" int nrk_rerank_user_stats(const float* logits, const float* prob, const int64_t* seg_off, const int64_t* pos,

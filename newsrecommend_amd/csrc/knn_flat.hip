@@ -2285,8 +2285,9 @@ extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe,
   int rc = exact_launch(xq, nq, xb, n, d, k, l2, ovl, fbc + 1, 256, D, I, S, id_offset, st, ivf);
   if (rc != NRK_OK) return rc;
   mark(4);
-  if (n_fallback && (hipMemcpyAsync(n_fallback, fbc, 4, hipMemcpyDeviceToDevice, st) != hipSuccess ||
-                     hipMemcpyAsync(n_fallback + 1, fbc, 4, hipMemcpyDeviceToDevice, st) != hipSuccess))
+  // [0] the tiled fp64 scan's queries (collect overflow / too few seeds), [1] of
+  // those, the ones its buffer could not hold either (the block-per-query scan)
+  if (n_fallback && hipMemcpyAsync(n_fallback, fbc, 8, hipMemcpyDeviceToDevice, st) != hipSuccess)
     return fail(NRK_ELAUNCH, "ivf_search: copy of fallback counts failed");
   return NRK_OK;
 }

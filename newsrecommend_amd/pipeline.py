@@ -23,6 +23,7 @@ from __future__ import annotations
 
 import ctypes
 import warnings
+import weakref
 
 import numpy as np
 import torch
@@ -84,7 +85,7 @@ def _split_bf16(w: torch.Tensor):
     return hi.contiguous(), (w - hi.float()).to(torch.bfloat16).contiguous()
 
 
-_PARAMS_CACHE: dict = {}
+_PARAMS_CACHE: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()  # model -> (key, params)
 
 
 def rerank_params(model, d: int):
@@ -93,13 +94,15 @@ def rerank_params(model, d: int):
     its three BatchNorms folded into the Linears after them (_fold_eval_head);
     every weight the kernel feeds to a bf16 MFMA split into hi + lo.  Returns
     (params struct, A, F, tensors kept alive) or None when the head has no
-    running statistics.  Cached per model until any parameter or buffer
-    changes (torch's version counters)."""
+    running statistics.  Cached per model (weakly: a dropped model frees its
+    copies) until any parameter or buffer changes (torch's version counters;
+    inference-mode tensors have none, so such a model is not cached)."""
     from . import _lib
 
     tens = list(model.parameters()) + list(model.buffers())
-    key = (id(model), tuple(t._version for t in tens), tuple(t.data_ptr() for t in tens))
-    hit = _PARAMS_CACHE.get(id(model))
+    cacheable = not any(t.is_inference() for t in tens)
+    key = (tuple(t._version for t in tens), tuple(t.data_ptr() for t in tens)) if cacheable else None
+    hit = _PARAMS_CACHE.get(model) if cacheable else None
     if hit is not None and hit[0] == key:
         return hit[1]
     head = _fold_eval_head(model.fc)
@@ -118,14 +121,28 @@ def rerank_params(model, d: int):
     keep["h3"] = H3.detach().reshape(-1).float().contiguous()
     prm = _lib.RerankParams(**{k: v.data_ptr() for k, v in keep.items()}, c3=float(c3.detach().reshape(-1)[0]))
     out = (prm, W1.shape[0], H1.shape[0], keep)
-    _PARAMS_CACHE[id(model)] = (key, out)
+    if cacheable:
+        _PARAMS_CACHE[model] = (key, out)
     return out
 
 
-def rerank_project(model, table: torch.Tensor, rows: torch.Tensor, prm=None) -> torch.Tensor:
+def _table_dtype(table: torch.Tensor) -> int:
+    from . import _lib
+
+    if table.dtype == torch.bfloat16:
+        return _lib.NRK_DTYPE_BF16
+    if table.dtype == torch.float32:
+        return _lib.NRK_DTYPE_F32
+    raise ValueError(f"re-rank: item table dtype {table.dtype} (bf16 or f32)")
+
+
+def rerank_project(model, table: torch.Tensor, rows: torch.Tensor, prm=None, hist: bool = False) -> torch.Tensor:
     """nrk_din_rerank_project: the candidate-only part of the re-rank for each
     row, [U' (A) | Q1 (F)] f32, with the arithmetic nrk_din_rerank applies per
-    candidate (a shared list is projected once instead of once per user)."""
+    candidate (a shared list is projected once instead of once per user).
+    hist: nrk_din_rerank_project_hist, the history-only part [P' (A) | R (F)]
+    of each row.  An f32 table enters split into bf16 hi + lo (the reference's
+    fp32 embeddings to ~2^-16)."""
     from . import _lib
 
     d = table.shape[1]
@@ -134,9 +151,10 @@ def rerank_project(model, table: torch.Tensor, rows: torch.Tensor, prm=None) -> 
     p, A, F, _keep = prm
     r = rows.to(torch.int32).contiguous()
     out = torch.empty((r.numel(), A + F), dtype=torch.float32, device=table.device)
-    _lib.check(_lib.load().nrk_din_rerank_project(_lib.ptr(table), table.shape[0], _lib.NRK_DTYPE_BF16, _lib.ptr(r),
-                                                  r.numel(), d, A, F, ctypes.byref(p), _lib.ptr(out),
-                                                  _lib.stream(table.device)), "din_rerank_project")
+    lib = _lib.load()
+    fn = lib.nrk_din_rerank_project_hist if hist else lib.nrk_din_rerank_project
+    _lib.check(fn(_lib.ptr(table), table.shape[0], _table_dtype(table), _lib.ptr(r), r.numel(), d, A, F, ctypes.byref(p),
+                  _lib.ptr(out), _lib.stream(table.device)), "din_rerank_project" + ("_hist" if hist else ""))
     return out
 
 
@@ -149,8 +167,11 @@ def rerank_ragged(model, table: torch.Tensor, hist_rows: torch.Tensor, cand: tor
     out[out_off[u] + c]; rows outside the table get -inf.  Returns out (n_out,)
     f32 (entries not covered by any user stay uninitialised).  shared: the
     lists are shared by many users (the flow's clusters): cand and extra are
-    projected once (rerank_project) and nrk_din_rerank_projected scores the
-    projections; the logits are bit-identical either way."""
+    projected once (rerank_project), the histories per slot, and
+    nrk_din_rerank_projected scores the projections; for a bf16 table the
+    logits are bit-identical either way.  An f32 table (the reference's own
+    embeddings) always takes the projected form: the projections split its rows
+    into bf16 hi + lo."""
     from . import _lib
 
     dev = table.device
@@ -173,15 +194,20 @@ def rerank_ragged(model, table: torch.Tensor, hist_rows: torch.Tensor, cand: tor
     ex = extra.to(torch.int32).contiguous() if extra is not None else None
     from .din import KernelTimer
 
-    t0 = KernelTimer.mark("rerank")  # (the projections included)
-    if shared:
+    if shared or table.dtype == torch.float32:
+        tp = KernelTimer.mark("rerank_project")
         cp = rerank_project(model, table, c, prm)
         xp = rerank_project(model, table, ex, prm) if ex is not None else None
-        _lib.check(lib.nrk_din_rerank_projected(_lib.ptr(table), table.shape[0], _lib.NRK_DTYPE_BF16, _lib.ptr(h), U, L,
+        hp = rerank_project(model, table, h.reshape(-1), prm, hist=True)
+        KernelTimer.push("rerank_project", tp)
+        t0 = KernelTimer.mark("rerank")  # (the main kernel alone)
+        _lib.check(lib.nrk_din_rerank_projected(_lib.ptr(table), table.shape[0], _table_dtype(table), _lib.ptr(h), U, L,
                                                 _lib.ptr(c), _lib.ptr(co), _lib.ptr(cl), _lib.ptr(ex), _lib.ptr(oo),
                                                 _lib.ptr(out), d, A, F, ctypes.byref(p), _lib.ptr(cp), _lib.ptr(xp),
-                                                _lib.ptr(ws), ws.numel(), _lib.stream(dev)), "din_rerank_projected")
+                                                _lib.ptr(hp), _lib.ptr(ws), ws.numel(), _lib.stream(dev)),
+                   "din_rerank_projected")
     else:
+        t0 = KernelTimer.mark("rerank")
         _lib.check(lib.nrk_din_rerank(_lib.ptr(table), table.shape[0], _lib.NRK_DTYPE_BF16, _lib.ptr(h), U, L,
                                       _lib.ptr(c), _lib.ptr(co), _lib.ptr(cl), _lib.ptr(ex), _lib.ptr(oo),
                                       _lib.ptr(out), d, A, F, ctypes.byref(p), _lib.ptr(ws), ws.numel(),
@@ -195,7 +221,7 @@ def fused_ok(model, table: torch.Tensor, L: int):
     W1 = model.attn.attn[0].weight
     A, F = W1.shape[0], model.fc[1].weight.shape[0]
     d = table.shape[1]
-    return [w for w, bad in (("table is not bf16", table.dtype != torch.bfloat16),
+    return [w for w, bad in (("table is neither bf16 nor f32", table.dtype not in (torch.bfloat16, torch.float32)),
                              (f"emb_dim {d} not in (64, 128, 256)", d not in (64, 128, 256)),
                              (f"history length {L} > {RERANK_MAX_L}", L > RERANK_MAX_L),
                              (f"attn_units {A} not in (32, 64, 96, 128)", A not in (32, 64, 96, 128)),
@@ -252,7 +278,10 @@ def rerank_clusters(model, table: torch.Tensor, hist_rows: torch.Tensor, user_cl
     (cluster_candidates), so all users of cluster c share one ragged list,
     rows cluster_rows[cluster_off[c]:cluster_off[c+1]] (corpus row order).
     Users are grouped by cluster and ALL of them are scored by one fused
-    launch (nrk_din_rerank: each user's offset points at its cluster's list).
+    launch (nrk_din_rerank_projected: each user's offset points at its
+    cluster's list, projected once).  A model / table the fused kernel cannot
+    run (fused_ok) falls back, with a warning, to rerank() per cluster (every
+    candidate its own DIN sample); `path` in the result says which ran.
 
     last_rows (U,) -- the row of each user's last click -- gives
     EvalDataset's labels (one-hot at the FIRST candidate equal to it, none when
@@ -273,8 +302,6 @@ def rerank_clusters(model, table: torch.Tensor, hist_rows: torch.Tensor, user_cl
     rows = cluster_rows.to(dev).to(torch.int32)
     nl = off.numel() - 1
     why = fused_ok(model, table, L)
-    if why:
-        raise ValueError("rerank_clusters: the fused re-rank cannot run this model / table: " + ", ".join(why))
     model.eval()
     order = torch.sort(uc, stable=True).indices
     ucs = uc[order]
@@ -284,12 +311,14 @@ def rerank_clusters(model, table: torch.Tensor, hist_rows: torch.Tensor, user_cl
     last = last_rows.to(dev).long()[order] if last_rows is not None else None
     pos_in = None
     if last is not None:
-        # position of the last click inside its user's cluster list (-1: absent),
-        # by a sorted search over (cluster, row) keys
+        # position of the FIRST occurrence of the last click inside its user's
+        # cluster list (-1: absent; EvalDataset's label, DIN.py:27-31), by a
+        # sorted search over (cluster, row) keys -- a stable sort, so among equal
+        # keys the leftmost is the earliest list position
         n_tab = table.shape[0]
         member_cl = torch.repeat_interleave(torch.arange(nl, device=dev), sizes)
         keys = member_cl * (n_tab + 1) + rows.long()
-        skeys, sidx = torch.sort(keys)
+        skeys, sidx = torch.sort(keys, stable=True)
         q = ucs * (n_tab + 1) + last.clamp(0, n_tab)
         if skeys.numel():
             at = torch.searchsorted(skeys, q).clamp_max(skeys.numel() - 1)
@@ -304,13 +333,34 @@ def rerank_clusters(model, table: torch.Tensor, hist_rows: torch.Tensor, user_cl
     oo = torch.zeros(U + 1, dtype=torch.int64, device=dev)
     torch.cumsum(width, 0, out=oo[1:])
     n_out = int(oo[-1].item())
-    flat = rerank_ragged(model, table, hist_rows[order], rows, coff, clen, extra, oo[:-1], n_out, shared=True)
-    rerank.path = "fused"
-    out = {"logits": [], "users": []}
     cnt = torch.bincount(ucs, minlength=nl)
     bh = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), torch.cumsum(cnt, 0)]).cpu().tolist()
     wh = (sizes + (1 if extra is not None else 0)).cpu().tolist()
     oh = oo.cpu().tolist()
+    if not why:
+        flat = rerank_ragged(model, table, hist_rows[order], rows, coff, clen, extra, oo[:-1], n_out, shared=True)
+        path = "fused"
+    else:
+        # the fused kernel cannot run this model / table: each cluster's users
+        # through rerank(), which scores every candidate as its own DIN sample
+        warnings.warn("rerank_clusters: " + ", ".join(why) + " -> per-candidate DIN forward per cluster (C x the "
+                      "attention work of the fused path)", stacklevel=2)
+        flat = torch.empty(n_out, dtype=torch.float32, device=dev)
+        ol = off.cpu().tolist()
+        for c in range(nl):
+            lo, hi = bh[c], bh[c + 1]
+            if hi <= lo or wh[c] == 0:
+                continue
+            cand = rows[ol[c]:ol[c + 1]][None, :].expand(hi - lo, -1)
+            if extra is not None:
+                cand = torch.cat([cand, extra[lo:hi, None]], 1)
+            with warnings.catch_warnings():
+                warnings.simplefilter("ignore")  # (warned once above)
+                lg = rerank(model, table, hist_rows[order[lo:hi]], cand.contiguous(), batch_samples=batch_samples)
+            flat[oh[lo]:oh[hi]] = lg.reshape(-1)
+        path = "per-candidate: " + ", ".join(why)
+    rerank.path = path
+    out = {"logits": [], "users": [], "path": path}
     for c in range(nl):
         lo, hi = bh[c], bh[c + 1]
         if hi > lo and wh[c] > 0:

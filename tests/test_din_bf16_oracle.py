@@ -279,16 +279,16 @@ def test_rerank_matches_reference_evaluate_fixture_c5(gpu):
     assert abs(ndcg - float(z["ev_ndcg"])) < 1e-9, (ndcg, float(z["ev_ndcg"]))
 
 
-def test_rerank_fp32_table_fixture_bf16_effect(gpu):
-    """An fp32 item table as embedding_generate.py produces (fixture
+def test_rerank_fp32_table_fixture(gpu):
+    """An fp32 item table as embedding_generate.py produces it (fixture
     din_rerank_f32, made by the reference's own evaluate(); NOT bf16-exact).
-    The fused re-rank consumes a bf16 table, so every embedding is rounded
-    once.  Asserted: (1) the kernel is exact on what it is given -- its logits
-    equal the fp64 oracle fed the bf16-ROUNDED table to <= 1e-4; (2) the
-    generic fp32 path (rerank on the fp32 table: every candidate its own DIN
-    sample) equals the reference's logits to <= 1e-4 and every NDCG.  Reported
-    (printed, and bounded loosely): the bf16 table's own effect on the logits
-    and how many users keep the reference's NDCG@5."""
+    The fused re-rank takes the f32 table through the row projections, which
+    split every element into bf16 hi + lo.  Asserted: (1) its logits equal the
+    reference's to <= 1e-4 (north_star's DIN tolerance) and every user's
+    NDCG@5 equals the reference's; (2) the same against the fp64 oracle on the
+    fp32 table; (3) the generic fp32 path (every candidate its own DIN sample)
+    also equals the reference.  Reported: what rounding the table to bf16 would
+    cost (the kernel is exact on the rounded table: <= 1e-4 vs the oracle)."""
     from newsrecommend_amd.din import DIN
     from newsrecommend_amd.pipeline import ndcg_at_k, rerank
 
@@ -305,25 +305,94 @@ def test_rerank_fp32_table_fixture_bf16_effect(gpu):
     model = model.to(dev).eval()
     t32 = torch.from_numpy(z["table"]).to(dev)
     assert not torch.equal(t32, t32.to(torch.bfloat16).float())  # really not bf16-exact
+    ref = z["ev_logits"]
+    # (1) the fused path on the fp32 table vs the reference's evaluate()
+    lg = rerank(model, t32, hist, cand)
+    assert rerank.path == "fused", rerank.path
+    err = float(np.abs(lg.cpu().numpy() - ref).max())
+    assert err < 1e-4, err
+    nd = ndcg_at_k(lg, lab, 5).cpu().numpy()
+    np.testing.assert_array_equal(nd, z["ev_ndcg_user"])  # every user
+    # (2) vs the fp64 oracle on the fp32 table
+    T = t32.cpu().numpy().astype(np.float64)
+    p_ref = _params_f64(model, False)
+    H, Cn, Lg = hist.cpu().numpy(), cand.cpu().numpy(), lg.cpu().numpy()
+    worst32 = max(float(np.abs(Lg[u] - _rerank_oracle(p_ref, T, H[u], Cn[u])).max()) for u in range(len(Cn)))
+    assert worst32 < 1e-4, worst32
+    # (3) the generic fp32 path
+    lg_gen = rerank(model, t32, hist, cand, shared=False)
+    assert rerank.path.startswith("per-candidate")
+    err_gen = float(np.abs(lg_gen.cpu().numpy() - ref).max())
+    assert err_gen < 1e-4, err_gen
+    np.testing.assert_array_equal(ndcg_at_k(lg_gen, lab, 5).cpu().numpy(), z["ev_ndcg_user"])
+    # the bf16 table's effect, reported; the kernel is exact on the rounded table
     lg_bf = rerank(model, t32.to(torch.bfloat16), hist, cand)
     assert rerank.path == "fused"
-    lg_32 = rerank(model, t32, hist, cand)
-    assert rerank.path.startswith("per-candidate")
-    ref = z["ev_logits"]
-    err32 = float(np.abs(lg_32.cpu().numpy() - ref).max())
-    assert err32 < 1e-4, err32
-    np.testing.assert_array_equal(ndcg_at_k(lg_32, lab, 5).cpu().numpy(), z["ev_ndcg_user"])
-    # (1) exactness on the rounded table
     Tb = t32.to(torch.bfloat16).float().cpu().numpy().astype(np.float64)
+    Lb = lg_bf.cpu().numpy()
+    worst_b = max(float(np.abs(Lb[u] - _rerank_oracle(p_ref, Tb, H[u], Cn[u])).max()) for u in range(len(Cn)))
+    assert worst_b < 1e-4, worst_b
+    eff = float(np.abs(Lb - ref).max())
+    print(f"fp32-table fixture: fused on the f32 table vs the reference {err:.3g} (vs the fp64 oracle {worst32:.3g}); "
+          f"generic path {err_gen:.3g}; a bf16-rounded table would cost {eff:.3g} (kernel vs oracle on it "
+          f"{worst_b:.3g})")
+
+
+def test_rerank_fp32_table_random_c5_shape(gpu):
+    """The fused f32-table re-rank at configs[4]'s shape (d 256, L 50, C 201,
+    A 128, F 32) on a random table that is far from bf16-exact, with padded
+    and out-of-table slots and an empty history: logits <= 1e-4 of the fp64
+    oracle, every user's NDCG@5 equal to the oracle's, -inf for invalid
+    candidates; and the ragged form (shared lists) bit-identical to the padded
+    one."""
+    from newsrecommend_amd.din import DIN
+    from newsrecommend_amd.pipeline import ndcg_at_k, rerank, rerank_ragged
+    from oracle import din_oracle as o
+
+    dev = torch.device("cuda")
+    d, L, C, U, N = 256, 50, 201, 24, 6000
+    g = torch.Generator(device=dev).manual_seed(57)
+    table = torch.randn((N, d), generator=g, device=dev) * 0.5
+    hist = torch.randint(0, N, (U, L), generator=g, device=dev, dtype=torch.int32)
+    lens = torch.randint(1, L + 1, (U,), generator=g, device=dev)
+    lens[0], lens[1] = 1, L
+    hist = torch.where(torch.arange(L, device=dev)[None] < lens[:, None], hist, torch.full_like(hist, -1))
+    hist[2] = -1
+    hist[3, 4] = N + 11  # outside the table: a padding slot
+    cand = torch.randint(0, N, (U, C), generator=g, device=dev, dtype=torch.int32)
+    cand[::5, -1] = -1
+    cand[3, 7] = N + 3
+    gt_col = torch.randint(0, C - 1, (U,), generator=g, device=dev)
+    labels = torch.zeros((U, C), dtype=torch.bool, device=dev)
+    labels[torch.arange(U, device=dev), gt_col] = True
+    torch.manual_seed(9)
+    model = DIN(d, 128, 32, 0.36).to(dev).eval()
+    with torch.no_grad():
+        for bn in (model.fc[0], model.fc[4], model.fc[8]):
+            bn.running_mean.uniform_(-0.3, 0.3)
+            bn.running_var.uniform_(0.4, 1.6)
+    logits = rerank(model, table, hist, cand)
+    assert rerank.path == "fused", rerank.path
+    nd = ndcg_at_k(logits, labels, 5).cpu().numpy()
+    T = table.cpu().numpy().astype(np.float64)
+    H, Cn, Lg, Lb = hist.cpu().numpy(), cand.cpu().numpy(), logits.cpu().numpy(), labels.cpu().numpy()
     p_ref = _params_f64(model, False)
-    H, Cn, Lg = hist.cpu().numpy(), cand.cpu().numpy(), lg_bf.cpu().numpy()
-    worst = max(float(np.abs(Lg[u] - _rerank_oracle(p_ref, Tb, H[u], Cn[u])).max()) for u in range(len(Cn)))
+    worst, refs = 0.0, []
+    for u in range(U):
+        valid = (Cn[u] >= 0) & (Cn[u] < N)
+        assert np.isneginf(Lg[u][~valid]).all()
+        ref = _rerank_oracle(p_ref, T, np.where((H[u] >= 0) & (H[u] < N), H[u], -1), np.where(valid, Cn[u], -1))
+        worst = max(worst, float(np.abs(Lg[u][valid] - ref).max()))
+        refs.append((ref, Lb[u][valid].astype(np.int64)))
+    print(f"fused re-rank on an f32 table: logits max abs err vs the fp64 oracle {worst:.3g}")
     assert worst < 1e-4, worst
-    # the bf16 table's effect, reported
-    eff = float(np.abs(Lg - ref).max())
-    nd = ndcg_at_k(lg_bf, lab, 5).cpu().numpy()
-    same = int((nd == z["ev_ndcg_user"]).sum())
-    print(f"fp32-table fixture: fused (bf16 table) vs oracle on the rounded table {worst:.3g}; vs the reference's "
-          f"fp32 logits {eff:.3g}; NDCG@5 equal for {same} of {len(nd)} users; mean NDCG {nd.mean():.4f} vs "
-          f"{float(z['ev_ndcg']):.4f}; fp32 generic path vs reference {err32:.3g}")
-    assert eff < 5e-2
+    for u, (ref, lab_u) in enumerate(refs):
+        # (the same rank gives the same 1 / log2(rank + 1) up to the last bit)
+        assert abs(nd[u] - o.ndcg_single(1 / (1 + np.exp(-ref)), lab_u, 5)) < 1e-12 or _margin(ref, lab_u) <= 2 * worst, u
+    # ragged (shared lists, each user pointing at the same flat list) == padded
+    flat = cand.reshape(-1)
+    off = torch.arange(U, device=dev, dtype=torch.int64) * C
+    lens_c = torch.full((U,), C, dtype=torch.int32, device=dev)
+    rag = rerank_ragged(model, table, hist, flat, off, lens_c, None, off, U * C, shared=True)
+    assert torch.equal(rag.view(U, C), logits)
+

@@ -167,6 +167,12 @@ def test_ivf_forced_fallback(gpu, monkeypatch, cap):
         np.testing.assert_array_equal(I, Io)
         np.testing.assert_array_equal(D, Do)
         assert int(ivf.last_fallback.item()) == 64
+        # n_fallback[1]: the queries whose tiled-scan buffer overflowed too (the
+        # block-per-query scan); a 3-candidate buffer cannot hold k = 6
+        nscan = int(ivf.last_exact_scan.item())
+        assert 0 <= nscan <= 64
+        if cap:
+            assert nscan > 0, nscan
 
 
 def test_ivf_k_exceeds_probed_items_pads(gpu):

@@ -198,3 +198,73 @@ def test_cluster_candidates_batched(gpu):
     got_fn = cluster_candidates(index, lambda c: lists[c], prof[:10], uids[:10])
     for i, u in enumerate(uids[:10]):
         np.testing.assert_array_equal(got_fn[u], lists[int(near[i])])
+
+
+def test_rerank_clusters_f32_table_bit_identical_on_bf16_exact_rows(gpu):
+    """The f32-table projections split each element into bf16 hi + lo; on a
+    bf16-exact table every lo is 0, so the f32 path must reproduce the bf16
+    path bit for bit (the f32 kernels' degenerate case), with `path` fused."""
+    from newsrecommend_amd.pipeline import rerank_clusters
+
+    dev = torch.device("cuda")
+    z, table, model, off, L = _fixture(dev)
+    hist = torch.from_numpy(z["ev_hist_rows"]).to(dev)
+    args = (hist, torch.from_numpy(z["user_cluster"]).to(dev), torch.from_numpy(off).to(dev),
+            torch.from_numpy(z["cluster_rows"]).to(dev))
+    r16 = rerank_clusters(model, table, *args)
+    r32 = rerank_clusters(model, table.float(), *args)
+    assert r16["path"] == r32["path"] == "fused"
+    for a, b in zip(r16["logits"], r32["logits"]):
+        assert torch.equal(a, b)
+
+
+def test_rerank_clusters_fallback_long_history_and_duplicate_positive(gpu):
+    """a history longer than the fused kernel holds (L = 96; the
+    reference's Optuna space goes to 128, DIN.py:207) falls back, with a
+    warning, to the per-candidate path per cluster instead of raising; its
+    logits match the fp64 oracle (<= 1e-4), and the label is the FIRST
+    occurrence of a positive row that appears twice in its cluster
+    (EvalDataset, DIN.py:27-31)."""
+    from newsrecommend_amd.din import DIN
+    from newsrecommend_amd.pipeline import rerank_clusters
+    from oracle import din_oracle as o
+
+    dev = torch.device("cuda")
+    d, L, N = 256, 96, 3000
+    g = torch.Generator(device=dev).manual_seed(5)
+    table = torch.randn((N, d), generator=g, device=dev) * 0.5
+    torch.manual_seed(2)
+    model = DIN(d, 64, 32, 0.2).to(dev).eval()
+    sizes = [40, 0, 75]
+    rows = torch.randint(0, N, (sum(sizes),), generator=g, device=dev, dtype=torch.int32)
+    rows[10] = rows[30]  # cluster 0 holds row rows[30] twice: positions 10 and 30
+    off = torch.tensor(np.concatenate([[0], np.cumsum(sizes)]), device=dev)
+    U = 6
+    hist = torch.randint(0, N, (U, L), generator=g, device=dev, dtype=torch.int32)
+    hist[1, 50:] = -1
+    uc = torch.tensor([0, 2, 0, 2, 1, 0], device=dev)
+    last = torch.tensor([int(rows[30]), int(rows[40 + 3]), -1, N + 5, int(rows[0]), int(rows[39])], device=dev)
+    with pytest.warns(UserWarning, match="per-candidate"):
+        res = rerank_clusters(model, table, hist, uc, off, rows, last, k=5)
+    assert res["path"].startswith("per-candidate") and "history length 96" in res["path"]
+    T = table.cpu().numpy().astype(np.float64)
+    p_ref = _params_f64(model, False)
+    H, R, ol = hist.cpu().numpy(), rows.cpu().numpy(), off.cpu().tolist()
+    worst = 0.0
+    for lg, us in zip(res["logits"], res["users"]):
+        for i, u in enumerate(us.cpu().tolist()):
+            c = int(uc[u])
+            ref = _rerank_oracle(p_ref, T, H[u], R[ol[c]:ol[c + 1]])
+            worst = max(worst, float(np.abs(lg[i].cpu().numpy() - ref).max()))
+    assert worst < 1e-4, worst
+    # user 0: positive = the first occurrence (position 10) of the duplicated row
+    lg0 = res["logits"][0][0].cpu().numpy().astype(np.float64)  # cluster 0's first user is user 0
+    assert int(res["users"][0][0]) == 0
+    lab = np.zeros(sizes[0], np.int64)
+    first = int(np.flatnonzero(R[:sizes[0]] == R[30])[0])
+    assert first <= 10
+    lab[first] = 1
+    assert abs(res["ndcg"][0].item() - o.ndcg_single(1 / (1 + np.exp(-lg0)), lab, 5)) < 1e-12
+    bce = np.mean(np.maximum(lg0, 0) - lg0 * lab + np.log1p(np.exp(-np.abs(lg0))))
+    assert abs(res["loss"][0].item() - bce) < 1e-9
+    assert np.isnan(res["loss"][4].item())  # user 4: empty cluster, nothing to score

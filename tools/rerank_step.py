@@ -30,6 +30,7 @@ ap.add_argument("--flow", action="store_true")
 ap.add_argument("--unshared", action="store_true", help="flow: score the rows, not the shared lists' projections")
 ap.add_argument("--A", type=int, default=128)
 ap.add_argument("--F", type=int, default=32)
+ap.add_argument("--f32", action="store_true", help="an fp32 item table (the projected path)")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 d = 256
@@ -37,7 +38,9 @@ L = 64 if a.flow else 50
 U = a.users or (50_000 if a.flow else 4096)
 N = a.items or (364_047 if a.flow else 10_000_000)
 g = torch.Generator(device=dev).manual_seed(3)
-table = (torch.randn((N, d), generator=g, device=dev) * 0.5).to(torch.bfloat16)
+table = torch.randn((N, d), generator=g, device=dev) * 0.5
+if not a.f32:
+    table = table.to(torch.bfloat16)
 hist = zipf_ids(U * L, N, generator=g, device=dev).view(U, L).to(torch.int32)
 lens = torch.randint(1, L + 1, (U,), generator=g, device=dev)
 hist = torch.where(torch.arange(L, device=dev)[None] < lens[:, None], hist, torch.full_like(hist, -1))
@@ -78,6 +81,7 @@ with KernelTimer() as kt:
     torch.cuda.synchronize()
 ms = (time.perf_counter() - t0) / a.reps * 1e3
 kms = kt.mean_ms("rerank")
+pms = kt.mean_ms("rerank_project")
 print(f"rerank {'flow' if a.flow else 'e2e'} {U} users, {samples} samples (A={a.A}, F={a.F}): {ms:.3f} ms/call wall, "
-      f"{kms:.3f} ms kernel (HIP events) = {samples / kms / 1e3:.1f} M samples/s, "
+      f"{kms:.3f} ms kernel + {pms:.3f} ms projections (HIP events) = {samples / kms / 1e3:.1f} M samples/s, "
       f"{U / kms * 1e3:.0f} users/s, finite {bool(torch.isfinite(out).any())}", flush=True)
