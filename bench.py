@@ -655,9 +655,12 @@ def bench_embed(args, rank, world, dev):
     ArticleEmbeddingModel in eval mode over N x 253 article features ->
     N x 256 embeddings (fp32, as the reference), inputs resident in HBM.
     Sizes: the reference's 364,047 articles and configs[4]'s 10M corpus, each
-    shard of N / world rows on its rank (replicas: no collective).  Roofline:
-    fp32 MFMA, 2 (253 * 512 + 512 * 256) flop per row; the dominant kernel is
-    the first GEMM, timed by rocprof (profiles/)."""
+    shard of N / world rows on its rank (replicas: no collective).  One
+    nrk_embed launch per pass (embed_mlp_kernel: both layers, h on chip).
+    Roofline: 2 (253 * 512 + 512 * 256) fp32 flop per row against the fp32
+    MFMA peak (the products are fp32-exact), and the bf16 MFMA work the kernel
+    issues for them, 6 x 2 (256 * 512 + 512 * 256) flop per row (three-plane
+    split, six products), against the dense bf16 peak."""
     from newsrecommend_amd.embedding import ArticleEmbeddingModel
 
     torch.manual_seed(5)
@@ -667,8 +670,12 @@ def bench_embed(args, rank, world, dev):
         bn.running_mean.uniform_(-0.2, 0.2)
         bn.running_var.uniform_(0.5, 1.5)
     flop_row = 2.0 * (253 * 512 + 512 * 256)
+    mfma_row = 6 * 2.0 * (256 * 512 + 512 * 256)
     out = {"metric": "article embeddings/s (corpus producer, fp32)", "unit": "rows/s",
-           "roofline_note": f"fp32 MFMA peak {FP32_MFMA_TFLOPS} TF; {flop_row:.0f} flop per row"}
+           "kernel": "embed_mlp_kernel (nrk_embed)",
+           "roofline_note": f"fp32 MFMA peak {FP32_MFMA_TFLOPS} TF; {flop_row:.0f} fp32 flop per row; "
+                            f"{mfma_row:.0f} bf16 MFMA flop per row issued (6 products of 3-plane splits) vs "
+                            f"{BF16_DENSE_TFLOPS} TF"}
     for name, n_total in (("reference_364047", 364_047), ("corpus_10m", args.e2e_nb)):
         n = -(-n_total // world)
         g = torch.Generator(device=dev).manual_seed(9 + rank)
@@ -684,7 +691,9 @@ def bench_embed(args, rank, world, dev):
         el = max_over_ranks(time.perf_counter() - t0, world, dev) / reps
         rec = {"value": n * world / el, "ms_per_pass": el * 1e3, "rows_per_gpu": n,
                "achieved_tflops": flop_row * n / el / 1e12,
-               "frac_fp32_mfma": flop_row * n / el / 1e12 / FP32_MFMA_TFLOPS}
+               "frac_fp32_mfma": flop_row * n / el / 1e12 / FP32_MFMA_TFLOPS,
+               "bf16_mfma_tflops": mfma_row * n / el / 1e12,
+               "frac_bf16_mfma": mfma_row * n / el / 1e12 / BF16_DENSE_TFLOPS}
         if rank == 0 and name == "reference_364047":
             # parity on a row sample: the reference's eval forward (fc as nn.Sequential, BN unfolded), fp32
             with torch.no_grad():

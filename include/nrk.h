@@ -272,6 +272,22 @@ int nrk_din_rerank_projected(const void* table, int64_t n_table, int32_t dtype, 
 int nrk_rerank_user_stats(const float* logits, const float* prob, const int64_t* seg_off, const int64_t* pos,
                           int32_t nU, double* loss_sum, int64_t* nval, int64_t* before, void* stream);
 
+/* ------------------------------------------------------ corpus producer --
+ * ArticleEmbeddingModel in eval mode for a whole corpus
+ * (embedding_generate.py:51-65 forward, :109-121 inference()):
+ *   out [n][out_dim] = relu(x W1^T + b1) W2^T + b2,
+ * x [n][ldx] f32 (in_dim <= 256 columns used: the reference's 253 features),
+ * W1 [hidden][in_dim], b1 [hidden] (fc.0), W2 [out_dim][hidden], b2 [out_dim]
+ * (fc.4 with the eval BatchNorm fc.3 folded in by the caller:
+ * W2 = fc.4.weight diag(s), b2 = fc.4.bias + fc.4.weight t).  hidden a
+ * multiple of 64, out_dim 256.  The hidden activations never leave the chip;
+ * products are fp32-exact (each operand split into three bf16 planes, six
+ * MFMA products).  ws: nrk_embed_workspace bytes (the weights' planes). */
+int nrk_embed_workspace(int32_t in_dim, int32_t hidden, int32_t out_dim, size_t* ws_bytes);
+int nrk_embed(const float* x, int64_t n, int64_t ldx, int32_t in_dim, const float* W1, const float* b1,
+              int32_t hidden, const float* W2, const float* b2, int32_t out_dim, float* out, void* ws,
+              size_t ws_bytes, void* stream);
+
 /* ------------------------------------------------------ inverted lists --
  * faiss Clustering / IndexIVFFlat building blocks (Retrieval.py:11-23).
  *

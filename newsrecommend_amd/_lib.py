@@ -75,6 +75,8 @@ SIGNATURES = {
     "nrk_din_rerank_projected": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p,
                                                 c_i32, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_size, c_p]),
     "nrk_rerank_user_stats": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_i32, c_p, c_p, c_p, c_p]),
+    "nrk_embed_workspace": (ctypes.c_int, [c_i32, c_i32, c_i32, ctypes.POINTER(c_size)]),
+    "nrk_embed": (ctypes.c_int, [c_p, c_i64, c_i64, c_i32, c_p, c_p, c_i32, c_p, c_p, c_i32, c_p, c_p, c_size, c_p]),
     "nrk_gather_rows": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_i64, c_i32, c_p, c_p]),
     "nrk_train_samples": (ctypes.c_int, [c_p, c_i64, c_p, c_i64, c_i32, c_p, c_i64, c_p, c_p, c_p, c_p]),
     "nrk_triplet_samples": (ctypes.c_int, [c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p]),

@@ -22,7 +22,7 @@ ORACLE_LIB = os.path.join(ROOT, "oracle", "liboracle_knn.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"]
-SOURCES = ["nrk_common.cpp", "click_log.cpp", "knn_flat.hip", "din_attn.hip", "ivf_build.hip", "din_head.hip", "din_rerank.hip",
+SOURCES = ["nrk_common.cpp", "click_log.cpp", "knn_flat.hip", "din_attn.hip", "ivf_build.hip", "din_head.hip", "din_rerank.hip", "embed.hip",
            "screen_dp32.hip", "screen_dp64.hip", "screen_dp128.hip", "screen_dp256.hip"]
 # din_rerank: no NaN inputs (finite weights and table rows; padded candidates are
 # written as -inf, never computed), so max / min need no IEEE canonicalisation

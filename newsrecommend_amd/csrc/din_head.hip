@@ -22,6 +22,8 @@
 #include <math.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "nrk_common.h"
 
 namespace nrk {
@@ -272,30 +274,38 @@ __global__ __launch_bounds__(256) void head_stats0(HeadArgs a) {
   }
 }
 
-// LDS: h0 [HR][D2+1], W1 [F][D2+1], mean/inv [D2] x 2, d1 [HR][F]
+// LDS: h0 [HR][D2+1], W1 chunk [FC][D2+1], mean/inv [D2] x 2, d1 [HR][F].
+// W1 passes through LDS FC = 32 output units at a time (2d = 512 and F = 128
+// would need 328 KB at once).
+constexpr int FC = 32;
 __global__ __launch_bounds__(256) void head_fwd1(HeadArgs a) {
   extern __shared__ float sm[];
   const int D2 = a.D2, F = a.F, ds = D2 + 1;
+  const int fc = F < FC ? F : FC;
   float* h0 = sm;
   float* w1 = h0 + HR * ds;
-  float* mean = w1 + F * ds;
+  float* mean = w1 + fc * ds;
   float* inv = mean + D2;
   float* d1 = inv + D2;
   const int64_t r0 = (int64_t)blockIdx.x * HR;
   bn_finalize(a, a.sum0, D2, mean, inv, a.stat0, a.p.bn0_rm, a.p.bn0_rv, a.p.bn0_nb, blockIdx.x == 0);
-  for (int e = threadIdx.x; e < F * D2; e += 256) w1[(e / D2) * ds + e % D2] = a.p.fc1_w[e];
   __syncthreads();
   for (int e = threadIdx.x; e < HR * D2; e += 256) {
     const int r = e / D2, c = e % D2;
     h0[r * ds + c] = (hx(a, r0 + r, c) - mean[c]) * inv[c] * a.p.bn0_w[c] + a.p.bn0_b[c];
   }
-  __syncthreads();
-  for (int o = threadIdx.x; o < HR * F; o += 256) {
-    const int r = o / F, j = o % F;
-    float acc = a.p.fc1_b[j];
-    acc = dot4(h0 + r * ds, 1, w1 + j * ds, 1, D2, acc);
-    a.a1[(r0 + r) * F + j] = acc;
-    d1[r * F + j] = fmaxf(acc, 0.f) * keep_scale(a, 1, r0 + r, j);
+  for (int j0 = 0; j0 < F; j0 += fc) {
+    const int nj = F - j0 < fc ? F - j0 : fc;
+    __syncthreads();  // (the previous chunk's dot products are done with w1)
+    for (int e = threadIdx.x; e < nj * D2; e += 256) w1[(e / D2) * ds + e % D2] = a.p.fc1_w[(int64_t)j0 * D2 + e];
+    __syncthreads();
+    for (int o = threadIdx.x; o < HR * nj; o += 256) {
+      const int r = o / nj, jj = o % nj, j = j0 + jj;
+      float acc = a.p.fc1_b[j];
+      acc = dot4(h0 + r * ds, 1, w1 + jj * ds, 1, D2, acc);
+      a.a1[(r0 + r) * F + j] = acc;
+      d1[r * F + j] = fmaxf(acc, 0.f) * keep_scale(a, 1, r0 + r, j);
+    }
   }
   __syncthreads();
   for (int j = threadIdx.x; j < F; j += 256) {
@@ -498,13 +508,17 @@ __global__ __launch_bounds__(256) void head_bwd2(HeadArgs a) {
   }
 }
 
-// part5 per block: [D2] sum dh0, [D2] sum dh0*xhat0, [F] db1; pw1 per block [F*D2] (f32)
+// part5 per block: [D2] sum dh0, [D2] sum dh0*xhat0, [F] db1; pw1 per block [F*D2] (f32).
+// W1 passes through LDS FC units at a time (as head_fwd1); dh0 = da1 W1 is
+// accumulated over the chunks in registers (2d <= 512: two columns of the
+// block's 32 rows per thread).
 __global__ __launch_bounds__(256) void head_bwd1(HeadArgs a) {
   extern __shared__ float sm[];
   const int D2 = a.D2, F = a.F, ds = D2 + 1;
+  const int fc = F < FC ? F : FC;
   float* h0 = sm;             // [HR][D2+1]
-  float* w1 = h0 + HR * ds;   // [F][D2+1]
-  float* da1 = w1 + F * ds;   // [HR][F]
+  float* w1 = h0 + HR * ds;   // [FC][D2+1]
+  float* da1 = w1 + fc * ds;  // [HR][F]
   float* m0 = da1 + HR * F;
   float* i0 = m0 + D2;
   float* m1 = i0 + D2;
@@ -518,7 +532,6 @@ __global__ __launch_bounds__(256) void head_bwd1(HeadArgs a) {
     sb1[j] = (float)a.sum4[j];
     sg1[j] = (float)a.sum4[F + j];
   }
-  for (int e = threadIdx.x; e < F * D2; e += 256) w1[(e / D2) * ds + e % D2] = a.p.fc1_w[e];
   __syncthreads();
   for (int e = threadIdx.x; e < HR * D2; e += 256) {  // h0 holds xhat0 here (h0 = xhat0 * w + b)
     const int r = e / D2, c = e % D2;
@@ -556,19 +569,47 @@ __global__ __launch_bounds__(256) void head_bwd1(HeadArgs a) {
     for (int r = 0; r < HR; ++r) s += da1[r * F + j];
     pp[2 * D2 + j] = s;
   }
-  // dh0 = da1 W1 and the BN0-backward sums over this block's rows
-  for (int c = threadIdx.x; c < D2; c += 256) {
-    double sb = 0.0, sg = 0.0;
-    for (int r = 0; r < HR; ++r) {
-      float s = 0.f;
-      s = dot4(da1 + r * F, 1, w1 + c, ds, F, s);
-      a.dh0[(r0 + r) * D2 + c] = s;
-      const float xhat = h0[r * ds + c];
-      sb += s;
-      sg += (double)s * xhat;
+  // dh0 = da1 W1 (summed over the W1 chunks) and the BN0-backward sums over
+  // this block's rows; thread t owns columns t and t + 256
+  float dh[2][HR];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int r = 0; r < HR; ++r) dh[u][r] = 0.f;
+  for (int j0 = 0; j0 < F; j0 += fc) {
+    const int nj = F - j0 < fc ? F - j0 : fc;
+    __syncthreads();  // (the previous chunk is done with w1)
+    for (int e = threadIdx.x; e < nj * D2; e += 256) w1[(e / D2) * ds + e % D2] = a.p.fc1_w[(int64_t)j0 * D2 + e];
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c = threadIdx.x + 256 * u;
+      if (c < D2) {
+        for (int jj = 0; jj < nj; ++jj) {
+          const float wv = w1[jj * ds + c];
+          const float* dr = da1 + j0 + jj;  // (a broadcast read per row)
+#pragma unroll
+          for (int r = 0; r < HR; ++r) dh[u][r] = fmaf(dr[r * F], wv, dh[u][r]);
+        }
+      }
     }
-    pp[c] = sb;
-    pp[D2 + c] = sg;
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int c = threadIdx.x + 256 * u;
+    if (c < D2) {
+      double sb = 0.0, sg = 0.0;
+#pragma unroll
+      for (int r = 0; r < HR; ++r) {
+        const float s = dh[u][r];
+        a.dh0[(r0 + r) * D2 + c] = s;
+        const float xhat = h0[r * ds + c];
+        sb += s;
+        sg += (double)s * xhat;
+      }
+      pp[c] = sb;
+      pp[D2 + c] = sg;
+    }
   }
 }
 
@@ -1631,7 +1672,7 @@ extern "C" int nrk_din_head_train(const float* q, const float* pooled, int64_t l
                                   uint64_t seed, const float* step, const nrk_din_head_params* prm, float* logits,
                                   float* loss, float* dpooled, void* ws, size_t ws_bytes, void* stream) {
   NRK_CHECK_ARG(B > 1 && B % HR == 0, "din_head_train: B=%d must be a positive multiple of %d", B, HR);
-  NRK_CHECK_ARG(d > 0 && 2 * d <= 512 && F >= 2 && F <= 64 && F % 2 == 0 && ld_pooled >= d,
+  NRK_CHECK_ARG(d > 0 && 2 * d <= 512 && F >= 2 && F <= 128 && F % 2 == 0 && ld_pooled >= d,
                 "din_head_train: unsupported d=%d F=%d ld=%lld", d, F, (long long)ld_pooled);
   NRK_CHECK_ARG(p_drop >= 0.f && p_drop < 1.f, "din_head_train: dropout %f", (double)p_drop);
   NRK_CHECK_ARG(q && pooled && labels && step && prm && logits && loss && ws, "din_head_train: null pointer");
@@ -1744,11 +1785,17 @@ extern "C" int nrk_din_head_train(const float* q, const float* pooled, int64_t l
     NRK_CHECK_LAUNCH("din_head_train (fast)");
     return NRK_OK;
   }
-  const size_t lds1 = ((size_t)(HR + F) * (D2 + 1) + 2 * D2 + HR * F) * 4;
+  const int fc = F < FC ? F : FC;  // W1 rows staged at a time (head_fwd1 / head_bwd1)
+  const size_t lds1 = ((size_t)(HR + fc) * (D2 + 1) + 2 * D2 + HR * F) * 4;
   const size_t lds2 = ((size_t)HR * F + F2 * F + 2 * F + HR * F2) * 4;
   const size_t lds3 = ((size_t)2 * HR * F2 + 2 * F2 + 2 * HR) * 4;
   const size_t lds4 = ((size_t)3 * HR * F + HR * F2 + 2 * F + 4 * F2 + F2 * F) * 4;
-  const size_t lds5 = ((size_t)(HR + F) * (D2 + 1) + HR * F + 2 * D2 + 4 * F) * 4;
+  const size_t lds5 = ((size_t)(HR + fc) * (D2 + 1) + HR * F + 2 * D2 + 4 * F) * 4;
+  {
+    const size_t mx = std::max(std::max(lds1, lds2), std::max(std::max(lds3, lds4), lds5));
+    // (+ head_fwd2 / fwd3 / bwd2's static prologue buffers, 3 KB)
+    NRK_CHECK_ARG(mx + 3072 <= 160 * 1024, "din_head_train: d=%d F=%d needs %zu B of LDS", d, F, mx + 3072);
+  }
   auto colsum = [&](const double* part, int stride, double* out) {
     hipLaunchKernelGGL(colsum_kernel<double>, dim3((unsigned)cdiv(stride, 32)), dim3(256), 0, st, part, nblk, stride,
                        stride, out);

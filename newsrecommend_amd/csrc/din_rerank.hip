@@ -900,98 +900,156 @@ __device__ __forceinline__ int slice_col(int n, int A) {
   return sj * SL + 4 * p4 + (w & 3);
 }
 
+// A chunk's rows in flight, in registers (no lambdas over arrays: the
+// compiler left such captured arrays in scratch).
 template <int D, bool F32>
-__global__ __launch_bounds__(256) void din_rerank_project_kernel(ProjArgs a) {
-  constexpr int CPR = D / 8, KSD = D / 32;
-  extern __shared__ __attribute__((aligned(16))) unsigned char pimg[];  // hi image [CH][D] bf16 (+ lo image)
-  unsigned char* iml = pimg + CH * D * 2;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l15 = lane & 15, l4 = lane >> 4;
-  const int64_t r0 = (int64_t)blockIdx.x * CH;
-  // every id, then every row load in flight before the first is used (a
-  // load -> split -> store loop would expose one HBM latency per chunk)
-  constexpr int NPT = CH * CPR / 256;  // 16-B (bf16) / 32-B (f32) chunks per thread
-  int ids[NPT];
-#pragma unroll
-  for (int k = 0; k < NPT; ++k) {
-    const int row = (tid + 256 * k) / CPR;
-    ids[k] = r0 + row < a.n ? a.rows[r0 + row] : -1;
-  }
-  if constexpr (F32) {
-    f32x4 x0[NPT], x1[NPT];
+struct ProjStage {
+  static constexpr int CPR = D / 8, NPT = CH * CPR / 512;
+  f32x4 x0[NPT], x1[NPT];
+  __device__ __forceinline__ void issue(const ProjArgs& a, const int (&idn)[NPT], int tid) {
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
-      const int cc = (tid + 256 * k) % CPR;
+      const int cc = (tid + 512 * k) % CPR;
       x0[k] = f32x4{0.f, 0.f, 0.f, 0.f};
       x1[k] = x0[k];
-      if (ids[k] >= 0 && ids[k] < a.n_table) {
-        const f32x4* src = reinterpret_cast<const f32x4*>(static_cast<const float*>(a.table) + (int64_t)ids[k] * D + 8 * cc);
+      if (idn[k] >= 0 && idn[k] < a.n_table) {
+        const f32x4* src = reinterpret_cast<const f32x4*>(static_cast<const float*>(a.table) + (int64_t)idn[k] * D + 8 * cc);
         x0[k] = __builtin_nontemporal_load(src);
         x1[k] = __builtin_nontemporal_load(src + 1);
       }
     }
+  }
+  __device__ __forceinline__ void store(unsigned char* hi, unsigned char* lo, int tid) const {
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
-      const int e = tid + 256 * k, row = e / CPR, cc = e % CPR;
-      const float xv[8] = {x0[k][0], x0[k][1], x0[k][2], x0[k][3], x1[k][0], x1[k][1], x1[k][2], x1[k][3]};
+      const int e = tid + 512 * k, row = e / CPR, cc = e % CPR;
       bf16x8 h, l;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int j = 0; j < 4; ++j) {
         short hj, lj;
-        split_bf16(xv[j], hj, lj);
+        split_bf16(x0[k][j], hj, lj);
         h[j] = hj;
         l[j] = lj;
+        split_bf16(x1[k][j], hj, lj);
+        h[4 + j] = hj;
+        l[4 + j] = lj;
       }
-      *reinterpret_cast<bf16x8*>(pimg + img_off<D>(row, cc)) = h;
-      *reinterpret_cast<bf16x8*>(iml + img_off<D>(row, cc)) = l;
-    }
-  } else {
-    bf16x8 v[NPT];
-#pragma unroll
-    for (int k = 0; k < NPT; ++k) {
-      const int cc = (tid + 256 * k) % CPR;
-      v[k] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (ids[k] >= 0 && ids[k] < a.n_table)
-        v[k] = __builtin_nontemporal_load(
-            reinterpret_cast<const bf16x8*>(static_cast<const uint16_t*>(a.table) + (int64_t)ids[k] * D + 8 * cc));
-    }
-#pragma unroll
-    for (int k = 0; k < NPT; ++k) {
-      const int e = tid + 256 * k, row = e / CPR, cc = e % CPR;
-      *reinterpret_cast<bf16x8*>(pimg + img_off<D>(row, cc)) = v[k];
+      *reinterpret_cast<bf16x8*>(hi + img_off<D>(row, cc)) = h;
+      *reinterpret_cast<bf16x8*>(lo + img_off<D>(row, cc)) = l;
     }
   }
-  __syncthreads();
-  const int NUT = a.A / 16, NFT = a.F / 16, AF = a.A + a.F;
-  for (int t = w; t < NUT + NFT; t += 4) {
-    const bool isA = t < NUT;
-    const int urow = isA ? 16 * t + l15 : 16 * (t - NUT) + l15;
-    const uint16_t* bh = (isA ? a.Wa_hi : a.Wb_hi) + (int64_t)urow * D + 8 * l4;
-    const uint16_t* bl = (isA ? a.Wa_lo : a.Wb_lo) + (int64_t)urow * D + 8 * l4;
-    bf16x8 fh[KSD], fl[KSD];
+};
+template <int D>
+struct ProjStage<D, false> {
+  static constexpr int CPR = D / 8, NPT = CH * CPR / 512;
+  bf16x8 v[NPT];
+  __device__ __forceinline__ void issue(const ProjArgs& a, const int (&idn)[NPT], int tid) {
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      const int cc = (tid + 512 * k) % CPR;
+      v[k] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (idn[k] >= 0 && idn[k] < a.n_table)
+        v[k] = __builtin_nontemporal_load(
+            reinterpret_cast<const bf16x8*>(static_cast<const uint16_t*>(a.table) + (int64_t)idn[k] * D + 8 * cc));
+    }
+  }
+  __device__ __forceinline__ void store(unsigned char* hi, unsigned char*, int tid) const {
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      const int e = tid + 512 * k, row = e / CPR, cc = e % CPR;
+      *reinterpret_cast<bf16x8*>(hi + img_off<D>(row, cc)) = v[k];
+    }
+  }
+};
+
+template <int D, bool F32>
+__global__ __launch_bounds__(512, 1) void din_rerank_project_kernel(ProjArgs a) {
+  // Persistent over 64-row chunks (one workgroup per CU): wave w owns the unit
+  // tiles w and w + 8 of [Wa ; Wb] (at most 16), whose hi / lo fragments stay
+  // in its registers for the whole launch (no per-chunk L2 re-reads); the next
+  // chunk's rows are in flight (registers) during this chunk's MFMAs, their ids
+  // one chunk further ahead.  HBM-bound: a chunk's MFMAs (<= 2 tiles x 4 row
+  // tiles per wave) take less than its rows' share of the bandwidth.
+  constexpr int CPR = D / 8, KSD = D / 32, NT = 512;
+  constexpr int NPT = CH * CPR / NT;  // 8-element pieces per thread per chunk
+  static_assert(NPT >= 1 && CH * CPR % NT == 0, "din_rerank_project: staging split");
+  extern __shared__ __attribute__((aligned(16))) unsigned char pimg[];  // hi image [CH][D] bf16 (+ lo image)
+  unsigned char* iml = pimg + CH * D * 2;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l15 = lane & 15, l4 = lane >> 4;
+  const int NUT = a.A / 16, T = NUT + a.F / 16, AF = a.A + a.F;
+  const int64_t nchunk = (a.n + CH - 1) / CH;
+  const int64_t G = gridDim.x;
+
+  // ---- the wave's tiles: fragments, and where their outputs go
+  bf16x8 fh[2][KSD], fl[2][KSD];
+  float b1u[2], w2u[2];
+  int oc[2];
+  bool isA[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int t = w + 8 * j;
+    const int tt = t < T ? t : 0;  // (an absent tile loads tile 0's and is skipped)
+    isA[j] = tt < NUT;
+    const int urow = isA[j] ? 16 * tt + l15 : 16 * (tt - NUT) + l15;
+    const uint16_t* bh = (isA[j] ? a.Wa_hi : a.Wb_hi) + (int64_t)urow * D + 8 * l4;
+    const uint16_t* bl = (isA[j] ? a.Wa_lo : a.Wb_lo) + (int64_t)urow * D + 8 * l4;
 #pragma unroll
     for (int s = 0; s < KSD; ++s) {
-      fh[s] = *reinterpret_cast<const bf16x8*>(bh + 32 * s);
-      fl[s] = *reinterpret_cast<const bf16x8*>(bl + 32 * s);
+      fh[j][s] = *reinterpret_cast<const bf16x8*>(bh + 32 * s);
+      fl[j][s] = *reinterpret_cast<const bf16x8*>(bl + 32 * s);
     }
-    const float b1u = isA && a.b1 ? a.b1[urow] : 0.f, w2u = isA ? a.w2[urow] : 0.f;
-    const int oc = isA ? slice_col(urow, a.A) : a.A + urow;
-#pragma unroll 1  // (unrolled, the compiler hoists all four tiles' A fragments: 1 wave per SIMD at d = 256)
-    for (int ct = 0; ct < 4; ++ct) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    b1u[j] = isA[j] && a.b1 ? a.b1[urow] : 0.f;
+    w2u[j] = isA[j] ? a.w2[urow] : 0.f;
+    oc[j] = isA[j] ? slice_col(urow, a.A) : a.A + urow;
+  }
+  const int ntile = (w < T ? 1 : 0) + (w + 8 < T ? 1 : 0);
+
+  // ---- staging (registers): ids a chunk ahead of the rows they name
+  int idn[NPT];
+  auto load_ids = [&](int64_t c) __attribute__((always_inline)) {
 #pragma unroll
-      for (int s = 0; s < KSD; ++s) {
-        const int o = img_off<D>(16 * ct + l15, 4 * s + l4);
-        const bf16x8 af = *reinterpret_cast<const bf16x8*>(pimg + o);
-        if constexpr (F32) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(iml + o), fh[s], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, fl[s], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, fh[s], acc, 0, 0, 0);
+    for (int k = 0; k < NPT; ++k) {
+      const int64_t r = c * CH + (tid + NT * k) / CPR;
+      idn[k] = c < nchunk && r < a.n ? a.rows[r] : -1;
+    }
+  };
+  ProjStage<D, F32> stg;
+  int64_t c = blockIdx.x;
+  load_ids(c);
+  stg.issue(a, idn, tid);
+  load_ids(c + G);
+  for (; c < nchunk; c += G) {
+    __syncthreads();  // the previous chunk's MFMAs are done with the image
+    stg.store(pimg, iml, tid);
+    __syncthreads();
+    if (c + G < nchunk) {  // the next chunk's rows in flight during the MFMAs, the one after's ids
+      stg.issue(a, idn, tid);
+      load_ids(c + 2 * G);
+    }
+    const int64_t r0 = c * CH;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (j < ntile) {
+#pragma unroll 1
+      for (int ct = 0; ct < 4; ++ct) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KSD; ++s) {
+          const int o = img_off<D>(16 * ct + l15, 4 * s + l4);
+          const bf16x8 af = *reinterpret_cast<const bf16x8*>(pimg + o);
+          if constexpr (F32)
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(iml + o), fh[j][s], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, fl[j][s], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, fh[j][s], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int64_t row = r0 + 16 * ct + 4 * l4 + i;
+          // (candidates: w2 (acc + b1), as the main kernel forms U'; history:
+          // w2 acc, as it forms P')
+          if (row < a.n) a.out[row * AF + oc[j]] = isA[j] ? w2u[j] * (a.b1 ? acc[i] + b1u[j] : acc[i]) : acc[i];
+        }
       }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int64_t row = r0 + 16 * ct + 4 * l4 + i;
-        // (candidates: w2 (acc + b1), as the main kernel forms U'; history:
-        // w2 acc, as it forms P' -- b1u is 0 there)
-        if (row < a.n) a.out[row * AF + oc] = isA ? w2u * (a.b1 ? acc[i] + b1u : acc[i]) : acc[i];
       }
     }
   }
@@ -999,9 +1057,10 @@ __global__ __launch_bounds__(256) void din_rerank_project_kernel(ProjArgs a) {
 
 template <int D, bool F32>
 int launch_proj(const ProjArgs& a, hipStream_t st) {
-  const int64_t grid = (a.n + CH - 1) / CH;
+  const int64_t nchunk = (a.n + CH - 1) / CH;
+  const int grid = nchunk < 256 ? (int)nchunk : 256;  // persistent: one workgroup per CU
   const size_t lds = (size_t)CH * D * 2 * (F32 ? 2 : 1);
-  hipLaunchKernelGGL((din_rerank_project_kernel<D, F32>), dim3((unsigned)grid), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((din_rerank_project_kernel<D, F32>), dim3(grid), dim3(512), lds, st, a);
   NRK_CHECK_LAUNCH("din_rerank_project_kernel");
   return NRK_OK;
 }

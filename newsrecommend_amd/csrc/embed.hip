@@ -1,0 +1,258 @@
+// embed.hip — the corpus producer (embedding_generate.py:51-65, 109-121):
+// ArticleEmbeddingModel in eval mode, out = relu(x W1^T + b1) W2'^T + b2'
+// (the eval BatchNorm folded into fc.4 by the caller), for a whole corpus in
+// one launch, h never leaving the chip.
+//
+// Precision: fp32 products from bf16 MFMAs.  Every fp32 operand is split
+// EXACTLY into three bf16 planes (x = h + m + l: 8 + 8 + 8 mantissa bits), and
+// a product keeps the six terms down to 2^-16 of the leading one (hh, hm, mh,
+// hl, lh, mm; the dropped ml, lm, ll are below 2^-24), accumulated in fp32 by
+// the MFMA: the error is that of an fp32 dot product (measured against the
+// reference's own inference() in tests/test_embedding.py).  Six
+// v_mfma_f32_16x16x32_bf16 per 16x16x32 block deliver 2.5 / 6 = 0.42 PF/s of
+// fp32-exact products at peak, 2.65x the 157 TF/s of v_mfma_f32_32x32x2_f32.
+//
+// One 512-thread workgroup (8 waves) per 64-row tile, one per CU (LDS):
+//   x tile -> three bf16 planes in LDS (swizzled 16-B chunks: conflict-free
+//   16x16x32 A-fragment reads), then per chunk of HC = 64 hidden units:
+//   layer 1  H_j = relu(x W1[j]^T + b1[j]) (wave w: hidden tile w & 3, row
+//            tiles 2 (w >> 2) + {0, 1}; W1 fragments from L2, reused over the
+//            two row tiles), split into three planes in LDS (double-buffered);
+//   layer 2  O += H_j W2[:, j]^T (wave w: output columns 32 w .. 32 w + 31,
+//            all 64 rows: 8 accumulator tiles resident over the chunks).
+// Finally O + b2' -> HBM.
+#include "nrk_common.h"
+
+namespace nrk {
+namespace emb {
+
+constexpr int NT = 512;  // 8 waves
+constexpr int RT = 64;   // rows per workgroup
+constexpr int KP = 256;  // input width, zero-padded (253 -> 256)
+constexpr int HC = 64;   // hidden units per chunk
+constexpr int OD = 256;  // output width
+
+// byte offset of 16-B chunk `chunk` of `row` in a [rows][W] bf16 plane
+template <int W>
+__device__ __forceinline__ int poff(int row, int chunk) {
+  constexpr int CPR = W / 8;
+  constexpr int SW = CPR >= 16 ? 15 : CPR - 1;
+  return row * 2 * W + 16 * (chunk ^ (row & SW));
+}
+
+__device__ __forceinline__ void split3(float x, short& h, short& m, short& l) {
+  const __bf16 bh = (__bf16)x;
+  const float r1 = x - (float)bh;  // exact
+  const __bf16 bm = (__bf16)r1;
+  const float r2 = r1 - (float)bm;  // exact, <= 8 significant bits: bf16-exact
+  h = __builtin_bit_cast(short, bh);
+  m = __builtin_bit_cast(short, bm);
+  l = __builtin_bit_cast(short, (__bf16)r2);
+}
+
+// the six products of a and b (three planes each), small terms first
+__device__ __forceinline__ f32x4 mfma6(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], acc, 0, 0, 0);  // mm
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], acc, 0, 0, 0);  // lh
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], acc, 0, 0, 0);  // hl
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], acc, 0, 0, 0);  // mh
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], acc, 0, 0, 0);  // hm
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc, 0, 0, 0);  // hh
+  return acc;
+}
+
+struct EmbedArgs {
+  const float* x;  // [n][ldx], in_dim <= KP used
+  int64_t n, ldx;
+  int in_dim, H;
+  const uint16_t* W1p;  // [3][H][KP] bf16 planes of fc.0.weight (zero-padded columns)
+  const float* b1;      // [H]
+  const uint16_t* W2p;  // [3][OD][H] bf16 planes of the folded fc.4 weight
+  const float* b2;      // [OD]
+  float* out;           // [n][OD]
+};
+
+__global__ __launch_bounds__(NT, 1) void embed_mlp_kernel(EmbedArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int XPL = RT * KP * 2;  // bytes per x plane
+  constexpr int HPL = RT * HC * 2;  // bytes per H plane
+  unsigned char* xs = smem;              // [3] x planes
+  unsigned char* hs = smem + 3 * XPL;    // [2 buffers][3] H planes
+  const int tid = threadIdx.x, lane = tid & 63, l15 = lane & 15, l4 = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t r0 = (int64_t)blockIdx.x * RT;
+
+  // ---- x tile -> three planes: thread = (row, 8-column chunk); 4 chunks per thread
+  {
+    constexpr int CPR = KP / 8, NPT = RT * CPR / NT;
+    float v[NPT][8];
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      const int e = tid + NT * k, row = e / CPR, c0 = 8 * (e % CPR);
+      const int64_t r = r0 + row;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[k][j] = r < a.n && c0 + j < a.in_dim ? a.x[r * a.ldx + c0 + j] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      const int e = tid + NT * k, row = e / CPR, cc = e % CPR;
+      bf16x8 ph, pm, pl;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        short h, m, l;
+        split3(v[k][j], h, m, l);
+        ph[j] = h;
+        pm[j] = m;
+        pl[j] = l;
+      }
+      const int o = poff<KP>(row, cc);
+      *reinterpret_cast<bf16x8*>(xs + o) = ph;
+      *reinterpret_cast<bf16x8*>(xs + XPL + o) = pm;
+      *reinterpret_cast<bf16x8*>(xs + 2 * XPL + o) = pl;
+    }
+  }
+
+  // layer 2's accumulators: rows 16 rt + 4 l4 + i, output columns 32 w + 16 oc + l15
+  f32x4 acc2[4][2];
+#pragma unroll
+  for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+    for (int oc = 0; oc < 2; ++oc) acc2[rt][oc] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int ht = w & 3, rp = w >> 2;  // layer 1: hidden tile, row-tile pair
+  const int nch = a.H / HC;
+  for (int j = 0; j < nch; ++j) {
+    unsigned char* hb = hs + (j & 1) * 3 * HPL;
+    // (this H buffer was last read by layer 2 of chunk j - 2, which every wave
+    // finished before chunk j - 1's second barrier)
+    if (j == 0) __syncthreads();  // the x planes published
+    // ---- layer 1: H_j tiles (rt = 2 rp + {0, 1}, ht)
+    {
+      const int u = j * HC + 16 * ht + l15;  // hidden unit of this lane's B column
+      const uint16_t* wb = a.W1p + (int64_t)u * KP + 8 * l4;
+      const int64_t ps = (int64_t)a.H * KP;  // plane stride
+      f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
+#pragma unroll 2
+      for (int s = 0; s < KP / 32; ++s) {
+        bf16x8 b[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) b[p] = *reinterpret_cast<const bf16x8*>(wb + p * ps + 32 * s);
+        bf16x8 x0[3], x1[3];
+        const int o0 = poff<KP>(16 * (2 * rp) + l15, 4 * s + l4), o1 = poff<KP>(16 * (2 * rp + 1) + l15, 4 * s + l4);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          x0[p] = *reinterpret_cast<const bf16x8*>(xs + p * XPL + o0);
+          x1[p] = *reinterpret_cast<const bf16x8*>(xs + p * XPL + o1);
+        }
+        c0 = mfma6(x0, b, c0);
+        c1 = mfma6(x1, b, c1);
+      }
+      const float bu = a.b1[u];
+      const int col = 16 * ht + l15;  // within the chunk
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const f32x4 c = t ? c1 : c0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = 16 * (2 * rp + t) + 4 * l4 + i;
+          short h, m, l;
+          split3(fmaxf(c[i] + bu, 0.f), h, m, l);
+          const int o = poff<HC>(row, col >> 3) + 2 * (col & 7);
+          *reinterpret_cast<short*>(hb + o) = h;
+          *reinterpret_cast<short*>(hb + HPL + o) = m;
+          *reinterpret_cast<short*>(hb + 2 * HPL + o) = l;
+        }
+      }
+    }
+    __syncthreads();  // H_j published
+    // ---- layer 2: O[:, 32 w .. 32 w + 31] += H_j W2[32 w .., j chunk]^T
+    {
+      const int64_t ps = (int64_t)OD * a.H;
+#pragma unroll
+      for (int s = 0; s < HC / 32; ++s) {
+        bf16x8 b[2][3];
+#pragma unroll
+        for (int oc = 0; oc < 2; ++oc) {
+          const uint16_t* wb = a.W2p + (int64_t)(32 * w + 16 * oc + l15) * a.H + j * HC + 32 * s + 8 * l4;
+#pragma unroll
+          for (int p = 0; p < 3; ++p) b[oc][p] = *reinterpret_cast<const bf16x8*>(wb + p * ps);
+        }
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt) {
+          bf16x8 hx[3];
+          const int o = poff<HC>(16 * rt + l15, 4 * s + l4);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) hx[p] = *reinterpret_cast<const bf16x8*>(hb + p * HPL + o);
+#pragma unroll
+          for (int oc = 0; oc < 2; ++oc) acc2[rt][oc] = mfma6(hx, b[oc], acc2[rt][oc]);
+        }
+      }
+    }
+  }
+  // ---- O + b2 -> HBM
+#pragma unroll
+  for (int oc = 0; oc < 2; ++oc) {
+    const int col = 32 * w + 16 * oc + l15;
+    const float bo = a.b2[col];
+#pragma unroll
+    for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t r = r0 + 16 * rt + 4 * l4 + i;
+        if (r < a.n) a.out[r * OD + col] = acc2[rt][oc][i] + bo;
+      }
+  }
+}
+
+// fp32 weights -> three bf16 planes (exact split), zero-padded to [rows][cols_p]
+__global__ void split_planes_kernel(const float* __restrict__ w, int rows, int cols, int cols_p,
+                                    uint16_t* __restrict__ planes) {
+  const int64_t n = (int64_t)rows * cols_p;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i / cols_p), c = (int)(i % cols_p);
+    short h, m, l;
+    split3(c < cols ? w[(int64_t)r * cols + c] : 0.f, h, m, l);
+    planes[i] = (uint16_t)h;
+    planes[n + i] = (uint16_t)m;
+    planes[2 * n + i] = (uint16_t)l;
+  }
+}
+
+}  // namespace emb
+}  // namespace nrk
+
+using namespace nrk;
+
+extern "C" int nrk_embed_workspace(int32_t in_dim, int32_t hidden, int32_t out_dim, size_t* ws_bytes) {
+  NRK_CHECK_ARG(ws_bytes, "embed_workspace: null");
+  NRK_CHECK_ARG(in_dim >= 1 && in_dim <= emb::KP && hidden >= emb::HC && hidden % emb::HC == 0 &&
+                    out_dim == emb::OD,
+                "embed: dims %d -> %d -> %d unsupported (in <= %d, hidden a multiple of %d, out %d)", in_dim, hidden,
+                out_dim, emb::KP, emb::HC, emb::OD);
+  *ws_bytes = align_up((size_t)3 * hidden * emb::KP * 2, 256) + (size_t)3 * emb::OD * hidden * 2;
+  return NRK_OK;
+}
+
+extern "C" int nrk_embed(const float* x, int64_t n, int64_t ldx, int32_t in_dim, const float* W1, const float* b1,
+                         int32_t hidden, const float* W2, const float* b2, int32_t out_dim, float* out, void* ws,
+                         size_t ws_bytes, void* stream) {
+  size_t need = 0;
+  int rc = nrk_embed_workspace(in_dim, hidden, out_dim, &need);
+  if (rc) return rc;
+  NRK_CHECK_ARG(n >= 0 && ldx >= in_dim, "embed: bad n=%lld / ldx=%lld", (long long)n, (long long)ldx);
+  if (n == 0) return NRK_OK;
+  NRK_CHECK_ARG(x && W1 && b1 && W2 && b2 && out && ws, "embed: null pointer");
+  if (ws_bytes < need) return fail(NRK_EWORKSPACE, "embed: workspace %zu < %zu", ws_bytes, need);
+  NRK_CHECK_ARG(n <= (int64_t)0x7fffffff * emb::RT, "embed: too many rows");
+  hipStream_t st = (hipStream_t)stream;
+  uint16_t* W1p = static_cast<uint16_t*>(ws);
+  uint16_t* W2p = reinterpret_cast<uint16_t*>(static_cast<char*>(ws) + align_up((size_t)3 * hidden * emb::KP * 2, 256));
+  hipLaunchKernelGGL(emb::split_planes_kernel, dim3(256), dim3(256), 0, st, W1, hidden, in_dim, emb::KP, W1p);
+  hipLaunchKernelGGL(emb::split_planes_kernel, dim3(256), dim3(256), 0, st, W2, emb::OD, hidden, hidden, W2p);
+  NRK_CHECK_LAUNCH("split_planes_kernel");
+  emb::EmbedArgs a{x, n, ldx, in_dim, hidden, W1p, b1, W2p, b2, out};
+  const size_t lds = (size_t)3 * emb::RT * emb::KP * 2 + (size_t)2 * 3 * emb::RT * emb::HC * 2;
+  hipLaunchKernelGGL(emb::embed_mlp_kernel, dim3((unsigned)cdiv(n, emb::RT)), dim3(emb::NT), lds, st, a);
+  NRK_CHECK_LAUNCH("embed_mlp_kernel");
+  return NRK_OK;
+}

@@ -8,10 +8,11 @@ the producer side of the retrieval path.
                           (best_eg_model.pth) loads with weights_only=True
   ArticleEmbeddingModel.embed   eval-mode inference for a whole corpus: the
                           BatchNorm is folded into fc.4 (W' = W diag(s),
-                          b' = b + W t) so a batch is two GEMMs with a fused
-                          bias+ReLU — library GEMMs (hipBLASLt through torch),
-                          batches of 64K rows instead of the reference's
-                          364,047 batch-1 forwards (embedding_generate.py:118-121)
+                          b' = b + W t) and both layers run in ONE hand-written
+                          kernel (libnrk nrk_embed, csrc/embed.hip: h stays on
+                          chip, fp32-exact products from three-plane bf16 MFMAs)
+                          instead of the reference's 364,047 batch-1 forwards
+                          (embedding_generate.py:118-121)
   inference               embedding_generate.py:109-131 with typed outputs:
                           ids int64 (N,) + embeddings float32 (N, 256) in one
                           .npz instead of the pickled dict / object array
@@ -67,14 +68,29 @@ class ArticleEmbeddingModel(nn.Module):
         return l1.weight, l1.bias, l2.weight * s[None, :], l2.bias + l2.weight @ t
 
     @torch.no_grad()
-    def embed(self, x: torch.Tensor, batch: int = 65536) -> torch.Tensor:
-        """Eval-mode embeddings of x (n, input_dim) -> (n, embedding_dim) f32 on x's device."""
-        W1, b1, W2, b2 = (p.detach().float() for p in self.folded())
-        out = torch.empty((x.shape[0], W2.shape[0]), dtype=torch.float32, device=x.device)
-        for lo in range(0, x.shape[0], batch):
-            xb = x[lo:lo + batch].float()
-            h = torch.addmm(b1, xb, W1.t()).clamp_min_(0.0)
-            torch.addmm(b2, h, W2.t(), out=out[lo:lo + batch])
+    def embed(self, x: torch.Tensor, batch: int | None = None) -> torch.Tensor:
+        """Eval-mode embeddings of x (n, input_dim) -> (n, embedding_dim) f32 on
+        x's device, in ONE launch of libnrk's nrk_embed (the hidden layer stays
+        on chip; fp32-exact products from bf16 MFMAs).  `batch` is accepted for
+        the older call form and ignored.  There is no CPU path: host tensors
+        raise (the module's own forward is the reference's arithmetic)."""
+        from . import _lib
+
+        dev = _lib.require_device(x, what="ArticleEmbeddingModel.embed")
+        W1, b1, W2, b2 = (p.detach().float().contiguous() for p in self.folded())
+        x = x.float()
+        if x.stride(-1) != 1:
+            x = x.contiguous()
+        n, in_dim = x.shape
+        hid, out_dim = W1.shape[0], W2.shape[0]
+        out = torch.empty((n, out_dim), dtype=torch.float32, device=dev)
+        lib = _lib.load()
+        sz = _lib.c_size(0)
+        _lib.check(lib.nrk_embed_workspace(in_dim, hid, out_dim, sz), "embed_workspace")
+        ws = torch.empty(sz.value, dtype=torch.uint8, device=dev)
+        _lib.check(lib.nrk_embed(_lib.ptr(x), n, x.stride(0), in_dim, _lib.ptr(W1), _lib.ptr(b1), hid, _lib.ptr(W2),
+                                 _lib.ptr(b2), out_dim, _lib.ptr(out), _lib.ptr(ws), ws.numel(), _lib.stream(dev)),
+                   "embed")
         return out
 
 

@@ -68,18 +68,24 @@ def _bn_inputs(cache, pooled, q):
     return [np.concatenate([q, pooled], 1), np.maximum(cache["pre.relu1"], 0), np.maximum(cache["pre.relu2"], 0)]
 
 
-@pytest.mark.parametrize("d,L,B,steps", [(128, 50, 512, 2), (256, 64, 64, 2), (256, 64, 4096, 1)])
-def test_fused_train_step_fast_path_vs_oracle_c3_shape(gpu, d, L, B, steps):
+@pytest.mark.parametrize("d,L,B,steps,A,F", [(128, 50, 512, 2, 128, 32), (256, 64, 64, 2, 128, 32),
+                                             (256, 64, 4096, 1, 128, 32), (128, 50, 512, 1, 64, 128),
+                                             (256, 128, 256, 1, 32, 128), (256, 96, 256, 1, 128, 96)])
+def test_fused_train_step_fast_path_vs_oracle_c3_shape(gpu, d, L, B, steps, A, F):
     """(128, 50, 512): configs[2]'s shape.  (256, 64, 64) and (256, 64, 4096):
     the reference's own training shape (DIN.py:16 EMBED_DIM from the 256-d
     corpus of embedding_generate.py:14; main(): A 128, F 32, max_history 64,
-    batch 64, DIN.py:233-237) and the bench's batch at that shape."""
+    batch 64, DIN.py:233-237) and the bench's batch at that shape.  The rest:
+    corners of the reference's Optuna space (DIN.py:203-207: attn_units 32..128,
+    fc_units 32..128, max_history 32..128) -- fc_units 96 / 128 take the
+    generic head kernels (W1 staged in 32-unit chunks), a d = 256 history
+    longer than 64 the generic attention step (with a warning)."""
     from newsrecommend_amd.data import synthetic_click_rows
     from newsrecommend_amd.din import DIN, FusedTrainStep
     from oracle import din_oracle as o
 
     dev = torch.device("cuda")
-    A, F, N = 128, 32, 6000
+    N = 6000
     lr, wd = 1.62e-3, 8.96e-5
     g = torch.Generator(device=dev).manual_seed(21)
     table = (torch.randn((N, d), generator=g, device=dev) * 0.5).to(torch.bfloat16)
@@ -87,8 +93,8 @@ def test_fused_train_step_fast_path_vs_oracle_c3_shape(gpu, d, L, B, steps):
     torch.manual_seed(3)
     model = DIN(d, A, F, 0.0).to(dev)
     fused = FusedTrainStep(model, table, hist, tgt, lab, B, lr=lr, weight_decay=wd, clip=1.0, graph=False)
-    print(f"FusedTrainStep path at d={d}, L={L}, B={B}: {fused.path}")
-    assert fused.fast
+    print(f"FusedTrainStep path at d={d}, L={L}, B={B}, A={A}, F={F}: {fused.path}")
+    assert fused.fast == (L <= (64 if d == 256 else 128)), fused.path
     T = table.float().cpu().numpy().astype(np.float64)
     H, Tg, Y = hist.cpu().numpy(), tgt.cpu().numpy(), lab.cpu().numpy().reshape(-1, 1).astype(np.float64)
     shapes = [(n, prm.shape, prm.numel()) for n, prm in model.named_parameters()]

@@ -31,20 +31,75 @@ def test_state_dict_keys_and_eval_forward_cpu():
     np.testing.assert_allclose(y, z["emb"], atol=1e-5, rtol=0)
 
 
-def test_typed_inference_and_loader(tmp_path):
+def test_article_table_loader(tmp_path):
+    """Retrieval.py:6-9's loader over the typed .npz inference() writes and a
+    plain numeric (N, d+1) table; the reference's own object-array table is
+    not loadable (fixture flag)."""
+    from newsrecommend_amd.embedding import load_article_table
+
+    z = np.load(os.path.join(GOLDEN, "embedding_infer.npz"))
+    path = str(tmp_path / "article_table.npz")
+    np.savez(path, ids=z["aids"], emb=z["emb"])
+    ids, emb = load_article_table(path)
+    np.testing.assert_array_equal(ids, z["aids"])
+    np.testing.assert_array_equal(emb, z["emb"])
+    num = str(tmp_path / "table.npy")
+    np.save(num, np.concatenate([z["emb"].astype(np.float64), z["aids"][:, None]], 1))
+    ids2, emb2 = load_article_table(num)
+    np.testing.assert_array_equal(ids2, z["aids"])
+    np.testing.assert_array_equal(emb2, z["emb"])
+    assert not bool(z["table_loadable"])  # the reference's own table fails Retrieval.py:6
+
+
+def test_embed_refuses_host_tensors():
+    from newsrecommend_amd._lib import NrkError
+
+    z = np.load(os.path.join(GOLDEN, "embedding_infer.npz"))
+    with pytest.raises(NrkError, match="GPU"):
+        _model(z).embed(torch.from_numpy(z["feats"]))
+
+
+@pytest.mark.gpu
+def test_typed_inference_and_loader_gpu(gpu, tmp_path):
+    """inference() (embedding_generate.py:109-131) through nrk_embed: the
+    reference's own output to 1e-5 (measured: the fp32 level), typed .npz
+    read back by the loader."""
     from newsrecommend_amd.embedding import inference, load_article_table
 
     z = np.load(os.path.join(GOLDEN, "embedding_infer.npz"))
-    m = _model(z)
+    m = _model(z).cuda()
     feats = {int(a): z["feats"][i] for i, a in enumerate(z["aids"])}
     path = str(tmp_path / "article_table.npz")
-    ids, emb = inference(m, feats, device=torch.device("cpu"), out_path=path, batch=7)
+    ids, emb = inference(m, feats, device=torch.device("cuda"), out_path=path)
     np.testing.assert_array_equal(ids, z["aids"])
-    np.testing.assert_allclose(emb, z["emb"], atol=1e-5, rtol=0)
+    err = float(np.abs(emb - z["emb"]).max())
+    print(f"nrk_embed vs the reference's inference(): {err:.3g}")
+    assert err < 1e-5, err
     ids2, emb2 = load_article_table(path)
     np.testing.assert_array_equal(ids2, ids)
     np.testing.assert_array_equal(emb2, emb)
-    assert not bool(z["table_loadable"])  # the reference's own table fails Retrieval.py:6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 4097])
+def test_embed_kernel_vs_fp64_ragged_rows(gpu, n):
+    """nrk_embed against the fp64 evaluation of the same folded model on
+    random features (row counts around the 64-row tile, a strided x view):
+    fp32-level error (<= 2e-6 relative to the output scale)."""
+    from newsrecommend_amd.embedding import ArticleEmbeddingModel
+
+    torch.manual_seed(n)
+    m = ArticleEmbeddingModel().cuda().eval()
+    with torch.no_grad():
+        m.fc[3].running_mean.uniform_(-0.2, 0.2)
+        m.fc[3].running_var.uniform_(0.5, 1.5)
+    big = torch.randn(n, 300, device="cuda") * 2
+    x = big[:, 5:258]  # rows 300 floats apart
+    y = m.embed(x).double().cpu()
+    W1, b1, W2, b2 = (p.detach().double().cpu() for p in m.folded())
+    ref = torch.relu(x.double().cpu() @ W1.t() + b1) @ W2.t() + b2
+    err = float((y - ref).abs().max())
+    assert err <= 2e-6 * max(1.0, float(ref.abs().max())), err
 
 
 def test_triplet_dataset_semantics():
@@ -64,7 +119,7 @@ def test_embed_gpu_and_triplet_step(gpu):
 
     z = np.load(os.path.join(GOLDEN, "embedding_infer.npz"))
     m = _model(z).cuda()
-    y = m.embed(torch.from_numpy(z["feats"]).cuda(), batch=16).cpu().numpy()
+    y = m.embed(torch.from_numpy(z["feats"]).cuda()).cpu().numpy()
     np.testing.assert_allclose(y, z["emb"], atol=1e-5, rtol=0)
     torch.manual_seed(0)
     mt = ArticleEmbeddingModel().cuda()
