@@ -108,6 +108,8 @@ def load(path: str = LIB_PATH):
                            "(there is no CPU fallback for the HIP path)")
         lib = ctypes.CDLL(path)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("NRK_LIB") and not hasattr(lib, name):
+                continue  # an A/B build of an older library: entry points it lacks stay unbound
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

@@ -121,22 +121,41 @@ __global__ __launch_bounds__(NT, 1) void embed_mlp_kernel(EmbedArgs a) {
 
   const int ht = w & 3, rp = w >> 2;  // layer 1: hidden tile, row-tile pair
   const int nch = a.H / HC;
+  const int64_t ps1 = (int64_t)a.H * KP, ps2 = (int64_t)OD * a.H;  // plane strides
+  // Weight fragments come from L2 one step ahead: layer 1's for chunk j + 1
+  // are loaded under layer 2 of chunk j, layer 2's for chunk j under layer 1
+  // of chunk j (an L2 round trip per K step would stall the MFMA chain).
+  bf16x8 b1f[KP / 32][3], b2f[HC / 32][2][3];
+  auto load_b1 = [&](int j) __attribute__((always_inline)) {
+    const uint16_t* wb = a.W1p + (int64_t)(j * HC + 16 * ht + l15) * KP + 8 * l4;
+#pragma unroll
+    for (int s = 0; s < KP / 32; ++s)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) b1f[s][p] = *reinterpret_cast<const bf16x8*>(wb + p * ps1 + 32 * s);
+  };
+  auto load_b2 = [&](int j) __attribute__((always_inline)) {
+#pragma unroll
+    for (int s = 0; s < HC / 32; ++s)
+#pragma unroll
+      for (int oc = 0; oc < 2; ++oc) {
+        const uint16_t* wb = a.W2p + (int64_t)(32 * w + 16 * oc + l15) * a.H + j * HC + 32 * s + 8 * l4;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) b2f[s][oc][p] = *reinterpret_cast<const bf16x8*>(wb + p * ps2);
+      }
+  };
+  load_b1(0);
   for (int j = 0; j < nch; ++j) {
     unsigned char* hb = hs + (j & 1) * 3 * HPL;
     // (this H buffer was last read by layer 2 of chunk j - 2, which every wave
     // finished before chunk j - 1's second barrier)
     if (j == 0) __syncthreads();  // the x planes published
+    load_b2(j);
     // ---- layer 1: H_j tiles (rt = 2 rp + {0, 1}, ht)
     {
       const int u = j * HC + 16 * ht + l15;  // hidden unit of this lane's B column
-      const uint16_t* wb = a.W1p + (int64_t)u * KP + 8 * l4;
-      const int64_t ps = (int64_t)a.H * KP;  // plane stride
       f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
-#pragma unroll 2
-      for (int s = 0; s < KP / 32; ++s) {
-        bf16x8 b[3];
 #pragma unroll
-        for (int p = 0; p < 3; ++p) b[p] = *reinterpret_cast<const bf16x8*>(wb + p * ps + 32 * s);
+      for (int s = 0; s < KP / 32; ++s) {
         bf16x8 x0[3], x1[3];
         const int o0 = poff<KP>(16 * (2 * rp) + l15, 4 * s + l4), o1 = poff<KP>(16 * (2 * rp + 1) + l15, 4 * s + l4);
 #pragma unroll
@@ -144,8 +163,8 @@ __global__ __launch_bounds__(NT, 1) void embed_mlp_kernel(EmbedArgs a) {
           x0[p] = *reinterpret_cast<const bf16x8*>(xs + p * XPL + o0);
           x1[p] = *reinterpret_cast<const bf16x8*>(xs + p * XPL + o1);
         }
-        c0 = mfma6(x0, b, c0);
-        c1 = mfma6(x1, b, c1);
+        c0 = mfma6(x0, b1f[s], c0);
+        c1 = mfma6(x1, b1f[s], c1);
       }
       const float bu = a.b1[u];
       const int col = 16 * ht + l15;  // within the chunk
@@ -165,27 +184,18 @@ __global__ __launch_bounds__(NT, 1) void embed_mlp_kernel(EmbedArgs a) {
       }
     }
     __syncthreads();  // H_j published
+    if (j + 1 < nch) load_b1(j + 1);
     // ---- layer 2: O[:, 32 w .. 32 w + 31] += H_j W2[32 w .., j chunk]^T
-    {
-      const int64_t ps = (int64_t)OD * a.H;
 #pragma unroll
-      for (int s = 0; s < HC / 32; ++s) {
-        bf16x8 b[2][3];
+    for (int s = 0; s < HC / 32; ++s) {
 #pragma unroll
-        for (int oc = 0; oc < 2; ++oc) {
-          const uint16_t* wb = a.W2p + (int64_t)(32 * w + 16 * oc + l15) * a.H + j * HC + 32 * s + 8 * l4;
+      for (int rt = 0; rt < 4; ++rt) {
+        bf16x8 hx[3];
+        const int o = poff<HC>(16 * rt + l15, 4 * s + l4);
 #pragma unroll
-          for (int p = 0; p < 3; ++p) b[oc][p] = *reinterpret_cast<const bf16x8*>(wb + p * ps);
-        }
+        for (int p = 0; p < 3; ++p) hx[p] = *reinterpret_cast<const bf16x8*>(hb + p * HPL + o);
 #pragma unroll
-        for (int rt = 0; rt < 4; ++rt) {
-          bf16x8 hx[3];
-          const int o = poff<HC>(16 * rt + l15, 4 * s + l4);
-#pragma unroll
-          for (int p = 0; p < 3; ++p) hx[p] = *reinterpret_cast<const bf16x8*>(hb + p * HPL + o);
-#pragma unroll
-          for (int oc = 0; oc < 2; ++oc) acc2[rt][oc] = mfma6(hx, b[oc], acc2[rt][oc]);
-        }
+        for (int oc = 0; oc < 2; ++oc) acc2[rt][oc] = mfma6(hx, b2f[s][oc], acc2[rt][oc]);
       }
     }
   }
