@@ -800,13 +800,18 @@ __global__ __launch_bounds__(256) void din_bwd_kernel(
           dz[g] = v;
           du += v;
         }
-        // dW1k[n][c] += sum_rows dz[row][n] K[row][c]
+        // dW1k[n][c] += sum_rows dz[row][n] K[row][c]; dz enters as bf16 hi + lo
+        // (this generic kernel is off the timed path: near-fp32 gradients)
         if constexpr (BF16) {
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
-            bf16x8 af;
+            bf16x8 af, afl;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) af[j] = (short)f32_to_bf16_rne(dz[8 * s + j]);
+            for (int j = 0; j < 8; ++j) {
+              const uint16_t hb = f32_to_bf16_rne(dz[8 * s + j]);
+              af[j] = (short)hb;
+              afl[j] = (short)f32_to_bf16_rne(dz[8 * s + j] - bf16_to_f32(hb));
+            }
             // B operand: lane (c, h) element j = K[16s + 8(j>>2) + 4h + (j&3)][c]
             const int grp = lane >> 4, i16 = lane & 15;
             const int rowq = 32 * ct + 16 * s + 4 * h + (i16 >> 2);
@@ -821,6 +826,7 @@ __global__ __launch_bounds__(256) void din_bwd_kernel(
               bf16x8 bf;
               bf[0] = lo[0]; bf[1] = lo[1]; bf[2] = lo[2]; bf[3] = lo[3];
               bf[4] = hi[0]; bf[5] = hi[1]; bf[6] = hi[2]; bf[7] = hi[3];
+              dw[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afl, bf, dw[c], 0, 0, 0);
               dw[c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, dw[c], 0, 0, 0);
             }
           }

@@ -12,24 +12,25 @@
 // v_mfma_f32_16x16x32_bf16 per 16x16x32 block deliver 2.5 / 6 = 0.42 PF/s of
 // fp32-exact products at peak, 2.65x the 157 TF/s of v_mfma_f32_32x32x2_f32.
 //
-// One 512-thread workgroup (8 waves) per 64-row tile, one per CU (LDS):
-//   x tile -> three bf16 planes in LDS (swizzled 16-B chunks: conflict-free
-//   16x16x32 A-fragment reads), then per chunk of HC = 64 hidden units:
-//   layer 1  H_j = relu(x W1[j]^T + b1[j]) (wave w: hidden tile w & 3, row
-//            tiles 2 (w >> 2) + {0, 1}; W1 fragments from L2, reused over the
-//            two row tiles), split into three planes in LDS (double-buffered);
-//   layer 2  O += H_j W2[:, j]^T (wave w: output columns 32 w .. 32 w + 31,
-//            all 64 rows: 8 accumulator tiles resident over the chunks).
+// One 256-thread workgroup (4 waves, one per SIMD) per 64-row tile, one per
+// CU (LDS): x tile -> three bf16 planes in LDS (swizzled 16-B chunks:
+// conflict-free 16x16x32 A-fragment reads), then per chunk of HC = 128
+// hidden units:
+//   layer 1  H_j = relu(x W1[j]^T + b1[j]) (wave w: hidden units 32 w ..
+//            32 w + 31 of the chunk, all 64 rows; W1 fragments from L2, each
+//            reused over the four row tiles), split into three planes in LDS;
+//   layer 2  O += H_j W2[:, j]^T (wave w: output columns 64 w .. 64 w + 63,
+//            all 64 rows: 16 accumulator tiles resident over the chunks).
 // Finally O + b2' -> HBM.
 #include "nrk_common.h"
 
 namespace nrk {
 namespace emb {
 
-constexpr int NT = 512;  // 8 waves
+constexpr int NT = 256;  // 4 waves: one per SIMD
 constexpr int RT = 64;   // rows per workgroup
 constexpr int KP = 256;  // input width, zero-padded (253 -> 256)
-constexpr int HC = 64;   // hidden units per chunk
+constexpr int HC = 128;  // hidden units per chunk
 constexpr int OD = 256;  // output width
 
 // byte offset of 16-B chunk `chunk` of `row` in a [rows][W] bf16 plane
@@ -72,26 +73,45 @@ struct EmbedArgs {
   float* out;           // [n][OD]
 };
 
+// Register blocking: one wave per SIMD, each with a 64-row x 32-column tile of
+// layer 1 (a chunk of HC = 128 hidden units over the four waves) and a 64-row
+// x 64-column tile of layer 2: per K step a wave reads 4 row fragments (x 3
+// planes) from LDS and 2 / 4 column fragments (x 3 planes) from L2 for 48 / 96
+// MFMAs, so neither LDS nor L2 bandwidth paces the MFMA chain.  The next K
+// step's weight fragments are loaded during the current one.
 __global__ __launch_bounds__(NT, 1) void embed_mlp_kernel(EmbedArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int XPL = RT * KP * 2;  // bytes per x plane
   constexpr int HPL = RT * HC * 2;  // bytes per H plane
-  unsigned char* xs = smem;              // [3] x planes
-  unsigned char* hs = smem + 3 * XPL;    // [2 buffers][3] H planes
+  unsigned char* xs = smem;            // [3] x planes
+  unsigned char* hs = smem + 3 * XPL;  // [3] H planes
   const int tid = threadIdx.x, lane = tid & 63, l15 = lane & 15, l4 = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t r0 = (int64_t)blockIdx.x * RT;
 
-  // ---- x tile -> three planes: thread = (row, 8-column chunk); 4 chunks per thread
+  // ---- x tile -> three planes: thread = (row, 8-column piece)
   {
     constexpr int CPR = KP / 8, NPT = RT * CPR / NT;
     float v[NPT][8];
+    // unconditional loads of clamped addresses, masked afterwards: all of them
+    // in flight at once (a conditional load per element became a branch each,
+    // and the tile's loads ran one HBM latency after another)
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
       const int e = tid + NT * k, row = e / CPR, c0 = 8 * (e % CPR);
-      const int64_t r = r0 + row;
+      const int64_t r = r0 + row, rc = r < a.n ? r : a.n - 1;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[k][j] = r < a.n && c0 + j < a.in_dim ? a.x[r * a.ldx + c0 + j] : 0.f;
+      for (int j = 0; j < 8; ++j) {
+        const int c = c0 + j < a.in_dim ? c0 + j : a.in_dim - 1;
+        v[k][j] = a.x[rc * a.ldx + c];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      const int e = tid + NT * k, row = e / CPR, c0 = 8 * (e % CPR);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (r0 + row >= a.n || c0 + j >= a.in_dim) v[k][j] = 0.f;
     }
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
@@ -111,98 +131,95 @@ __global__ __launch_bounds__(NT, 1) void embed_mlp_kernel(EmbedArgs a) {
       *reinterpret_cast<bf16x8*>(xs + 2 * XPL + o) = pl;
     }
   }
-
-  // layer 2's accumulators: rows 16 rt + 4 l4 + i, output columns 32 w + 16 oc + l15
-  f32x4 acc2[4][2];
+  f32x4 acc2[4][4];  // layer 2: row tile rt, column tile oc (columns 64 w + 16 oc + l15)
 #pragma unroll
   for (int rt = 0; rt < 4; ++rt)
 #pragma unroll
-    for (int oc = 0; oc < 2; ++oc) acc2[rt][oc] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int ht = w & 3, rp = w >> 2;  // layer 1: hidden tile, row-tile pair
+    for (int oc = 0; oc < 4; ++oc) acc2[rt][oc] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nch = a.H / HC;
   const int64_t ps1 = (int64_t)a.H * KP, ps2 = (int64_t)OD * a.H;  // plane strides
-  // Weight fragments come from L2 one step ahead: layer 1's for chunk j + 1
-  // are loaded under layer 2 of chunk j, layer 2's for chunk j under layer 1
-  // of chunk j (an L2 round trip per K step would stall the MFMA chain).
-  bf16x8 b1f[KP / 32][3], b2f[HC / 32][2][3];
-  auto load_b1 = [&](int j) __attribute__((always_inline)) {
-    const uint16_t* wb = a.W1p + (int64_t)(j * HC + 16 * ht + l15) * KP + 8 * l4;
-#pragma unroll
-    for (int s = 0; s < KP / 32; ++s)
-#pragma unroll
-      for (int p = 0; p < 3; ++p) b1f[s][p] = *reinterpret_cast<const bf16x8*>(wb + p * ps1 + 32 * s);
-  };
-  auto load_b2 = [&](int j) __attribute__((always_inline)) {
-#pragma unroll
-    for (int s = 0; s < HC / 32; ++s)
-#pragma unroll
-      for (int oc = 0; oc < 2; ++oc) {
-        const uint16_t* wb = a.W2p + (int64_t)(32 * w + 16 * oc + l15) * a.H + j * HC + 32 * s + 8 * l4;
-#pragma unroll
-        for (int p = 0; p < 3; ++p) b2f[s][oc][p] = *reinterpret_cast<const bf16x8*>(wb + p * ps2);
-      }
-  };
-  load_b1(0);
   for (int j = 0; j < nch; ++j) {
-    unsigned char* hb = hs + (j & 1) * 3 * HPL;
-    // (this H buffer was last read by layer 2 of chunk j - 2, which every wave
-    // finished before chunk j - 1's second barrier)
-    if (j == 0) __syncthreads();  // the x planes published
-    load_b2(j);
-    // ---- layer 1: H_j tiles (rt = 2 rp + {0, 1}, ht)
+    __syncthreads();  // j = 0: the x planes published; else layer 2 of chunk j - 1 is done with H
+    // ---- layer 1: hidden units j HC + 32 w + 16 ct + l15, all 64 rows
     {
-      const int u = j * HC + 16 * ht + l15;  // hidden unit of this lane's B column
-      f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
+      const uint16_t* wb = a.W1p + (int64_t)(j * HC + 32 * w + l15) * KP + 8 * l4;
+      bf16x8 bf[2][2][3];  // [buffer][ct][plane]
+      auto load_b = [&](int s, int nb) __attribute__((always_inline)) {
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+            bf[nb][ct][p] = *reinterpret_cast<const bf16x8*>(wb + (int64_t)16 * ct * KP + p * ps1 + 32 * s);
+      };
+      f32x4 c[4][2];
+#pragma unroll
+      for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) c[rt][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+      load_b(0, 0);
 #pragma unroll
       for (int s = 0; s < KP / 32; ++s) {
-        bf16x8 x0[3], x1[3];
-        const int o0 = poff<KP>(16 * (2 * rp) + l15, 4 * s + l4), o1 = poff<KP>(16 * (2 * rp + 1) + l15, 4 * s + l4);
+        if (s + 1 < KP / 32) load_b(s + 1, (s + 1) & 1);
 #pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          x0[p] = *reinterpret_cast<const bf16x8*>(xs + p * XPL + o0);
-          x1[p] = *reinterpret_cast<const bf16x8*>(xs + p * XPL + o1);
+        for (int rt = 0; rt < 4; ++rt) {
+          bf16x8 xa[3];
+          const int o = poff<KP>(16 * rt + l15, 4 * s + l4);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) xa[p] = *reinterpret_cast<const bf16x8*>(xs + p * XPL + o);
+#pragma unroll
+          for (int ct = 0; ct < 2; ++ct) c[rt][ct] = mfma6(xa, bf[s & 1][ct], c[rt][ct]);
         }
-        c0 = mfma6(x0, b1f[s], c0);
-        c1 = mfma6(x1, b1f[s], c1);
       }
-      const float bu = a.b1[u];
-      const int col = 16 * ht + l15;  // within the chunk
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const f32x4 c = t ? c1 : c0;
+      for (int ct = 0; ct < 2; ++ct) {
+        const int col = 32 * w + 16 * ct + l15;  // within the chunk
+        const float bu = a.b1[j * HC + col];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = 16 * (2 * rp + t) + 4 * l4 + i;
-          short h, m, l;
-          split3(fmaxf(c[i] + bu, 0.f), h, m, l);
-          const int o = poff<HC>(row, col >> 3) + 2 * (col & 7);
-          *reinterpret_cast<short*>(hb + o) = h;
-          *reinterpret_cast<short*>(hb + HPL + o) = m;
-          *reinterpret_cast<short*>(hb + 2 * HPL + o) = l;
-        }
+        for (int rt = 0; rt < 4; ++rt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int row = 16 * rt + 4 * l4 + i;
+            short h, m, l;
+            split3(fmaxf(c[rt][ct][i] + bu, 0.f), h, m, l);
+            const int o = poff<HC>(row, col >> 3) + 2 * (col & 7);
+            *reinterpret_cast<short*>(hs + o) = h;
+            *reinterpret_cast<short*>(hs + HPL + o) = m;
+            *reinterpret_cast<short*>(hs + 2 * HPL + o) = l;
+          }
       }
     }
     __syncthreads();  // H_j published
-    if (j + 1 < nch) load_b1(j + 1);
-    // ---- layer 2: O[:, 32 w .. 32 w + 31] += H_j W2[32 w .., j chunk]^T
+    // ---- layer 2: O[:, 64 w .. 64 w + 63] += H_j W2[64 w .., chunk j]^T
+    {
+      const uint16_t* wb = a.W2p + (int64_t)(64 * w + l15) * a.H + j * HC + 8 * l4;
+      bf16x8 bf[2][4][3];
+      auto load_b = [&](int s, int nb) __attribute__((always_inline)) {
 #pragma unroll
-    for (int s = 0; s < HC / 32; ++s) {
+        for (int oc = 0; oc < 4; ++oc)
 #pragma unroll
-      for (int rt = 0; rt < 4; ++rt) {
-        bf16x8 hx[3];
-        const int o = poff<HC>(16 * rt + l15, 4 * s + l4);
+          for (int p = 0; p < 3; ++p)
+            bf[nb][oc][p] = *reinterpret_cast<const bf16x8*>(wb + (int64_t)16 * oc * a.H + p * ps2 + 32 * s);
+      };
+      load_b(0, 0);
 #pragma unroll
-        for (int p = 0; p < 3; ++p) hx[p] = *reinterpret_cast<const bf16x8*>(hb + p * HPL + o);
+      for (int s = 0; s < HC / 32; ++s) {
+        if (s + 1 < HC / 32) load_b(s + 1, (s + 1) & 1);
 #pragma unroll
-        for (int oc = 0; oc < 2; ++oc) acc2[rt][oc] = mfma6(hx, b2f[s][oc], acc2[rt][oc]);
+        for (int rt = 0; rt < 4; ++rt) {
+          bf16x8 hx[3];
+          const int o = poff<HC>(16 * rt + l15, 4 * s + l4);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) hx[p] = *reinterpret_cast<const bf16x8*>(hs + p * HPL + o);
+#pragma unroll
+          for (int oc = 0; oc < 4; ++oc) acc2[rt][oc] = mfma6(hx, bf[s & 1][oc], acc2[rt][oc]);
+        }
       }
     }
   }
   // ---- O + b2 -> HBM
 #pragma unroll
-  for (int oc = 0; oc < 2; ++oc) {
-    const int col = 32 * w + 16 * oc + l15;
+  for (int oc = 0; oc < 4; ++oc) {
+    const int col = 64 * w + 16 * oc + l15;
     const float bo = a.b2[col];
 #pragma unroll
     for (int rt = 0; rt < 4; ++rt)
@@ -261,7 +278,7 @@ extern "C" int nrk_embed(const float* x, int64_t n, int64_t ldx, int32_t in_dim,
   hipLaunchKernelGGL(emb::split_planes_kernel, dim3(256), dim3(256), 0, st, W2, emb::OD, hidden, hidden, W2p);
   NRK_CHECK_LAUNCH("split_planes_kernel");
   emb::EmbedArgs a{x, n, ldx, in_dim, hidden, W1p, b1, W2p, b2, out};
-  const size_t lds = (size_t)3 * emb::RT * emb::KP * 2 + (size_t)2 * 3 * emb::RT * emb::HC * 2;
+  const size_t lds = (size_t)3 * emb::RT * emb::KP * 2 + (size_t)3 * emb::RT * emb::HC * 2;
   hipLaunchKernelGGL(emb::embed_mlp_kernel, dim3((unsigned)cdiv(n, emb::RT)), dim3(emb::NT), lds, st, a);
   NRK_CHECK_LAUNCH("embed_mlp_kernel");
   return NRK_OK;
