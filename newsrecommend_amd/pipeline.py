@@ -227,7 +227,8 @@ def fused_ok(model, table: torch.Tensor, L: int):
                              (f"attn_units {A} not in (32, 64, 96, 128)", A not in (32, 64, 96, 128)),
                              (f"fc_units {F} not in (32, 64, 96, 128)", F not in (32, 64, 96, 128)),
                              ("model emb_dim != table width", W1.shape[1] != 2 * d),
-                             ("BatchNorm without running statistics", _fold_eval_head(model.fc) is None)) if bad]
+                             ("BatchNorm without running statistics",
+                              any(model.fc[i].running_mean is None for i in (0, 4, 8)))) if bad]
 
 
 @torch.no_grad()
@@ -236,10 +237,11 @@ def rerank(model, table: torch.Tensor, hist_rows: torch.Tensor, cand_rows: torch
     """DIN logits (U, C) for candidate rows (U, C) (-1 = padding -> -inf) of
     users with history rows (U, L) (-1 = padding), all rows of `table` on the
     device.  Eval-mode BatchNorm is row-independent, so one forward over many
-    users equals the reference's per-user forwards.  With a bf16 table,
-    d in {64, 128, 256}, L <= 64, A and F in {32, 64, 96, 128} the whole
-    evaluate() forward is one fused kernel (nrk_din_rerank); otherwise every
-    candidate is a DIN sample (model.forward_ids, C x the attention work)."""
+    users equals the reference's per-user forwards.  With a bf16 or f32
+    table, d in {64, 128, 256}, L <= 64, A and F in {32, 64, 96, 128} the whole
+    evaluate() forward is one fused kernel (nrk_din_rerank; an f32 table
+    through the row projections, rerank_ragged); otherwise every candidate is
+    a DIN sample (model.forward_ids, C x the attention work)."""
     model.eval()
     U, C = cand_rows.shape
     L = hist_rows.shape[1]
