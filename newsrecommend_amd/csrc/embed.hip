@@ -89,46 +89,37 @@ __global__ __launch_bounds__(NT, 1) void embed_mlp_kernel(EmbedArgs a) {
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t r0 = (int64_t)blockIdx.x * RT;
 
-  // ---- x tile -> three planes: thread = (row, 8-column piece)
+  // ---- x tile -> three planes.  Wave w loads rows 16 w .. 16 w + 15, lane l the
+  // columns l, l + 64, l + 128, l + 192 of each: every load instruction reads
+  // 256 contiguous bytes of one row (a (row, 8-column piece) split made each
+  // instruction touch 16 cache lines for 256 B).  All loads are in flight before
+  // the first is used (clamped addresses, masked afterwards); the planes are
+  // written element by element.
   {
-    constexpr int CPR = KP / 8, NPT = RT * CPR / NT;
-    float v[NPT][8];
-    // unconditional loads of clamped addresses, masked afterwards: all of them
-    // in flight at once (a conditional load per element became a branch each,
-    // and the tile's loads ran one HBM latency after another)
+    constexpr int RPW = RT / 4;  // rows per wave
+    float v[RPW][4];
 #pragma unroll
-    for (int k = 0; k < NPT; ++k) {
-      const int e = tid + NT * k, row = e / CPR, c0 = 8 * (e % CPR);
-      const int64_t r = r0 + row, rc = r < a.n ? r : a.n - 1;
+    for (int i = 0; i < RPW; ++i) {
+      const int64_t r = r0 + RPW * w + i, rc = r < a.n ? r : a.n - 1;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int c = c0 + j < a.in_dim ? c0 + j : a.in_dim - 1;
-        v[k][j] = a.x[rc * a.ldx + c];
+      for (int q = 0; q < 4; ++q) {
+        const int c = 64 * q + lane, cc = c < a.in_dim ? c : a.in_dim - 1;
+        v[i][q] = __builtin_nontemporal_load(a.x + rc * a.ldx + cc);
       }
     }
 #pragma unroll
-    for (int k = 0; k < NPT; ++k) {
-      const int e = tid + NT * k, row = e / CPR, c0 = 8 * (e % CPR);
+    for (int i = 0; i < RPW; ++i) {
+      const int row = RPW * w + i;
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (r0 + row >= a.n || c0 + j >= a.in_dim) v[k][j] = 0.f;
-    }
-#pragma unroll
-    for (int k = 0; k < NPT; ++k) {
-      const int e = tid + NT * k, row = e / CPR, cc = e % CPR;
-      bf16x8 ph, pm, pl;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int q = 0; q < 4; ++q) {
+        const int c = 64 * q + lane;
         short h, m, l;
-        split3(v[k][j], h, m, l);
-        ph[j] = h;
-        pm[j] = m;
-        pl[j] = l;
+        split3(r0 + row < a.n && c < a.in_dim ? v[i][q] : 0.f, h, m, l);
+        const int o = poff<KP>(row, c >> 3) + 2 * (c & 7);
+        *reinterpret_cast<short*>(xs + o) = h;
+        *reinterpret_cast<short*>(xs + XPL + o) = m;
+        *reinterpret_cast<short*>(xs + 2 * XPL + o) = l;
       }
-      const int o = poff<KP>(row, cc);
-      *reinterpret_cast<bf16x8*>(xs + o) = ph;
-      *reinterpret_cast<bf16x8*>(xs + XPL + o) = pm;
-      *reinterpret_cast<bf16x8*>(xs + 2 * XPL + o) = pl;
     }
   }
   f32x4 acc2[4][4];  // layer 2: row tile rt, column tile oc (columns 64 w + 16 oc + l15)
@@ -160,6 +151,9 @@ __global__ __launch_bounds__(NT, 1) void embed_mlp_kernel(EmbedArgs a) {
 #pragma unroll
       for (int s = 0; s < KP / 32; ++s) {
         if (s + 1 < KP / 32) load_b(s + 1, (s + 1) & 1);
+        // keep the prefetch ahead of this step's MFMAs (the scheduler otherwise
+        // sinks each load next to its first use and waits out the L2 latency)
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int rt = 0; rt < 4; ++rt) {
           bf16x8 xa[3];
@@ -204,6 +198,7 @@ __global__ __launch_bounds__(NT, 1) void embed_mlp_kernel(EmbedArgs a) {
 #pragma unroll
       for (int s = 0; s < HC / 32; ++s) {
         if (s + 1 < HC / 32) load_b(s + 1, (s + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int rt = 0; rt < 4; ++rt) {
           bf16x8 hx[3];
@@ -226,7 +221,7 @@ __global__ __launch_bounds__(NT, 1) void embed_mlp_kernel(EmbedArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int64_t r = r0 + 16 * rt + 4 * l4 + i;
-        if (r < a.n) a.out[r * OD + col] = acc2[rt][oc][i] + bo;
+        if (r < a.n) __builtin_nontemporal_store(acc2[rt][oc][i] + bo, a.out + r * OD + col);  // (streamed: keep L2 for the weights)
       }
   }
 }
