@@ -66,9 +66,14 @@ struct EmbedArgs {
   const float* x;  // [n][ldx], in_dim <= KP used
   int64_t n, ldx;
   int in_dim, H;
-  const uint16_t* W1p;  // [3][H][KP] bf16 planes of fc.0.weight (zero-padded columns)
+  // Weights as bf16 planes in MFMA B-fragment order: fragment (n16, s, plane) =
+  // rows 16 n16 .. + 15, columns 32 s .. + 31 of that plane, 1 KiB, lane
+  // l15 + 16 l4 holding row 16 n16 + l15, columns 32 s + 8 l4 .. + 7 — one
+  // fragment is one contiguous wave load (row-major planes made each load 16
+  // half-lines of 16 rows).
+  const uint16_t* W1p;  // fc.0.weight, [H / 16][KP / 32][3] fragments (zero-padded columns)
   const float* b1;      // [H]
-  const uint16_t* W2p;  // [3][OD][H] bf16 planes of the folded fc.4 weight
+  const uint16_t* W2p;  // the folded fc.4 weight, [OD / 16][H / 32][3] fragments
   const float* b2;      // [OD]
   float* out;           // [n][OD]
 };
@@ -128,42 +133,58 @@ __global__ __launch_bounds__(NT, 1) void embed_mlp_kernel(EmbedArgs a) {
 #pragma unroll
     for (int oc = 0; oc < 4; ++oc) acc2[rt][oc] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nch = a.H / HC;
-  const int64_t ps1 = (int64_t)a.H * KP, ps2 = (int64_t)OD * a.H;  // plane strides
+  // Software pipeline, pinned with scheduling barriers (the scheduler otherwise
+  // sinks each load next to its first use and waits out its latency with one
+  // wave per SIMD and nothing else to issue): per (K step, row tile) pair the
+  // next pair's A fragments are read from LDS, and per K step the next step's
+  // weight fragments are loaded from L2, one step (4 pairs) ahead.  The first
+  // weight step of each layer is loaded while the other layer finishes.
+  bf16x8 b1f[2][2][3];  // layer-1 weights [buffer][ct][plane]
+  bf16x8 b2f[2][4][3];  // layer-2 weights [buffer][oc][plane]
+  auto load_b1 = [&](int j, int s, int nb) __attribute__((always_inline)) {
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      const uint16_t* wb = a.W1p + ((int64_t)((j * HC / 16 + 2 * w + ct) * (KP / 32) + s) * 3) * 512 + 8 * lane;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) b1f[nb][ct][p] = *reinterpret_cast<const bf16x8*>(wb + 512 * p);
+    }
+  };
+  auto load_b2 = [&](int j, int s, int nb) __attribute__((always_inline)) {
+#pragma unroll
+    for (int oc = 0; oc < 4; ++oc) {
+      const uint16_t* wb = a.W2p + ((int64_t)((4 * w + oc) * (a.H / 32) + j * (HC / 32) + s) * 3) * 512 + 8 * lane;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) b2f[nb][oc][p] = *reinterpret_cast<const bf16x8*>(wb + 512 * p);
+    }
+  };
+  load_b1(0, 0, 0);
   for (int j = 0; j < nch; ++j) {
     __syncthreads();  // j = 0: the x planes published; else layer 2 of chunk j - 1 is done with H
     // ---- layer 1: hidden units j HC + 32 w + 16 ct + l15, all 64 rows
     {
-      const uint16_t* wb = a.W1p + (int64_t)(j * HC + 32 * w + l15) * KP + 8 * l4;
-      bf16x8 bf[2][2][3];  // [buffer][ct][plane]
-      auto load_b = [&](int s, int nb) __attribute__((always_inline)) {
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-          for (int p = 0; p < 3; ++p)
-            bf[nb][ct][p] = *reinterpret_cast<const bf16x8*>(wb + (int64_t)16 * ct * KP + p * ps1 + 32 * s);
-      };
       f32x4 c[4][2];
 #pragma unroll
       for (int rt = 0; rt < 4; ++rt)
 #pragma unroll
         for (int ct = 0; ct < 2; ++ct) c[rt][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-      load_b(0, 0);
+      bf16x8 xa[2][3];
+      auto load_a = [&](int it, int nb) __attribute__((always_inline)) {
+        const int o = poff<KP>(16 * (it & 3) + l15, 4 * (it >> 2) + l4);
 #pragma unroll
-      for (int s = 0; s < KP / 32; ++s) {
-        if (s + 1 < KP / 32) load_b(s + 1, (s + 1) & 1);
-        // keep the prefetch ahead of this step's MFMAs (the scheduler otherwise
-        // sinks each load next to its first use and waits out the L2 latency)
+        for (int p = 0; p < 3; ++p) xa[nb][p] = *reinterpret_cast<const bf16x8*>(xs + p * XPL + o);
+      };
+      load_a(0, 0);
+#pragma unroll
+      for (int it = 0; it < 4 * (KP / 32); ++it) {
+        const int s = it >> 2, rt = it & 3;
+        if (rt == 0 && s + 1 < KP / 32) load_b1(j, s + 1, (s + 1) & 1);
+        if (it + 1 < 4 * (KP / 32)) load_a(it + 1, (it + 1) & 1);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int rt = 0; rt < 4; ++rt) {
-          bf16x8 xa[3];
-          const int o = poff<KP>(16 * rt + l15, 4 * s + l4);
-#pragma unroll
-          for (int p = 0; p < 3; ++p) xa[p] = *reinterpret_cast<const bf16x8*>(xs + p * XPL + o);
-#pragma unroll
-          for (int ct = 0; ct < 2; ++ct) c[rt][ct] = mfma6(xa, bf[s & 1][ct], c[rt][ct]);
-        }
+        for (int ct = 0; ct < 2; ++ct) c[rt][ct] = mfma6(xa[it & 1], b1f[s & 1][ct], c[rt][ct]);
+        __builtin_amdgcn_sched_barrier(0);
       }
+      load_b2(j, 0, 0);
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct) {
         const int col = 32 * w + 16 * ct + l15;  // within the chunk
@@ -185,29 +206,23 @@ __global__ __launch_bounds__(NT, 1) void embed_mlp_kernel(EmbedArgs a) {
     __syncthreads();  // H_j published
     // ---- layer 2: O[:, 64 w .. 64 w + 63] += H_j W2[64 w .., chunk j]^T
     {
-      const uint16_t* wb = a.W2p + (int64_t)(64 * w + l15) * a.H + j * HC + 8 * l4;
-      bf16x8 bf[2][4][3];
-      auto load_b = [&](int s, int nb) __attribute__((always_inline)) {
+      bf16x8 hx[2][3];
+      auto load_h = [&](int it, int nb) __attribute__((always_inline)) {
+        const int o = poff<HC>(16 * (it & 3) + l15, 4 * (it >> 2) + l4);
 #pragma unroll
-        for (int oc = 0; oc < 4; ++oc)
-#pragma unroll
-          for (int p = 0; p < 3; ++p)
-            bf[nb][oc][p] = *reinterpret_cast<const bf16x8*>(wb + (int64_t)16 * oc * a.H + p * ps2 + 32 * s);
+        for (int p = 0; p < 3; ++p) hx[nb][p] = *reinterpret_cast<const bf16x8*>(hs + p * HPL + o);
       };
-      load_b(0, 0);
+      load_h(0, 0);
 #pragma unroll
-      for (int s = 0; s < HC / 32; ++s) {
-        if (s + 1 < HC / 32) load_b(s + 1, (s + 1) & 1);
+      for (int it = 0; it < 4 * (HC / 32); ++it) {
+        const int s = it >> 2, rt = it & 3;
+        if (rt == 0 && s + 1 < HC / 32) load_b2(j, s + 1, (s + 1) & 1);
+        if (rt == 0 && s + 1 == HC / 32 && j + 1 < nch) load_b1(j + 1, 0, 0);
+        if (it + 1 < 4 * (HC / 32)) load_h(it + 1, (it + 1) & 1);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int rt = 0; rt < 4; ++rt) {
-          bf16x8 hx[3];
-          const int o = poff<HC>(16 * rt + l15, 4 * s + l4);
-#pragma unroll
-          for (int p = 0; p < 3; ++p) hx[p] = *reinterpret_cast<const bf16x8*>(hs + p * HPL + o);
-#pragma unroll
-          for (int oc = 0; oc < 4; ++oc) acc2[rt][oc] = mfma6(hx, bf[s & 1][oc], acc2[rt][oc]);
-        }
+        for (int oc = 0; oc < 4; ++oc) acc2[rt][oc] = mfma6(hx[it & 1], b2f[s & 1][oc], acc2[rt][oc]);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
   }
@@ -226,17 +241,19 @@ __global__ __launch_bounds__(NT, 1) void embed_mlp_kernel(EmbedArgs a) {
   }
 }
 
-// fp32 weights -> three bf16 planes (exact split), zero-padded to [rows][cols_p]
+// fp32 weights [rows][cols] -> three bf16 planes (exact split), zero-padded to
+// cols_p columns, in B-fragment order (EmbedArgs::W1p); rows % 16 == 0, cols_p % 32 == 0
 __global__ void split_planes_kernel(const float* __restrict__ w, int rows, int cols, int cols_p,
-                                    uint16_t* __restrict__ planes) {
+                                    uint16_t* __restrict__ frags) {
   const int64_t n = (int64_t)rows * cols_p;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int r = (int)(i / cols_p), c = (int)(i % cols_p);
     short h, m, l;
     split3(c < cols ? w[(int64_t)r * cols + c] : 0.f, h, m, l);
-    planes[i] = (uint16_t)h;
-    planes[n + i] = (uint16_t)m;
-    planes[2 * n + i] = (uint16_t)l;
+    const int64_t f = ((int64_t)(r >> 4) * (cols_p >> 5) + (c >> 5)) * 3 * 512 + 8 * ((r & 15) + 16 * ((c & 31) >> 3)) + (c & 7);
+    frags[f] = (uint16_t)h;
+    frags[f + 512] = (uint16_t)m;
+    frags[f + 1024] = (uint16_t)l;
   }
 }
 
