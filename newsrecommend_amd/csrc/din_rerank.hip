@@ -1030,26 +1030,46 @@ __global__ __launch_bounds__(512, 1) void din_rerank_project_kernel(ProjArgs a) 
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       if (j < ntile) {
+        // two row tiles at a time, their A fragments one k-step ahead (pinned
+        // by scheduling barriers: left alone the scheduler put every MFMA
+        // right behind its own LDS read and waited out the latency each time)
 #pragma unroll 1
-      for (int ct = 0; ct < 4; ++ct) {
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        for (int cp = 0; cp < 2; ++cp) {
+          f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+          bf16x8 ah[2][2], al[2][2];  // [buffer][row tile]
+          auto rd = [&](int s, int nb) __attribute__((always_inline)) {
 #pragma unroll
-        for (int s = 0; s < KSD; ++s) {
-          const int o = img_off<D>(16 * ct + l15, 4 * s + l4);
-          const bf16x8 af = *reinterpret_cast<const bf16x8*>(pimg + o);
-          if constexpr (F32)
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(iml + o), fh[j][s], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, fl[j][s], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, fh[j][s], acc, 0, 0, 0);
-        }
+            for (int q = 0; q < 2; ++q) {
+              const int o = img_off<D>(16 * (2 * cp + q) + l15, 4 * s + l4);
+              ah[nb][q] = *reinterpret_cast<const bf16x8*>(pimg + o);
+              if constexpr (F32) al[nb][q] = *reinterpret_cast<const bf16x8*>(iml + o);
+            }
+          };
+          rd(0, 0);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int64_t row = r0 + 16 * ct + 4 * l4 + i;
-          // (candidates: w2 (acc + b1), as the main kernel forms U'; history:
-          // w2 acc, as it forms P')
-          if (row < a.n) a.out[row * AF + oc[j]] = isA[j] ? w2u[j] * (a.b1 ? acc[i] + b1u[j] : acc[i]) : acc[i];
+          for (int s = 0; s < KSD; ++s) {
+            if (s + 1 < KSD) rd(s + 1, (s + 1) & 1);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+              if constexpr (F32) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[s & 1][q], fh[j][s], acc[q], 0, 0, 0);
+              acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[s & 1][q], fl[j][s], acc[q], 0, 0, 0);
+            }
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+              acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[s & 1][q], fh[j][s], acc[q], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+#pragma unroll
+          for (int q = 0; q < 2; ++q)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int64_t row = r0 + 16 * (2 * cp + q) + 4 * l4 + i;
+              // (candidates: w2 (acc + b1), as the main kernel forms U'; history:
+              // w2 acc, as it forms P')
+              if (row < a.n) a.out[row * AF + oc[j]] = isA[j] ? w2u[j] * (a.b1 ? acc[q][i] + b1u[j] : acc[q][i]) : acc[q][i];
+            }
         }
-      }
       }
     }
   }
