@@ -22,11 +22,12 @@ ORACLE_LIB = os.path.join(ROOT, "oracle", "liboracle_knn.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"]
-SOURCES = ["nrk_common.cpp", "click_log.cpp", "knn_flat.hip", "din_attn.hip", "ivf_build.hip", "din_head.hip", "din_rerank.hip", "embed.hip",
+SOURCES = ["nrk_common.cpp", "click_log.cpp", "knn_flat.hip", "din_attn.hip", "ivf_build.hip", "din_head.hip", "din_rerank.hip", "din_rerank_lane.hip", "embed.hip",
            "screen_dp32.hip", "screen_dp64.hip", "screen_dp128.hip", "screen_dp256.hip"]
 # din_rerank: no NaN inputs (finite weights and table rows; padded candidates are
 # written as -inf, never computed), so max / min need no IEEE canonicalisation
-FILE_FLAGS = {"din_rerank.hip": ["-fno-honor-nans", "-mno-amdgpu-ieee"]}
+FILE_FLAGS = {"din_rerank.hip": ["-fno-honor-nans", "-mno-amdgpu-ieee"],
+              "din_rerank_lane.hip": ["-fno-honor-nans", "-mno-amdgpu-ieee", "-fno-slp-vectorize"]}
 
 
 def _run(cmd):
@@ -44,7 +45,7 @@ def _newer(target, deps):
 
 
 def build_lib(force: bool = False) -> str:
-    headers = [os.path.join(CSRC, "nrk_common.h"), os.path.join(CSRC, "screen.h"), os.path.join(CSRC, "screen16.h"), os.path.join(ROOT, "include", "nrk.h")]
+    headers = [os.path.join(CSRC, "nrk_common.h"), os.path.join(CSRC, "din_rerank.h"), os.path.join(CSRC, "screen.h"), os.path.join(CSRC, "screen16.h"), os.path.join(ROOT, "include", "nrk.h")]
     objdir = os.path.join(CSRC, "build")
     os.makedirs(objdir, exist_ok=True)
     jobs = []

@@ -45,47 +45,15 @@
 //   5. logits -> HBM (-inf for padded candidates).
 #include <math.h>
 
-#include "nrk_common.h"
+#include "din_rerank.h"
 
 namespace nrk {
 namespace rr {
 
 constexpr int NT = 512;  // 8 waves
 constexpr int CH = 64;   // candidates per chunk
-constexpr int LP = 64;   // history rows held (L <= 64)
 constexpr int SST = 68;  // S row stride (floats): per-candidate scores / softmax weights
 
-struct RerankArgs {
-  const uint16_t* table;
-  int64_t n_table;
-  const int32_t* hist;  // [nU][L]
-  int L, nU;
-  const int32_t* cand;       // candidate rows
-  const int64_t* cand_off;   // [nU] user u: cand[cand_off[u] .. + cand_len[u])
-  const int32_t* cand_len;   // [nU]
-  const int32_t* extra;      // [nU] appended candidate (< 0: a padded slot), or null
-  const int64_t* out_off;    // [nU] logits of user u at out[out_off[u] ..]
-  float* out;
-  const uint16_t *W1q_hi, *W1q_lo, *W1k_hi, *W1k_lo;  // [A][d]
-  const float* b1;                                    // [A]
-  const float* w2;                                    // [A]
-  const uint16_t *H1q_hi, *H1q_lo, *H1p_hi, *H1p_lo;  // [F][d]
-  const float* c1;                                    // [F]
-  const uint16_t *H2_hi, *H2_lo;                      // [F/2][F]
-  const float* c2;                                    // [F/2]
-  const float* h3;                                    // [F/2]
-  float c3;
-  int F;
-  int* queue;  // user counter, zero at launch
-  // projected candidates (PROJ): [U' (A) | Q1 (F)] f32 per candidate, cproj
-  // parallel to cand, xproj [nU] for the extras (nrk_din_rerank_project), and
-  // the history projected per slot: hproj [nU][L] x [P' (A) | R (F)] f32
-  // (nrk_din_rerank_project_hist).  The PROJ kernel never reads the table, so
-  // it serves bf16 and f32 tables alike.
-  const float* cproj;
-  const float* xproj;
-  const float* hproj;
-};
 
 // LDS image of 64 rows of D bf16: 16-B chunks XOR-swizzled by row, so the
 // 16x16x32 A-fragment reads (16 rows x one chunk per lane group) are
@@ -161,11 +129,6 @@ __device__ __forceinline__ const T* pinned(const T* p) {
   return p + z;
 }
 
-__device__ __forceinline__ void split_bf16(float x, short& hi, short& lo) {
-  const __bf16 h = (__bf16)x;
-  hi = __builtin_bit_cast(short, h);
-  lo = __builtin_bit_cast(short, (__bf16)(x - (float)h));
-}
 
 template <int D, int A, int F, bool PROJ>
 __global__ __launch_bounds__(NT, 1) void din_rerank_kernel(RerankArgs a) {
@@ -893,12 +856,6 @@ struct ProjArgs {
   float* out;  // [n][A + F]
 };
 
-// Geo<D, A>::col with A at run time
-__device__ __forceinline__ int slice_col(int n, int A) {
-  const int SL = A / 8, sj = n / SL, w = n % SL;
-  const int p4 = SL == 16 ? ((w >> 2) + 2 * (sj >> 2)) & 3 : (w >> 2);
-  return sj * SL + 4 * p4 + (w & 3);
-}
 
 // A chunk's rows in flight, in registers (no lambdas over arrays: the
 // compiler left such captured arrays in scratch).
@@ -1092,6 +1049,7 @@ int launch_proj_d(int d, const ProjArgs& a, hipStream_t st) {
   return launch_proj<64, F32>(a, st);
 }
 
+
 // ---- the evaluate() tail per user (DIN.py:176-189 as pipeline.rerank_clusters
 // states it), over the logits of user u = [seg[u], seg[u + 1]): the BCE sum
 // over the valid (finite) candidates in f64 (label 1 at pos[u], -1 = none),
@@ -1148,7 +1106,7 @@ using namespace nrk;
 
 extern "C" int nrk_din_rerank_workspace(size_t* ws_bytes) {
   NRK_CHECK_ARG(ws_bytes, "din_rerank_workspace: null");
-  *ws_bytes = 256;
+  *ws_bytes = 1024;  // [0, 4): the user queue; [64, 64 + 2 A): sgn(w2) per projection column (f16)
   return NRK_OK;
 }
 
@@ -1172,7 +1130,7 @@ static int rerank_impl(const void* table, int64_t n_table, int32_t dtype, const 
                 "din_rerank: null parameter pointer");
   NRK_CHECK_ARG(!extra || !cand_proj || extra_proj, "din_rerank_projected: extra without extra_proj");
   NRK_CHECK_ARG(!cand_proj || hist_proj, "din_rerank_projected: null hist_proj");
-  if (ws_bytes < 256) return fail(NRK_EWORKSPACE, "din_rerank: workspace %zu < 256", ws_bytes);
+  if (ws_bytes < 1024) return fail(NRK_EWORKSPACE, "din_rerank: workspace %zu < 1024", ws_bytes);
   hipStream_t st = (hipStream_t)stream;
   if (hipMemsetAsync(ws, 0, 4, st) != hipSuccess) return fail(NRK_ELAUNCH, "din_rerank: memset failed");
   rr::RerankArgs a;
@@ -1208,7 +1166,10 @@ static int rerank_impl(const void* table, int64_t n_table, int32_t dtype, const 
   a.cproj = cand_proj;
   a.xproj = extra_proj;
   a.hproj = hist_proj;
-  if (cand_proj) return rr::launch_a<64, true>(A, a, st);  // (the projected kernel does not depend on d)
+  a.sgn = static_cast<char*>(ws) + 64;
+  // (the projected kernels do not depend on d)
+  if (cand_proj && F <= 64) return rr::launch_lane(A, a, st);
+  if (cand_proj) return rr::launch_a<64, true>(A, a, st);
   if (d == 256) return rr::launch_a<256, false>(A, a, st);
   if (d == 128) return rr::launch_a<128, false>(A, a, st);
   return rr::launch_a<64, false>(A, a, st);

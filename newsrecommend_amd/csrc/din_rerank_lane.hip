@@ -1,0 +1,401 @@
+// din_rerank_lane.hip — nrk_din_rerank_projected for F <= 64 (DIN.py:166-189
+// evaluate() over the row projections; see din_rerank.hip for the algebra).
+// Built with -fno-slp-vectorize (build.py): the SLP vectorizer turns the
+// scoring's |y|-fmas into v_and + v_pk_fma pairs, more instructions than the
+// fmas with an |.| source modifier.
+#include <math.h>
+
+#include "din_rerank.h"
+
+namespace nrk {
+namespace rr {
+
+// ---- the projected re-rank, one wave per 32 candidates (nrk_din_rerank_projected
+// for F <= 64).  The scoring is the VALU-bound part: per (candidate, history
+// row, attention unit) one add and one |.|-fma, the add packed two units at a
+// time.  Lane (cs, h) = (candidate cs of the wave's 32, unit half h): the
+// candidate's U' half stays in registers for all rows, each P' row is read by
+// one LDS wave-instruction for 32 candidates (two addresses, one per half, on
+// different banks), the unit signs sgn(w2) of the half are f16 pairs in A / 4
+// registers (v_fma_mix operands), and the halves' partial sums meet by one
+// permlane32 swap per row.  Every other step of a candidate (softmax,
+// e R, the head) is wave-local too: a wave waits for another only when the
+// block moves to the next user (one staging of the history projections
+// [P' | R], three barriers per user, against five per 64-candidate chunk in
+// din_rerank_kernel).
+//   s[c][r] = (SU[c] + SP[r] + sum_n sgn_n |U'[c][n] + P'[r][n]|) / 2
+//   e = exp(s - max_r s) (the padding row weighted L - nv), as bf16 hi + lo;
+//   h1 = relu((Q1 den + e R^T) / den + c1) on MFMA (three products), h2 and
+//   the logit on MFMA as in din_rerank_kernel.
+namespace lk {
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+constexpr int NT = 512;  // 8 waves, two per SIMD (the partner wave's LDS reads issue beside this one's VALU)
+constexpr int CPI = 32;  // candidates per wave item
+template <int A, int F>
+struct Lay {  // byte offsets
+  static constexpr int F2 = F / 2;
+  static constexpr int PST = A + 8;       // P' row stride (floats): unit half 1 at A / 2 + 4 (other banks than half 0)
+  static constexpr int HOFF = A / 2 + 4;
+  static constexpr int SST = LP + 2;      // scores [CPI][SST] f32: lanes (cs, h) write 2 cs + h apart, no conflicts
+  static constexpr int EST = LP + 8;      // e planes [CPI][EST] bf16: conflict-free 16-B fragment reads
+  static constexpr int c1 = 0;                          // [F]
+  static constexpr int c2 = c1 + F * 4;                 // [F2]
+  static constexpr int h3 = c2 + F2 * 4;                // [F2]
+  static constexpr int h2 = h3 + F2 * 4;                // H2 hi, lo bf16 [F2][F]
+  static constexpr int pp = h2 + 2 * F2 * F * 2;        // P' [LP][PST] f32
+  static constexpr int hsp = pp + LP * PST * 4;         // SP / 2 [LP]
+  static constexpr int rt = hsp + LP * 4;               // R^T hi, lo bf16 [F][LP]
+  static constexpr int wv = rt + 2 * F * LP * 2;        // per wave: scores, then e hi / lo, then h1
+  static constexpr int SB = CPI * SST * 4, EB = 2 * CPI * EST * 2, HB = CPI * (F + 4) * 4;
+  static constexpr int XB = SB > EB ? SB : EB;
+  static constexpr int WB = ((XB > HB ? XB : HB) + 2 * CPI * 4 + 15) & ~15;  // + den, valid [CPI]
+  static constexpr int qs = wv + 8 * WB;
+  static constexpr int total = qs + 16;
+};
+
+template <int A, int F>
+__global__ __launch_bounds__(NT, 1) void din_rerank_lane_kernel(RerankArgs a) {
+  using LY = Lay<A, F>;
+  constexpr int F2 = F / 2, AH = A / 2, NG = AH / 8, AF = A + F, PST = LY::PST, SST = LY::SST, EST = LY::EST;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* c1s = reinterpret_cast<float*>(smem + LY::c1);
+  float* c2s = reinterpret_cast<float*>(smem + LY::c2);
+  float* h3s = reinterpret_cast<float*>(smem + LY::h3);
+  uint16_t* H2h = reinterpret_cast<uint16_t*>(smem + LY::h2);
+  uint16_t* H2l = H2h + F2 * F;
+  float* Pp = reinterpret_cast<float*>(smem + LY::pp);
+  float* hSP = reinterpret_cast<float*>(smem + LY::hsp);
+  uint16_t* Rth = reinterpret_cast<uint16_t*>(smem + LY::rt);
+  uint16_t* Rtl = Rth + F * LP;
+  int* qslot = reinterpret_cast<int*>(smem + LY::qs);
+  const int tid = threadIdx.x;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  unsigned char* wreg = smem + LY::wv + w * LY::WB;
+  float* Sw = reinterpret_cast<float*>(wreg);              // scores [CPI][SST]
+  uint16_t* Eh = reinterpret_cast<uint16_t*>(wreg);        // e hi [CPI][EST] (over the scores, once read)
+  uint16_t* El = Eh + CPI * EST;
+  float* H1w = reinterpret_cast<float*>(wreg);             // h1 [CPI][F + 4] (over e, once read)
+  const int XB = (LY::XB > LY::HB ? LY::XB : LY::HB);
+  float* dnw = reinterpret_cast<float*>(wreg + XB);        // sum_r e [CPI]
+  int* cvw = reinterpret_cast<int*>(dnw + CPI);            // candidate valid [CPI]
+
+  for (int i = tid; i < F; i += NT) c1s[i] = a.c1[i];
+  for (int i = tid; i < F2; i += NT) {
+    c2s[i] = a.c2[i];
+    h3s[i] = a.h3[i];
+  }
+  for (int i = tid; i < F2 * F; i += NT) {
+    H2h[i] = a.H2_hi[i];
+    H2l[i] = a.H2_lo[i];
+  }
+  if (tid == 0) qslot[0] = atomicAdd(a.queue, 1);
+  __syncthreads();
+  // sgn(w2) of this lane's unit half, resident as f16 pairs (+-1 exactly; the
+  // |y|-fmas take them as v_fma_mix operands): A / 4 registers
+  h2 sgh[A / 4];
+#pragma unroll
+  for (int j = 0; j < A / 4; ++j) sgh[j] = reinterpret_cast<const h2*>(a.sgn)[((tid >> 5) & 1) * (A / 4) + j];
+  int u = qslot[0];
+
+  while (u < a.nU) {
+    const int64_t coff = a.cand_off[u];
+    const int clen = a.cand_len[u];
+    const int ctot = clen + (a.extra ? 1 : 0);
+    const int ln = tid & 63;
+    const int hid = ln < a.L ? a.hist[(int64_t)u * a.L + ln] : -1;
+    const uint64_t vm = __ballot(ln < a.L && hid >= 0 && hid < a.n_table);
+    const int nv = __popcll(vm), npad = a.L - nv, nr = nv + (npad > 0 ? 1 : 0);
+    const int nrp = (nr + 31) & ~31;
+    __syncthreads();  // the previous user's items are done with P', SP, R
+    if (tid == 0) qslot[1] = atomicAdd(a.queue, 1);
+    if (ctot > 0) {
+      // [P' | R] of the valid slots, compacted; rows nv .. LP - 1 zero (the
+      // shared padding row, and the e R MFMA's K padding)
+      for (int e = tid; e < LP * (AF / 4); e += NT) {
+        const int row = e / (AF / 4), part = e % (AF / 4);
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (row < nv) v = *reinterpret_cast<const float4*>(a.hproj + ((int64_t)u * a.L + nth_set_bit(vm, row)) * AF + 4 * part);
+        if (part < A / 4) {
+          const int c = 4 * part;
+          *reinterpret_cast<float4*>(Pp + row * PST + (c < AH ? c : c + 4)) = v;
+        } else {
+          const int f0 = 4 * (part - A / 4);
+          const float x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            short hi, lo;
+            split_bf16(x[j], hi, lo);
+            Rth[(f0 + j) * LP + row] = (uint16_t)hi;
+            Rtl[(f0 + j) * LP + row] = (uint16_t)lo;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (ctot > 0) {  // SP / 2 per row: thread = (row, eighth of the units)
+      const int r = tid >> 3, j = tid & 7;
+      const float* pr = Pp + r * PST + (j < 4 ? 0 : 4) + j * (A / 8);  // (an eighth never straddles the halves)
+      float sp = 0.f;
+#pragma unroll
+      for (int i = 0; i < A / 8; ++i) sp += pr[i];
+      sp = oct_sum(sp);
+      if (j == 0) hSP[r] = 0.5f * sp;
+    }
+    __syncthreads();
+    const int un = qslot[1];
+    const int nitem = (ctot + CPI - 1) / CPI;
+
+    for (int it = w; it < nitem; it += 8) {
+      // lane indices re-derived per item from a thread id the compiler cannot
+      // see through: otherwise it hoists every per-lane LDS / global address
+      // of the item to the kernel entry and spills them
+      int tq = threadIdx.x;
+      asm volatile("" : "+v"(tq));
+      const int lane = tq & 63, l15 = lane & 15, l4 = lane >> 4, cs = lane & 31, h = lane >> 5;
+      const int c0 = it * CPI, nci = ctot - c0 < CPI ? ctot - c0 : CPI;
+      // ---- this lane's candidate: U' half in registers, SU / 2
+      const int ci = c0 + cs;
+      const float* src = nullptr;
+      int cid = -1;
+      if (ci < clen) {
+        src = a.cproj + (coff + ci) * AF;
+        cid = a.cand[coff + ci];
+      } else if (ci == clen && a.extra) {
+        src = a.xproj + (int64_t)u * AF;
+        cid = a.extra[u];
+      }
+      const bool has = src != nullptr;
+      const float* us = (has ? src : a.hproj) + h * AH;  // (loads stay unconditional: a valid row, masked below)
+      float uq[AH];
+#pragma unroll
+      for (int q = 0; q < AH / 4; ++q) {
+        const float4 x = *reinterpret_cast<const float4*>(us + 4 * q);
+        uq[4 * q] = has ? x.x : 0.f;
+        uq[4 * q + 1] = has ? x.y : 0.f;
+        uq[4 * q + 2] = has ? x.z : 0.f;
+        uq[4 * q + 3] = has ? x.w : 0.f;
+      }
+      if (h == 0) cvw[cs] = cid >= 0 && cid < a.n_table ? 1 : 0;
+      float hsu = 0.f;
+#pragma unroll
+      for (int j = 0; j < AH; ++j) hsu += uq[j];
+      hsu = 0.5f * half_swap_sum(hsu);
+
+      // ---- scores: step p = rows 2p, 2p + 1 over this lane's unit half; the
+      // halves' partial sums meet by a permlane32 swap, lane h keeps row
+      // 2p + h.  P' in groups of 8 units per row, the next group read during
+      // this one (the next step's first during the last), pinned by
+      // scheduling barriers so that the reads never pile up in registers.
+      const float* const pbase = Pp + (h ? LY::HOFF : 0);
+      float4 pa[2][2], pb[2][2];  // [buffer][float4 of the group] of the two rows
+      // (a macro, not a lambda: arrays captured by a lambda were left in scratch)
+#define NRK_LK_RDG(p_, g, nb)                                                     \
+  {                                                                               \
+    const float* r0_ = pbase + (2 * (p_)) * PST + 8 * (g);                        \
+    _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_) {                           \
+      pa[nb][i_] = *reinterpret_cast<const float4*>(r0_ + 4 * i_);               \
+      pb[nb][i_] = *reinterpret_cast<const float4*>(r0_ + PST + 4 * i_);         \
+    }                                                                             \
+  }
+      float m = -INFINITY;
+      NRK_LK_RDG(0, 0, 0)
+      for (int p = 0; 2 * p < nr; ++p) {
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f, b0 = 0.f, b1 = 0.f, b2 = 0.f, b3 = 0.f;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+          // (the next step's first group unconditionally: past the last step it
+          // reads rows < 66, inside the block's LDS, and is never used)
+          if (g + 1 < NG) NRK_LK_RDG(p, g + 1, (g + 1) & 1)
+          else NRK_LK_RDG(p + 1, 0, 0)
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const int q = 2 * g + i;  // float4 of the half row
+            const float4 x0 = pa[g & 1][i], x1 = pb[g & 1][i];
+            const h2 sa = sgh[2 * q], sb = sgh[2 * q + 1];
+            const f32x2 ua = {uq[4 * q], uq[4 * q + 1]}, ub = {uq[4 * q + 2], uq[4 * q + 3]};
+            const f32x2 y0a = ua + f32x2{x0.x, x0.y}, y0b = ub + f32x2{x0.z, x0.w};
+            const f32x2 y1a = ua + f32x2{x1.x, x1.y}, y1b = ub + f32x2{x1.z, x1.w};
+            a0 = fmaf(fabsf(y0a.x), (float)sa.x, a0);
+            a1 = fmaf(fabsf(y0a.y), (float)sa.y, a1);
+            b0 = fmaf(fabsf(y1a.x), (float)sa.x, b0);
+            b1 = fmaf(fabsf(y1a.y), (float)sa.y, b1);
+            a2 = fmaf(fabsf(y0b.x), (float)sb.x, a2);
+            a3 = fmaf(fabsf(y0b.y), (float)sb.y, a3);
+            b2 = fmaf(fabsf(y1b.x), (float)sb.x, b2);
+            b3 = fmaf(fabsf(y1b.y), (float)sb.y, b3);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        const float f0 = half_swap_sum((a0 + a1) + (a2 + a3)), f1 = half_swap_sum((b0 + b1) + (b2 + b3));
+        const int r = 2 * p + h;
+        const float sc = fmaf(0.5f, h ? f1 : f0, hsu + hSP[r]);
+        Sw[cs * SST + r] = sc;
+        if (r < nr) m = fmaxf(m, sc);
+      }
+#undef NRK_LK_RDG
+      {
+        const auto mm = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+        m = fmaxf(__uint_as_float(mm[0]), __uint_as_float(mm[1]));
+      }
+      // ---- softmax weights -> bf16 hi + lo planes (rows nr .. nrp - 1 zero), sum e
+      float ev[LP / 2];
+      float sum = 0.f;
+#pragma unroll
+      for (int p = 0; p < LP / 2; ++p) {
+        const int r = 2 * p + h;
+        ev[p] = 0.f;
+        if (r < nr) {
+          ev[p] = __expf(Sw[cs * SST + r] - m);
+          sum = fmaf(r < nv ? 1.f : (float)npad, ev[p], sum);
+        }
+      }
+      sum = half_swap_sum(sum);
+#pragma unroll
+      for (int p = 0; p < LP / 2; ++p) {
+        const int r = 2 * p + h;
+        if (r < nrp) {
+          short hi, lo;
+          split_bf16(ev[p], hi, lo);
+          Eh[cs * EST + r] = (uint16_t)hi;
+          El[cs * EST + r] = (uint16_t)lo;
+        }
+      }
+      if (h == 0) dnw[cs] = sum;
+
+      // ---- h1 = relu(Q1 + (e R) / sum e + c1): C tile rows = candidates 16 ct + 4 l4 + k
+      const int nks = nrp / 32;
+      bf16x8 eh[2][2], el[2][2];  // [ct][ks] (all read before h1 is written over them)
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const int o = (16 * ct + l15) * EST + 32 * ks + 8 * l4;
+          eh[ct][ks] = *reinterpret_cast<const bf16x8*>(Eh + o);
+          el[ct][ks] = *reinterpret_cast<const bf16x8*>(El + o);
+        }
+      float q1v[2][F / 16][4];  // Q1 of the C tile's candidates (from the candidate projections)
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int cc = c0 + 16 * ct + 4 * l4 + k;
+          const float* qs = cc < clen ? a.cproj + (coff + cc) * AF : (cc == clen && a.extra ? a.xproj + (int64_t)u * AF : nullptr);
+          const float* qa = (qs ? qs : a.hproj) + A + l15;
+#pragma unroll
+          for (int ft = 0; ft < F / 16; ++ft) {
+            const float x = qa[16 * ft];
+            q1v[ct][ft][k] = qs ? x : 0.f;
+          }
+        }
+      float dv[2][4];
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dv[ct][k] = dnw[16 * ct + 4 * l4 + k];
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        if (16 * ct >= nci) continue;
+        float rden[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) rden[k] = __builtin_amdgcn_rcpf(dv[ct][k]);
+#pragma unroll
+        for (int ft = 0; ft < F / 16; ++ft) {
+          const int f = 16 * ft + l15;
+          f32x4 acc;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) acc[k] = q1v[ct][ft][k] * dv[ct][k];
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) {
+            if (ks < nks) {
+              const bf16x8 rh = *reinterpret_cast<const bf16x8*>(Rth + f * LP + 32 * ks + 8 * l4);
+              const bf16x8 rl = *reinterpret_cast<const bf16x8*>(Rtl + f * LP + 32 * ks + 8 * l4);
+              acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(el[ct][ks], rh, acc, 0, 0, 0);
+              acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(eh[ct][ks], rl, acc, 0, 0, 0);
+              acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(eh[ct][ks], rh, acc, 0, 0, 0);
+            }
+          }
+          const float cb = c1s[f];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) H1w[(16 * ct + 4 * l4 + k) * (F + 4) + f] = fmaxf(acc[k] * rden[k] + cb, 0.f);
+        }
+      }
+
+      // ---- h2 = relu(H2 h1 + c2), logit = h3 . h2 + c3 (16-unit tiles t2)
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        if (16 * ct >= nci) continue;
+        const int ca = 16 * ct + l15;
+        float z[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t2 = 0; t2 < F2 / 16; ++t2) {
+          const int v = 16 * t2 + l15;
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ks = 0; ks < F / 32; ++ks) {
+            const float4 x0 = *reinterpret_cast<const float4*>(H1w + ca * (F + 4) + 32 * ks + 8 * l4);
+            const float4 x1 = *reinterpret_cast<const float4*>(H1w + ca * (F + 4) + 32 * ks + 8 * l4 + 4);
+            const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+            bf16x8 hh, hl;
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) {
+              short hi, lo;
+              split_bf16(xv[jj], hi, lo);
+              hh[jj] = hi;
+              hl[jj] = lo;
+            }
+            const bf16x8 bh = *reinterpret_cast<const bf16x8*>(H2h + v * F + 32 * ks + 8 * l4);
+            const bf16x8 bl = *reinterpret_cast<const bf16x8*>(H2l + v * F + 32 * ks + 8 * l4);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hl, bh, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hh, bl, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hh, bh, acc, 0, 0, 0);
+          }
+          const float cv = c2s[v], hv = h3s[v];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) z[k] += row_sum16(hv * fmaxf(acc[k] + cv, 0.f));
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int cc = 16 * ct + 4 * l4 + k;
+          if (l15 == 0 && cc < nci) a.out[a.out_off[u] + c0 + cc] = cvw[cc] ? a.c3 + z[k] : -INFINITY;
+        }
+      }
+    }
+    u = un;
+  }
+}
+
+// sgn(w2) per P' / U' column (the projections' slice order)
+__global__ void sign_cols_kernel(const float* __restrict__ w2, int A, _Float16* __restrict__ sgn) {
+  for (int n = threadIdx.x; n < A; n += blockDim.x) sgn[slice_col(n, A)] = w2[n] >= 0.f ? (_Float16)1.f : (_Float16)-1.f;
+}
+
+template <int A, int F>
+int launch(const RerankArgs& a, hipStream_t st) {
+  constexpr size_t lds = Lay<A, F>::total;
+  static_assert(lds <= 160 * 1024, "din_rerank_lane: LDS");
+  const int grid = a.nU < 256 ? a.nU : 256;
+  hipLaunchKernelGGL((din_rerank_lane_kernel<A, F>), dim3(grid), dim3(NT), lds, st, a);
+  NRK_CHECK_LAUNCH("din_rerank_lane_kernel");
+  return NRK_OK;
+}
+template <int A>
+int launch_f(const RerankArgs& a, hipStream_t st) {
+  return a.F == 32 ? launch<A, 32>(a, st) : launch<A, 64>(a, st);
+}
+inline int launch_a(int A, const RerankArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(sign_cols_kernel, dim3(1), dim3(128), 0, st, a.w2, A, reinterpret_cast<_Float16*>(const_cast<void*>(a.sgn)));
+  NRK_CHECK_LAUNCH("sign_cols_kernel");
+  switch (A) {
+    case 32: return launch_f<32>(a, st);
+    case 64: return launch_f<64>(a, st);
+    case 96: return launch_f<96>(a, st);
+    default: return launch_f<128>(a, st);
+  }
+}
+}  // namespace lk
+
+int launch_lane(int A, const RerankArgs& a, hipStream_t st) { return lk::launch_a(A, a, st); }
+
+}  // namespace rr
+}  // namespace nrk

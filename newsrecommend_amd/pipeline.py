@@ -160,18 +160,20 @@ def rerank_project(model, table: torch.Tensor, rows: torch.Tensor, prm=None, his
 
 def rerank_ragged(model, table: torch.Tensor, hist_rows: torch.Tensor, cand: torch.Tensor, cand_off: torch.Tensor,
                   cand_len: torch.Tensor, extra: torch.Tensor | None, out_off: torch.Tensor, n_out: int,
-                  prm=None, shared: bool = False) -> torch.Tensor:
-    """nrk_din_rerank: one launch for all users.  User u scores
+                  prm=None, shared: bool = False, direct: bool = False) -> torch.Tensor:
+    """The fused re-rank, one launch for all users.  User u scores
     cand[cand_off[u] : cand_off[u] + cand_len[u]] (+ extra[u] when given, -1 =
     a padded slot) against its history hist_rows[u] and writes
     out[out_off[u] + c]; rows outside the table get -inf.  Returns out (n_out,)
-    f32 (entries not covered by any user stay uninitialised).  shared: the
-    lists are shared by many users (the flow's clusters): cand and extra are
-    projected once (rerank_project), the histories per slot, and
-    nrk_din_rerank_projected scores the projections; for a bf16 table the
-    logits are bit-identical either way.  An f32 table (the reference's own
-    embeddings) always takes the projected form: the projections split its rows
-    into bf16 hi + lo."""
+    f32 (entries not covered by any user stay uninitialised).  The rows are
+    projected (rerank_project: the candidates' [U' | Q1], the history slots'
+    [P' | R]; an f32 table split into bf16 hi + lo) and
+    nrk_din_rerank_projected scores the projections (for F <= 64 one wave per
+    32 candidates, din_rerank_lane.hip).  shared: a hint only (the lists are
+    shared by many users; either way every row is projected once per call).
+    direct: a bf16 table through nrk_din_rerank instead (the per-chunk kernel
+    that reads the rows itself; its arithmetic order differs, within the same
+    tolerance of the reference)."""
     from . import _lib
 
     dev = table.device
@@ -194,7 +196,7 @@ def rerank_ragged(model, table: torch.Tensor, hist_rows: torch.Tensor, cand: tor
     ex = extra.to(torch.int32).contiguous() if extra is not None else None
     from .din import KernelTimer
 
-    if shared or table.dtype == torch.float32:
+    if not direct:
         tp = KernelTimer.mark("rerank_project")
         cp = rerank_project(model, table, c, prm)
         xp = rerank_project(model, table, ex, prm) if ex is not None else None
