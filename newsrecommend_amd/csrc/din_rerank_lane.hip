@@ -145,6 +145,29 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_lane_kernel(RerankArgs a) {
     const int un = qslot[1];
     const int nitem = (ctot + CPI - 1) / CPI;
 
+    // U' of this lane's candidate (half h) for item it_: loaded one item ahead
+    // (during the previous item's softmax and head).  An absent candidate
+    // reads a valid row (a history projection): finite values in its own row
+    // of every product, never written out.  (A macro: see NRK_LK_RDG.)
+    float uq[AH];
+#define NRK_LK_LDU(it_)                                                                              \
+  {                                                                                                  \
+    int tq_ = threadIdx.x;                                                                           \
+    asm volatile("" : "+v"(tq_));                                                                    \
+    const int ci_ = (it_) * CPI + (tq_ & 31);                                                        \
+    const float* src_ = ci_ < clen ? a.cproj + (coff + ci_) * AF                                     \
+                                   : (ci_ == clen && a.extra ? a.xproj + (int64_t)u * AF : a.hproj); \
+    const float* us_ = src_ + ((tq_ >> 5) & 1) * AH;                                                 \
+    _Pragma("unroll") for (int q_ = 0; q_ < AH / 4; ++q_) {                                         \
+      const float4 x_ = *reinterpret_cast<const float4*>(us_ + 4 * q_);                              \
+      uq[4 * q_] = x_.x;                                                                             \
+      uq[4 * q_ + 1] = x_.y;                                                                         \
+      uq[4 * q_ + 2] = x_.z;                                                                         \
+      uq[4 * q_ + 3] = x_.w;                                                                         \
+    }                                                                                                \
+  }
+    if (w < nitem) NRK_LK_LDU(w)
+
     for (int it = w; it < nitem; it += 8) {
       // lane indices re-derived per item from a thread id the compiler cannot
       // see through: otherwise it hoists every per-lane LDS / global address
@@ -153,30 +176,12 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_lane_kernel(RerankArgs a) {
       asm volatile("" : "+v"(tq));
       const int lane = tq & 63, l15 = lane & 15, l4 = lane >> 4, cs = lane & 31, h = lane >> 5;
       const int c0 = it * CPI, nci = ctot - c0 < CPI ? ctot - c0 : CPI;
-      // ---- this lane's candidate: U' half in registers, SU / 2
-      const int ci = c0 + cs;
-      const float* src = nullptr;
-      int cid = -1;
-      if (ci < clen) {
-        src = a.cproj + (coff + ci) * AF;
-        cid = a.cand[coff + ci];
-      } else if (ci == clen && a.extra) {
-        src = a.xproj + (int64_t)u * AF;
-        cid = a.extra[u];
+      {  // validity of this lane's candidate (its id; -1 past the list)
+        const int ci = c0 + cs;
+        const int cid = ci < clen ? a.cand[coff + ci] : (ci == clen && a.extra ? a.extra[u] : -1);
+        if (h == 0) cvw[cs] = cid >= 0 && cid < a.n_table ? 1 : 0;
       }
-      const bool has = src != nullptr;
-      const float* us = (has ? src : a.hproj) + h * AH;  // (loads stay unconditional: a valid row, masked below)
-      float uq[AH];
-#pragma unroll
-      for (int q = 0; q < AH / 4; ++q) {
-        const float4 x = *reinterpret_cast<const float4*>(us + 4 * q);
-        uq[4 * q] = has ? x.x : 0.f;
-        uq[4 * q + 1] = has ? x.y : 0.f;
-        uq[4 * q + 2] = has ? x.z : 0.f;
-        uq[4 * q + 3] = has ? x.w : 0.f;
-      }
-      if (h == 0) cvw[cs] = cid >= 0 && cid < a.n_table ? 1 : 0;
-      float hsu = 0.f;
+      float hsu = 0.f;  // SU / 2
 #pragma unroll
       for (int j = 0; j < AH; ++j) hsu += uq[j];
       hsu = 0.5f * half_swap_sum(hsu);
@@ -234,6 +239,22 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_lane_kernel(RerankArgs a) {
         if (r < nr) m = fmaxf(m, sc);
       }
 #undef NRK_LK_RDG
+      float q1v[2][F / 16][4];  // Q1 of the C tile's candidates (from the candidate projections)
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int cc = c0 + 16 * ct + 4 * l4 + k;
+          const float* qs = cc < clen ? a.cproj + (coff + cc) * AF : (cc == clen && a.extra ? a.xproj + (int64_t)u * AF : nullptr);
+          const float* qa = (qs ? qs : a.hproj) + A + l15;  // (an absent candidate: finite values in its own row, never written)
+#pragma unroll
+          for (int ft = 0; ft < F / 16; ++ft) q1v[ct][ft][k] = qa[16 * ft];
+        }
+      // the next item's U' (after the Q1 loads: the h1 MFMA's wait for Q1 then
+      // does not cover them)
+      __builtin_amdgcn_sched_barrier(0);
+      if (it + 8 < nitem) NRK_LK_LDU(it + 8)
+      __builtin_amdgcn_sched_barrier(0);
       {
         const auto mm = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
         m = fmaxf(__uint_as_float(mm[0]), __uint_as_float(mm[1]));
@@ -273,20 +294,6 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_lane_kernel(RerankArgs a) {
           const int o = (16 * ct + l15) * EST + 32 * ks + 8 * l4;
           eh[ct][ks] = *reinterpret_cast<const bf16x8*>(Eh + o);
           el[ct][ks] = *reinterpret_cast<const bf16x8*>(El + o);
-        }
-      float q1v[2][F / 16][4];  // Q1 of the C tile's candidates (from the candidate projections)
-#pragma unroll
-      for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int cc = c0 + 16 * ct + 4 * l4 + k;
-          const float* qs = cc < clen ? a.cproj + (coff + cc) * AF : (cc == clen && a.extra ? a.xproj + (int64_t)u * AF : nullptr);
-          const float* qa = (qs ? qs : a.hproj) + A + l15;
-#pragma unroll
-          for (int ft = 0; ft < F / 16; ++ft) {
-            const float x = qa[16 * ft];
-            q1v[ct][ft][k] = qs ? x : 0.f;
-          }
         }
       float dv[2][4];
 #pragma unroll
@@ -363,6 +370,7 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_lane_kernel(RerankArgs a) {
     }
     u = un;
   }
+#undef NRK_LK_LDU
 }
 
 // sgn(w2) per P' / U' column (the projections' slice order)
