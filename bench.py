@@ -543,7 +543,7 @@ def _rerank_roofline(ms, ms_proj, hist, d, A, F, L, key, es, n_samples, proj_row
     pw = 4 * (A + F)
     byt = n_samples * (pw + 8) + float((4 * L + pw * nv).sum())
     byt_p = proj_rows * (es * d + 4 + pw) + U * L * (4 + pw) + float(nv.sum()) * es * d
-    kern = f"din_rerank_kernel<.., {A}, {F}, PROJ> (projected)"
+    kern = f"din_rerank_lane_kernel<{A}, {F}> (projected)" if F <= 64 else f"din_rerank_kernel<.., {A}, {F}, PROJ> (projected)"
     sec = ms * 1e-3
     gbs = byt / sec / 1e9
     gbs_p = byt_p / (ms_proj * 1e-3) / 1e9 if ms_proj > 0 else 0.0

@@ -214,8 +214,9 @@ int nrk_din_batch_u(const float* q, int32_t B, int32_t d, const float* W1, const
  *   params: the model with its three eval-mode BatchNorms folded into the
  *   Linears after them and every weight split into bf16 hi + lo
  *   (newsrecommend_amd.pipeline.rerank_params).
- * d in {64, 128, 256}, A and F in {32, 64, 96, 128}, L <= 64.  ws: >= 256 B
- * (nrk_din_rerank_workspace), reset by the call (graph-capturable). */
+ * d in {64, 128, 256}, A and F in {32, 64, 96, 128}, L <= 64.  ws: >= 1024 B
+ * (nrk_din_rerank_workspace: the user queue and, for the projected form,
+ * sgn(w2) per projection column), reset by the call (graph-capturable). */
 typedef struct nrk_din_rerank_params_s {
   const void *W1q_hi, *W1q_lo;  /* bf16 [A][d]: W1[:, :d] (attention query half) */
   const void *W1k_hi, *W1k_lo;  /* bf16 [A][d]: W1[:, d:] (key half) */
@@ -244,13 +245,16 @@ int nrk_din_rerank(const void* table, int64_t n_table, int32_t dtype, const int3
  *   (slice order) | R(k) = H1p k ], k = table[rows[i]] (rows = hist [nU][L]
  *   flattened, so out is per history slot);
  * a zero row where rows[i] is outside [0, N).  table: bf16 (the MFMA sequence
- * nrk_din_rerank applies, so logits stay bit-identical to its) or f32 (each
+ * nrk_din_rerank applies to a row) or f32 (each
  * element split into bf16 hi + lo, three products: the reference's fp32
  * embeddings, embedding_generate.py:119-122 / DIN.py:45-56, to ~2^-16).
  * nrk_din_rerank_projected then stages projections instead of rows and never
  * reads the table (any dtype): cand_proj [.][A + F] parallel to cand,
  * extra_proj [nU][A + F] (required when extra != NULL), hist_proj
- * [nU * L][A + F] (required).  cand / extra / hist still decide validity. */
+ * [nU * L][A + F] (required).  cand / extra / hist still decide validity.
+ * For F <= 64 it runs one wave per 32 candidates (din_rerank_lane.hip; its
+ * arithmetic order differs from nrk_din_rerank's, both within 1e-4 of the
+ * reference), for F in {96, 128} the per-chunk kernel of nrk_din_rerank. */
 int nrk_din_rerank_project(const void* table, int64_t n_table, int32_t dtype, const int32_t* rows, int64_t n,
                            int32_t d, int32_t A, int32_t F, const nrk_din_rerank_params* params, float* out,
                            void* stream);
