@@ -858,52 +858,55 @@ struct ProjArgs {
 
 
 // A chunk's rows in flight, in registers (no lambdas over arrays: the
-// compiler left such captured arrays in scratch).
+// compiler left such captured arrays in scratch).  Thread piece k covers row
+// row_of(tid, k); consecutive lanes take consecutive pieces of a row, so each
+// load instruction reads whole rows (contiguous bytes).
 template <int D, bool F32>
-struct ProjStage {
-  static constexpr int CPR = D / 8, NPT = CH * CPR / 512;
-  f32x4 x0[NPT], x1[NPT];
-  __device__ __forceinline__ void issue(const ProjArgs& a, const int (&idn)[NPT], int tid) {
+struct ProjStage {  // f32 rows: pieces of 4 floats, split into bf16 hi + lo planes
+  static constexpr int PPR = D / 4, NPC = CH * PPR / 512;
+  f32x4 v[NPC];
+  // (PPR = 64: a wave's pieces are one row, its id wave-uniform: scalar registers)
+  __device__ static int row_of(int tid, int k) {
+    const int r = (tid + 512 * k) / PPR;
+    return PPR == 64 ? __builtin_amdgcn_readfirstlane(r) : r;
+  }
+  __device__ __forceinline__ void issue(const ProjArgs& a, const int (&idn)[NPC], int tid) {
 #pragma unroll
-    for (int k = 0; k < NPT; ++k) {
-      const int cc = (tid + 512 * k) % CPR;
-      x0[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-      x1[k] = x0[k];
-      if (idn[k] >= 0 && idn[k] < a.n_table) {
-        const f32x4* src = reinterpret_cast<const f32x4*>(static_cast<const float*>(a.table) + (int64_t)idn[k] * D + 8 * cc);
-        x0[k] = __builtin_nontemporal_load(src);
-        x1[k] = __builtin_nontemporal_load(src + 1);
-      }
+    for (int k = 0; k < NPC; ++k) {
+      const int c4 = (tid + 512 * k) % PPR;
+      v[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (idn[k] >= 0 && idn[k] < a.n_table)
+        v[k] = __builtin_nontemporal_load(
+            reinterpret_cast<const f32x4*>(static_cast<const float*>(a.table) + (int64_t)idn[k] * D + 4 * c4));
     }
   }
   __device__ __forceinline__ void store(unsigned char* hi, unsigned char* lo, int tid) const {
 #pragma unroll
-    for (int k = 0; k < NPT; ++k) {
-      const int e = tid + 512 * k, row = e / CPR, cc = e % CPR;
-      bf16x8 h, l;
+    for (int k = 0; k < NPC; ++k) {
+      const int e = tid + 512 * k, row = e / PPR, c4 = e % PPR;
+      bf16x4 h, l;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         short hj, lj;
-        split_bf16(x0[k][j], hj, lj);
+        split_bf16(v[k][j], hj, lj);
         h[j] = hj;
         l[j] = lj;
-        split_bf16(x1[k][j], hj, lj);
-        h[4 + j] = hj;
-        l[4 + j] = lj;
       }
-      *reinterpret_cast<bf16x8*>(hi + img_off<D>(row, cc)) = h;
-      *reinterpret_cast<bf16x8*>(lo + img_off<D>(row, cc)) = l;
+      const int o = img_off<D>(row, c4 >> 1) + 8 * (c4 & 1);
+      *reinterpret_cast<bf16x4*>(hi + o) = h;
+      *reinterpret_cast<bf16x4*>(lo + o) = l;
     }
   }
 };
 template <int D>
-struct ProjStage<D, false> {
-  static constexpr int CPR = D / 8, NPT = CH * CPR / 512;
-  bf16x8 v[NPT];
-  __device__ __forceinline__ void issue(const ProjArgs& a, const int (&idn)[NPT], int tid) {
+struct ProjStage<D, false> {  // bf16 rows: pieces of 8 elements
+  static constexpr int PPR = D / 8, NPC = CH * PPR / 512;
+  bf16x8 v[NPC];
+  __device__ static int row_of(int tid, int k) { return (tid + 512 * k) / PPR; }
+  __device__ __forceinline__ void issue(const ProjArgs& a, const int (&idn)[NPC], int tid) {
 #pragma unroll
-    for (int k = 0; k < NPT; ++k) {
-      const int cc = (tid + 512 * k) % CPR;
+    for (int k = 0; k < NPC; ++k) {
+      const int cc = (tid + 512 * k) % PPR;
       v[k] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
       if (idn[k] >= 0 && idn[k] < a.n_table)
         v[k] = __builtin_nontemporal_load(
@@ -912,8 +915,8 @@ struct ProjStage<D, false> {
   }
   __device__ __forceinline__ void store(unsigned char* hi, unsigned char*, int tid) const {
 #pragma unroll
-    for (int k = 0; k < NPT; ++k) {
-      const int e = tid + 512 * k, row = e / CPR, cc = e % CPR;
+    for (int k = 0; k < NPC; ++k) {
+      const int e = tid + 512 * k, row = e / PPR, cc = e % PPR;
       *reinterpret_cast<bf16x8*>(hi + img_off<D>(row, cc)) = v[k];
     }
   }
@@ -927,9 +930,9 @@ __global__ __launch_bounds__(512, 1) void din_rerank_project_kernel(ProjArgs a) 
   // chunk's rows are in flight (registers) during this chunk's MFMAs, their ids
   // one chunk further ahead.  HBM-bound: a chunk's MFMAs (<= 2 tiles x 4 row
   // tiles per wave) take less than its rows' share of the bandwidth.
-  constexpr int CPR = D / 8, KSD = D / 32, NT = 512;
-  constexpr int NPT = CH * CPR / NT;  // 8-element pieces per thread per chunk
-  static_assert(NPT >= 1 && CH * CPR % NT == 0, "din_rerank_project: staging split");
+  constexpr int KSD = D / 32, NT = 512;
+  constexpr int NPT = ProjStage<D, F32>::NPC;  // row pieces per thread per chunk
+  static_assert(NPT >= 1 && CH * ProjStage<D, F32>::PPR % NT == 0, "din_rerank_project: staging split");
   extern __shared__ __attribute__((aligned(16))) unsigned char pimg[];  // hi image [CH][D] bf16 (+ lo image)
   unsigned char* iml = pimg + CH * D * 2;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l15 = lane & 15, l4 = lane >> 4;
@@ -966,7 +969,7 @@ __global__ __launch_bounds__(512, 1) void din_rerank_project_kernel(ProjArgs a) 
   auto load_ids = [&](int64_t c) __attribute__((always_inline)) {
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
-      const int64_t r = c * CH + (tid + NT * k) / CPR;
+      const int64_t r = c * CH + ProjStage<D, F32>::row_of(tid, k);
       idn[k] = c < nchunk && r < a.n ? a.rows[r] : -1;
     }
   };

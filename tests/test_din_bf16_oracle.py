@@ -229,6 +229,19 @@ def test_rerank_fused_vs_oracle_c5_shape(gpu):
         refs.append((ref, Lb[u][valid].astype(np.int64)))
     print(f"fused re-rank logits max abs err vs the fp64 reference: {worst:.3g}")
     assert worst < 1e-4, worst
+    # the row-reading kernel (nrk_din_rerank, kept for C callers with a bf16
+    # table; its arithmetic order differs from the projected lane kernel's)
+    from newsrecommend_amd.pipeline import rerank_ragged
+    off = torch.arange(U, device=dev, dtype=torch.int64) * C
+    direct = rerank_ragged(model, table, hist, cand.reshape(-1), off, torch.full((U,), C, dtype=torch.int32, device=dev),
+                           None, off, U * C, direct=True).view(U, C).cpu().numpy()
+    worst_d = 0.0
+    for u in range(U):
+        valid = (Cn[u] >= 0) & (Cn[u] < N)
+        assert np.isneginf(direct[u][~valid]).all()
+        worst_d = max(worst_d, float(np.abs(direct[u][valid] - refs[u][0]).max()))
+    print(f"row-reading re-rank kernel: max abs err vs the fp64 reference {worst_d:.3g}")
+    assert worst_d < 1e-4, worst_d
     # every user's NDCG@5 is compared; a difference is only admissible where the
     # positive lies within 2 x the measured logit error of another candidate
     near, differ = 0, 0
