@@ -13,12 +13,15 @@ namespace rr {
 // ---- the projected re-rank, one wave per 32 candidates (nrk_din_rerank_projected
 // for F <= 64).  The scoring is the VALU-bound part: per (candidate, history
 // row, attention unit) one add and one |.|-fma, the add packed two units at a
-// time.  Lane (cs, h) = (candidate cs of the wave's 32, unit half h): the
-// candidate's U' half stays in registers for all rows, each P' row is read by
-// one LDS wave-instruction for 32 candidates (two addresses, one per half, on
-// different banks), the unit signs sgn(w2) of the half are f16 pairs in A / 4
-// registers (v_fma_mix operands), and the halves' partial sums meet by one
-// permlane32 swap per row.  Every other step of a candidate (softmax,
+// time.  Lane (pc, q) = (candidate pair pc of the wave's 32 candidates, unit
+// quarter q): the pair's U' quarter stays in registers for all rows, each P'
+// row is read by one LDS wave-instruction for all 32 candidates (four
+// addresses, one per quarter, on different banks) and each value it brings
+// serves two candidates (one LDS read per 12 VALU; one per 6 with a candidate
+// per lane over unit halves cost 5 % more), the quarter's unit signs sgn(w2)
+// are f16 pairs in A / 8 registers (v_fma_mix operands), and the quarters'
+// partial sums meet by a reduce-scatter of the four (candidate, row) values of
+// a row pair (three permlane swaps).  Every other step of a candidate (softmax,
 // e R, the head) is wave-local too: a wave waits for another only when the
 // block moves to the next user (one staging of the history projections
 // [P' | R], three barriers per user, against five per 64-candidate chunk in
@@ -34,8 +37,8 @@ constexpr int CPI = 32;  // candidates per wave item
 template <int A, int F>
 struct Lay {  // byte offsets
   static constexpr int F2 = F / 2;
-  static constexpr int PST = A + 8;       // P' row stride (floats): unit half 1 at A / 2 + 4 (other banks than half 0)
-  static constexpr int HOFF = A / 2 + 4;
+  static constexpr int QST = A / 4 + 4;  // P' unit quarter q at q QST floats: the four quarters on other banks
+  static constexpr int PST = 4 * QST;     // P' row stride (floats)
   static constexpr int SST = LP + 2;      // scores [CPI][SST] f32: lanes (cs, h) write 2 cs + h apart, no conflicts
   static constexpr int EST = LP + 8;      // e planes [CPI][EST] bf16: conflict-free 16-B fragment reads
   static constexpr int c1 = 0;                          // [F]
@@ -56,7 +59,7 @@ struct Lay {  // byte offsets
 template <int A, int F>
 __global__ __launch_bounds__(NT, 1) void din_rerank_lane_kernel(RerankArgs a) {
   using LY = Lay<A, F>;
-  constexpr int F2 = F / 2, AH = A / 2, NG = AH / 8, AF = A + F, PST = LY::PST, SST = LY::SST, EST = LY::EST;
+  constexpr int F2 = F / 2, AQ = A / 4, NG = AQ / 8, AF = A + F, PST = LY::PST, QST = LY::QST, SST = LY::SST, EST = LY::EST;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* c1s = reinterpret_cast<float*>(smem + LY::c1);
   float* c2s = reinterpret_cast<float*>(smem + LY::c2);
@@ -90,11 +93,11 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_lane_kernel(RerankArgs a) {
   }
   if (tid == 0) qslot[0] = atomicAdd(a.queue, 1);
   __syncthreads();
-  // sgn(w2) of this lane's unit half, resident as f16 pairs (+-1 exactly; the
-  // |y|-fmas take them as v_fma_mix operands): A / 4 registers
-  h2 sgh[A / 4];
+  // sgn(w2) of this lane's unit quarter, resident as f16 pairs (+-1 exactly;
+  // the |y|-fmas take them as v_fma_mix operands): A / 8 registers
+  h2 sgh[A / 8];
 #pragma unroll
-  for (int j = 0; j < A / 4; ++j) sgh[j] = reinterpret_cast<const h2*>(a.sgn)[((tid >> 5) & 1) * (A / 4) + j];
+  for (int j = 0; j < A / 8; ++j) sgh[j] = reinterpret_cast<const h2*>(a.sgn)[((tid >> 4) & 3) * (A / 8) + j];
   int u = qslot[0];
 
   while (u < a.nU) {
@@ -117,7 +120,7 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_lane_kernel(RerankArgs a) {
         if (row < nv) v = *reinterpret_cast<const float4*>(a.hproj + ((int64_t)u * a.L + nth_set_bit(vm, row)) * AF + 4 * part);
         if (part < A / 4) {
           const int c = 4 * part;
-          *reinterpret_cast<float4*>(Pp + row * PST + (c < AH ? c : c + 4)) = v;
+          *reinterpret_cast<float4*>(Pp + row * PST + (c / AQ) * QST + c % AQ) = v;
         } else {
           const int f0 = 4 * (part - A / 4);
           const float x[4] = {v.x, v.y, v.z, v.w};
@@ -134,7 +137,7 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_lane_kernel(RerankArgs a) {
     __syncthreads();
     if (ctot > 0) {  // SP / 2 per row: thread = (row, eighth of the units)
       const int r = tid >> 3, j = tid & 7;
-      const float* pr = Pp + r * PST + (j < 4 ? 0 : 4) + j * (A / 8);  // (an eighth never straddles the halves)
+      const float* pr = Pp + r * PST + (j >> 1) * QST + (j & 1) * (A / 8);  // (an eighth never straddles the quarters)
       float sp = 0.f;
 #pragma unroll
       for (int i = 0; i < A / 8; ++i) sp += pr[i];
@@ -145,26 +148,29 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_lane_kernel(RerankArgs a) {
     const int un = qslot[1];
     const int nitem = (ctot + CPI - 1) / CPI;
 
-    // U' of this lane's candidate (half h) for item it_: loaded one item ahead
-    // (during the previous item's softmax and head).  An absent candidate
-    // reads a valid row (a history projection): finite values in its own row
-    // of every product, never written out.  (A macro: see NRK_LK_RDG.)
-    float uq[AH];
-#define NRK_LK_LDU(it_)                                                                              \
-  {                                                                                                  \
-    int tq_ = threadIdx.x;                                                                           \
-    asm volatile("" : "+v"(tq_));                                                                    \
-    const int ci_ = (it_) * CPI + (tq_ & 31);                                                        \
-    const float* src_ = ci_ < clen ? a.cproj + (coff + ci_) * AF                                     \
-                                   : (ci_ == clen && a.extra ? a.xproj + (int64_t)u * AF : a.hproj); \
-    const float* us_ = src_ + ((tq_ >> 5) & 1) * AH;                                                 \
-    _Pragma("unroll") for (int q_ = 0; q_ < AH / 4; ++q_) {                                         \
-      const float4 x_ = *reinterpret_cast<const float4*>(us_ + 4 * q_);                              \
-      uq[4 * q_] = x_.x;                                                                             \
-      uq[4 * q_ + 1] = x_.y;                                                                         \
-      uq[4 * q_ + 2] = x_.z;                                                                         \
-      uq[4 * q_ + 3] = x_.w;                                                                         \
-    }                                                                                                \
+    // U' of this lane's two candidates (2 pc, 2 pc + 1 of the item, unit quarter
+    // q) for item it_: loaded one item ahead (during the previous item's
+    // softmax and head).  An absent candidate reads a valid row (a history
+    // projection): finite values in its own row of every product, never
+    // written out.  (A macro: see NRK_LK_RDG.)
+    float uq[2][AQ];
+#define NRK_LK_LDU(it_)                                                                                  \
+  {                                                                                                      \
+    int tq_ = threadIdx.x;                                                                               \
+    asm volatile("" : "+v"(tq_));                                                                        \
+    _Pragma("unroll") for (int c_ = 0; c_ < 2; ++c_) {                                                  \
+      const int ci_ = (it_) * CPI + 2 * (tq_ & 15) + c_;                                                 \
+      const float* src_ = ci_ < clen ? a.cproj + (coff + ci_) * AF                                       \
+                                     : (ci_ == clen && a.extra ? a.xproj + (int64_t)u * AF : a.hproj);   \
+      const float* us_ = src_ + ((tq_ >> 4) & 3) * AQ;                                                   \
+      _Pragma("unroll") for (int q_ = 0; q_ < AQ / 4; ++q_) {                                           \
+        const float4 x_ = *reinterpret_cast<const float4*>(us_ + 4 * q_);                                \
+        uq[c_][4 * q_] = x_.x;                                                                           \
+        uq[c_][4 * q_ + 1] = x_.y;                                                                       \
+        uq[c_][4 * q_ + 2] = x_.z;                                                                       \
+        uq[c_][4 * q_ + 3] = x_.w;                                                                       \
+      }                                                                                                  \
+    }                                                                                                    \
   }
     if (w < nitem) NRK_LK_LDU(w)
 
@@ -174,24 +180,40 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_lane_kernel(RerankArgs a) {
       // of the item to the kernel entry and spills them
       int tq = threadIdx.x;
       asm volatile("" : "+v"(tq));
-      const int lane = tq & 63, l15 = lane & 15, l4 = lane >> 4, cs = lane & 31, h = lane >> 5;
+      const int lane = tq & 63, l15 = lane & 15, l4 = lane >> 4;
+      // scoring lanes: candidate pair pc, unit quarter q; after the quarters'
+      // sums meet, lane q keeps candidate cs = 2 pc + (q >> 1), rows of parity h = q & 1
+      const int pc = lane & 15, qq = lane >> 4, cs = 2 * pc + (qq >> 1), h = qq & 1;
       const int c0 = it * CPI, nci = ctot - c0 < CPI ? ctot - c0 : CPI;
-      {  // validity of this lane's candidate (its id; -1 past the list)
+      {  // validity of this lane's kept candidate (its id; -1 past the list)
         const int ci = c0 + cs;
         const int cid = ci < clen ? a.cand[coff + ci] : (ci == clen && a.extra ? a.extra[u] : -1);
         if (h == 0) cvw[cs] = cid >= 0 && cid < a.n_table ? 1 : 0;
       }
-      float hsu = 0.f;  // SU / 2
+      float hsu;  // SU / 2 of the kept candidate
+      {
+        float s0 = 0.f, s1 = 0.f;
 #pragma unroll
-      for (int j = 0; j < AH; ++j) hsu += uq[j];
-      hsu = 0.5f * half_swap_sum(hsu);
+        for (int j = 0; j < AQ; ++j) {
+          s0 += uq[0][j];
+          s1 += uq[1][j];
+        }
+        s0 = half_swap_sum(s0);
+        s1 = half_swap_sum(s1);
+        const auto r0 = __builtin_amdgcn_permlane16_swap(__float_as_uint(s0), __float_as_uint(s0), false, false);
+        const auto r1 = __builtin_amdgcn_permlane16_swap(__float_as_uint(s1), __float_as_uint(s1), false, false);
+        s0 = __uint_as_float(r0[0]) + __uint_as_float(r0[1]);
+        s1 = __uint_as_float(r1[0]) + __uint_as_float(r1[1]);
+        hsu = 0.5f * ((qq >> 1) ? s1 : s0);
+      }
 
-      // ---- scores: step p = rows 2p, 2p + 1 over this lane's unit half; the
-      // halves' partial sums meet by a permlane32 swap, lane h keeps row
-      // 2p + h.  P' in groups of 8 units per row, the next group read during
-      // this one (the next step's first during the last), pinned by
-      // scheduling barriers so that the reads never pile up in registers.
-      const float* const pbase = Pp + (h ? LY::HOFF : 0);
+      // ---- scores: step p = rows 2p, 2p + 1 for both candidates over this
+      // lane's unit quarter; the quarters' partial sums meet by a reduce-
+      // scatter of the four (candidate, row) values (two permlane32 and one
+      // permlane16 swap), lane q keeping value q.  P' in groups of 8 units per
+      // row, the next group read during this one (the next step's first during
+      // the last), pinned by scheduling barriers.
+      const float* const pbase = Pp + qq * QST;
       float4 pa[2][2], pb[2][2];  // [buffer][float4 of the group] of the two rows
       // (a macro, not a lambda: arrays captured by a lambda were left in scratch)
 #define NRK_LK_RDG(p_, g, nb)                                                     \
@@ -205,36 +227,48 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_lane_kernel(RerankArgs a) {
       float m = -INFINITY;
       NRK_LK_RDG(0, 0, 0)
       for (int p = 0; 2 * p < nr; ++p) {
-        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f, b0 = 0.f, b1 = 0.f, b2 = 0.f, b3 = 0.f;
+        float acc[2][2][2] = {};  // [candidate][row][even / odd unit]
 #pragma unroll
         for (int g = 0; g < NG; ++g) {
           // (the next step's first group unconditionally: past the last step it
           // reads rows < 66, inside the block's LDS, and is never used)
           if (g + 1 < NG) NRK_LK_RDG(p, g + 1, (g + 1) & 1)
-          else NRK_LK_RDG(p + 1, 0, 0)
+          else if (NG % 2 == 0) NRK_LK_RDG(p + 1, 0, 0)
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
-            const int q = 2 * g + i;  // float4 of the half row
+            const int qf = 2 * g + i;  // float4 of the quarter row
             const float4 x0 = pa[g & 1][i], x1 = pb[g & 1][i];
-            const h2 sa = sgh[2 * q], sb = sgh[2 * q + 1];
-            const f32x2 ua = {uq[4 * q], uq[4 * q + 1]}, ub = {uq[4 * q + 2], uq[4 * q + 3]};
-            const f32x2 y0a = ua + f32x2{x0.x, x0.y}, y0b = ub + f32x2{x0.z, x0.w};
-            const f32x2 y1a = ua + f32x2{x1.x, x1.y}, y1b = ub + f32x2{x1.z, x1.w};
-            a0 = fmaf(fabsf(y0a.x), (float)sa.x, a0);
-            a1 = fmaf(fabsf(y0a.y), (float)sa.y, a1);
-            b0 = fmaf(fabsf(y1a.x), (float)sa.x, b0);
-            b1 = fmaf(fabsf(y1a.y), (float)sa.y, b1);
-            a2 = fmaf(fabsf(y0b.x), (float)sb.x, a2);
-            a3 = fmaf(fabsf(y0b.y), (float)sb.y, a3);
-            b2 = fmaf(fabsf(y1b.x), (float)sb.x, b2);
-            b3 = fmaf(fabsf(y1b.y), (float)sb.y, b3);
+            const h2 sa = sgh[2 * qf], sb = sgh[2 * qf + 1];
+            const f32x2 p0a = {x0.x, x0.y}, p0b = {x0.z, x0.w}, p1a = {x1.x, x1.y}, p1b = {x1.z, x1.w};
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+              const f32x2 ua = {uq[c][4 * qf], uq[c][4 * qf + 1]}, ub = {uq[c][4 * qf + 2], uq[c][4 * qf + 3]};
+              const f32x2 y0a = ua + p0a, y0b = ub + p0b, y1a = ua + p1a, y1b = ub + p1b;
+              acc[c][0][0] = fmaf(fabsf(y0a.x), (float)sa.x, acc[c][0][0]);
+              acc[c][0][1] = fmaf(fabsf(y0a.y), (float)sa.y, acc[c][0][1]);
+              acc[c][1][0] = fmaf(fabsf(y1a.x), (float)sa.x, acc[c][1][0]);
+              acc[c][1][1] = fmaf(fabsf(y1a.y), (float)sa.y, acc[c][1][1]);
+              acc[c][0][0] = fmaf(fabsf(y0b.x), (float)sb.x, acc[c][0][0]);
+              acc[c][0][1] = fmaf(fabsf(y0b.y), (float)sb.y, acc[c][0][1]);
+              acc[c][1][0] = fmaf(fabsf(y1b.x), (float)sb.x, acc[c][1][0]);
+              acc[c][1][1] = fmaf(fabsf(y1b.y), (float)sb.y, acc[c][1][1]);
+            }
           }
           __builtin_amdgcn_sched_barrier(0);
         }
-        const float f0 = half_swap_sum((a0 + a1) + (a2 + a3)), f1 = half_swap_sum((b0 + b1) + (b2 + b3));
+        if (NG % 2 != 0) NRK_LK_RDG(p + 1, 0, 0)  // (odd group count: buffer 0 was this step's last)
+        // v[k], k = 2 candidate + row; lanes q < 2 keep k in {0, 1}, q >= 2 k in {2, 3}
+        const float v0 = acc[0][0][0] + acc[0][0][1], v1 = acc[0][1][0] + acc[0][1][1];
+        const float v2 = acc[1][0][0] + acc[1][0][1], v3 = acc[1][1][0] + acc[1][1][1];
+        const auto e02 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v0), __float_as_uint(v2), false, false);
+        const auto e13 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v1), __float_as_uint(v3), false, false);
+        const float t0 = __uint_as_float(e02[0]) + __uint_as_float(e02[1]);  // k = 0 (q < 2) / 2 (q >= 2)
+        const float t1 = __uint_as_float(e13[0]) + __uint_as_float(e13[1]);  // k = 1 / 3
+        const auto e01 = __builtin_amdgcn_permlane16_swap(__float_as_uint(t0), __float_as_uint(t1), false, false);
+        const float tot = __uint_as_float(e01[0]) + __uint_as_float(e01[1]);  // k = q
         const int r = 2 * p + h;
-        const float sc = fmaf(0.5f, h ? f1 : f0, hsu + hSP[r]);
+        const float sc = fmaf(0.5f, tot, hsu + hSP[r]);
         Sw[cs * SST + r] = sc;
         if (r < nr) m = fmaxf(m, sc);
       }
@@ -255,8 +289,8 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_lane_kernel(RerankArgs a) {
       __builtin_amdgcn_sched_barrier(0);
       if (it + 8 < nitem) NRK_LK_LDU(it + 8)
       __builtin_amdgcn_sched_barrier(0);
-      {
-        const auto mm = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+      {  // the kept candidate's other row parity: lane ^ 16
+        const auto mm = __builtin_amdgcn_permlane16_swap(__float_as_uint(m), __float_as_uint(m), false, false);
         m = fmaxf(__uint_as_float(mm[0]), __uint_as_float(mm[1]));
       }
       // ---- softmax weights -> bf16 hi + lo planes (rows nr .. nrp - 1 zero), sum e
@@ -271,7 +305,10 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_lane_kernel(RerankArgs a) {
           sum = fmaf(r < nv ? 1.f : (float)npad, ev[p], sum);
         }
       }
-      sum = half_swap_sum(sum);
+      {
+        const auto ss = __builtin_amdgcn_permlane16_swap(__float_as_uint(sum), __float_as_uint(sum), false, false);
+        sum = __uint_as_float(ss[0]) + __uint_as_float(ss[1]);
+      }
 #pragma unroll
       for (int p = 0; p < LP / 2; ++p) {
         const int r = 2 * p + h;
