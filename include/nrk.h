@@ -261,6 +261,11 @@ int nrk_din_rerank_project(const void* table, int64_t n_table, int32_t dtype, co
 int nrk_din_rerank_project_hist(const void* table, int64_t n_table, int32_t dtype, const int32_t* rows, int64_t n,
                                 int32_t d, int32_t A, int32_t F, const nrk_din_rerank_params* params, float* out,
                                 void* stream);
+/* The longest history L nrk_din_rerank_projected takes for (A, F): 128 where
+ * the one-wave-per-32-candidates kernel's 128-row form fits the LDS (F <= 64
+ * and A * F not (96, 64) / (128, 64)), else 64 (the reference's max_history
+ * reaches 128, DIN.py:207). */
+int nrk_din_rerank_max_history(int32_t A, int32_t F, int32_t* max_l);
 int nrk_din_rerank_projected(const void* table, int64_t n_table, int32_t dtype, const int32_t* hist, int32_t nU,
                              int32_t L, const int32_t* cand, const int64_t* cand_off, const int32_t* cand_len,
                              const int32_t* extra, const int64_t* out_off, float* out, int32_t d, int32_t A,

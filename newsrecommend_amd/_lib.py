@@ -72,6 +72,7 @@ SIGNATURES = {
                                       c_i32, c_p, c_p, c_size, c_p]),
     "nrk_din_rerank_project": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_i64, c_i32, c_i32, c_i32, c_p, c_p, c_p]),
     "nrk_din_rerank_project_hist": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_i64, c_i32, c_i32, c_i32, c_p, c_p, c_p]),
+    "nrk_din_rerank_max_history": (ctypes.c_int, [c_i32, c_i32, ctypes.POINTER(c_i32)]),
     "nrk_din_rerank_projected": (ctypes.c_int, [c_p, c_i64, c_i32, c_p, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_p,
                                                 c_i32, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p, c_size, c_p]),
     "nrk_rerank_user_stats": (ctypes.c_int, [c_p, c_p, c_p, c_p, c_i32, c_p, c_p, c_p, c_p]),

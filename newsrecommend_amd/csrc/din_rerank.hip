@@ -1124,7 +1124,8 @@ static int rerank_impl(const void* table, int64_t n_table, int32_t dtype, const 
   NRK_CHECK_ARG(d == 64 || d == 128 || d == 256, "din_rerank: emb_dim %d unsupported (64, 128, 256)", d);
   NRK_CHECK_ARG(A >= 32 && A <= 128 && A % 32 == 0, "din_rerank: attn_units %d unsupported (32..128 step 32)", A);
   NRK_CHECK_ARG(F >= 32 && F <= 128 && F % 32 == 0, "din_rerank: fc_units %d unsupported (32..128 step 32)", F);
-  NRK_CHECK_ARG(L >= 1 && L <= rr::LP, "din_rerank: history length %d unsupported (1..%d)", L, rr::LP);
+  const int maxl = cand_proj && F <= 64 ? rr::lane_max_l(A, F) : rr::LP;  // (the lane kernel holds up to 128 rows)
+  NRK_CHECK_ARG(L >= 1 && L <= maxl, "din_rerank: history length %d unsupported (1..%d)", L, maxl);
   NRK_CHECK_ARG(nU >= 0, "din_rerank: bad user count %d", nU);
   if (nU == 0) return NRK_OK;
   NRK_CHECK_ARG(table && hist && cand_off && cand_len && out_off && out && p && ws, "din_rerank: null pointer");
@@ -1184,6 +1185,14 @@ extern "C" int nrk_din_rerank(const void* table, int64_t n_table, int32_t dtype,
                               const nrk_din_rerank_params* p, void* ws, size_t ws_bytes, void* stream) {
   return rerank_impl(table, n_table, dtype, hist, nU, L, cand, cand_off, cand_len, extra, out_off, out, d, A, F, p,
                      nullptr, nullptr, nullptr, ws, ws_bytes, stream);
+}
+
+extern "C" int nrk_din_rerank_max_history(int32_t A, int32_t F, int32_t* max_l) {
+  NRK_CHECK_ARG(max_l, "din_rerank_max_history: null");
+  NRK_CHECK_ARG(A >= 32 && A <= 128 && A % 32 == 0 && F >= 32 && F <= 128 && F % 32 == 0,
+                "din_rerank_max_history: A %d / F %d unsupported", A, F);
+  *max_l = F <= 64 ? rr::lane_max_l(A, F) : rr::LP;
+  return NRK_OK;
 }
 
 extern "C" int nrk_din_rerank_projected(const void* table, int64_t n_table, int32_t dtype, const int32_t* hist,

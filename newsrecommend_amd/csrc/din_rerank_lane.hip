@@ -32,10 +32,14 @@ namespace rr {
 //   the logit on MFMA as in din_rerank_kernel.
 namespace lk {
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-constexpr int NT = 512;  // 8 waves, two per SIMD (the partner wave's LDS reads issue beside this one's VALU)
 constexpr int CPI = 32;  // candidates per wave item
-template <int A, int F>
+// LPK: history rows held.  64: 8 waves per block, two per SIMD (the partner
+// wave's LDS reads issue beside this one's VALU); 128 (histories of 65..128
+// slots, the reference's max_history range): 4 waves, the LDS holds twice the
+// rows and four waves' score regions.
+template <int A, int F, int LPK>
 struct Lay {  // byte offsets
+  static constexpr int LP = LPK, NW = LPK == 64 ? 8 : 4, NT = 64 * NW;
   static constexpr int F2 = F / 2;
   static constexpr int QST = A / 4 + 4;  // P' unit quarter q at q QST floats: the four quarters on other banks
   static constexpr int PST = 4 * QST;     // P' row stride (floats)
@@ -52,14 +56,15 @@ struct Lay {  // byte offsets
   static constexpr int SB = CPI * SST * 4, EB = 2 * CPI * EST * 2, HB = CPI * (F + 4) * 4;
   static constexpr int XB = SB > EB ? SB : EB;
   static constexpr int WB = ((XB > HB ? XB : HB) + 2 * CPI * 4 + 15) & ~15;  // + den, valid [CPI]
-  static constexpr int qs = wv + 8 * WB;
+  static constexpr int qs = wv + NW * WB;
   static constexpr int total = qs + 16;
 };
 
-template <int A, int F>
-__global__ __launch_bounds__(NT, 1) void din_rerank_lane_kernel(RerankArgs a) {
-  using LY = Lay<A, F>;
+template <int A, int F, int LPK>
+__global__ __launch_bounds__((LPK == 64 ? 512 : 256), 1) void din_rerank_lane_kernel(RerankArgs a) {
+  using LY = Lay<A, F, LPK>;
   constexpr int F2 = F / 2, AQ = A / 4, NG = AQ / 8, AF = A + F, PST = LY::PST, QST = LY::QST, SST = LY::SST, EST = LY::EST;
+  constexpr int LP = LPK, NT = LY::NT, NW = LY::NW;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* c1s = reinterpret_cast<float*>(smem + LY::c1);
   float* c2s = reinterpret_cast<float*>(smem + LY::c2);
@@ -107,7 +112,12 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_lane_kernel(RerankArgs a) {
     const int ln = tid & 63;
     const int hid = ln < a.L ? a.hist[(int64_t)u * a.L + ln] : -1;
     const uint64_t vm = __ballot(ln < a.L && hid >= 0 && hid < a.n_table);
-    const int nv = __popcll(vm), npad = a.L - nv, nr = nv + (npad > 0 ? 1 : 0);
+    uint64_t vm1 = 0;  // slots 64 .. 127 (LPK = 128)
+    if constexpr (LP > 64) {
+      const int hid1 = ln + 64 < a.L ? a.hist[(int64_t)u * a.L + ln + 64] : -1;
+      vm1 = __ballot(ln + 64 < a.L && hid1 >= 0 && hid1 < a.n_table);
+    }
+    const int nv0 = __popcll(vm), nv = nv0 + __popcll(vm1), npad = a.L - nv, nr = nv + (npad > 0 ? 1 : 0);
     const int nrp = (nr + 31) & ~31;
     __syncthreads();  // the previous user's items are done with P', SP, R
     if (tid == 0) qslot[1] = atomicAdd(a.queue, 1);
@@ -117,7 +127,10 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_lane_kernel(RerankArgs a) {
       for (int e = tid; e < LP * (AF / 4); e += NT) {
         const int row = e / (AF / 4), part = e % (AF / 4);
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (row < nv) v = *reinterpret_cast<const float4*>(a.hproj + ((int64_t)u * a.L + nth_set_bit(vm, row)) * AF + 4 * part);
+        if (row < nv) {
+          const int slot = row < nv0 ? nth_set_bit(vm, row) : 64 + nth_set_bit(vm1, row - nv0);
+          v = *reinterpret_cast<const float4*>(a.hproj + ((int64_t)u * a.L + slot) * AF + 4 * part);
+        }
         if (part < A / 4) {
           const int c = 4 * part;
           *reinterpret_cast<float4*>(Pp + row * PST + (c / AQ) * QST + c % AQ) = v;
@@ -136,13 +149,15 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_lane_kernel(RerankArgs a) {
     }
     __syncthreads();
     if (ctot > 0) {  // SP / 2 per row: thread = (row, eighth of the units)
-      const int r = tid >> 3, j = tid & 7;
-      const float* pr = Pp + r * PST + (j >> 1) * QST + (j & 1) * (A / 8);  // (an eighth never straddles the quarters)
-      float sp = 0.f;
+      for (int r = tid >> 3; r < LP; r += NT / 8) {
+        const int j = tid & 7;
+        const float* pr = Pp + r * PST + (j >> 1) * QST + (j & 1) * (A / 8);  // (an eighth never straddles the quarters)
+        float sp = 0.f;
 #pragma unroll
-      for (int i = 0; i < A / 8; ++i) sp += pr[i];
-      sp = oct_sum(sp);
-      if (j == 0) hSP[r] = 0.5f * sp;
+        for (int i = 0; i < A / 8; ++i) sp += pr[i];
+        sp = oct_sum(sp);
+        if (j == 0) hSP[r] = 0.5f * sp;
+      }
     }
     __syncthreads();
     const int un = qslot[1];
@@ -174,7 +189,7 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_lane_kernel(RerankArgs a) {
   }
     if (w < nitem) NRK_LK_LDU(w)
 
-    for (int it = w; it < nitem; it += 8) {
+    for (int it = w; it < nitem; it += NW) {
       // lane indices re-derived per item from a thread id the compiler cannot
       // see through: otherwise it hoists every per-lane LDS / global address
       // of the item to the kernel entry and spills them
@@ -287,7 +302,7 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_lane_kernel(RerankArgs a) {
       // the next item's U' (after the Q1 loads: the h1 MFMA's wait for Q1 then
       // does not cover them)
       __builtin_amdgcn_sched_barrier(0);
-      if (it + 8 < nitem) NRK_LK_LDU(it + 8)
+      if (it + NW < nitem) NRK_LK_LDU(it + NW)
       __builtin_amdgcn_sched_barrier(0);
       {  // the kept candidate's other row parity: lane ^ 16
         const auto mm = __builtin_amdgcn_permlane16_swap(__float_as_uint(m), __float_as_uint(m), false, false);
@@ -323,11 +338,12 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_lane_kernel(RerankArgs a) {
 
       // ---- h1 = relu(Q1 + (e R) / sum e + c1): C tile rows = candidates 16 ct + 4 l4 + k
       const int nks = nrp / 32;
-      bf16x8 eh[2][2], el[2][2];  // [ct][ks] (all read before h1 is written over them)
+      constexpr int KS = LP / 32;
+      bf16x8 eh[2][KS], el[2][KS];  // [ct][ks] (all read before h1 is written over them)
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
+        for (int ks = 0; ks < KS; ++ks) {
           const int o = (16 * ct + l15) * EST + 32 * ks + 8 * l4;
           eh[ct][ks] = *reinterpret_cast<const bf16x8*>(Eh + o);
           el[ct][ks] = *reinterpret_cast<const bf16x8*>(El + o);
@@ -350,7 +366,7 @@ __global__ __launch_bounds__(NT, 1) void din_rerank_lane_kernel(RerankArgs a) {
 #pragma unroll
           for (int k = 0; k < 4; ++k) acc[k] = q1v[ct][ft][k] * dv[ct][k];
 #pragma unroll
-          for (int ks = 0; ks < 2; ++ks) {
+          for (int ks = 0; ks < KS; ++ks) {
             if (ks < nks) {
               const bf16x8 rh = *reinterpret_cast<const bf16x8*>(Rth + f * LP + 32 * ks + 8 * l4);
               const bf16x8 rl = *reinterpret_cast<const bf16x8*>(Rtl + f * LP + 32 * ks + 8 * l4);
@@ -415,18 +431,30 @@ __global__ void sign_cols_kernel(const float* __restrict__ w2, int A, _Float16* 
   for (int n = threadIdx.x; n < A; n += blockDim.x) sgn[slice_col(n, A)] = w2[n] >= 0.f ? (_Float16)1.f : (_Float16)-1.f;
 }
 
-template <int A, int F>
+template <int A, int F, int LPK>
 int launch(const RerankArgs& a, hipStream_t st) {
-  constexpr size_t lds = Lay<A, F>::total;
+  using LY = Lay<A, F, LPK>;
+  constexpr size_t lds = LY::total;
   static_assert(lds <= 160 * 1024, "din_rerank_lane: LDS");
   const int grid = a.nU < 256 ? a.nU : 256;
-  hipLaunchKernelGGL((din_rerank_lane_kernel<A, F>), dim3(grid), dim3(NT), lds, st, a);
+  hipLaunchKernelGGL((din_rerank_lane_kernel<A, F, LPK>), dim3(grid), dim3(LY::NT), lds, st, a);
   NRK_CHECK_LAUNCH("din_rerank_lane_kernel");
   return NRK_OK;
 }
+// the longest history the lane kernel holds for (A, F): 128 where the
+// 128-row form's LDS fits, else 64
+template <int A, int F>
+constexpr int max_l() { return Lay<A, F, 128>::total <= 160 * 1024 ? 128 : 64; }
+template <int A, int F>
+int launch_l(const RerankArgs& a, hipStream_t st) {
+  if constexpr (max_l<A, F>() == 128) {
+    if (a.L > 64) return launch<A, F, 128>(a, st);
+  }
+  return launch<A, F, 64>(a, st);
+}
 template <int A>
 int launch_f(const RerankArgs& a, hipStream_t st) {
-  return a.F == 32 ? launch<A, 32>(a, st) : launch<A, 64>(a, st);
+  return a.F == 32 ? launch_l<A, 32>(a, st) : launch_l<A, 64>(a, st);
 }
 inline int launch_a(int A, const RerankArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(sign_cols_kernel, dim3(1), dim3(128), 0, st, a.w2, A, reinterpret_cast<_Float16*>(const_cast<void*>(a.sgn)));
@@ -441,6 +469,20 @@ inline int launch_a(int A, const RerankArgs& a, hipStream_t st) {
 }  // namespace lk
 
 int launch_lane(int A, const RerankArgs& a, hipStream_t st) { return lk::launch_a(A, a, st); }
+
+int lane_max_l(int A, int F) {
+  switch (A * 1000 + F) {
+    case 32032: return lk::max_l<32, 32>();
+    case 32064: return lk::max_l<32, 64>();
+    case 64032: return lk::max_l<64, 32>();
+    case 64064: return lk::max_l<64, 64>();
+    case 96032: return lk::max_l<96, 32>();
+    case 96064: return lk::max_l<96, 64>();
+    case 128032: return lk::max_l<128, 32>();
+    case 128064: return lk::max_l<128, 64>();
+    default: return 0;
+  }
+}
 
 }  // namespace rr
 }  // namespace nrk

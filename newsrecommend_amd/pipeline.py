@@ -218,14 +218,28 @@ def rerank_ragged(model, table: torch.Tensor, hist_rows: torch.Tensor, cand: tor
     return out
 
 
+def rerank_max_history(A: int, F: int) -> int:
+    """nrk_din_rerank_max_history: the longest history the fused re-rank holds
+    for (A, F) (128 for F <= 64 where the lane kernel's 128-row form fits, else
+    RERANK_MAX_L)."""
+    from . import _lib
+
+    if A not in (32, 64, 96, 128) or F not in (32, 64, 96, 128):
+        return RERANK_MAX_L
+    v = ctypes.c_int32(0)
+    _lib.check(_lib.load().nrk_din_rerank_max_history(A, F, ctypes.byref(v)), "din_rerank_max_history")
+    return int(v.value)
+
+
 def fused_ok(model, table: torch.Tensor, L: int):
     """Why the fused re-rank kernel cannot run this model / table (empty: it can)."""
     W1 = model.attn.attn[0].weight
     A, F = W1.shape[0], model.fc[1].weight.shape[0]
     d = table.shape[1]
+    max_l = rerank_max_history(A, F) if L > RERANK_MAX_L else RERANK_MAX_L
     return [w for w, bad in (("table is neither bf16 nor f32", table.dtype not in (torch.bfloat16, torch.float32)),
                              (f"emb_dim {d} not in (64, 128, 256)", d not in (64, 128, 256)),
-                             (f"history length {L} > {RERANK_MAX_L}", L > RERANK_MAX_L),
+                             (f"history length {L} > {max_l}", L > max_l),
                              (f"attn_units {A} not in (32, 64, 96, 128)", A not in (32, 64, 96, 128)),
                              (f"fc_units {F} not in (32, 64, 96, 128)", F not in (32, 64, 96, 128)),
                              ("model emb_dim != table width", W1.shape[1] != 2 * d),

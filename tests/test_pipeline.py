@@ -147,15 +147,18 @@ def _oracle_logits(model, T, hist_u, cand_u):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("d,L,C,A,F", [(256, 50, 201, 128, 32), (64, 20, 90, 32, 64), (128, 64, 70, 96, 128),
-                                       (256, 64, 130, 64, 96), (128, 33, 37, 128, 32)])
+                                       (256, 64, 130, 64, 96), (128, 33, 37, 128, 32),
+                                       # histories past 64 slots (max_history reaches 128, DIN.py:207):
+                                       # the lane kernel's 128-row form
+                                       (256, 128, 75, 128, 32), (128, 96, 40, 64, 64), (64, 100, 33, 32, 32)])
 def test_rerank_fused_vs_oracle_and_per_candidate(d, L, C, A, F):
     """nrk_din_rerank over the reference's hyper-parameter space (Optuna
     DIN.py:203-204: attn_units and fc_units 32..128 step 32) against the fp64
     oracle (<= 1e-4 of the logit scale) and against every candidate as its own
     DIN sample (model.forward_ids: the same logits up to that path's bf16 W1k,
     2e-3); padded histories (an empty one included) and padded candidates.
-    Chunks of 64 candidates and tails of 37 / 26 / 9 / 6 / 2 cover the kernel's
-    2, 4 and 8 row-group forms."""
+    Candidate counts that are not multiples of the 32-candidate wave item, and
+    histories of 65..128 slots (the 128-row form)."""
     from newsrecommend_amd.pipeline import rerank
 
     dev = torch.device("cuda")

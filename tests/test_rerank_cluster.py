@@ -219,9 +219,10 @@ def test_rerank_clusters_f32_table_bit_identical_on_bf16_exact_rows(gpu):
 
 
 def test_rerank_clusters_fallback_long_history_and_duplicate_positive(gpu):
-    """a history longer than the fused kernel holds (L = 96; the
-    reference's Optuna space goes to 128, DIN.py:207) falls back, with a
-    warning, to the per-candidate path per cluster instead of raising; its
+    """a history longer than the fused kernels hold for the model
+    (L = 96 at A = 128, F = 64, where the lane kernel's 128-row form does not
+    fit the LDS; the reference's Optuna space goes to 128, DIN.py:207) falls
+    back, with a warning, to the per-candidate path per cluster instead of raising; its
     logits match the fp64 oracle (<= 1e-4), and the label is the FIRST
     occurrence of a positive row that appears twice in its cluster
     (EvalDataset, DIN.py:27-31)."""
@@ -234,7 +235,7 @@ def test_rerank_clusters_fallback_long_history_and_duplicate_positive(gpu):
     g = torch.Generator(device=dev).manual_seed(5)
     table = torch.randn((N, d), generator=g, device=dev) * 0.5
     torch.manual_seed(2)
-    model = DIN(d, 64, 32, 0.2).to(dev).eval()
+    model = DIN(d, 128, 64, 0.2).to(dev).eval()
     sizes = [40, 0, 75]
     rows = torch.randint(0, N, (sum(sizes),), generator=g, device=dev, dtype=torch.int32)
     rows[10] = rows[30]  # cluster 0 holds row rows[30] twice: positions 10 and 30
