@@ -879,6 +879,12 @@ def _din_d256(args, dev):
         path = []
         rate = _din_rate(table, hist, tgt, lab, d, A, F, B, dev, steps=200 if B == 64 else 40, path=path)
         out[f"B={B}"] = {"samples_per_s": rate, "us_per_step": B / rate * 1e6, "path": path[0]}
+    # max_history 128, the top of the reference's Optuna range (DIN.py:207): two
+    # half-samples per sample in the column-split backward
+    hist, tgt, lab = synthetic_click_rows(1_000_000, args.din_items, 128, seed=8, device=dev)
+    path = []
+    rate = _din_rate(table, hist, tgt, lab, d, A, F, 4096, dev, steps=40, path=path)
+    out["L=128,B=4096"] = {"samples_per_s": rate, "us_per_step": 4096 / rate * 1e6, "path": path[0]}
     del table, hist, tgt, lab
     torch.cuda.empty_cache()
     return out

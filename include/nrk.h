@@ -150,7 +150,8 @@ int nrk_din_attn_bwd(const void* keys, const int32_t* hist_ids, int64_t n_table,
                      void* ws, size_t ws_bytes, void* stream);
 
 /* The same backward with the query half folded in (train step, id form, bf16
- * table, d in {64, 128}): also accumulates dW1q = sum_b dU[b] q[b]^T and
+ * table, d in {64, 128}, or 256 with dU == NULL — L 65..128 there as two
+ * half-samples per sample after a softmax-term pass): also accumulates dW1q = sum_b dU[b] q[b]^T and
  * db1 = sum_b dU[b] per workgroup, and WRITES the layer's parameter gradients
  * straight into the model's tensors: gW1 [A][2d] = [dW1q | dW1k], gb1 [A],
  * gw2 [A], gb2 [1] (DIN.py:146 loss.backward() for attn.attn.{0,2}).

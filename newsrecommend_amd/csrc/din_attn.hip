@@ -2050,13 +2050,21 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8g_kernel(
 // also accumulates dw2, db1 and the sample's dU row (its partner stores zeros
 // in the second dU half the dW1q kernel adds).  Small pieces per sample:
 // dpooled [256] (4 pieces), alpha [LP <= 64] (1), U [128] (2), one unused.
-template <int D, int LP, int NSLOT>
+//
+// SPLIT (histories of 65..128 rows, LP = 64): every sample runs as two
+// half-samples (rows [0, 64) and [64, L)).  Past the softmax the backward is
+// row-local, so the halves only share the softmax term cdot = sum_l alpha_l
+// dalpha_l, which din_cdot_kernel forms beforehand (cdv[b], loaded into the
+// alpha slot's second half by the otherwise unused small piece); half h's dU
+// row goes to dUp[h] (the dW1q kernel adds both), its other partials to the
+// same accumulators as any sample's.
+template <int D, int LP, int NSLOT, bool SPLIT = false>
 __global__ __launch_bounds__(512, 1) void din_bwd_deep8c_kernel(
     const uint16_t* __restrict__ table, const int32_t* __restrict__ ids, int64_t n_table, const float* __restrict__ U,
     const uint16_t* __restrict__ W1k, const float* __restrict__ w2, int B, int L, int A,
     const float* __restrict__ dpooled, const float* __restrict__ alpha, float* __restrict__ slabs,
-    float* __restrict__ dUp, float* __restrict__ dummy) {
-  static_assert(D == 256 && LP <= 64, "deep8c: D = 256, LP <= 64");
+    float* __restrict__ dUp, float* __restrict__ dummy, const float* __restrict__ cdv = nullptr) {
+  static_assert(D == 256 && LP <= 64 && (!SPLIT || LP == 64), "deep8c: D = 256, LP <= 64 (SPLIT: 64)");
   constexpr int DH = D / 2;
   constexpr int CPR = D / 8, KSH = DH / 16, NCTH = DH / 32, NC = LP / 32;
   constexpr int NPW = LP * CPR / 512;  // key-image DMA pieces per wave
@@ -2100,17 +2108,28 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8c_kernel(
   float du_keep = 0.f;
   int64_t b_keep = -1;
   float* const dmy = dummy + (size_t)blockIdx.x * 512 + tid;
+  // work items: samples, or (SPLIT) half-samples v -> sample v >> 1, rows [64 (v & 1), ...)
+  const int64_t NV = SPLIT ? 2 * (int64_t)B : B;
+  auto rows_of = [&](int64_t v) { return SPLIT ? min(LP, L - 64 * (int)(v & 1)) : L; };
+  auto row0_of = [&](int64_t v) { return SPLIT ? 64 * (int)(v & 1) : 0; };
   auto store_du = [&]() {  // half ch of dUp: the ch = 0 wave's full row sum, zeros from ch = 1
-    float* dst = (b_keep >= 0 && us < nsl && h == 0) ? dUp + ((size_t)ch * B + b_keep) * A + 32 * us + r : dmy;
+    const int64_t bs = SPLIT ? b_keep >> 1 : b_keep;
+    const int part = SPLIT ? (int)(b_keep & 1) : ch;
+    float* dst = (b_keep >= 0 && us < nsl && h == 0 && (!SPLIT || ch == 0))
+                     ? dUp + ((size_t)part * B + bs) * A + 32 * us + r : dmy;
     const float v = ch == 0 ? du_keep : 0.f;
     asm volatile("global_store_dword %0, %1, off" ::"v"(dst), "v"(v) : "memory");
   };
   auto issue_ids = [&](int64_t b, int e) {
-    const int64_t bc = b < B ? b : 0;
+    const int64_t vc = b < NV ? b : 0;
+    const int64_t bc = SPLIT ? vc >> 1 : vc;
+    const int le = rows_of(vc), r0 = row0_of(vc);
     const int i = lane < LP ? lane : 0;
-    glds4_asm(ids + bc * L + (i < L ? i : 0), lds_u32(idring + e * 64));
+    glds4_asm(ids + bc * L + r0 + (i < le ? i : 0), lds_u32(idring + e * 64));
   };
   auto issue_data = [&](int64_t b, int sl, int e) {
+    const int64_t vc = b < NV ? b : 0;
+    const int le = rows_of(vc), r0 = row0_of(vc);
     float* sp = slot0 + sl * SLOT_F;
     uint16_t* img = reinterpret_cast<uint16_t*>(sp + 4 * 128);
 #pragma unroll
@@ -2120,19 +2139,20 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8c_kernel(
       const int row = p / CPR, pc = p % CPR;
       const int cc = pc ^ kswz<CPR>(row);
       const int32_t idv0 = idring[e * 64 + row];
-      const int32_t idr = row < L && b < B ? idv0 : -1;
+      const int32_t idr = row < le && b < NV ? idv0 : -1;
       const uint16_t* src = (idr >= 0 && idr < n_table) ? table + (int64_t)idr * D + cc * 8 : zero_row(b, row) + cc * 8;
       glds16_asm(src, lds_u32(img + u * 64 * 8));
     }
-    const int64_t bc = b < B ? b : 0;
-    {  // small piece w of [dp0, dp1, dp2, dp3, al0, u0, u1, (u1 again: unused slot)]
+    const int64_t bc = SPLIT ? vc >> 1 : vc;
+    {  // small piece w of [dp0, dp1, dp2, dp3, al0, u0, u1, (u1 again: unused slot | SPLIT: cdot)]
       const float* base;
       int i, lim;
       float* dst;
       if (w < 4) { base = dpooled + bc * D; i = 64 * w + lane; lim = D; dst = sp + 64 * w; }
-      else if (w == 4) { base = alpha + bc * L; i = lane; lim = L; dst = sp + 256; }
+      else if (w == 4) { base = alpha + bc * L + r0; i = lane; lim = le; dst = sp + 256; }
       else { base = U + bc * A; i = 64 * ((w - 5) & 1) + lane; lim = A; dst = sp + 384 + 64 * ((w - 5) & 1); }
       if (w == 7) dst = sp + 320;  // the alpha slot's unused second half (LP <= 64)
+      if (SPLIT && w == 7) { base = cdv + bc; i = 0; lim = 1; }
       glds4_asm(base + (i < lim ? i : 0), lds_u32(dst));
     }
   };
@@ -2149,7 +2169,7 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8c_kernel(
     issue_data(b + k * grid, k, k);
   }
   int sl = 0, e = P % RING;
-  for (; b < B; b += grid) {
+  for (; b < NV; b += grid) {
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"((P - 1) * N_D) : "memory");
     store_du();
     issue_ids(b + (P + X) * grid, e + X < RING ? e + X : e + X - RING);
@@ -2162,6 +2182,7 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8c_kernel(
     const float* sal = sp + 256;
     const float* sU = sp + 384;
     const unsigned char* img = reinterpret_cast<const unsigned char*>(sp + 512);
+    const int Le = rows_of(b);
     {  // dalpha[row] = dpooled . K[row]: wave w owns rows [w R, (w+1) R)
       constexpr int R = LP / 8, LPR = 64 / R, CHK = CPR / LPR;
       const int row = w * R + lane / LPR, part = lane % LPR;
@@ -2215,14 +2236,14 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8c_kernel(
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         const int row = 32 * c + r;
-        t += (row < L && h == 0) ? sal[row] * da[c] : 0.f;
+        t += (row < Le && h == 0) ? sal[row] * da[c] : 0.f;
       }
-      const float cdot = wave_sum_fast(t);
+      const float cdot = SPLIT ? sal[64] : wave_sum_fast(t);
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         const int row = 32 * c + r;
         if (h == 0) {
-          const float ds = row < L ? sal[row] * (da[c] - cdot) : 0.f;
+          const float ds = row < Le ? sal[row] * (da[c] - cdot) : 0.f;
           dsbuf[row] = ds;
           if (w == 0) db2_acc += ds;
         }
@@ -2258,13 +2279,20 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8c_kernel(
         }
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          bf16x8 af;
+          bf16x8 af, afl;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const bf16x2_hw pk = {(__bf16)dz[8 * s + 2 * j], (__bf16)dz[8 * s + 2 * j + 1]};
             const uint32_t u = __builtin_bit_cast(uint32_t, pk);
             af[2 * j] = (short)(u & 0xFFFF);
             af[2 * j + 1] = (short)(u >> 16);
+            if constexpr (SPLIT) {  // dz as bf16 hi + lo: 96..128 rows of bf16 dz round past 2e-3 of dW1k
+              const bf16x2_hw pl = {(__bf16)(dz[8 * s + 2 * j] - (float)pk[0]),
+                                    (__bf16)(dz[8 * s + 2 * j + 1] - (float)pk[1])};
+              const uint32_t ul = __builtin_bit_cast(uint32_t, pl);
+              afl[2 * j] = (short)(ul & 0xFFFF);
+              afl[2 * j + 1] = (short)(ul >> 16);
+            }
           }
           const int grp = lane >> 4, i16 = lane & 15;
           const int rowq = 32 * c + 16 * s + 4 * h + (i16 >> 2);
@@ -2277,6 +2305,7 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8c_kernel(
                 __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(img + KImg<true, D>::off(rowq + 8, col)));
             const bf16x8 bfr = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
             dw[cc] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bfr, dw[cc], 0, 0, 0);
+            if constexpr (SPLIT) dw[cc] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afl, bfr, dw[cc], 0, 0, 0);
           }
         }
       }
@@ -2305,6 +2334,42 @@ __global__ __launch_bounds__(512, 1) void din_bwd_deep8c_kernel(
     const float tb2 = wave_sum(db2_acc);
     if (lane == 0) slab[(size_t)A * D + A] = tb2;
   }
+}
+
+// Softmax term of the SPLIT backward (d = 256, L 65..128): cd[b] = sum_l
+// alpha[b][l] (dpooled[b] . K[b][l]) over the bf16 key rows (an invalid id is a
+// zero row).  One wave per sample, a lane per 4 columns; the per-lane partial
+// is linear in the rows, so the wave reduces once at the end.
+template <int D>
+__global__ __launch_bounds__(256) void din_cdot_kernel(const uint16_t* __restrict__ table,
+                                                       const int32_t* __restrict__ ids, int64_t n_table,
+                                                       const float* __restrict__ dpooled,
+                                                       const float* __restrict__ alpha, int B, int L,
+                                                       float* __restrict__ cd) {
+  static_assert(D == 256, "din_cdot: D = 256");
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const float4 dp = *reinterpret_cast<const float4*>(dpooled + b * D + 4 * lane);
+  const int32_t id0 = lane < L ? ids[b * L + lane] : -1;
+  const int32_t id1 = lane + 64 < L ? ids[b * L + 64 + lane] : -1;
+  const float a0 = lane < L ? alpha[b * L + lane] : 0.f;
+  const float a1 = lane + 64 < L ? alpha[b * L + 64 + lane] : 0.f;
+  float t = 0.f;
+#pragma unroll 8
+  for (int l = 0; l < L; ++l) {
+    const int32_t id = __builtin_amdgcn_readlane(l < 64 ? id0 : id1, l & 63);
+    const float al = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(l < 64 ? a0 : a1), l & 63));
+    const bool ok = id >= 0 && id < n_table;
+    const uint2 kv = *reinterpret_cast<const uint2*>(table + (int64_t)(ok ? id : 0) * D + 4 * lane);
+    float s = dp.x * __uint_as_float(kv.x << 16);
+    s = fmaf(dp.y, __uint_as_float(kv.x & 0xFFFF0000u), s);
+    s = fmaf(dp.z, __uint_as_float(kv.y << 16), s);
+    s = fmaf(dp.w, __uint_as_float(kv.y & 0xFFFF0000u), s);
+    t = fmaf(ok ? al : 0.f, s, t);
+  }
+  t = wave_sum(t);
+  if (lane == 0) cd[b] = t;
 }
 
 // dW1q partial tiles for nrk_din_attn_bwd_params (8-wave backward):
@@ -2925,8 +2990,8 @@ static int bwd_params_impl(const void* table, const int32_t* hist_ids, int64_t n
   int rc = check_common(table, dtype, B, L, d, A);
   if (rc) return rc;
   NRK_CHECK_ARG(dtype == NRK_DTYPE_BF16 && hist_ids != nullptr &&
-                    (d == 64 || d == 128 || (d == 256 && dU == nullptr && L <= 64)),
-                "din_bwd_params: needs a bf16 table, history ids and emb_dim 64 or 128 (256: L <= 64, no dU output)");
+                    (d == 64 || d == 128 || (d == 256 && dU == nullptr)),
+                "din_bwd_params: needs a bf16 table, history ids and emb_dim 64 or 128 (256: no dU output)");
   NRK_CHECK_ARG(B > 0, "din_bwd_params: empty batch");
   NRK_CHECK_ARG(q && U && W1k && w2 && (dpooled || dps) && alpha && gW1 && gb1 && gw2 && gb2 && ws,
                 "din_bwd_params: null pointer");
@@ -2952,7 +3017,16 @@ static int bwd_params_impl(const void* table, const int32_t* hist_ids, int64_t n
     constexpr int NS = 3, RING = 4;
     const size_t dsm = (size_t)(NS * (4 * 128 + LPk * d / 2) + 8 * RING * 64 + 8 * 64 + 64 + 8 * 1024) * 4;
     NRK_CHECK_ARG(dsm <= 160 * 1024, "din_bwd_params: L=%d d=%d needs %zu B LDS", L, d, dsm);
-    if (LPk == 32)
+    if (L > 64) {  // two half-samples per sample; the softmax term first (into the dW1q chunk area,
+                   // which din_dwq_kernel only writes after the backward)
+      NRK_CHECK_ARG((size_t)B <= (size_t)DWQ_KC * A * d, "din_bwd_params: batch %d too large for L > 64", B);
+      float* cd = qpart_w8;
+      hipLaunchKernelGGL(din_cdot_kernel<256>, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, st, tb, hist_ids, n_table,
+                         dpooled, alpha, B, L, cd);
+      NRK_CHECK_LAUNCH("din_cdot_kernel");
+      hipLaunchKernelGGL((din_bwd_deep8c_kernel<256, 64, NS, true>), dim3(grid), dim3(512), dsm, st, tb, hist_ids,
+                         n_table, U, wk, w2, B, L, A, dpooled, alpha, slabs, dUp, dmy, cd);
+    } else if (LPk == 32)
       hipLaunchKernelGGL((din_bwd_deep8c_kernel<256, 32, NS>), dim3(grid), dim3(512), dsm, st, tb, hist_ids, n_table, U,
                          wk, w2, B, L, A, dpooled, alpha, slabs, dUp, dmy);
     else

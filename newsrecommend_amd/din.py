@@ -488,7 +488,7 @@ class FusedTrainStep:
         # attention backward that also forms dW1q / db1 and writes every
         # attention gradient in place: no torch ops left inside the step
         Lh = hist_ids.shape[1]
-        max_l = 64 if d == 256 else 128  # d = 256: the column-split backward holds L <= 64 rows
+        max_l = 128  # d = 256, L > 64: the column-split backward in two half-samples per sample
         why = [w for w, bad in (("table is not bf16", table.dtype != torch.bfloat16),
                                 (f"emb_dim {d} not in (64, 128, 256)", d not in (64, 128, 256)),
                                 (f"history length {Lh} > {max_l}", Lh > max_l)) if bad]

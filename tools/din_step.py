@@ -15,13 +15,15 @@ ap.add_argument("--drop", type=float, default=0.36)
 ap.add_argument("--items", type=int, default=2_000_000)
 ap.add_argument("--rows", type=int, default=1_000_000)
 ap.add_argument("--k", type=int, default=1, help="steps per graph launch (FusedTrainStep.step_many)")
+ap.add_argument("--d", type=int, default=128, help="emb_dim (256: the reference's corpus width)")
+ap.add_argument("--L", type=int, default=50, help="history length")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 g = torch.Generator(device=dev).manual_seed(1)
-table = (torch.randn((a.items, 128), generator=g, device=dev) * 0.5).to(torch.bfloat16)
-hist, tgt, lab = synthetic_click_rows(a.rows, a.items, 50, seed=7, device=dev)
+table = (torch.randn((a.items, a.d), generator=g, device=dev) * 0.5).to(torch.bfloat16)
+hist, tgt, lab = synthetic_click_rows(a.rows, a.items, a.L, seed=7, device=dev)
 torch.manual_seed(42)
-model = DIN(128, 128, 32, a.drop).to(dev)
+model = DIN(a.d, 128, 32, a.drop).to(dev)
 tr = FusedTrainStep(model, table, hist, tgt, lab, a.B, lr=1.62e-3, weight_decay=8.96e-5, clip=1.0, steps_per_graph=a.k)
 perm = torch.randperm(a.rows, device=dev)
 nb = a.rows // a.B
@@ -35,4 +37,4 @@ for s in range(0, a.steps, a.k):
             tr.step_many(perm[b * a.B:(b + a.k) * a.B].view(a.k, a.B))[-1])
 torch.cuda.synchronize()
 dt = (time.perf_counter() - t0) / a.steps
-print(f"B={a.B}: {dt * 1e6:.1f} us/step = {a.B / dt / 1e6:.2f} M samples/s, loss {loss.item():.4f}", flush=True)
+print(f"d={a.d} L={a.L} B={a.B} ({tr.path}): {dt * 1e6:.1f} us/step = {a.B / dt / 1e6:.2f} M samples/s, loss {loss.item():.4f}", flush=True)
