@@ -71,7 +71,7 @@ def _bn_inputs(cache, pooled, q):
 @pytest.mark.parametrize("d,L,B,steps,A,F", [(128, 50, 512, 2, 128, 32), (256, 64, 64, 2, 128, 32),
                                              (256, 64, 4096, 1, 128, 32), (128, 50, 512, 1, 64, 128),
                                              (256, 128, 256, 1, 32, 128), (256, 96, 256, 1, 128, 96),
-                                             (256, 100, 512, 2, 128, 32)])
+                                             (256, 100, 512, 2, 128, 32), (256, 65, 320, 1, 64, 64)])
 def test_fused_train_step_fast_path_vs_oracle_c3_shape(gpu, d, L, B, steps, A, F):
     """(128, 50, 512): configs[2]'s shape.  (256, 64, 64) and (256, 64, 4096):
     the reference's own training shape (DIN.py:16 EMBED_DIM from the 256-d
@@ -82,7 +82,8 @@ def test_fused_train_step_fast_path_vs_oracle_c3_shape(gpu, d, L, B, steps, A, F
     generic head kernels (W1 staged in 32-unit chunks), a d = 256 history
     longer than 64 the column-split backward in two half-samples per sample
     (din_cdot_kernel's softmax term first); (256, 100, 512): a ragged second
-    half (36 rows) over two steps."""
+    half (36 rows) over two steps; (256, 65, 320): a one-row second half and a
+    batch that is not a multiple of the workgroup count."""
     from newsrecommend_amd.data import synthetic_click_rows
     from newsrecommend_amd.din import DIN, FusedTrainStep
     from oracle import din_oracle as o
