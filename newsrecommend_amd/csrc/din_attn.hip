@@ -2656,40 +2656,58 @@ __global__ __launch_bounds__(256) void din_u_kernel(const float* __restrict__ q,
   // enters as hi + mid + lo bf16 parts (truncation: every product is the exact
   // f32 product).  Wave w owns the 16-unit tiles w, w + 4, ...
   constexpr int KS = D / 32;
+  constexpr int MAXT = 2;  // A <= 128: at most two of the A / 16 unit tiles per wave
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, l15 = lane & 15, l4 = lane >> 4;
   const int b0 = blockIdx.x * 16;
+  const int b = b0 + l15;
+  // every load of the block in flight before any math: the query rows, then both
+  // unit tiles' W1q rows and biases (L2-resident after the first blocks)
+  float4 qlo[KS], qhi[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    qlo[s] = make_float4(0.f, 0.f, 0.f, 0.f);
+    qhi[s] = qlo[s];
+    if (b < B) {
+      qlo[s] = *reinterpret_cast<const float4*>(q + (int64_t)b * D + 32 * s + 8 * l4);
+      qhi[s] = *reinterpret_cast<const float4*>(q + (int64_t)b * D + 32 * s + 8 * l4 + 4);
+    }
+  }
+  float4 wv0[MAXT][KS], wv1[MAXT][KS];
+  float bv[MAXT];
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) {
+    const int ut = w + 4 * t;
+    const int u = 16 * (ut < A / 16 ? ut : 0) + l15;
+    bv[t] = b1[u];
+    const float* wrow = W1 + (int64_t)u * 2 * D + 8 * l4;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      wv0[t][s] = *reinterpret_cast<const float4*>(wrow + 32 * s);
+      wv1[t][s] = *reinterpret_cast<const float4*>(wrow + 32 * s + 4);
+    }
+  }
   for (int64_t e = (int64_t)blockIdx.x * 256 + tid; e < (int64_t)A * D; e += (int64_t)gridDim.x * 256) {
     const int64_t n = e / D, k = e % D;
     W1k_bf[e] = f32_to_bf16_rne(W1[n * 2 * D + D + k]);
   }
-  const int b = b0 + l15;
   bf16x8 qf[KS];
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
-    float4 lo4 = make_float4(0.f, 0.f, 0.f, 0.f), hi4 = lo4;
-    if (b < B) {
-      lo4 = *reinterpret_cast<const float4*>(q + (int64_t)b * D + 32 * s + 8 * l4);
-      hi4 = *reinterpret_cast<const float4*>(q + (int64_t)b * D + 32 * s + 8 * l4 + 4);
-    }
-    qf[s][0] = (short)f32_to_bf16_rne(lo4.x); qf[s][1] = (short)f32_to_bf16_rne(lo4.y);
-    qf[s][2] = (short)f32_to_bf16_rne(lo4.z); qf[s][3] = (short)f32_to_bf16_rne(lo4.w);
-    qf[s][4] = (short)f32_to_bf16_rne(hi4.x); qf[s][5] = (short)f32_to_bf16_rne(hi4.y);
-    qf[s][6] = (short)f32_to_bf16_rne(hi4.z); qf[s][7] = (short)f32_to_bf16_rne(hi4.w);
+    qf[s][0] = (short)f32_to_bf16_rne(qlo[s].x); qf[s][1] = (short)f32_to_bf16_rne(qlo[s].y);
+    qf[s][2] = (short)f32_to_bf16_rne(qlo[s].z); qf[s][3] = (short)f32_to_bf16_rne(qlo[s].w);
+    qf[s][4] = (short)f32_to_bf16_rne(qhi[s].x); qf[s][5] = (short)f32_to_bf16_rne(qhi[s].y);
+    qf[s][6] = (short)f32_to_bf16_rne(qhi[s].z); qf[s][7] = (short)f32_to_bf16_rne(qhi[s].w);
   }
-  for (int ut = w; ut < A / 16; ut += 4) {
-    const int u = 16 * ut + l15;
-    const float bv = b1[u];
-    const float* wrow = W1 + (int64_t)u * 2 * D + 8 * l4;
-    float4 wv0[KS], wv1[KS];
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {  // every load of the tile in flight at once
-      wv0[s] = *reinterpret_cast<const float4*>(wrow + 32 * s);
-      wv1[s] = *reinterpret_cast<const float4*>(wrow + 32 * s + 4);
-    }
+  for (int t = 0; t < MAXT; ++t) {
+    const int ut = w + 4 * t;
+    if (ut >= A / 16) break;
+    const int u = 16 * ut + l15;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      const float wv[8] = {wv0[s].x, wv0[s].y, wv0[s].z, wv0[s].w, wv1[s].x, wv1[s].y, wv1[s].z, wv1[s].w};
+      const float wv[8] = {wv0[t][s].x, wv0[t][s].y, wv0[t][s].z, wv0[t][s].w,
+                           wv1[t][s].x, wv1[t][s].y, wv1[t][s].z, wv1[t][s].w};
       bf16x8 fh, fm, fl;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -2706,7 +2724,7 @@ __global__ __launch_bounds__(256) void din_u_kernel(const float* __restrict__ q,
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int bb = b0 + 4 * l4 + i;
-      if (bb < B) U[(int64_t)bb * A + u] = acc[i] + bv;
+      if (bb < B) U[(int64_t)bb * A + u] = acc[i] + bv[t];
     }
   }
 }
