@@ -156,11 +156,14 @@ int nrk_din_attn_bwd(const void* keys, const int32_t* hist_ids, int64_t n_table,
  * straight into the model's tensors: gW1 [A][2d] = [dW1q | dW1k], gb1 [A],
  * gw2 [A], gb2 [1] (DIN.py:146 loss.backward() for attn.attn.{0,2}).
  *   q [B][d] f32 (the query rows), dU [B][A] optional (NULL: not written).
+ *   pooled [B][d] f32: the forward's pooled rows, optional (d = 256, L > 64: the
+ *   softmax term sum_l alpha_l dalpha_l is read off them as dpooled . pooled;
+ *   NULL: formed from the key rows, one more pass over them).
  *   ws as nrk_din_attn_bwd_workspace(B, d, A). */
 int nrk_din_attn_bwd_params(const void* table, const int32_t* hist_ids, int64_t n_table, int32_t dtype,
                             const float* q, const float* U, const void* W1k, const float* w2,
                             int32_t B, int32_t L, int32_t d, int32_t A,
-                            const float* dpooled, const float* alpha,
+                            const float* dpooled, const float* alpha, const float* pooled,
                             float* gW1, float* gb1, float* gw2, float* gb2, float* dU,
                             void* ws, size_t ws_bytes, void* stream);
 

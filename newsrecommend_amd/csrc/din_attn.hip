@@ -2372,6 +2372,27 @@ __global__ __launch_bounds__(256) void din_cdot_kernel(const uint16_t* __restric
   if (lane == 0) cd[b] = t;
 }
 
+// The same term from the forward's pooled rows: sum_l alpha_l (dp . k_l) =
+// dp . (sum_l alpha_l k_l) = dp . pooled (equal up to the fp32 rounding of the
+// two summation orders).  One wave per sample.
+template <int D>
+__global__ __launch_bounds__(256) void din_cdot_pooled_kernel(const float* __restrict__ dpooled,
+                                                              const float* __restrict__ pooled, int B,
+                                                              float* __restrict__ cd) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  float t = 0.f;
+#pragma unroll
+  for (int c = 0; c < D / 256; ++c) {
+    const float4 x = *reinterpret_cast<const float4*>(dpooled + b * D + 256 * c + 4 * lane);
+    const float4 y = *reinterpret_cast<const float4*>(pooled + b * D + 256 * c + 4 * lane);
+    t = fmaf(x.x, y.x, fmaf(x.y, y.y, fmaf(x.z, y.z, fmaf(x.w, y.w, t))));
+  }
+  t = wave_sum(t);
+  if (lane == 0) cd[b] = t;
+}
+
 // dW1q partial tiles for nrk_din_attn_bwd_params (8-wave backward):
 //   part[kc][n][k] = sum over the samples b of chunk kc and both row groups
 //   of dUp[rg][b][n] q[b][k], on f32 MFMA (lane half h = row group).
@@ -2815,18 +2836,25 @@ extern "C" int nrk_din_attn_fwd(const void* keys, const int32_t* hist_ids, int64
   NRK_CHECK_ARG(smem <= 160 * 1024, "din_fwd: L=%d d=%d needs %zu B LDS", L, d, smem);
   const bool wave_ok = bf && hist_ids && (d == 64 || d == 128);
   const size_t pair_sm = ((size_t)((A + 63) & ~63) * 3 + (size_t)((L + 31) & ~31) * d + 4 * 128 + 2 * 256) * 4;
-  if (bf && hist_ids && d == 256 && pair_sm <= 80 * 1024) {  // L <= 64: a wave pair per sample, two WGs per CU
-    const size_t AP = (size_t)((A + 63) & ~63);
+  if (bf && hist_ids && d == 256 && pair_sm <= 160 * 1024) {
+    // a wave pair per sample: L <= 64 two WGs per CU; L 65..128 (twice the key image) one
+    const bool two = pair_sm <= 80 * 1024;
     const size_t psm = pair_sm;
     int grid = (int)cdiv(B, 2);
-    if (grid > 512) grid = 512;
+    if (grid > (two ? 512 : 256)) grid = two ? 512 : 256;
     const uint16_t* tb = static_cast<const uint16_t*>(keys);
     const uint16_t* wk = static_cast<const uint16_t*>(W1k);
     hipStream_t st = (hipStream_t)stream;
     const int na = A / 32;
 #define NRK_FWD_PAIR(NN)                                                                                          \
-  hipLaunchKernelGGL((din_fwd_pair_kernel<256, NN>), dim3(grid), dim3(256), psm, st, tb, hist_ids, n_table, U, wk, \
-                     w2, B, L, pooled, alpha)
+  do {                                                                                                            \
+    if (two)                                                                                                      \
+      hipLaunchKernelGGL((din_fwd_pair_kernel<256, NN>), dim3(grid), dim3(256), psm, st, tb, hist_ids, n_table, U, \
+                         wk, w2, B, L, pooled, alpha);                                                            \
+    else                                                                                                          \
+      hipLaunchKernelGGL((din_fwd_pair_kernel<256, NN, 1>), dim3(grid), dim3(256), psm, st, tb, hist_ids, n_table, \
+                         U, wk, w2, B, L, pooled, alpha);                                                         \
+  } while (0)
     if (na == 1) NRK_FWD_PAIR(1); else if (na == 2) NRK_FWD_PAIR(2); else if (na == 3) NRK_FWD_PAIR(3);
     else NRK_FWD_PAIR(4);
 #undef NRK_FWD_PAIR
@@ -3002,9 +3030,9 @@ extern "C" int nrk_din_batch(const int64_t* idx, int32_t B, const int32_t* hist_
 
 static int bwd_params_impl(const void* table, const int32_t* hist_ids, int64_t n_table, int32_t dtype,
                            const float* q, const float* U, const void* W1k, const float* w2, int32_t B, int32_t L,
-                           int32_t d, int32_t A, const float* dpooled, const float* alpha, float* gW1, float* gb1,
-                           float* gw2, float* gb2, float* dU, void* ws, size_t ws_bytes, void* stream,
-                           const DpSrc* dps, int64_t n_flat = 0, double* norm_part = nullptr) {
+                           int32_t d, int32_t A, const float* dpooled, const float* alpha, const float* pooled,
+                           float* gW1, float* gb1, float* gw2, float* gb2, float* dU, void* ws, size_t ws_bytes,
+                           void* stream, const DpSrc* dps, int64_t n_flat = 0, double* norm_part = nullptr) {
   int rc = check_common(table, dtype, B, L, d, A);
   if (rc) return rc;
   NRK_CHECK_ARG(dtype == NRK_DTYPE_BF16 && hist_ids != nullptr &&
@@ -3039,8 +3067,12 @@ static int bwd_params_impl(const void* table, const int32_t* hist_ids, int64_t n
                    // which din_dwq_kernel only writes after the backward)
       NRK_CHECK_ARG((size_t)B <= (size_t)DWQ_KC * A * d, "din_bwd_params: batch %d too large for L > 64", B);
       float* cd = qpart_w8;
-      hipLaunchKernelGGL(din_cdot_kernel<256>, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, st, tb, hist_ids, n_table,
-                         dpooled, alpha, B, L, cd);
+      if (pooled)  // sum_l alpha_l (dp . k_l) = dp . pooled: 8 KB per sample instead of the key rows
+        hipLaunchKernelGGL(din_cdot_pooled_kernel<256>, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, st, dpooled, pooled,
+                           B, cd);
+      else
+        hipLaunchKernelGGL(din_cdot_kernel<256>, dim3((unsigned)cdiv(B, 4)), dim3(256), 0, st, tb, hist_ids, n_table,
+                           dpooled, alpha, B, L, cd);
       NRK_CHECK_LAUNCH("din_cdot_kernel");
       hipLaunchKernelGGL((din_bwd_deep8c_kernel<256, 64, NS, true>), dim3(grid), dim3(512), dsm, st, tb, hist_ids,
                          n_table, U, wk, w2, B, L, A, dpooled, alpha, slabs, dUp, dmy, cd);
@@ -3151,10 +3183,10 @@ static int bwd_params_impl(const void* table, const int32_t* hist_ids, int64_t n
 extern "C" int nrk_din_attn_bwd_params(const void* table, const int32_t* hist_ids, int64_t n_table, int32_t dtype,
                                        const float* q, const float* U, const void* W1k, const float* w2, int32_t B,
                                        int32_t L, int32_t d, int32_t A, const float* dpooled, const float* alpha,
-                                       float* gW1, float* gb1, float* gw2, float* gb2, float* dU, void* ws,
-                                       size_t ws_bytes, void* stream) {
-  return bwd_params_impl(table, hist_ids, n_table, dtype, q, U, W1k, w2, B, L, d, A, dpooled, alpha, gW1, gb1, gw2,
-                         gb2, dU, ws, ws_bytes, stream, nullptr);
+                                       const float* pooled, float* gW1, float* gb1, float* gw2, float* gb2, float* dU,
+                                       void* ws, size_t ws_bytes, void* stream) {
+  return bwd_params_impl(table, hist_ids, n_table, dtype, q, U, W1k, w2, B, L, d, A, dpooled, alpha, pooled, gW1, gb1,
+                         gw2, gb2, dU, ws, ws_bytes, stream, nullptr);
 }
 
 extern "C" int nrk_din_attn_bwd_params_head(const void* table, const int32_t* hist_ids, int64_t n_table,
@@ -3174,7 +3206,7 @@ extern "C" int nrk_din_attn_bwd_params_head(const void* table, const int32_t* hi
   dps.w1 = hp->fc1_w;
   dps.bn0w = hp->bn0_w;
   dps.invB = 1.f / (float)B;
-  return bwd_params_impl(table, hist_ids, n_table, dtype, q, U, W1k, w2, B, L, d, A, nullptr, alpha, gW1, gb1, gw2,
+  return bwd_params_impl(table, hist_ids, n_table, dtype, q, U, W1k, w2, B, L, d, A, nullptr, alpha, nullptr, gW1, gb1, gw2,
                          gb2, nullptr, ws, ws_bytes, stream, &dps, n_flat, norm_part);
 }
 

@@ -633,7 +633,7 @@ class FusedTrainStep:
             _lib.check(L_.nrk_din_attn_bwd_params(
                 _lib.ptr(self.table), _lib.ptr(self.hist_b), N, dt, _lib.ptr(self.q_b), _lib.ptr(self.U_b),
                 _lib.ptr(self.W1k_b), _lib.ptr(w2), B, L, d, A, _lib.ptr(self.dpooled), _lib.ptr(self.alpha),
-                _lib.ptr(W1.grad), _lib.ptr(b1.grad), _lib.ptr(w2.grad), _lib.ptr(m.attn.attn[2].bias.grad), None,
+                _lib.ptr(self.pooled), _lib.ptr(W1.grad), _lib.ptr(b1.grad), _lib.ptr(w2.grad), _lib.ptr(m.attn.attn[2].bias.grad), None,
                 _lib.ptr(self.ws_attn), self.ws_attn.numel(), st), "din_attn_bwd_params")
         KernelTimer.push("bwd", t0)
         if self.grad_hook is not None:
