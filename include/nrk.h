@@ -159,12 +159,17 @@ int nrk_din_attn_bwd(const void* keys, const int32_t* hist_ids, int64_t n_table,
  *   pooled [B][d] f32: the forward's pooled rows, optional (d = 256, L > 64: the
  *   softmax term sum_l alpha_l dalpha_l is read off them as dpooled . pooled;
  *   NULL: formed from the key rows, one more pass over them).
+ *   norm_part (optional, n_flat): as nrk_din_attn_bwd_params_head — gW1 .. gb2 are
+ *   the start of the model's flat gradient of n_flat floats, and the reduction
+ *   also writes the per-64-block squared-norm partials nrk_clip_adam_partials
+ *   reads (NULL: not written).
  *   ws as nrk_din_attn_bwd_workspace(B, d, A). */
 int nrk_din_attn_bwd_params(const void* table, const int32_t* hist_ids, int64_t n_table, int32_t dtype,
                             const float* q, const float* U, const void* W1k, const float* w2,
                             int32_t B, int32_t L, int32_t d, int32_t A,
                             const float* dpooled, const float* alpha, const float* pooled,
                             float* gW1, float* gb1, float* gw2, float* gb2, float* dU,
+                            int64_t n_flat, double* norm_part,
                             void* ws, size_t ws_bytes, void* stream);
 
 /* The same backward, forming dpooled itself from the train-mode head's state

@@ -57,7 +57,7 @@ SIGNATURES = {
     "nrk_din_attn_bwd": (ctypes.c_int, [c_p, c_p, c_i64, c_i32, c_p, c_p, c_p, c_f32, c_i32, c_i32, c_i32, c_i32,
                                         c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_size, c_p]),
     "nrk_din_attn_bwd_params": (ctypes.c_int, [c_p, c_p, c_i64, c_i32, c_p, c_p, c_p, c_p, c_i32, c_i32, c_i32, c_i32,
-                                               c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_size, c_p]),
+                                               c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_p, c_size, c_p]),
     "nrk_din_attn_bwd_params_head": (ctypes.c_int, [c_p, c_p, c_i64, c_i32, c_p, c_p, c_p, c_p, c_i32, c_i32, c_i32,
                                                     c_i32, c_p, c_p, c_i32, c_p, c_p, c_size, c_p, c_p, c_p, c_p, c_i64,
                                                     c_p, c_p, c_size, c_p]),

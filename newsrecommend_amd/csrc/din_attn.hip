@@ -3184,9 +3184,9 @@ extern "C" int nrk_din_attn_bwd_params(const void* table, const int32_t* hist_id
                                        const float* q, const float* U, const void* W1k, const float* w2, int32_t B,
                                        int32_t L, int32_t d, int32_t A, const float* dpooled, const float* alpha,
                                        const float* pooled, float* gW1, float* gb1, float* gw2, float* gb2, float* dU,
-                                       void* ws, size_t ws_bytes, void* stream) {
+                                       int64_t n_flat, double* norm_part, void* ws, size_t ws_bytes, void* stream) {
   return bwd_params_impl(table, hist_ids, n_table, dtype, q, U, W1k, w2, B, L, d, A, dpooled, alpha, pooled, gW1, gb1,
-                         gw2, gb2, dU, ws, ws_bytes, stream, nullptr);
+                         gw2, gb2, dU, ws, ws_bytes, stream, nullptr, n_flat, norm_part);
 }
 
 extern "C" int nrk_din_attn_bwd_params_head(const void* table, const int32_t* hist_ids, int64_t n_table,

@@ -504,10 +504,10 @@ class FusedTrainStep:
         Lk = 32 if Lh <= 32 else 64
         self.fuse_dp = (self.fast and d in (64, 128) and Lh <= 64 and Lk * d >= 4096 and self.F == 32
                         and os.environ.get("NRK_DIN_FUSE_DP", "1") != "0")
-        # with fuse_dp and no grad_hook, the gradient reduction also writes the
+        # fast path without a grad_hook: the gradient reduction also writes the
         # squared-norm partials clip_grad_norm_ reads (nrk_clip_adam_partials)
         self.norm_part = (torch.zeros(-(-n // 64), dtype=torch.float64, device=dev)
-                          if self.fuse_dp and grad_hook is None else None)
+                          if self.fast and grad_hook is None else None)
         # gathers ahead (fast path): one nrk_din_batch launch assembles the rows of
         # all K steps of a graph (history ids, query rows, labels: nothing there
         # depends on the parameters); each step then only forms U and bf16 W1k
@@ -633,8 +633,9 @@ class FusedTrainStep:
             _lib.check(L_.nrk_din_attn_bwd_params(
                 _lib.ptr(self.table), _lib.ptr(self.hist_b), N, dt, _lib.ptr(self.q_b), _lib.ptr(self.U_b),
                 _lib.ptr(self.W1k_b), _lib.ptr(w2), B, L, d, A, _lib.ptr(self.dpooled), _lib.ptr(self.alpha),
-                _lib.ptr(self.pooled), _lib.ptr(W1.grad), _lib.ptr(b1.grad), _lib.ptr(w2.grad), _lib.ptr(m.attn.attn[2].bias.grad), None,
-                _lib.ptr(self.ws_attn), self.ws_attn.numel(), st), "din_attn_bwd_params")
+                _lib.ptr(self.pooled), _lib.ptr(W1.grad), _lib.ptr(b1.grad), _lib.ptr(w2.grad),
+                _lib.ptr(m.attn.attn[2].bias.grad), None, self.n, _lib.ptr(self.norm_part), _lib.ptr(self.ws_attn),
+                self.ws_attn.numel(), st), "din_attn_bwd_params")
         KernelTimer.push("bwd", t0)
         if self.grad_hook is not None:
             self.grad_hook(self.G)

@@ -602,21 +602,26 @@ def test_fused_step_dpooled_in_backward_matches_head_bwd0(gpu, B, monkeypatch):
             (n, (pa.grad - ref).abs().max().item())
 
 
-def test_fused_graph_k_norm_partials_multi_step(gpu, monkeypatch):
+@pytest.mark.parametrize("d", [128, 256])
+def test_fused_graph_k_norm_partials_multi_step(gpu, d, monkeypatch):
     """the gradient reduction's squared-norm partials
-    (nrk_clip_adam_partials, fuse_dp without a grad hook) over K > 1 graphed
-    steps with clipping ACTIVE (max_norm 0.05), against the same trainer with
-    NRK_DIN_FUSE_DP=0 (head bwd0 + nrk_din_attn_bwd_params + the norm read by
-    nrk_clip_adam from the whole gradient): every step's loss, and after each
-    K-step launch the stored (clipped) gradients, whose norm must equal
-    max_norm.  Two launches of K = 4 steps, dropout on."""
+    (nrk_clip_adam_partials, any fast path without a grad hook: d = 128 from
+    nrk_din_attn_bwd_params_head, d = 256 from nrk_din_attn_bwd_params) over
+    K > 1 graphed steps with clipping ACTIVE (max_norm 0.05), against the same
+    trainer with NRK_DIN_FUSE_DP=0 and a no-op grad hook (head bwd0 +
+    nrk_din_attn_bwd_params + the norm read by nrk_clip_adam from the whole
+    gradient): every step's loss, and after each K-step launch the stored
+    (clipped) gradients, whose norm must equal max_norm.  Two launches of K = 4
+    steps, dropout on."""
     from newsrecommend_amd.din import FusedTrainStep
 
-    dev, table, hist, tgt, lab, ma, mb = _setup_fused(0.36, d=128, L=50)
+    dev, table, hist, tgt, lab, ma, mb = _setup_fused(0.36, d=d, L=50)
     K, B, clip = 4, 512, 0.05
     ta = FusedTrainStep(ma, table, hist, tgt, lab, B, lr=1e-4, weight_decay=1e-4, clip=clip, steps_per_graph=K)
     monkeypatch.setenv("NRK_DIN_FUSE_DP", "0")
-    tb = FusedTrainStep(mb, table, hist, tgt, lab, B, lr=1e-4, weight_decay=1e-4, clip=clip, steps_per_graph=K)
+    # a (no-op) grad hook: the norm is read by nrk_clip_adam from the whole gradient
+    tb = FusedTrainStep(mb, table, hist, tgt, lab, B, lr=1e-4, weight_decay=1e-4, clip=clip, steps_per_graph=K,
+                        grad_hook=lambda G: None)
     assert ta.norm_part is not None and tb.norm_part is None
     perm = torch.randperm(hist.shape[0], device=dev)
     for r in range(2):
