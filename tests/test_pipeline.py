@@ -190,18 +190,20 @@ def test_rerank_fused_vs_oracle_and_per_candidate(d, L, C, A, F):
 
 
 @pytest.mark.gpu
-def test_rerank_ragged_shared_lists_extra_and_gaps():
+@pytest.mark.parametrize("L", [40, 100])
+def test_rerank_ragged_shared_lists_extra_and_gaps(L):
     """nrk_din_rerank's ragged form (the flow's): users sharing one candidate
     list (same offset), lists of 0, 1, 63, 64, 65 and 300 candidates, an
     appended extra candidate (-1 = a padded slot, a row past the table = -inf),
     duplicated candidates, out_off with gaps between users; every logit equals
     the rectangular rerank() of the same list, bit for bit, staged from the rows
-    and from the lists' projections (nrk_din_rerank_projected)."""
+    and from the lists' projections (nrk_din_rerank_projected).  L = 100 (75
+    valid slots): the lane kernel's 128-row form."""
     from newsrecommend_amd.pipeline import rerank, rerank_ragged
 
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(11)
-    d, L, N = 128, 40, 3000
+    d, N = 128, 3000
     table = (torch.randn((N, d), generator=g, device=dev) * 0.5).to(torch.bfloat16)
     model = _din_model(d, 128, 32, dev, seed=3)
     pool = torch.randint(0, N, (600,), generator=g, device=dev, dtype=torch.int32)
@@ -210,7 +212,7 @@ def test_rerank_ragged_shared_lists_extra_and_gaps():
     extra = torch.tensor([7, -1, 12, N + 4, -1, 99, 5, -1], dtype=torch.int32, device=dev)
     U = len(lists)
     hist = torch.randint(0, N, (U, L), generator=g, device=dev, dtype=torch.int32)
-    hist[:, 30:] = -1
+    hist[:, (3 * L) // 4:] = -1
     hist[3] = -1
     co = torch.tensor([o for o, _ in lists], dtype=torch.int64, device=dev)
     cl = torch.tensor([n for _, n in lists], dtype=torch.int32, device=dev)
