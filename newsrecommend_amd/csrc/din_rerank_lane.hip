@@ -141,8 +141,9 @@ __global__ __launch_bounds__((LPK == 64 ? 512 : 256), 1) void din_rerank_lane_ke
           for (int j = 0; j < 4; ++j) {
             short hi, lo;
             split_bf16(x[j], hi, lo);
-            Rth[(f0 + j) * LP + row] = (uint16_t)hi;
-            Rtl[(f0 + j) * LP + row] = (uint16_t)lo;
+            const int rs = row ^ (((f0 + j) & 7) << 3);  // 8-row chunks XOR-swizzled per f (h1 reads)
+            Rth[(f0 + j) * LP + rs] = (uint16_t)hi;
+            Rtl[(f0 + j) * LP + rs] = (uint16_t)lo;
           }
         }
       }
@@ -368,8 +369,11 @@ __global__ __launch_bounds__((LPK == 64 ? 512 : 256), 1) void din_rerank_lane_ke
 #pragma unroll
           for (int ks = 0; ks < KS; ++ks) {
             if (ks < nks) {
-              const bf16x8 rh = *reinterpret_cast<const bf16x8*>(Rth + f * LP + 32 * ks + 8 * l4);
-              const bf16x8 rl = *reinterpret_cast<const bf16x8*>(Rtl + f * LP + 32 * ks + 8 * l4);
+              // rows 32 ks + 8 l4 .. +7: chunk 4 ks + l4, stored XOR (f & 7) (a 128-B / 256-B row
+              // stride would put every f of a lane group on the same banks)
+              const int rc = (32 * ks + 8 * l4) ^ ((f & 7) << 3);
+              const bf16x8 rh = *reinterpret_cast<const bf16x8*>(Rth + f * LP + rc);
+              const bf16x8 rl = *reinterpret_cast<const bf16x8*>(Rtl + f * LP + rc);
               acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(el[ct][ks], rh, acc, 0, 0, 0);
               acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(eh[ct][ks], rl, acc, 0, 0, 0);
               acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(eh[ct][ks], rh, acc, 0, 0, 0);
