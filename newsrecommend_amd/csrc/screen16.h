@@ -65,7 +65,7 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_kernel(
   constexpr int NQ2 = 2 * QT;   // 16-query half-tiles per wave
   constexpr int WQ = WAVES * 32 * QT;
   constexpr int BUF = TI * DP;
-  static_assert(PD >= 1 && PD <= KS2, "prefetch depth");
+  static_assert(PD >= 1 && PD <= KS2 && KS2 % PD == 0, "prefetch depth: a divisor of the K steps (fragment ring)");
   constexpr int NBUF = PD == KS2 ? 2 : 3;
   __shared__ __attribute__((aligned(16))) uint16_t lds[NBUF * BUF];
 
