@@ -353,6 +353,16 @@ int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe, int32_t np
                    int32_t d, int32_t k, int32_t metric, float* D, int64_t* I, double* S,
                    int64_t id_offset, int32_t* n_fallback, void* ws, size_t ws_bytes,
                    void* const* stage_events, void* stream);
+/* Guard word of the last nrk_ivf_search on workspace `ws` -> device int32
+ * `guard` (async on `stream`).  Every index the search reads back from its own
+ * workspace (candidate and seed positions, query slots, probed lists) is range
+ * checked where it addresses memory; a violation sets a bit and skips the
+ * access instead of faulting: 1 seed position, 2 candidate position, 4 collect
+ * query row, 8 candidate count, 16 fallback query, 32 probed list, 64 gathered
+ * (query, probe) pair, 128 collected position.  0 = all in range (the result
+ * is valid); nonzero = a broken invariant, the result must not be used.
+ * (Python: IndexIVFFlat.search_device(check=True) raises NrkError.) */
+int nrk_ivf_search_status(const void* ws, size_t ws_bytes, int32_t* guard, void* stream);
 
 /* ------------------------------------------------------------ DIN head --
  * The MLP head of DIN in train mode, forward and backward (DIN.py:117-123,

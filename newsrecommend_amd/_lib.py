@@ -45,6 +45,7 @@ SIGNATURES = {
     "nrk_ivf_search_workspace": (ctypes.c_int, [c_i64, c_i32, c_i32, c_i64, c_i32, c_i32, ctypes.POINTER(c_size)]),
     "nrk_ivf_search": (ctypes.c_int, [c_p, c_i64, c_p, c_i32, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i32, c_i64, c_i64,
                                       c_i32, c_i32, c_i32, c_p, c_p, c_p, c_i64, c_p, c_p, c_size, c_p, c_p]),
+    "nrk_ivf_search_status": (ctypes.c_int, [c_p, c_size, c_p, c_p]),
     "nrk_din_head_workspace": (ctypes.c_int, [c_i32, c_i32, c_i32, ctypes.POINTER(c_size)]),
     "nrk_din_head_train": (ctypes.c_int, [c_p, c_p, c_i64, c_p, c_i32, c_i32, c_i32, c_f32, c_f32, c_f32,
                                           ctypes.c_uint64, c_p, c_p, c_p, c_p, c_p, c_p, c_size, c_p]),

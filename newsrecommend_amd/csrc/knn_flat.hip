@@ -232,6 +232,9 @@ struct IvfFb {
   const int64_t* list_off;  // [nlist + 1]
   const int64_t* probe;     // [nq][nprobe] probed lists (-1: none)
   int nprobe;
+  int nlist;
+  int64_t nq;               // queries of the search (0: slot queries unchecked)
+  int* err;                 // the search's guard word (GuardCode bits), or nullptr
 };
 
 // Top-kp selection for merge_rescore_kernel (256 threads, EPT union entries
@@ -609,6 +612,7 @@ __global__ __launch_bounds__(256) void exact_topk_kernel(
   const int64_t nwork = qcount ? (int64_t)*qcount : nq;
   for (int64_t wi = blockIdx.x; wi < nwork; wi += gridDim.x) {
     const int64_t qi = qlist ? (int64_t)qlist[wi] : wi;
+    if (!guard_ok((uint64_t)qi < (uint64_t)nq, iv.err, GUARD_FB_QUERY)) continue;  // (block-uniform)
     for (int i = tid; i < P; i += 256) {
       g[i] = -INFINITY;
       id[i] = INT64_MAX;
@@ -624,8 +628,9 @@ __global__ __launch_bounds__(256) void exact_topk_kernel(
     int64_t lo = 0, hi = nb;
     if (iv.pos2id) {
       const int64_t l = iv.probe[qi * iv.nprobe + pr];
-      lo = l >= 0 ? iv.list_off[l] : 0;
-      hi = l >= 0 ? iv.list_off[l + 1] : 0;
+      const bool ok = l >= 0 && guard_ok(l < iv.nlist, iv.err, GUARD_PROBE_LIST);
+      lo = ok ? iv.list_off[l] : 0;
+      hi = ok ? iv.list_off[l + 1] : 0;
     }
     for (int64_t base = lo; base < hi; base += 256) {
       const int64_t pp = base + tid;  // position (== id for a flat index)
@@ -960,6 +965,7 @@ __global__ __launch_bounds__(256) void fallback_scan_kernel(const float* __restr
     const int mylist = iv.pos2id ? iv.pos2list[r0 + lane] : 0;
     for (int s = wv; s < cnt; s += 4) {
       const int qi = fb.list[s];
+      if (iv.nq > 0 && !guard_ok((uint64_t)qi < (uint64_t)iv.nq, iv.err, GUARD_FB_QUERY)) continue;
       if (iv.pos2id) {
         bool member = false;
         for (int pr = 0; pr < iv.nprobe; ++pr) member |= iv.probe[(int64_t)qi * iv.nprobe + pr] == mylist;
@@ -986,7 +992,8 @@ __global__ __launch_bounds__(256) void fallback_select_kernel(FbState fb, const 
                                                               const int64_t* __restrict__ cand_i, int cap, int k,
                                                               int l2, float* __restrict__ D, int64_t* __restrict__ I,
                                                               double* __restrict__ S, int64_t id_offset,
-                                                              int* __restrict__ ov_list) {
+                                                              int* __restrict__ ov_list, int64_t nq,
+                                                              int* __restrict__ err = nullptr) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* g = reinterpret_cast<double*>(smem);
   int64_t* id = reinterpret_cast<int64_t*>(g + pow2ceil(cap));  // the sort pads n up to a power of two
@@ -994,6 +1001,7 @@ __global__ __launch_bounds__(256) void fallback_select_kernel(FbState fb, const 
   const int tid = threadIdx.x;
   for (int s = blockIdx.x; s < cnt; s += gridDim.x) {
     const int qi = fb.list[s];
+    if (!guard_ok((uint64_t)qi < (uint64_t)nq, err, GUARD_FB_QUERY)) continue;  // (block-uniform)
     const int n = s < fb.slots ? fb.n[s] : cap + 1;
     if (n > cap || n < k) {
       if (tid == 0) ov_list[atomicAdd(&fb.count[1], 1)] = qi;
@@ -1187,11 +1195,13 @@ __global__ void ivf_scatter_kernel(const int64_t* __restrict__ probe, int64_t np
 // gathered query rows: one wave per slot row (padding rows are zeroed)
 __global__ void ivf_gather_kernel(const uint16_t* __restrict__ qh, int dp, int nprobe,
                                   const int* __restrict__ slot_pair, const int* __restrict__ seg_off, int nlist,
-                                  int64_t max_rows, uint16_t* __restrict__ qh_ivf) {
+                                  int64_t max_rows, uint16_t* __restrict__ qh_ivf, int64_t npairs,
+                                  int* __restrict__ err) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (row >= max_rows || row >= seg_off[nlist]) return;
-  const int pair = slot_pair[row];
+  int pair = slot_pair[row];
+  if (pair >= 0 && !guard_ok(pair < npairs, err, GUARD_GATHER_PAIR)) pair = -1;
   const int64_t q = pair >= 0 ? pair / nprobe : 0;
   for (int j = lane * 4; j < dp; j += 256) {
     uint2 v = make_uint2(0u, 0u);
@@ -1236,7 +1246,7 @@ __global__ __launch_bounds__(256) void ivf_seed_kernel(const int* __restrict__ s
                                                        const float* __restrict__ stats, int dp,
                                                        float* __restrict__ thr, double* __restrict__ lb_g,
                                                        int64_t* __restrict__ lb_i, int* __restrict__ cand_cnt,
-                                                       int cap) {
+                                                       int cap, int64_t n, int* __restrict__ err) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int q = blockIdx.x, tid = threadIdx.x;
   const int P = pow2ceil(R);
@@ -1249,7 +1259,7 @@ __global__ __launch_bounds__(256) void ivf_seed_kernel(const int* __restrict__ s
   __syncthreads();
   for (int i = tid; i < P; i += 256) {
     const int pos = i < R ? seed_pos[(int64_t)q * R + i] : -1;
-    if (pos >= 0) {
+    if (pos >= 0 && guard_ok(pos < n, err, GUARD_SEED_POS)) {
       const int64_t item = pos2id[pos];
       const double sc = exact_score(qs, xb + item * d, d, l2 != 0);
       g[i] = l2 ? -sc : sc;
@@ -1291,15 +1301,17 @@ __global__ __launch_bounds__(256) void collect_rescore_kernel(
     const int* __restrict__ cand_cnt, const int* __restrict__ cand_pos, int cap, const int64_t* __restrict__ pos2id,
     const float* __restrict__ xq, const float* __restrict__ xb, int d, int k, int l2,
     const double* __restrict__ lb_g, const int64_t* __restrict__ lb_i, float* __restrict__ D,
-    int64_t* __restrict__ I, double* __restrict__ S, int64_t id_offset, FbState fb,
-    const int* __restrict__ qlist = nullptr, const int* __restrict__ qcount = nullptr) {
+    int64_t* __restrict__ I, double* __restrict__ S, int64_t id_offset, FbState fb, int64_t nq, int64_t n,
+    int* __restrict__ err, const int* __restrict__ qlist = nullptr, const int* __restrict__ qcount = nullptr) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   // IVF: slot = query.  Flat collect pass: slot b holds query qlist[b], if any.
   const int sl = blockIdx.x;
   if (qlist && sl >= *qcount) return;
   const int qi = qlist ? qlist[sl] : sl;
-  const int c = cand_cnt[sl];
+  if (!guard_ok((uint64_t)qi < (uint64_t)nq, err, GUARD_FB_QUERY)) return;
+  int c = cand_cnt[sl];
+  if (!guard_ok(c >= 0, err, GUARD_CAND_COUNT)) c = 0;
   if (c > cap) {
     if (tid == 0) fb.push(qi, lb_g[sl], lb_i[sl]);
     return;
@@ -1313,7 +1325,9 @@ __global__ __launch_bounds__(256) void collect_rescore_kernel(
   for (int i = tid; i < P; i += 256) {
     if (i < c) {
       const int pos = cand_pos[(int64_t)sl * cap + i];
-      id[i] = pos2id ? pos2id[pos] : (int64_t)pos;
+      // an out-of-range position (a broken invariant) is flagged and read as row 0
+      const int64_t p = guard_ok((uint64_t)pos < (uint64_t)n, err, GUARD_CAND_POS) ? pos : 0;
+      id[i] = pos2id ? pos2id[p] : p;
     } else {
       g[i] = -INFINITY;
       id[i] = INT64_MAX;
@@ -1953,7 +1967,8 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
                          nb, 0, 0, 0, 1, nullptr, nullptr, nullptr, nullptr, isc);
       NRK_CHECK_LAUNCH("screen_kernel (flat collect)");
       hipLaunchKernelGGL(collect_rescore_kernel, dim3((unsigned)p.fb_slots), dim3(256), smem, st, ccnt, cpos, p.ccap,
-                         nullptr, xq, xb, d, k, l2, clbg, clbi, D, I, S, id_offset, fbt, clist, ccount);
+                         nullptr, xq, xb, d, k, l2, clbg, clbi, D, I, S, id_offset, fbt, nq, nb, nullptr, clist,
+                         ccount);
       NRK_CHECK_LAUNCH("collect_rescore_kernel (flat)");
     }
   }
@@ -1964,7 +1979,7 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
                        l2, fbt, fcg, fci, p.fb_cap, IvfFb{});
     NRK_CHECK_LAUNCH("fallback_scan_kernel");
     hipLaunchKernelGGL(fallback_select_kernel, dim3(256), dim3(256), (size_t)host_pow2ceil(p.fb_cap) * 16, st, fbt, fcg,
-                       fci, p.fb_cap, k, l2, D, I, S, id_offset, ovl);
+                       fci, p.fb_cap, k, l2, D, I, S, id_offset, ovl, nq);
     NRK_CHECK_LAUNCH("fallback_select_kernel");
   }
   int rc = exact_launch(xq, nq, xb, nb, d, k, l2, ovl, fbt.count + 1, 256, D, I, S, id_offset, st, IvfFb{}, n_fallback,
@@ -2072,7 +2087,9 @@ static IvfPlan make_ivf_plan(int64_t nq, int nprobe, int nlist, int64_t max_list
     off = align_up(off + bytes, 256);
     return o;
   };
-  p.off_fbc = take(64);  // fallback counters [0, 16), collect work tickets [32, 64)
+  // fallback counters [0, 16), guard word [16, 20) (nrk_ivf_search_status reads it
+  // at this fixed offset: keep this the first region), collect work tickets [32, 64)
+  p.off_fbc = take(64);
   p.off_cnt = take((size_t)nlist * 4);
   p.off_fill = take((size_t)nlist * 4);
   p.off_hist = take((size_t)GROUP_BLOCKS * nlist * 4);
@@ -2106,7 +2123,7 @@ static IvfPlan make_ivf_plan(int64_t nq, int nprobe, int nlist, int64_t max_list
 // group (query, probe) pairs by list and gather the probing queries list-major
 static int ivf_group(const int64_t* probe, int64_t nq, int nprobe, int nlist, const int64_t* list_off, int wq, int ch,
                      int dp, int64_t max_rows, const uint16_t* qh, int* cnt, int* fill, int* seg, int* work, int* sp,
-                     uint16_t* qi, int* H, hipStream_t st) {
+                     uint16_t* qi, int* H, int* err, hipStream_t st) {
   const int64_t npairs = nq * nprobe;
   if (hipMemsetAsync(sp, 0xff, (size_t)max_rows * 4, st) != hipSuccess)
     return fail(NRK_ELAUNCH, "ivf_search: memset failed");
@@ -2133,7 +2150,7 @@ static int ivf_group(const int64_t* probe, int64_t nq, int nprobe, int nlist, co
     NRK_CHECK_LAUNCH("ivf_scatter_kernel");
   }
   hipLaunchKernelGGL(ivf_gather_kernel, dim3((unsigned)cdiv(max_rows, 4)), dim3(256), 0, st, qh, dp, nprobe, sp, seg,
-                     nlist, max_rows, qi);
+                     nlist, max_rows, qi, npairs, err);
   NRK_CHECK_LAUNCH("ivf_gather_kernel");
   return NRK_OK;
 }
@@ -2207,7 +2224,8 @@ extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe,
   double* fcg = reinterpret_cast<double*>(w + p.off_fcg);
   int64_t* fci = reinterpret_cast<int64_t*>(w + p.off_fci);
   int* ovl = reinterpret_cast<int*>(w + p.off_ovl);
-  IvfFb ivf{pos2id, pos2list, list_off, probe, nprobe};
+  int* gerr = fbc + 4;  // the guard word (zeroed with the counters; nrk_ivf_search_status)
+  IvfFb ivf{pos2id, pos2list, list_off, probe, nprobe, nlist, nq, gerr};
   const bool force_fb = test_hook("NRK_FORCE_FALLBACK", 0) != 0;
 
   mark(0);
@@ -2222,11 +2240,12 @@ extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe,
         hipMemsetAsync(ccnt, 0, (size_t)nq * 4, st) != hipSuccess)
       return fail(NRK_ELAUNCH, "ivf_search: copy/memset failed");
     int rc =
-        ivf_group(p0, nq, p.nA, nlist, list_off, p.wqA, p.chA, p.dp, p.max_rows, qh, cnt, fill, seg, work, sp, qi, hist, st);
+        ivf_group(p0, nq, p.nA, nlist, list_off, p.wqA, p.chA, p.dp, p.max_rows, qh, cnt, fill, seg, work, sp, qi, hist, gerr,
+                  st);
     if (rc != NRK_OK) return rc;
     screen_fn fa = pick_screen(p.dp, p.qtA, p.M, l2 != 0, 4);
     if (!fa) return fail(NRK_EUNSUPPORTED, "ivf_search: no screen kernel for dp=%d", p.dp);
-    IvfScreen isa{work, list_off, seg, sp, nlist, p.chA, p.cmaxA, nullptr, nullptr, nullptr, 0, p.nA};
+    IvfScreen isa{work, list_off, seg, sp, nlist, p.chA, p.cmaxA, nullptr, nullptr, nullptr, 0, p.nA, nullptr, gerr};
     hipLaunchKernelGGL(fa, dim3((unsigned)p.ubA), dim3(p.waves * 64), 0, st, qi, xbh_ivf, meta_ivf, nq, n, 0, 0, 0,
                        3, nullptr, pa, pt, nullptr, isa);  // every third tile: seeds from a third of the rows
     // (tile strides 2 / 3 / 4 / 6: search 3.49 / 3.46 / 3.48 / 3.50 ms, phase A falling and the
@@ -2237,12 +2256,12 @@ extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe,
     hipLaunchKernelGGL(tsel, dim3((unsigned)cdiv(nq, 4)), dim3(256), 0, st, pt, nva, p.R, nq, tau, pa, seed);
     NRK_CHECK_LAUNCH("tau_select_kernel (ivf)");
     hipLaunchKernelGGL(ivf_seed_kernel, dim3((unsigned)nq), dim3(256), (size_t)host_pow2ceil(p.R) * 16 + (size_t)d * 4,
-                       st, seed, p.R, k, pos2id, xq, xb, d, l2, qmeta, stats, p.dp, thr, lbg, lbi, ccnt, p.cap);
+                       st, seed, p.R, k, pos2id, xq, xb, d, l2, qmeta, stats, p.dp, thr, lbg, lbi, ccnt, p.cap, n, gerr);
     NRK_CHECK_LAUNCH("ivf_seed_kernel");
     NRK_CHECK_LAUNCH("ivf_thr_kernel");
     // ---- phase B grouping: every probed list
     rc = ivf_group(probe, nq, nprobe, nlist, list_off, p.wq, p.chB, p.dp, p.max_rows, qh, cnt, fill, seg, work, sp, qi,
-                   hist, st);
+                   hist, gerr, st);
     if (rc != NRK_OK) return rc;
   } else if (hipMemsetAsync(ccnt, 0, (size_t)nq * 4, st) != hipSuccess) {  // empty index: all -1
     return fail(NRK_ELAUNCH, "ivf_search: memset");
@@ -2255,7 +2274,7 @@ extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe,
     // the 16x16x32 collect where built (NRK_SCREEN16=0: the 32x32x16 one; a test hook)
     if (p.dp == 128 && p.qt == 2 && p.wavesB == 4 && test_hook("NRK_SCREEN16", 1)) fbk = pick_collect16_dp128(l2 != 0);
     if (!fbk) return fail(NRK_EUNSUPPORTED, "ivf_search: no collect kernel for dp=%d", p.dp);
-    IvfScreen isb{work, list_off, seg, sp, nlist, p.chB, p.cmaxB, thr, ccnt, cpos, p.cap, nprobe, fbc + 8};
+    IvfScreen isb{work, list_off, seg, sp, nlist, p.chB, p.cmaxB, thr, ccnt, cpos, p.cap, nprobe, fbc + 8, gerr};
     hipLaunchKernelGGL(fbk, dim3((unsigned)p.ubB), dim3(p.wavesB * 64), 0, st, qi, xbh_ivf, meta_ivf, nq, n, 0, 0, 0, 1,
                        nullptr, nullptr, nullptr, nullptr, isb);
     NRK_CHECK_LAUNCH("screen_kernel (ivf collect)");
@@ -2267,7 +2286,7 @@ extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe,
       return fail(NRK_ELAUNCH, "ivf_search: memset failed");
     const size_t smem = collect_rescore_smem(p.cap, d);
     hipLaunchKernelGGL(collect_rescore_kernel, dim3((unsigned)nq), dim3(256), smem, st, ccnt, cpos, p.cap, pos2id, xq,
-                       xb, d, k, l2, lbg, lbi, D, I, S, id_offset, fb);
+                       xb, d, k, l2, lbg, lbi, D, I, S, id_offset, fb, nq, n, gerr);
     NRK_CHECK_LAUNCH("collect_rescore_kernel");
   }
 
@@ -2280,7 +2299,7 @@ extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe,
     NRK_CHECK_LAUNCH("fallback_scan_kernel (ivf)");
   }
   hipLaunchKernelGGL(fallback_select_kernel, dim3(256), dim3(256), (size_t)host_pow2ceil(p.fb_cap) * 16, st, fb, fcg,
-                     fci, p.fb_cap, k, l2, D, I, S, id_offset, ovl);
+                     fci, p.fb_cap, k, l2, D, I, S, id_offset, ovl, nq, gerr);
   NRK_CHECK_LAUNCH("fallback_select_kernel (ivf)");
   int rc = exact_launch(xq, nq, xb, n, d, k, l2, ovl, fbc + 1, 256, D, I, S, id_offset, st, ivf);
   if (rc != NRK_OK) return rc;
@@ -2289,5 +2308,16 @@ extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe,
   // those, the ones its buffer could not hold either (the block-per-query scan)
   if (n_fallback && hipMemcpyAsync(n_fallback, fbc, 8, hipMemcpyDeviceToDevice, st) != hipSuccess)
     return fail(NRK_ELAUNCH, "ivf_search: copy of fallback counts failed");
+  return NRK_OK;
+}
+
+// The guard word of the last nrk_ivf_search on this workspace (GuardCode bits,
+// 0 = every workspace-derived index was in range) -> device int32 (async).
+extern "C" int nrk_ivf_search_status(const void* ws, size_t ws_bytes, int32_t* guard, void* stream) {
+  NRK_CHECK_ARG(ws != nullptr && guard != nullptr && ws_bytes >= 64, "ivf_search_status: bad arguments");
+  // make_ivf_plan: off_fbc == 0, guard word = fbc[4]
+  if (hipMemcpyAsync(guard, static_cast<const char*>(ws) + 16, 4, hipMemcpyDeviceToDevice, (hipStream_t)stream) !=
+      hipSuccess)
+    return fail(NRK_ELAUNCH, "ivf_search_status: copy failed");
   return NRK_OK;
 }

@@ -150,6 +150,28 @@ __device__ __forceinline__ int nth_set_bit(uint64_t m, int j) {
   return pos;
 }
 
+// ------------------------------------------------------ index guards --
+// Indices the IVF search reads back from its own workspace (list positions,
+// query slots, probed lists) are range-checked where they address memory: a
+// violation sets bit `code` of the search's guard word and the access is
+// skipped, so a broken invariant surfaces as nrk_ivf_search_status() != 0
+// (NrkError on the host) instead of an illegal-address fault.  One compare on
+// paths that are rare or per candidate, not per screened item.
+enum GuardCode : int {
+  GUARD_SEED_POS = 1,       // ivf_seed_kernel: seed position outside [0, n)
+  GUARD_CAND_POS = 2,       // collect_rescore: candidate position outside [0, n)
+  GUARD_COLLECT_QUERY = 4,  // collect: a row's query outside [0, nq)
+  GUARD_CAND_COUNT = 8,     // collect_rescore: negative candidate count
+  GUARD_FB_QUERY = 16,      // fallback / exact scans: slot query outside [0, nq)
+  GUARD_PROBE_LIST = 32,    // exact scans: probed list outside [-1, nlist)
+  GUARD_GATHER_PAIR = 64,   // ivf_gather: (query, probe) pair outside [0, nq * nprobe)
+  GUARD_COLLECT_POS = 128,  // collect: appended position outside [0, n)
+};
+__device__ __forceinline__ bool guard_ok(bool ok, int* err, int code) {
+  if (!ok && err) atomicOr(err, code);
+  return ok;
+}
+
 // --------------------------------------------------- ordering (k-NN) --
 // "goodness" g: larger is better.  IP: g = score; L2: g = -distance.
 // Ties on g break toward the lower id.

@@ -152,6 +152,8 @@ struct IvfScreen {
   int cap, nprobe;
   // screen16 collect: per-XCD work tickets (8 ints, zero at launch)
   int* ticket;
+  // MODE 3: the search's guard word (GuardCode bits; nullptr: unchecked)
+  int* err;
 };
 
 // MODE 3 block-local candidate staging: hits are appended with LDS atomics and
@@ -375,7 +377,8 @@ __global__ __launch_bounds__(WAVES * 64, (MODE == 3 && WAVES == 8) ? 1 : 2) void
                       const int row = (w * QT + t) * 32 + r;
                       const int rank = atomicAdd(&cl.qcnt[row], 1);
                       cl.ent[e] = make_int2(row | (rank << 10), (int)(i0 + ir));
-                    } else if (__builtin_nontemporal_load(&iv.cand_cnt[cq[t]]) <= iv.cap) {
+                    } else if (guard_ok((uint64_t)cq[t] < (uint64_t)nq, iv.err, GUARD_COLLECT_QUERY) &&
+                               __builtin_nontemporal_load(&iv.cand_cnt[cq[t]]) <= iv.cap) {
                       // staging full: append directly (stop once the query overflowed)
                       const int pos = atomicAdd(&iv.cand_cnt[cq[t]], 1);
                       if (pos < iv.cap) iv.cand_pos[(int64_t)cq[t] * iv.cap + pos] = (int)(i0 + ir);
@@ -476,7 +479,8 @@ __global__ __launch_bounds__(WAVES * 64, (MODE == 3 && WAVES == 8) ? 1 : 2) void
                   const int row = (w * QT + t) * 32 + r;
                   const int rank = atomicAdd(&cl.qcnt[row], 1);
                   cl.ent[e] = make_int2(row | (rank << 10), pos);
-                } else if (__builtin_nontemporal_load(&iv.cand_cnt[cq[t]]) <= iv.cap) {
+                } else if (guard_ok((uint64_t)cq[t] < (uint64_t)nq, iv.err, GUARD_COLLECT_QUERY) &&
+                           __builtin_nontemporal_load(&iv.cand_cnt[cq[t]]) <= iv.cap) {
                   const int slot = atomicAdd(&iv.cand_cnt[cq[t]], 1);
                   if (slot < iv.cap) iv.cand_pos[(int64_t)cq[t] * iv.cap + slot] = pos;
                 }
@@ -645,14 +649,17 @@ __global__ __launch_bounds__(WAVES * 64, (MODE == 3 && WAVES == 8) ? 1 : 2) void
       __syncthreads();
       for (int row = tid; row < WQ; row += NT) {
         const int n_r = cl.qcnt[row];
-        cl.base[row] = n_r > 0 ? atomicAdd(&iv.cand_cnt[cl.qid[row]], n_r) : 0;
+        const int qy = cl.qid[row];
+        cl.base[row] = n_r > 0 && guard_ok((uint64_t)qy < (uint64_t)nq, iv.err, GUARD_COLLECT_QUERY)
+                           ? atomicAdd(&iv.cand_cnt[qy], n_r) : iv.cap;
       }
       __syncthreads();
       const int ne = cl.n < CollectLds<WQ>::CAP ? cl.n : CollectLds<WQ>::CAP;
       for (int e = tid; e < ne; e += NT) {
         const int2 en = cl.ent[e];
         const int row = en.x & 1023, dst = cl.base[row] + (en.x >> 10);
-        if (dst < iv.cap) iv.cand_pos[(int64_t)cl.qid[row] * iv.cap + dst] = en.y;
+        if (dst < iv.cap && guard_ok((uint64_t)en.y < (uint64_t)nb, iv.err, GUARD_COLLECT_POS))
+          iv.cand_pos[(int64_t)cl.qid[row] * iv.cap + dst] = en.y;
       }
       continue;
     }

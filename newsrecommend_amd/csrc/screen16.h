@@ -298,8 +298,6 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_collect_kernel(
     const uint16_t* __restrict__ qh, const uint16_t* __restrict__ xbh, const float* __restrict__ xmeta, int64_t nq,
     int64_t nb, int64_t chunk, int nch, int nqt, int tstride, float* __restrict__ part_s, int* __restrict__ part_i,
     float* __restrict__ part_t, const float* __restrict__ tau_q, IvfScreen iv) {
-  (void)nq;
-  (void)nb;
   (void)chunk;
   (void)nch;
   (void)nqt;
@@ -444,7 +442,9 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_collect_kernel(
         cl.ent[e] = make_int2(row | (rank << 10), pos);
       } else {
         const int qy = cl.qid[w * QT * 32 + 16 * t + q16];
-        if (__builtin_nontemporal_load(&iv.cand_cnt[qy]) <= iv.cap) {
+        if (guard_ok((uint64_t)qy < (uint64_t)nq, iv.err, GUARD_COLLECT_QUERY) &&
+            guard_ok((uint64_t)pos < (uint64_t)nb, iv.err, GUARD_COLLECT_POS) &&
+            __builtin_nontemporal_load(&iv.cand_cnt[qy]) <= iv.cap) {
           // staging full: append directly (stop once the query overflowed)
           const int slot = atomicAdd(&iv.cand_cnt[qy], 1);
           if (slot < iv.cap) iv.cand_pos[(int64_t)qy * iv.cap + slot] = pos;
@@ -620,14 +620,17 @@ __global__ __launch_bounds__(WAVES * 64, 2) void screen16_collect_kernel(
     __syncthreads();
     for (int row = tid; row < WQ; row += NT) {
       const int n_r = cl.qcnt[row];
-      cl.base[row] = n_r > 0 ? atomicAdd(&iv.cand_cnt[cl.qid[row]], n_r) : 0;
+      const int qy = cl.qid[row];
+      cl.base[row] = n_r > 0 && guard_ok((uint64_t)qy < (uint64_t)nq, iv.err, GUARD_COLLECT_QUERY)
+                         ? atomicAdd(&iv.cand_cnt[qy], n_r) : iv.cap;
     }
     __syncthreads();
     const int ne = cl.n < CL::CAP ? cl.n : CL::CAP;
     for (int e = tid; e < ne; e += NT) {
       const int2 en = cl.ent[e];
       const int row = en.x & 1023, dst = cl.base[row] + (en.x >> 10);
-      if (dst < iv.cap) iv.cand_pos[(int64_t)cl.qid[row] * iv.cap + dst] = en.y;
+      if (dst < iv.cap && guard_ok((uint64_t)en.y < (uint64_t)nb, iv.err, GUARD_COLLECT_POS))
+        iv.cand_pos[(int64_t)cl.qid[row] * iv.cap + dst] = en.y;
     }
     if (tid == 0) next_item = nxt;  // (every thread read this item's index before its first barrier)
   }

@@ -146,8 +146,10 @@ class IndexFlat(_FallbackCounters):
 
     # --------------------------------------------------------------- search
     def _workspace(self, nbytes: int):
+        # zero-filled on growth: no slot of a fresh workspace holds garbage, even
+        # one a kernel reads before writing (the search re-initialises what it uses)
         if self._ws is None or self._ws.numel() < nbytes:
-            self._ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=self.device)
+            self._ws = torch.zeros(max(nbytes, 1), dtype=torch.uint8, device=self.device)
         return self._ws
 
     def search_device(self, xq: torch.Tensor, k: int, exact_scores: bool = False, id_offset: int = 0,
@@ -372,6 +374,7 @@ class IndexIVFFlat(_FallbackCounters):
         self._assign = torch.empty(0, dtype=torch.int64, device=self.device)
         self._ws = None
         self.fallback_counts = None
+        self.guard_word = None  # device int32[1]: the last search's guard word (check_guards)
         self._lists_valid = True
         self._n_lists = 0
         self.list_off = torch.zeros(self.nlist + 1, dtype=torch.int64, device=self.device)
@@ -441,12 +444,16 @@ class IndexIVFFlat(_FallbackCounters):
         return self.pos2id[lo:hi].cpu().numpy()
 
     def _workspace(self, nbytes: int):
+        # zero-filled on growth: no slot of a fresh workspace holds garbage, even
+        # one a kernel reads before writing (the search re-initialises what it uses)
         if self._ws is None or self._ws.numel() < nbytes:
-            self._ws = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=self.device)
+            self._ws = torch.zeros(max(nbytes, 1), dtype=torch.uint8, device=self.device)
         return self._ws
 
     def search_device(self, xq: torch.Tensor, k: int, exact_scores: bool = False, id_offset: int = 0,
-                      stage_events=None, probe: torch.Tensor | None = None):
+                      stage_events=None, probe: torch.Tensor | None = None, check: bool = False):
+        """Device-in, device-out IVF search -> (D, I[, S]).  check=True syncs and
+        raises if the search's index guards tripped (check_guards)."""
         k = int(k)
         if k <= 0:
             raise ValueError("k must be positive")
@@ -470,6 +477,8 @@ class IndexIVFFlat(_FallbackCounters):
         S = torch.empty((nq, k), dtype=torch.float64, device=dev) if exact_scores else None
         if self.fallback_counts is None:
             self.fallback_counts = torch.zeros(2, dtype=torch.int32, device=dev)
+        if self.guard_word is None:
+            self.guard_word = torch.zeros(1, dtype=torch.int32, device=dev)
         n = self.ntotal
         f = self.flat
         with torch.cuda.device(dev):
@@ -484,7 +493,23 @@ class IndexIVFFlat(_FallbackCounters):
                 _lib.ptr(self.pos2list) if n else None, self.nlist, n, self.max_list, self.d, k, self.metric_type,
                 _lib.ptr(D), _lib.ptr(I), _lib.ptr(S), int(id_offset), _lib.ptr(self.fallback_counts), _lib.ptr(ws),
                 ws.numel(), stage_events.ev if stage_events is not None else None, _lib.stream(dev)), "ivf_search")
+            # the search's guard word -> self.guard_word (device, no sync; include/nrk.h)
+            _lib.check(L.nrk_ivf_search_status(_lib.ptr(ws), ws.numel(), _lib.ptr(self.guard_word),
+                                               _lib.stream(dev)), "ivf_search_status")
+        if check:
+            self.check_guards()
         return (D, I, S) if exact_scores else (D, I)
+
+    def check_guards(self):
+        """Raise NrkError if the last search's guard word is nonzero: an index
+        it read back from its own workspace was out of range (the access was
+        skipped, the result is not valid).  Synchronises with the device."""
+        g = int(self.guard_word.item())
+        if g:
+            names = [n for b, n in ((1, "seed position"), (2, "candidate position"), (4, "collect query row"),
+                                    (8, "candidate count"), (16, "fallback query"), (32, "probed list"),
+                                    (64, "gathered pair"), (128, "collected position")) if g & b]
+            raise _lib.NrkError(f"ivf_search: index guard tripped (0x{g:x}: {', '.join(names)})")
 
     def search(self, x, k):
         xt, was_numpy = self.flat._as_input(x)

@@ -244,3 +244,43 @@ def test_ivf_c4_geometry_unbalanced_lists_and_collect_overflow(gpu, metric):
     if metric == ko.METRIC_L2:
         assert I[0].tolist() == [999, 1000, 1001, 1002, 1003]
     assert int(ivf.last_fallback.item()) >= 1
+
+
+def test_ivf_configs3_full_size_repeated_searches(gpu):
+    """configs[3] at FULL size, as bench.py's `ivf` record runs it (the record
+    that faulted in round 5's driver bench): bench's clustered 10M x 128 corpus
+    and 4096 queries, nlist 300, nprobe 32, k-means niter 20, k 5, L2; 5
+    warm-up + 20 timed-loop searches on one index (a 213K-row max list, 2048-
+    block persistent grids with per-XCD tickets, 4096-row phase-A chunks).
+    Every search: index guards clear, ids in [0, n) and unique per query,
+    distances ascending, results identical to the first search's; a query
+    sample against oracle/ivf_oracle.ivf_search over the full corpus."""
+    from newsrecommend_amd import faiss as nf
+    from newsrecommend_amd.data import clustered_corpus
+
+    n, d, nlist, nprobe, k, nq = 10_000_000, 128, 300, 32, 5, 4096
+    xb = clustered_corpus(n, d, seed=1234, device="cuda")
+    xq = clustered_corpus(nq, d, seed=4321, device="cuda")
+    ivf = nf.IndexIVFFlat(nf.IndexFlatL2(d), d, nlist, nf.METRIC_L2)
+    ivf.cp.niter = 20
+    ivf.train(xb)
+    ivf.add(xb)
+    ivf.nprobe = nprobe
+    assert ivf.max_list > 100_000
+    D0 = I0 = None
+    for s in range(25):
+        D, I = ivf.search_device(xq, k, check=True)
+        if D0 is None:
+            D0, I0 = D.clone(), I.clone()
+            assert bool(((I >= 0) & (I < n)).all())
+            assert bool((D[:, 1:] >= D[:, :-1]).all())
+            srt = torch.sort(I, 1).values
+            assert bool((srt[:, 1:] != srt[:, :-1]).all())
+        else:
+            assert torch.equal(I, I0) and torch.equal(D, D0), f"search {s} differs from search 0"
+    assert int(ivf.last_fallback.item()) == 0
+    sample = np.arange(0, nq, nq // 8)
+    Do, Io, _, _ = io.ivf_search(xq[sample].cpu().numpy(), xb.cpu().numpy(), ivf.quantizer._xb[:nlist].cpu().numpy(),
+                                 ivf._assign.cpu().numpy(), nprobe, k, ko.METRIC_L2)
+    np.testing.assert_array_equal(I0[sample].cpu().numpy(), Io)
+    np.testing.assert_array_equal(D0[sample].cpu().numpy(), Do)
