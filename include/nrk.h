@@ -298,7 +298,7 @@ int nrk_rerank_user_stats(const float* logits, const float* prob, const int64_t*
  * W1 [hidden][in_dim], b1 [hidden] (fc.0), W2 [out_dim][hidden], b2 [out_dim]
  * (fc.4 with the eval BatchNorm fc.3 folded in by the caller:
  * W2 = fc.4.weight diag(s), b2 = fc.4.bias + fc.4.weight t).  hidden a
- * multiple of 64, out_dim 256.  The hidden activations never leave the chip;
+ * multiple of 128, out_dim 256.  The hidden activations never leave the chip;
  * products are fp32-exact (each operand split into three bf16 planes, six
  * MFMA products).  ws: nrk_embed_workspace bytes (the weights' planes). */
 int nrk_embed_workspace(int32_t in_dim, int32_t hidden, int32_t out_dim, size_t* ws_bytes);

@@ -78,11 +78,26 @@ class ArticleEmbeddingModel(nn.Module):
 
         dev = _lib.require_device(x, what="ArticleEmbeddingModel.embed")
         W1, b1, W2, b2 = (p.detach().float().contiguous() for p in self.folded())
+        if W1.device != dev:
+            raise _lib.NrkError(f"ArticleEmbeddingModel.embed: input on {dev}, model on {W1.device}")
         x = x.float()
+        if x.dim() != 2 or x.shape[1] != W1.shape[1]:  # the reference's forward raises here too
+            raise RuntimeError(f"ArticleEmbeddingModel.embed: expected (n, {W1.shape[1]}) input, got "
+                               f"{tuple(x.shape)}")
         if x.stride(-1) != 1:
             x = x.contiguous()
         n, in_dim = x.shape
         hid, out_dim = W1.shape[0], W2.shape[0]
+        if not embed_supported(in_dim, hid, out_dim):
+            # a non-default architecture (nrk_embed: in_dim <= 256, hidden a multiple
+            # of 128, out_dim 256): the folded layers as two GPU GEMMs, said loudly
+            import warnings
+
+            warnings.warn(f"ArticleEmbeddingModel.embed: dims {in_dim} -> {hid} -> {out_dim} outside nrk_embed's "
+                          f"(<= 256, k*128, 256): two torch GEMMs on {dev}")
+            self.embed_path = "torch-gemm"
+            return torch.addmm(b2, torch.relu(torch.addmm(b1, x, W1.t())), W2.t())
+        self.embed_path = "nrk_embed"
         out = torch.empty((n, out_dim), dtype=torch.float32, device=dev)
         lib = _lib.load()
         sz = _lib.c_size(0)
@@ -92,6 +107,12 @@ class ArticleEmbeddingModel(nn.Module):
                                  _lib.ptr(b2), out_dim, _lib.ptr(out), _lib.ptr(ws), ws.numel(), _lib.stream(dev)),
                    "embed")
         return out
+
+
+def embed_supported(in_dim: int, hidden: int, out_dim: int) -> bool:
+    """Shapes nrk_embed runs (csrc/embed.hip: KP = 256 input columns, HC = 128
+    hidden units per chunk, OD = 256 outputs); the reference's 253 -> 512 -> 256."""
+    return 1 <= in_dim <= 256 and hidden >= 128 and hidden % 128 == 0 and out_dim == 256
 
 
 def inference(model: ArticleEmbeddingModel, article_features, device=None, out_path: str | None = None,
@@ -108,7 +129,11 @@ def inference(model: ArticleEmbeddingModel, article_features, device=None, out_p
         ids = np.asarray(ids, dtype=np.int64)
         feats = np.ascontiguousarray(feats, dtype=np.float32)
     if device is None:
+        # the model's device, or the GPU for a model loaded on the host (a
+        # checkpoint read with map_location="cpu"): embed() runs on the GPU only
         device = next(model.parameters()).device
+        if device.type != "cuda" and torch.cuda.is_available():
+            device = torch.device("cuda", torch.cuda.current_device())
     model = model.to(device).eval()
     x = torch.from_numpy(feats).to(device)
     emb = model.embed(x, batch=batch).cpu().numpy()

@@ -158,6 +158,22 @@ def rerank_project(model, table: torch.Tensor, rows: torch.Tensor, prm=None, his
     return out
 
 
+HIST_PROJ_BUDGET = 4 << 30  # bytes of per-slot history projections per rerank_ragged launch
+_RERANK_WS: dict = {}  # (device, stream) -> nrk_din_rerank workspace (each call resets what it uses)
+
+
+def _rerank_workspace(dev) -> torch.Tensor:
+    from . import _lib
+
+    key = (dev, _lib.stream(dev))
+    ws = _RERANK_WS.get(key)
+    if ws is None:
+        sz = _lib.c_size(0)
+        _lib.check(_lib.load().nrk_din_rerank_workspace(sz), "din_rerank_workspace")
+        ws = _RERANK_WS[key] = torch.zeros(max(sz.value, 1), dtype=torch.uint8, device=dev)
+    return ws
+
+
 def rerank_ragged(model, table: torch.Tensor, hist_rows: torch.Tensor, cand: torch.Tensor, cand_off: torch.Tensor,
                   cand_len: torch.Tensor, extra: torch.Tensor | None, out_off: torch.Tensor, n_out: int,
                   prm=None, shared: bool = False, direct: bool = False) -> torch.Tensor:
@@ -185,10 +201,10 @@ def rerank_ragged(model, table: torch.Tensor, hist_rows: torch.Tensor, cand: tor
     out = torch.empty(n_out, dtype=torch.float32, device=dev)
     if U == 0:
         return out
+    if direct and table.dtype != torch.bfloat16:
+        raise ValueError("rerank_ragged(direct=True) reads bf16 table rows; an f32 table takes the projected form")
     lib = _lib.load()
-    sz = _lib.c_size(0)
-    _lib.check(lib.nrk_din_rerank_workspace(sz), "din_rerank_workspace")
-    ws = torch.empty(sz.value, dtype=torch.uint8, device=dev)
+    ws = _rerank_workspace(dev)
     h = hist_rows.to(torch.int32).contiguous()
     c = cand.to(torch.int32).contiguous()
     co, cl, oo = cand_off.to(torch.int64).contiguous(), cand_len.to(torch.int32).contiguous(), \
@@ -200,20 +216,31 @@ def rerank_ragged(model, table: torch.Tensor, hist_rows: torch.Tensor, cand: tor
         tp = KernelTimer.mark("rerank_project")
         cp = rerank_project(model, table, c, prm)
         xp = rerank_project(model, table, ex, prm) if ex is not None else None
-        hp = rerank_project(model, table, h.reshape(-1), prm, hist=True)
         KernelTimer.push("rerank_project", tp)
-        t0 = KernelTimer.mark("rerank")  # (the main kernel alone)
-        _lib.check(lib.nrk_din_rerank_projected(_lib.ptr(table), table.shape[0], _table_dtype(table), _lib.ptr(h), U, L,
-                                                _lib.ptr(c), _lib.ptr(co), _lib.ptr(cl), _lib.ptr(ex), _lib.ptr(oo),
-                                                _lib.ptr(out), d, A, F, ctypes.byref(p), _lib.ptr(cp), _lib.ptr(xp),
-                                                _lib.ptr(hp), _lib.ptr(ws), ws.numel(), _lib.stream(dev)),
-                   "din_rerank_projected")
-    else:
-        t0 = KernelTimer.mark("rerank")
-        _lib.check(lib.nrk_din_rerank(_lib.ptr(table), table.shape[0], _lib.NRK_DTYPE_BF16, _lib.ptr(h), U, L,
-                                      _lib.ptr(c), _lib.ptr(co), _lib.ptr(cl), _lib.ptr(ex), _lib.ptr(oo),
-                                      _lib.ptr(out), d, A, F, ctypes.byref(p), _lib.ptr(ws), ws.numel(),
-                                      _lib.stream(dev)), "din_rerank")
+        # the history projections are per slot (U L (A + F) f32): users in chunks
+        # whose projections fit HIST_PROJ_BUDGET (one chunk up to ~100K users at
+        # L = 64, A + F = 160), the candidates' projections shared by all chunks
+        ub = max(1, HIST_PROJ_BUDGET // (L * (A + F) * 4))
+        for lo in range(0, U, ub):
+            hi = min(U, lo + ub)
+            tp = KernelTimer.mark("rerank_project")
+            hp = rerank_project(model, table, h[lo:hi].reshape(-1), prm, hist=True)
+            KernelTimer.push("rerank_project", tp)
+            t0 = KernelTimer.mark("rerank")  # (the main kernel alone)
+            _lib.check(lib.nrk_din_rerank_projected(
+                _lib.ptr(table), table.shape[0], _table_dtype(table), _lib.ptr(h[lo:hi]), hi - lo, L, _lib.ptr(c),
+                _lib.ptr(co[lo:hi]), _lib.ptr(cl[lo:hi]), _lib.ptr(ex[lo:hi]) if ex is not None else None,
+                _lib.ptr(oo[lo:hi]), _lib.ptr(out), d, A, F, ctypes.byref(p), _lib.ptr(cp),
+                _lib.ptr(xp[lo:hi]) if xp is not None else None, _lib.ptr(hp), _lib.ptr(ws), ws.numel(),
+                _lib.stream(dev)), "din_rerank_projected")
+            KernelTimer.push("rerank", t0)
+            del hp
+        return out
+    t0 = KernelTimer.mark("rerank")
+    _lib.check(lib.nrk_din_rerank(_lib.ptr(table), table.shape[0], _lib.NRK_DTYPE_BF16, _lib.ptr(h), U, L,
+                                  _lib.ptr(c), _lib.ptr(co), _lib.ptr(cl), _lib.ptr(ex), _lib.ptr(oo),
+                                  _lib.ptr(out), d, A, F, ctypes.byref(p), _lib.ptr(ws), ws.numel(),
+                                  _lib.stream(dev)), "din_rerank")
     KernelTimer.push("rerank", t0)
     return out
 
@@ -280,7 +307,8 @@ def rerank(model, table: torch.Tensor, hist_rows: torch.Tensor, cand_rows: torch
         cr = cand_rows[lo:hi].reshape(-1).to(torch.int32)
         hr = hist_rows[lo:hi, None, :].expand(hi - lo, C, L).reshape(-1, L).to(torch.int32)
         lg = model.forward_ids(table, cr, hr).view(hi - lo, C)
-        out[lo:hi] = torch.where(cand_rows[lo:hi] >= 0, lg, torch.full_like(lg, -float("inf")))
+        ok = (cand_rows[lo:hi] >= 0) & (cand_rows[lo:hi] < table.shape[0])  # rows outside the table: -inf, as fused
+        out[lo:hi] = torch.where(ok, lg, torch.full_like(lg, -float("inf")))
     return out
 
 

@@ -7,7 +7,7 @@
       the Retrieval.py flow's geometry: 364,047 items, 300 clusters of skewed
       sizes (mean ~1,210), every user scoring its whole cluster + the appended
       ground truth, L 64 (pipeline.rerank_ragged, shared lists projected once;
-      --unshared: every user stages the rows)
+      --direct: a bf16 table through the row-staged nrk_din_rerank)
 Prints ms per call (wall, synchronised) and the kernel's HIP-event time."""
 import argparse
 import os
@@ -27,7 +27,7 @@ ap.add_argument("--items", type=int, default=None)
 ap.add_argument("--cands", type=int, default=201)
 ap.add_argument("--reps", type=int, default=10)
 ap.add_argument("--flow", action="store_true")
-ap.add_argument("--unshared", action="store_true", help="flow: score the rows, not the shared lists' projections")
+ap.add_argument("--direct", action="store_true", help="flow: the row-staged kernel (bf16 table, L <= 64)")
 ap.add_argument("--A", type=int, default=128)
 ap.add_argument("--F", type=int, default=32)
 ap.add_argument("--f32", action="store_true", help="an fp32 item table (the projected path)")
@@ -63,7 +63,7 @@ if a.flow:
     n_out = int(width.sum())
 
     def call():
-        return rerank_ragged(model, table, hist, rows, co, cl, extra, oo, n_out, shared=not a.unshared)
+        return rerank_ragged(model, table, hist, rows, co, cl, extra, oo, n_out, direct=a.direct)
     samples = n_out
 else:
     cand = torch.randint(0, N, (U, a.cands), generator=g, device=dev, dtype=torch.int32)
