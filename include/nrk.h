@@ -263,7 +263,11 @@ int nrk_din_rerank(const void* table, int64_t n_table, int32_t dtype, const int3
  * [nU * L][A + F] (required).  cand / extra / hist still decide validity.
  * For F <= 64 it runs one wave per 32 candidates (din_rerank_lane.hip; its
  * arithmetic order differs from nrk_din_rerank's, both within 1e-4 of the
- * reference), for F in {96, 128} the per-chunk kernel of nrk_din_rerank. */
+ * reference), for F in {96, 128} the per-chunk kernel of nrk_din_rerank.
+ * Histories of 65..128 slots (L <= nrk_din_rerank_max_history = 128 for every
+ * (A, F)) take the lane kernel's 128-row form; where [P' | R^T] and H2 do not
+ * fit its LDS together ((A, F) = (96, 64), (128, 64), F in {96, 128}) it stages
+ * P' only and reads R and H2 from global memory. */
 int nrk_din_rerank_project(const void* table, int64_t n_table, int32_t dtype, const int32_t* rows, int64_t n,
                            int32_t d, int32_t A, int32_t F, const nrk_din_rerank_params* params, float* out,
                            void* stream);

@@ -2866,9 +2866,11 @@ extern "C" int nrk_din_attn_fwd(const void* keys, const int32_t* hist_ids, int64
   // per sample at 8 waves per CU (profiles/r03_din_fwd_pair_ab.log)
   if (wave_ok && d == 128) {
     const size_t psm = pair_sm;
-    NRK_CHECK_ARG(3 * psm <= 160 * 1024, "din_fwd: L=%d d=%d needs %zu B LDS (pair)", L, d, psm);
+    // histories of 65..128 slots (twice the key image): fewer workgroups per CU
+    NRK_CHECK_ARG(psm <= 160 * 1024, "din_fwd: L=%d d=%d needs %zu B LDS (pair)", L, d, psm);
+    const int per_cu = (int)((160 * 1024) / psm) < 3 ? (int)((160 * 1024) / psm) : 3;
     int grid = (int)cdiv(B, 2);
-    if (grid > 768) grid = 768;
+    if (grid > 256 * per_cu) grid = 256 * per_cu;
     const uint16_t* tb = static_cast<const uint16_t*>(keys);
     const uint16_t* wk = static_cast<const uint16_t*>(W1k);
     hipStream_t st = (hipStream_t)stream;

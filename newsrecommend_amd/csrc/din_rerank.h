@@ -57,10 +57,11 @@ __device__ __forceinline__ int slice_col(int n, int A) {
   return sj * SL + 4 * p4 + (w & 3);
 }
 
-// the projected re-rank for F <= 64 (din_rerank_lane.hip); a.sgn: 2 A bytes of
-// workspace the launch fills with sgn(w2) per projection column
+// the projected re-rank for F <= 64, and for every F at histories of 65..128
+// slots (din_rerank_lane.hip); a.sgn: 2 A bytes of workspace the launch fills
+// with sgn(w2) per projection column
 int launch_lane(int A, const RerankArgs& a, hipStream_t st);
-// the longest history (L) launch_lane holds for (A, F <= 64): 64 or 128
+// the longest history (L) launch_lane holds for (A, F): 128
 int lane_max_l(int A, int F);
 
 }  // namespace rr

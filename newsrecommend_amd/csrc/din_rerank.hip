@@ -1124,7 +1124,7 @@ static int rerank_impl(const void* table, int64_t n_table, int32_t dtype, const 
   NRK_CHECK_ARG(d == 64 || d == 128 || d == 256, "din_rerank: emb_dim %d unsupported (64, 128, 256)", d);
   NRK_CHECK_ARG(A >= 32 && A <= 128 && A % 32 == 0, "din_rerank: attn_units %d unsupported (32..128 step 32)", A);
   NRK_CHECK_ARG(F >= 32 && F <= 128 && F % 32 == 0, "din_rerank: fc_units %d unsupported (32..128 step 32)", F);
-  const int maxl = cand_proj && F <= 64 ? rr::lane_max_l(A, F) : rr::LP;  // (the lane kernel holds up to 128 rows)
+  const int maxl = cand_proj ? rr::lane_max_l(A, F) : rr::LP;  // (the lane kernel holds up to 128 rows)
   NRK_CHECK_ARG(L >= 1 && L <= maxl, "din_rerank: history length %d unsupported (1..%d)", L, maxl);
   NRK_CHECK_ARG(nU >= 0, "din_rerank: bad user count %d", nU);
   if (nU == 0) return NRK_OK;
@@ -1172,7 +1172,8 @@ static int rerank_impl(const void* table, int64_t n_table, int32_t dtype, const 
   a.hproj = hist_proj;
   a.sgn = static_cast<char*>(ws) + 64;
   // (the projected kernels do not depend on d)
-  if (cand_proj && F <= 64) return rr::launch_lane(A, a, st);
+  // the lane kernel: F <= 64, and every F for histories of 65..128 slots
+  if (cand_proj && (F <= 64 || L > rr::LP)) return rr::launch_lane(A, a, st);
   if (cand_proj) return rr::launch_a<64, true>(A, a, st);
   if (d == 256) return rr::launch_a<256, false>(A, a, st);
   if (d == 128) return rr::launch_a<128, false>(A, a, st);
@@ -1191,7 +1192,7 @@ extern "C" int nrk_din_rerank_max_history(int32_t A, int32_t F, int32_t* max_l) 
   NRK_CHECK_ARG(max_l, "din_rerank_max_history: null");
   NRK_CHECK_ARG(A >= 32 && A <= 128 && A % 32 == 0 && F >= 32 && F <= 128 && F % 32 == 0,
                 "din_rerank_max_history: A %d / F %d unsupported", A, F);
-  *max_l = F <= 64 ? rr::lane_max_l(A, F) : rr::LP;
+  *max_l = rr::lane_max_l(A, F);  // (the projected form; nrk_din_rerank itself holds rr::LP)
   return NRK_OK;
 }
 

@@ -37,7 +37,13 @@ constexpr int CPI = 32;  // candidates per wave item
 // wave's LDS reads issue beside this one's VALU); 128 (histories of 65..128
 // slots, the reference's max_history range): 4 waves, the LDS holds twice the
 // rows and four waves' score regions.
-template <int A, int F, int LPK>
+// RG (128 rows where [P' | R^T] and H2 do not fit the LDS together: (A, F) =
+// (96, 64), (128, 64) and every F in {96, 128}): only P' is staged; the e R
+// product reads R from the history projections in global memory (the user's
+// rows, L2-resident after the staging read them), the softmax weights laid out
+// by history SLOT instead of by compacted row (an invalid slot's R is zero), and
+// the head's H2 comes from global memory too.
+template <int A, int F, int LPK, bool RG = false>
 struct Lay {  // byte offsets
   static constexpr int LP = LPK, NW = LPK == 64 ? 8 : 4, NT = 64 * NW;
   static constexpr int F2 = F / 2;
@@ -48,11 +54,11 @@ struct Lay {  // byte offsets
   static constexpr int c1 = 0;                          // [F]
   static constexpr int c2 = c1 + F * 4;                 // [F2]
   static constexpr int h3 = c2 + F2 * 4;                // [F2]
-  static constexpr int h2 = h3 + F2 * 4;                // H2 hi, lo bf16 [F2][F]
-  static constexpr int pp = h2 + 2 * F2 * F * 2;        // P' [LP][PST] f32
+  static constexpr int h2 = h3 + F2 * 4;                // H2 hi, lo bf16 [F2][F] (RG: none)
+  static constexpr int pp = h2 + (RG ? 0 : 2 * F2 * F * 2);  // P' [LP][PST] f32
   static constexpr int hsp = pp + LP * PST * 4;         // SP / 2 [LP]
-  static constexpr int rt = hsp + LP * 4;               // R^T hi, lo bf16 [F][LP]
-  static constexpr int wv = rt + 2 * F * LP * 2;        // per wave: scores, then e hi / lo, then h1
+  static constexpr int rt = hsp + LP * 4;               // R^T hi, lo bf16 [F][LP] (RG: none)
+  static constexpr int wv = rt + (RG ? 0 : 2 * F * LP * 2);  // per wave: scores, then e hi / lo, then h1
   static constexpr int SB = CPI * SST * 4, EB = 2 * CPI * EST * 2, HB = CPI * (F + 4) * 4;
   static constexpr int XB = SB > EB ? SB : EB;
   static constexpr int WB = ((XB > HB ? XB : HB) + 2 * CPI * 4 + 15) & ~15;  // + den, valid [CPI]
@@ -60,17 +66,16 @@ struct Lay {  // byte offsets
   static constexpr int total = qs + 16;
 };
 
-template <int A, int F, int LPK>
+template <int A, int F, int LPK, bool RG>
 __global__ __launch_bounds__((LPK == 64 ? 512 : 256), 1) void din_rerank_lane_kernel(RerankArgs a) {
-  using LY = Lay<A, F, LPK>;
+  using LY = Lay<A, F, LPK, RG>;
   constexpr int F2 = F / 2, AQ = A / 4, NG = AQ / 8, AF = A + F, PST = LY::PST, QST = LY::QST, SST = LY::SST, EST = LY::EST;
   constexpr int LP = LPK, NT = LY::NT, NW = LY::NW;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* c1s = reinterpret_cast<float*>(smem + LY::c1);
   float* c2s = reinterpret_cast<float*>(smem + LY::c2);
   float* h3s = reinterpret_cast<float*>(smem + LY::h3);
-  uint16_t* H2h = reinterpret_cast<uint16_t*>(smem + LY::h2);
-  uint16_t* H2l = H2h + F2 * F;
+  uint16_t* H2s = reinterpret_cast<uint16_t*>(smem + LY::h2);
   float* Pp = reinterpret_cast<float*>(smem + LY::pp);
   float* hSP = reinterpret_cast<float*>(smem + LY::hsp);
   uint16_t* Rth = reinterpret_cast<uint16_t*>(smem + LY::rt);
@@ -92,9 +97,11 @@ __global__ __launch_bounds__((LPK == 64 ? 512 : 256), 1) void din_rerank_lane_ke
     c2s[i] = a.c2[i];
     h3s[i] = a.h3[i];
   }
-  for (int i = tid; i < F2 * F; i += NT) {
-    H2h[i] = a.H2_hi[i];
-    H2l[i] = a.H2_lo[i];
+  if constexpr (!RG) {
+    for (int i = tid; i < F2 * F; i += NT) {
+      H2s[i] = a.H2_hi[i];
+      H2s[F2 * F + i] = a.H2_lo[i];
+    }
   }
   if (tid == 0) qslot[0] = atomicAdd(a.queue, 1);
   __syncthreads();
@@ -124,14 +131,15 @@ __global__ __launch_bounds__((LPK == 64 ? 512 : 256), 1) void din_rerank_lane_ke
     if (ctot > 0) {
       // [P' | R] of the valid slots, compacted; rows nv .. LP - 1 zero (the
       // shared padding row, and the e R MFMA's K padding)
-      for (int e = tid; e < LP * (AF / 4); e += NT) {
-        const int row = e / (AF / 4), part = e % (AF / 4);
+      constexpr int SPARTS = RG ? A / 4 : AF / 4;  // float4 parts staged per row (RG: P' only)
+      for (int e = tid; e < LP * SPARTS; e += NT) {
+        const int row = e / SPARTS, part = e % SPARTS;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (row < nv) {
           const int slot = row < nv0 ? nth_set_bit(vm, row) : 64 + nth_set_bit(vm1, row - nv0);
           v = *reinterpret_cast<const float4*>(a.hproj + ((int64_t)u * a.L + slot) * AF + 4 * part);
         }
-        if (part < A / 4) {
+        if (RG || part < A / 4) {
           const int c = 4 * part;
           *reinterpret_cast<float4*>(Pp + row * PST + (c / AQ) * QST + c % AQ) = v;
         } else {
@@ -310,35 +318,66 @@ __global__ __launch_bounds__((LPK == 64 ? 512 : 256), 1) void din_rerank_lane_ke
         m = fmaxf(__uint_as_float(mm[0]), __uint_as_float(mm[1]));
       }
       // ---- softmax weights -> bf16 hi + lo planes (rows nr .. nrp - 1 zero), sum e
-      float ev[LP / 2];
+      // (RG: planes by history slot, slots nks * 32 of them; invalid slots zero)
       float sum = 0.f;
+      const int nks = RG ? (a.L + 31) / 32 : nrp / 32;
+      if constexpr (RG) {
+        // every score is read before the planes are written over them
+        float es[LP / 2];
 #pragma unroll
-      for (int p = 0; p < LP / 2; ++p) {
-        const int r = 2 * p + h;
-        ev[p] = 0.f;
-        if (r < nr) {
-          ev[p] = __expf(Sw[cs * SST + r] - m);
-          sum = fmaf(r < nv ? 1.f : (float)npad, ev[p], sum);
+        for (int p = 0; p < LP / 2; ++p) {
+          const int sl = 2 * p + h;  // history slot
+          es[p] = 0.f;
+          if (sl < a.L) {
+            const uint64_t bits = sl < 64 ? vm : vm1;
+            const int b = sl & 63;
+            if ((bits >> b) & 1ull) {
+              const int r = (sl < 64 ? 0 : nv0) + __popcll(bits & ((1ull << b) - 1ull));  // its compacted row
+              es[p] = __expf(Sw[cs * SST + r] - m);
+              sum += es[p];
+            }
+          }
+        }
+        if (npad > 0 && h == 0) sum = fmaf((float)npad, __expf(Sw[cs * SST + nv] - m), sum);  // the padding row
+#pragma unroll
+        for (int p = 0; p < LP / 2; ++p) {
+          const int sl = 2 * p + h;
+          if (sl < 32 * nks) {
+            short hi, lo;
+            split_bf16(es[p], hi, lo);
+            Eh[cs * EST + sl] = (uint16_t)hi;
+            El[cs * EST + sl] = (uint16_t)lo;
+          }
+        }
+      } else {
+        float ev[LP / 2];
+#pragma unroll
+        for (int p = 0; p < LP / 2; ++p) {
+          const int r = 2 * p + h;
+          ev[p] = 0.f;
+          if (r < nr) {
+            ev[p] = __expf(Sw[cs * SST + r] - m);
+            sum = fmaf(r < nv ? 1.f : (float)npad, ev[p], sum);
+          }
+        }
+#pragma unroll
+        for (int p = 0; p < LP / 2; ++p) {
+          const int r = 2 * p + h;
+          if (r < nrp) {
+            short hi, lo;
+            split_bf16(ev[p], hi, lo);
+            Eh[cs * EST + r] = (uint16_t)hi;
+            El[cs * EST + r] = (uint16_t)lo;
+          }
         }
       }
       {
         const auto ss = __builtin_amdgcn_permlane16_swap(__float_as_uint(sum), __float_as_uint(sum), false, false);
         sum = __uint_as_float(ss[0]) + __uint_as_float(ss[1]);
       }
-#pragma unroll
-      for (int p = 0; p < LP / 2; ++p) {
-        const int r = 2 * p + h;
-        if (r < nrp) {
-          short hi, lo;
-          split_bf16(ev[p], hi, lo);
-          Eh[cs * EST + r] = (uint16_t)hi;
-          El[cs * EST + r] = (uint16_t)lo;
-        }
-      }
       if (h == 0) dnw[cs] = sum;
 
       // ---- h1 = relu(Q1 + (e R) / sum e + c1): C tile rows = candidates 16 ct + 4 l4 + k
-      const int nks = nrp / 32;
       constexpr int KS = LP / 32;
       bf16x8 eh[2][KS], el[2][KS];  // [ct][ks] (all read before h1 is written over them)
 #pragma unroll
@@ -354,6 +393,53 @@ __global__ __launch_bounds__((LPK == 64 ? 512 : 256), 1) void din_rerank_lane_ke
       for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
         for (int k = 0; k < 4; ++k) dv[ct][k] = dnw[16 * ct + 4 * l4 + k];
+      if constexpr (RG) {
+        // R from the user's history projections: rows (slots) 32 ks + 8 l4 .. + 7 of
+        // column A + f, split into bf16 hi + lo in registers; each fragment serves
+        // both candidate tiles
+        const float* hb = a.hproj + (int64_t)u * a.L * AF + A;
+#pragma unroll
+        for (int ft = 0; ft < F / 16; ++ft) {
+          const int f = 16 * ft + l15;
+          f32x4 acc[2];
+#pragma unroll
+          for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) acc[ct][k] = q1v[ct][ft][k] * dv[ct][k];
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) {
+            if (ks < nks) {
+              bf16x8 rh, rl;
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                const int sl = 32 * ks + 8 * l4 + j;
+                const float x = sl < a.L ? hb[(int64_t)sl * AF + f] : 0.f;
+                short hi, lo;
+                split_bf16(x, hi, lo);
+                rh[j] = hi;
+                rl[j] = lo;
+              }
+#pragma unroll
+              for (int ct = 0; ct < 2; ++ct) {
+                if (16 * ct < nci) {
+                  acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(el[ct][ks], rh, acc[ct], 0, 0, 0);
+                  acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(eh[ct][ks], rl, acc[ct], 0, 0, 0);
+                  acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(eh[ct][ks], rh, acc[ct], 0, 0, 0);
+                }
+              }
+            }
+          }
+          const float cb = c1s[f];
+#pragma unroll
+          for (int ct = 0; ct < 2; ++ct) {
+            if (16 * ct >= nci) continue;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              H1w[(16 * ct + 4 * l4 + k) * (F + 4) + f] =
+                  fmaxf(acc[ct][k] * __builtin_amdgcn_rcpf(dv[ct][k]) + cb, 0.f);
+          }
+        }
+      } else {
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct) {
         if (16 * ct >= nci) continue;
@@ -384,6 +470,7 @@ __global__ __launch_bounds__((LPK == 64 ? 512 : 256), 1) void din_rerank_lane_ke
           for (int k = 0; k < 4; ++k) H1w[(16 * ct + 4 * l4 + k) * (F + 4) + f] = fmaxf(acc[k] * rden[k] + cb, 0.f);
         }
       }
+      }  // (RG)
 
       // ---- h2 = relu(H2 h1 + c2), logit = h3 . h2 + c3 (16-unit tiles t2)
 #pragma unroll
@@ -408,8 +495,14 @@ __global__ __launch_bounds__((LPK == 64 ? 512 : 256), 1) void din_rerank_lane_ke
               hh[jj] = hi;
               hl[jj] = lo;
             }
-            const bf16x8 bh = *reinterpret_cast<const bf16x8*>(H2h + v * F + 32 * ks + 8 * l4);
-            const bf16x8 bl = *reinterpret_cast<const bf16x8*>(H2l + v * F + 32 * ks + 8 * l4);
+            bf16x8 bh, bl;
+            if constexpr (RG) {  // H2 from global memory
+              bh = *reinterpret_cast<const bf16x8*>(a.H2_hi + v * F + 32 * ks + 8 * l4);
+              bl = *reinterpret_cast<const bf16x8*>(a.H2_lo + v * F + 32 * ks + 8 * l4);
+            } else {
+              bh = *reinterpret_cast<const bf16x8*>(H2s + v * F + 32 * ks + 8 * l4);
+              bl = *reinterpret_cast<const bf16x8*>(H2s + F2 * F + v * F + 32 * ks + 8 * l4);
+            }
             acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hl, bh, acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hh, bl, acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(hh, bh, acc, 0, 0, 0);
@@ -435,30 +528,34 @@ __global__ void sign_cols_kernel(const float* __restrict__ w2, int A, _Float16* 
   for (int n = threadIdx.x; n < A; n += blockDim.x) sgn[slice_col(n, A)] = w2[n] >= 0.f ? (_Float16)1.f : (_Float16)-1.f;
 }
 
-template <int A, int F, int LPK>
+template <int A, int F, int LPK, bool RG>
 int launch(const RerankArgs& a, hipStream_t st) {
-  using LY = Lay<A, F, LPK>;
+  using LY = Lay<A, F, LPK, RG>;
   constexpr size_t lds = LY::total;
   static_assert(lds <= 160 * 1024, "din_rerank_lane: LDS");
   const int grid = a.nU < 256 ? a.nU : 256;
-  hipLaunchKernelGGL((din_rerank_lane_kernel<A, F, LPK>), dim3(grid), dim3(LY::NT), lds, st, a);
+  hipLaunchKernelGGL((din_rerank_lane_kernel<A, F, LPK, RG>), dim3(grid), dim3(LY::NT), lds, st, a);
   NRK_CHECK_LAUNCH("din_rerank_lane_kernel");
   return NRK_OK;
 }
-// the longest history the lane kernel holds for (A, F): 128 where the
-// 128-row form's LDS fits, else 64
+// the 128-row form: R^T and H2 in the LDS where they fit beside P', else RG
 template <int A, int F>
-constexpr int max_l() { return Lay<A, F, 128>::total <= 160 * 1024 ? 128 : 64; }
+constexpr bool rg128() { return Lay<A, F, 128, false>::total > 160 * 1024; }
+static_assert(Lay<128, 128, 128, true>::total <= 160 * 1024, "din_rerank_lane: the largest RG form must fit");
 template <int A, int F>
 int launch_l(const RerankArgs& a, hipStream_t st) {
-  if constexpr (max_l<A, F>() == 128) {
-    if (a.L > 64) return launch<A, F, 128>(a, st);
-  }
-  return launch<A, F, 64>(a, st);
+  if (a.L > 64) return launch<A, F, 128, rg128<A, F>()>(a, st);
+  if constexpr (F <= 64) return launch<A, F, 64, false>(a, st);
+  return fail(NRK_EUNSUPPORTED, "din_rerank_lane: F = %d takes histories of 65..128 only", F);
 }
 template <int A>
 int launch_f(const RerankArgs& a, hipStream_t st) {
-  return a.F == 32 ? launch_l<A, 32>(a, st) : launch_l<A, 64>(a, st);
+  switch (a.F) {
+    case 32: return launch_l<A, 32>(a, st);
+    case 64: return launch_l<A, 64>(a, st);
+    case 96: return launch_l<A, 96>(a, st);
+    default: return launch_l<A, 128>(a, st);
+  }
 }
 inline int launch_a(int A, const RerankArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(sign_cols_kernel, dim3(1), dim3(128), 0, st, a.w2, A, reinterpret_cast<_Float16*>(const_cast<void*>(a.sgn)));
@@ -475,17 +572,8 @@ inline int launch_a(int A, const RerankArgs& a, hipStream_t st) {
 int launch_lane(int A, const RerankArgs& a, hipStream_t st) { return lk::launch_a(A, a, st); }
 
 int lane_max_l(int A, int F) {
-  switch (A * 1000 + F) {
-    case 32032: return lk::max_l<32, 32>();
-    case 32064: return lk::max_l<32, 64>();
-    case 64032: return lk::max_l<64, 32>();
-    case 64064: return lk::max_l<64, 64>();
-    case 96032: return lk::max_l<96, 32>();
-    case 96064: return lk::max_l<96, 64>();
-    case 128032: return lk::max_l<128, 32>();
-    case 128064: return lk::max_l<128, 64>();
-    default: return 0;
-  }
+  // every (A, F) of the grid: 128 (F > 64 through the RG form only, for L > 64)
+  return (A % 32 == 0 && A >= 32 && A <= 128 && F % 32 == 0 && F >= 32 && F <= 128) ? 128 : 0;
 }
 
 }  // namespace rr

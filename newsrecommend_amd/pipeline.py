@@ -246,9 +246,9 @@ def rerank_ragged(model, table: torch.Tensor, hist_rows: torch.Tensor, cand: tor
 
 
 def rerank_max_history(A: int, F: int) -> int:
-    """nrk_din_rerank_max_history: the longest history the fused re-rank holds
-    for (A, F) (128 for F <= 64 where the lane kernel's 128-row form fits, else
-    RERANK_MAX_L)."""
+    """nrk_din_rerank_max_history: the longest history the fused (projected)
+    re-rank holds for (A, F): 128 over the whole Optuna grid (DIN.py:203-207;
+    the lane kernel's 128-row form), RERANK_MAX_L outside it."""
     from . import _lib
 
     if A not in (32, 64, 96, 128) or F not in (32, 64, 96, 128):
@@ -281,10 +281,10 @@ def rerank(model, table: torch.Tensor, hist_rows: torch.Tensor, cand_rows: torch
     users with history rows (U, L) (-1 = padding), all rows of `table` on the
     device.  Eval-mode BatchNorm is row-independent, so one forward over many
     users equals the reference's per-user forwards.  With a bf16 or f32
-    table, d in {64, 128, 256}, L <= 64, A and F in {32, 64, 96, 128} the whole
-    evaluate() forward is one fused kernel (nrk_din_rerank; an f32 table
-    through the row projections, rerank_ragged); otherwise every candidate is
-    a DIN sample (model.forward_ids, C x the attention work)."""
+    table, d in {64, 128, 256}, L <= 128, A and F in {32, 64, 96, 128} the
+    whole evaluate() forward is one fused launch over the row projections
+    (rerank_ragged); otherwise every candidate is a DIN sample
+    (model.forward_ids, C x the attention work)."""
     model.eval()
     U, C = cand_rows.shape
     L = hist_rows.shape[1]

@@ -110,16 +110,16 @@ def test_library_exports_every_header_symbol():
 
 
 def test_rerank_max_history_query():
-    """nrk_din_rerank_max_history (host only): 128 history slots where the
-    lane kernel's 128-row form fits its LDS (F <= 64 but (96, 64), (128, 64)),
-    64 otherwise; an unsupported (A, F) is an error."""
+    """nrk_din_rerank_max_history (host only): 128 history slots for every
+    (A, F) of the reference's Optuna grid (DIN.py:203-207; the lane kernel's
+    128-row form, R and H2 from global memory where they do not fit its LDS);
+    an unsupported (A, F) is an error."""
     from newsrecommend_amd import _lib
     from newsrecommend_amd.pipeline import rerank_max_history
 
     for A in (32, 64, 96, 128):
         for F in (32, 64, 96, 128):
-            want = 128 if F <= 64 and (A, F) not in ((96, 64), (128, 64)) else 64
-            assert rerank_max_history(A, F) == want, (A, F)
+            assert rerank_max_history(A, F) == 128, (A, F)
     v = ctypes.c_int32(0)
     assert _lib.load().nrk_din_rerank_max_history(48, 32, ctypes.byref(v)) != 0
 

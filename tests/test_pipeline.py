@@ -150,7 +150,12 @@ def _oracle_logits(model, T, hist_u, cand_u):
                                        (256, 64, 130, 64, 96), (128, 33, 37, 128, 32),
                                        # histories past 64 slots (max_history reaches 128, DIN.py:207):
                                        # the lane kernel's 128-row form
-                                       (256, 128, 75, 128, 32), (128, 96, 40, 64, 64), (64, 100, 33, 32, 32)])
+                                       (256, 128, 75, 128, 32), (128, 96, 40, 64, 64), (64, 100, 33, 32, 32),
+                                       # ... where [P' | R^T] and H2 do not fit the LDS together (R and H2
+                                       # read from global memory, the RG form): fc_units 96 / 128 and
+                                       # (A, F) = (96, 64), (128, 64)
+                                       (256, 128, 75, 128, 128), (256, 96, 70, 96, 64), (128, 100, 40, 128, 64),
+                                       (64, 128, 33, 32, 96), (256, 65, 66, 64, 128)])
 def test_rerank_fused_vs_oracle_and_per_candidate(d, L, C, A, F):
     """nrk_din_rerank over the reference's hyper-parameter space (Optuna
     DIN.py:203-204: attn_units and fc_units 32..128 step 32) against the fp64

@@ -218,20 +218,21 @@ def test_rerank_clusters_f32_table_bit_identical_on_bf16_exact_rows(gpu):
         assert torch.equal(a, b)
 
 
-def test_rerank_clusters_fallback_long_history_and_duplicate_positive(gpu):
-    """a history longer than the fused kernels hold for the model
-    (L = 96 at A = 128, F = 64, where the lane kernel's 128-row form does not
-    fit the LDS; the reference's Optuna space goes to 128, DIN.py:207) falls
-    back, with a warning, to the per-candidate path per cluster instead of raising; its
-    logits match the fp64 oracle (<= 1e-4), and the label is the FIRST
-    occurrence of a positive row that appears twice in its cluster
-    (EvalDataset, DIN.py:27-31)."""
+@pytest.mark.parametrize("d,expect", [(256, "fused"), (16, "per-candidate")])
+def test_rerank_clusters_long_history_fallback_and_duplicate_positive(gpu, d, expect):
+    """A 96-slot history at A = 128, F = 64 (the reference's Optuna space goes
+    to max_history 128, DIN.py:207): fused through the lane kernel's 128-row
+    RG form at d = 256; a model the fused kernels cannot run (emb_dim 16) falls
+    back, with a warning, to the per-candidate path per cluster instead of
+    raising.  Either way the logits match the fp64 oracle (<= 1e-4)
+    and the label is the FIRST occurrence of a positive row that appears twice
+    in its cluster (EvalDataset, DIN.py:27-31)."""
     from newsrecommend_amd.din import DIN
     from newsrecommend_amd.pipeline import rerank_clusters
     from oracle import din_oracle as o
 
     dev = torch.device("cuda")
-    d, L, N = 256, 96, 3000
+    L, N = 96, 3000
     g = torch.Generator(device=dev).manual_seed(5)
     table = torch.randn((N, d), generator=g, device=dev) * 0.5
     torch.manual_seed(2)
@@ -245,9 +246,13 @@ def test_rerank_clusters_fallback_long_history_and_duplicate_positive(gpu):
     hist[1, 50:] = -1
     uc = torch.tensor([0, 2, 0, 2, 1, 0], device=dev)
     last = torch.tensor([int(rows[30]), int(rows[40 + 3]), -1, N + 5, int(rows[0]), int(rows[39])], device=dev)
-    with pytest.warns(UserWarning, match="per-candidate"):
+    if expect == "fused":
         res = rerank_clusters(model, table, hist, uc, off, rows, last, k=5)
-    assert res["path"].startswith("per-candidate") and "history length 96" in res["path"]
+        assert res["path"] == "fused", res["path"]
+    else:
+        with pytest.warns(UserWarning, match="per-candidate"):
+            res = rerank_clusters(model, table, hist, uc, off, rows, last, k=5)
+        assert res["path"].startswith("per-candidate") and "emb_dim 16" in res["path"]
     T = table.cpu().numpy().astype(np.float64)
     p_ref = _params_f64(model, False)
     H, R, ol = hist.cpu().numpy(), rows.cpu().numpy(), off.cpu().tolist()
