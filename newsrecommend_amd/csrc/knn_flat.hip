@@ -846,6 +846,45 @@ __global__ __launch_bounds__(256) void small_select_kernel(const double* __restr
 // rounds of wave argmax in the bitonic sort's order (goodness descending, id
 // ascending).  A block sort per query spends most of its time in barriers.
 constexpr int SW_K = 64;
+// (value, index) argmax over the wave, every lane receiving the winner: larger
+// value first, ties -> lower index (a total order, so any combining tree picks
+// the same winner).  DPP row ops and the CDNA4 permlane swaps instead of
+// __shfl_xor, which moves each 32-bit half through a ds_bpermute round trip (18
+// dependent LDS trips per selection round: 46 us for 4096 queries at k = 32).
+__device__ __forceinline__ void am_take(double& v, int& i, double ov, int oi) {
+  const bool t = ov > v || (ov == v && oi < i);
+  v = t ? ov : v;
+  i = t ? oi : i;
+}
+template <int CTRL>
+__device__ __forceinline__ void am_dpp(double& v, int& i) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xf, 0xf, true);
+  const int oi = __builtin_amdgcn_mov_dpp(i, CTRL, 0xf, 0xf, true);
+  am_take(v, i, __hiloint2double(hi, lo), oi);
+}
+__device__ __forceinline__ void am_swap(double& v, int& i, bool half32) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  const auto rl = half32 ? __builtin_amdgcn_permlane32_swap(lo, lo, false, false)
+                         : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto rh = half32 ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false)
+                         : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  const auto ri = half32 ? __builtin_amdgcn_permlane32_swap(i, i, false, false)
+                         : __builtin_amdgcn_permlane16_swap(i, i, false, false);
+  double a = __hiloint2double((int)rh[0], (int)rl[0]);
+  int ia = (int)ri[0];
+  am_take(a, ia, __hiloint2double((int)rh[1], (int)rl[1]), (int)ri[1]);
+  v = a;
+  i = ia;
+}
+__device__ __forceinline__ void wave_argmax(double& v, int& i) {
+  am_dpp<0xB1>(v, i);   // quad_perm [1,0,3,2]
+  am_dpp<0x4E>(v, i);   // quad_perm [2,3,0,1]
+  am_dpp<0x141>(v, i);  // row_half_mirror
+  am_dpp<0x140>(v, i);  // row_mirror
+  am_swap(v, i, false); // rows 2k <-> 2k+1
+  am_swap(v, i, true);  // halves
+}
 template <int VPL>
 __global__ __launch_bounds__(256) void small_select_wave_kernel(const double* __restrict__ G, int64_t ldg, int64_t q0,
                                                                 int64_t nc, int64_t nq, int64_t nb, int k, int l2,
@@ -875,15 +914,7 @@ __global__ __launch_bounds__(256) void small_select_wave_kernel(const double* __
         bj = j;
       }
     int bi = bj < VPL ? bj * 64 + lane : INT_MAX;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const double ov = __shfl_xor(bv, o, 64);
-      const int oi = __shfl_xor(bi, o, 64);
-      if (ov > bv || (ov == bv && oi < bi)) {
-        bv = ov;
-        bi = oi;
-      }
-    }
+    wave_argmax(bv, bi);
     const bool valid = r < nb && bi != INT_MAX;
     if (valid && lane == (bi & 63)) {
 #pragma unroll
@@ -1192,21 +1223,26 @@ __global__ void ivf_scatter_kernel(const int64_t* __restrict__ probe, int64_t np
   slot_pair[seg_off[l] + atomicAdd(&fill[l], 1)] = (int)i;
 }
 
-// gathered query rows: one wave per slot row (padding rows are zeroed)
+// gathered query rows: one wave per slot row (padding rows are zeroed), a
+// grid-stride loop over the rows the grouping produced (seg_off[nlist]; a grid
+// sized for the upper bound launched ~50K blocks of which most exited: 25 us)
+constexpr int GATHER_BLOCKS = 2048;
 __global__ void ivf_gather_kernel(const uint16_t* __restrict__ qh, int dp, int nprobe,
                                   const int* __restrict__ slot_pair, const int* __restrict__ seg_off, int nlist,
                                   int64_t max_rows, uint16_t* __restrict__ qh_ivf, int64_t npairs,
                                   int* __restrict__ err) {
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (row >= max_rows || row >= seg_off[nlist]) return;
-  int pair = slot_pair[row];
-  if (pair >= 0 && !guard_ok(pair < npairs, err, GUARD_GATHER_PAIR)) pair = -1;
-  const int64_t q = pair >= 0 ? pair / nprobe : 0;
-  for (int j = lane * 4; j < dp; j += 256) {
-    uint2 v = make_uint2(0u, 0u);
-    if (pair >= 0) v = *reinterpret_cast<const uint2*>(qh + q * dp + j);
-    *reinterpret_cast<uint2*>(qh_ivf + row * dp + j) = v;
+  const int64_t nrows = seg_off[nlist] < max_rows ? seg_off[nlist] : max_rows;
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t row = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); row < nrows; row += nw) {
+    int pair = slot_pair[row];
+    if (pair >= 0 && !guard_ok(pair < npairs, err, GUARD_GATHER_PAIR)) pair = -1;
+    const int64_t q = pair >= 0 ? pair / nprobe : 0;
+    for (int j = lane * 4; j < dp; j += 256) {
+      uint2 v = make_uint2(0u, 0u);
+      if (pair >= 0) v = *reinterpret_cast<const uint2*>(qh + q * dp + j);
+      *reinterpret_cast<uint2*>(qh_ivf + row * dp + j) = v;
+    }
   }
 }
 
@@ -1239,7 +1275,7 @@ __device__ __forceinline__ float collect_threshold(double ek, const double* __re
 // screened(x) >= exact(x) - B >= e_k - B =: T (screened units, rounded down;
 // same error bound B_q as the flat certificate), and (e_k, id) is the
 // fallback threshold.  Fewer than k seeds: the query goes to the fallback.
-__global__ __launch_bounds__(256) void ivf_seed_kernel(const int* __restrict__ seed_pos, int R, int k,
+__global__ __launch_bounds__(64) void ivf_seed_kernel(const int* __restrict__ seed_pos, int R, int k,
                                                        const int64_t* __restrict__ pos2id,
                                                        const float* __restrict__ xq, const float* __restrict__ xb,
                                                        int d, int l2, const double* __restrict__ qmeta,
@@ -1255,9 +1291,11 @@ __global__ __launch_bounds__(256) void ivf_seed_kernel(const int* __restrict__ s
   float* qs = reinterpret_cast<float*>(id + P);
   __shared__ int s_valid;
   if (tid == 0) s_valid = 0;
-  for (int i = tid; i < d; i += 256) qs[i] = xq[(int64_t)q * d + i];
+  // one wave per query (a 256-thread block idled 7/8 of its lanes and paid the
+  // sort's barriers across four waves)
+  for (int i = tid; i < d; i += blockDim.x) qs[i] = xq[(int64_t)q * d + i];
   __syncthreads();
-  for (int i = tid; i < P; i += 256) {
+  for (int i = tid; i < P; i += blockDim.x) {
     const int pos = i < R ? seed_pos[(int64_t)q * R + i] : -1;
     if (pos >= 0 && guard_ok(pos < n, err, GUARD_SEED_POS)) {
       const int64_t item = pos2id[pos];
@@ -2042,6 +2080,8 @@ static IvfPlan make_ivf_plan(int64_t nq, int nprobe, int nlist, int64_t max_list
   // phase A: the nA nearest lists per query in chunks of max_list / 128 items (2 lane
   // streams per chunk and query; more streams -> tighter seeds); tau_select
   // takes <= 1024 values per query
+  // (one list per query left too few seeds for some queries: fp64 scans, 3.4 -> 248 ms
+  // per search; profiles/r06_ivf_phaseA_ab.log)
   p.nA = nprobe < 2 ? nprobe : 2;
   // chunks scale with the lists (max_list / 128, in [64, 4096] rows): a
   // corpus shard's short lists (the 8-GPU configs[3]: ~4K rows) otherwise
@@ -2149,7 +2189,8 @@ static int ivf_group(const int64_t* probe, int64_t nq, int nprobe, int nlist, co
                        seg, fill, sp);
     NRK_CHECK_LAUNCH("ivf_scatter_kernel");
   }
-  hipLaunchKernelGGL(ivf_gather_kernel, dim3((unsigned)cdiv(max_rows, 4)), dim3(256), 0, st, qh, dp, nprobe, sp, seg,
+  const int64_t gblk = cdiv(max_rows, 4) < GATHER_BLOCKS ? cdiv(max_rows, 4) : GATHER_BLOCKS;
+  hipLaunchKernelGGL(ivf_gather_kernel, dim3((unsigned)gblk), dim3(256), 0, st, qh, dp, nprobe, sp, seg,
                      nlist, max_rows, qi, npairs, err);
   NRK_CHECK_LAUNCH("ivf_gather_kernel");
   return NRK_OK;
@@ -2252,10 +2293,11 @@ extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe,
     // exact rescore of the wider collect rising; profiles/r04_ivf_phaseA_stride_ab.log)
     NRK_CHECK_LAUNCH("screen_kernel (ivf phase A)");
     const int nva = 2 * p.nA * p.cmaxA;
-    auto tsel = nva <= 64 ? tau_select_kernel<1> : nva <= 256 ? tau_select_kernel<4> : tau_select_kernel<16>;
+    auto tsel = nva <= 64 ? tau_select_kernel<1> : nva <= 256 ? tau_select_kernel<4>
+              : nva <= 512 ? tau_select_kernel<8> : tau_select_kernel<16>;
     hipLaunchKernelGGL(tsel, dim3((unsigned)cdiv(nq, 4)), dim3(256), 0, st, pt, nva, p.R, nq, tau, pa, seed);
     NRK_CHECK_LAUNCH("tau_select_kernel (ivf)");
-    hipLaunchKernelGGL(ivf_seed_kernel, dim3((unsigned)nq), dim3(256), (size_t)host_pow2ceil(p.R) * 16 + (size_t)d * 4,
+    hipLaunchKernelGGL(ivf_seed_kernel, dim3((unsigned)nq), dim3(64), (size_t)host_pow2ceil(p.R) * 16 + (size_t)d * 4,
                        st, seed, p.R, k, pos2id, xq, xb, d, l2, qmeta, stats, p.dp, thr, lbg, lbi, ccnt, p.cap, n, gerr);
     NRK_CHECK_LAUNCH("ivf_seed_kernel");
     NRK_CHECK_LAUNCH("ivf_thr_kernel");

@@ -243,12 +243,13 @@ def test_collect_rounds_beyond_the_slot_budget(gpu, monkeypatch, metric):
 
 @pytest.mark.parametrize("metric", [ko.METRIC_IP, ko.METRIC_L2])
 @pytest.mark.parametrize("nb,nq,d,k", [(300, 4100, 128, 32), (300, 777, 256, 1), (1, 70, 32, 3), (63, 65, 100, 63),
-                                       (4096, 5000, 32, 10), (2048, 300, 300, 200), (500, 129, 64, 700)])
+                                       (4096, 5000, 32, 10), (2048, 300, 300, 200), (500, 129, 64, 700),
+                                       (512, 1000, 256, 64), (257, 33, 36, 17), (64, 16, 4, 64)])
 def test_small_corpus_exact_path(gpu, metric, nb, nq, d, k):
     """nb <= 4096 (the coarse quantizer, k-means assignment, IndexIVFFlat.add):
     the fp64 tile-GEMM path (k = 1: fused arg-best; k > 1: goodness chunks +
-    per-query bitonic select, several chunks at nb = 4096) equals the oracle
-    bit for bit, including k > nb padding, d > 256 and exact duplicates."""
+    per-query select, several chunks at nb = 4096) equals the oracle bit for
+    bit, including k > nb padding, d > 256 and exact duplicates."""
     xq, xb = _mixture(nb, nq, d, seed=nb + nq + d + k)
     if nb > 10:
         xb[nb // 2] = xb[3]
