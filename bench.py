@@ -488,6 +488,18 @@ def bench_e2e(args, rank, world, dev):
     rr = _rerank_roofline(kt.mean_ms("rerank"), kt.mean_ms("rerank_project"), hist[ulo:uhi], d, 128, 32, L,
                           f"rerank:e2e,users={uhi - ulo},C={kr + 1},d={d},gpus={world}", table.element_size(),
                           n_samples=float(cand.shape[0] * cand.shape[1]), proj_rows=cand.numel())
+    # the dominant kernel (the top-200 screen, ~95 % of the step): the local search's
+    # stages with HIP events on the library's launch stream
+    from newsrecommend_amd import _lib
+
+    evs = [_lib.StageEvents() for _ in range(3)]
+    for e in evs:
+        index.local.search_device(profiles, kr, exact_scores=True, id_offset=index.offset, stage_events=e)
+    torch.cuda.synchronize()
+    st = np.array([e.elapsed_ms() for e in evs]).mean(0)
+    nb_local = index.local.ntotal
+    flops = 2.0 * U * nb_local * d
+    achieved = flops / (st[1] * 1e-3) / 1e12
     out = {
         "metric": "end-to-end users/s (retrieve top-200 + DIN re-rank + NDCG@5)", "value": U * args.steps / el,
         "unit": "users/s", "ms_per_step": el / args.steps * 1e3,
@@ -496,6 +508,14 @@ def bench_e2e(args, rank, world, dev):
                    "parallelism": (f"corpus-shard{world} retrieval, RCCL all_to_all of each user slice's lists, "
                                    f"user-shard{world} re-rank") if world > 1 else "single GPU"},
         "stages_ms": {"retrieve": (t2 - t1) / 3 * 1e3, "rerank": (t3 - t2) / 3 * 1e3},
+        "retrieve_stages_ms": {"query_prepare+tau_prepass": float(st[0]), "screen": float(st[1]),
+                               "merge_rescore": float(st[2]), "exact_fallback": float(st[3])},
+        "roofline": {"bound": "mfma", "kernel": _screen_kernel_name(U, nb_local, d, kr, 0),
+                     "achieved": achieved, "peak": BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / BF16_DENSE_TFLOPS,
+                     "traffic": _pmc_traffic(f"e2e:nb={n},d={d},nq={U},k={kr},metric=ip,gpus={world}"),
+                     "algorithmic": f"2*users*nb_local*d = {flops:.4g} flop per launch (the top-{kr} screen, "
+                                    f"{st[1]:.3f} ms HIP events)"},
         "rerank_samples_per_step": int((uhi - ulo) * (kr + 1)),
         "rerank_kernel_ms": kt.mean_ms("rerank"), "rerank_project_ms": kt.mean_ms("rerank_project"),
         "rerank_path": __import__("newsrecommend_amd.pipeline", fromlist=["rerank"]).rerank.path,
@@ -519,9 +539,64 @@ def bench_e2e(args, rank, world, dev):
                 ref = model(table[c].float(), keys.expand(len(c), -1, -1)).view(-1)
                 errs.append(float((logits[u][cand[u] >= 0] - ref).abs().max()))
         out["rerank_vs_per_user_forward_max_abs"] = max(errs)
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = _cpu_e2e(args, profiles, table, hist, gt, model, kr)
     del index, table
     torch.cuda.empty_cache()
     return out
+
+
+def _cpu_torch_din(model, d, A, F):
+    """oracle/din_torch_ref.TorchDIN (the reference's module restated in torch)
+    holding `model`'s weights, eval mode, on the CPU."""
+    from oracle.din_torch_ref import TorchDIN
+
+    m = TorchDIN(d, A, F, 0.0).eval()
+    m.load_state_dict({k: v.detach().float().cpu() for k, v in model.state_dict().items()})
+    return m
+
+
+def _cpu_rerank_user(m, xb, h, cand, chunk=1024):
+    """DIN.py:166-173 for one user on the CPU: model(cand_emb, his.expand(C, -1, -1)),
+    zero rows for padded history slots, candidates in chunks."""
+    keys = torch.where(h[:, None] >= 0, xb[h.clamp_min(0)], 0.0)
+    out = []
+    for c0 in range(0, cand.shape[0], chunk):
+        c = cand[c0:c0 + chunk]
+        out.append(m(xb[c], keys[None].expand(c.shape[0], -1, -1)).view(-1))
+    return torch.cat(out)
+
+
+def _cpu_e2e(args, profiles, table, hist, gt, model, kr):
+    """configs[4] end to end on the host cores over a bounded user sample:
+    faiss-cpu's flat IP top-200 (oracle/cpu_baselines.flat_search) over the FULL
+    corpus, the ground truth appended when missing, the reference's per-user
+    DIN forward (TorchDIN) over the 200-201 candidates and NDCG@5."""
+    from oracle import cpu_baselines as cb
+
+    cores = cpu_cores()
+    torch.set_num_threads(cores)
+    xb = table.float().cpu()
+    q, h, g = profiles.float().cpu(), hist.long().cpu(), gt.long().cpu()
+    m = _cpu_torch_din(model, xb.shape[1], 128, 32)
+
+    def run(n):
+        _, I = cb.flat_search(q[:n], xb, kr, 0)
+        with torch.no_grad():
+            for u in range(n):
+                c = I[u]
+                if not bool((c == g[u]).any()):
+                    c = torch.cat([c, g[u:u + 1]])
+                lg = _cpu_rerank_user(m, xb, h[u], c)
+                top = torch.topk(lg, 5).indices
+                hit = (c[top] == g[u]).double()
+                float((hit / torch.log2(torch.arange(2, 7, dtype=torch.float64))).sum())
+
+    n, dt = _timed_sample(run, q.shape[0], 16, args.cpu_seconds, align=16)
+    return {"value": n / dt, "unit": "users/s", "cores": cores, "kind": "port",
+            "sample": f"{n} of the {q.shape[0]} users: flat IP top-{kr} over the full {xb.shape[0]}x{xb.shape[1]} "
+                      f"corpus (oracle.cpu_baselines.flat_search), GT appended, the reference's per-user DIN "
+                      f"forward (oracle.din_torch_ref, PyTorch-CPU fp32) and NDCG@5, {cores} threads, {dt:.1f} s"}
 
 
 def _rerank_roofline(ms, ms_proj, hist, d, A, F, L, key, es, n_samples, proj_rows):
@@ -642,9 +717,48 @@ def bench_retrieval_flow(args, rank, world, dev):
                n_samples=float(cand_per_user.sum()) + (hi - lo), proj_rows=int(xb.shape[0]) + (hi - lo)).values())},
            "rerank_path": __import__("newsrecommend_amd.pipeline", fromlist=["rerank"]).rerank.path,
            "ndcg_at_5_mean_rank0": float(res["ndcg"].mean()), "loss_mean_rank0": float(res["loss"].mean())}
+    out["roofline"] = dict(out["rerank_roofline"])  # the dominant kernel (the re-rank, ~99 % of the stage)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = _cpu_flow(args, xb, centroids, cluster_off, cluster_rows, profiles, hist, last, model)
     del xb, table, index, centroid_index
     torch.cuda.empty_cache()
     return out
+
+
+def _cpu_flow(args, xb, centroids, cluster_off, cluster_rows, profiles, hist, last, model):
+    """The Retrieval.py -> evaluate() stage on the host cores over a bounded user
+    sample: nearest centroid (flat L2), the whole cluster as candidates with the
+    ground truth appended when missing, the reference's per-user DIN forward
+    (TorchDIN, chunks of 1024 candidates), per-user BCE and NDCG@5."""
+    from oracle import cpu_baselines as cb
+
+    cores = cpu_cores()
+    torch.set_num_threads(cores)
+    x, cen = xb.float().cpu(), centroids.float().cpu()
+    off, rows = cluster_off.cpu(), cluster_rows.long().cpu()
+    q, h, g = profiles.float().cpu(), hist.long().cpu(), last.long().cpu()
+    m = _cpu_torch_din(model, x.shape[1], 128, 32)
+
+    def run(n):
+        _, I = cb.flat_search(q[:n], cen, 1, 1)
+        with torch.no_grad():
+            for u in range(n):
+                cl = int(I[u, 0])
+                c = rows[int(off[cl]):int(off[cl + 1])]
+                lab = (c == g[u]).float()
+                if not bool(lab.any()):
+                    c = torch.cat([c, g[u:u + 1]])
+                    lab = torch.cat([lab, torch.ones(1)])
+                lg = _cpu_rerank_user(m, x, h[u], c)
+                float(torch.nn.functional.binary_cross_entropy_with_logits(lg, lab))
+                top = torch.topk(lg, min(5, lg.shape[0])).indices
+                float((lab[top].double() / torch.log2(torch.arange(2, 2 + top.shape[0], dtype=torch.float64))).sum())
+
+    n, dt = _timed_sample(run, q.shape[0], 4, args.cpu_seconds, align=4)
+    return {"value": n / dt, "unit": "users/s", "cores": cores, "kind": "port",
+            "sample": f"{n} of the {q.shape[0]} users: nearest of {cen.shape[0]} centroids, the whole cluster "
+                      f"(+ GT) through the reference's per-user DIN forward (oracle.din_torch_ref, PyTorch-CPU "
+                      f"fp32, 1024-candidate chunks), BCE and NDCG@5, {cores} threads, {dt:.1f} s"}
 
 
 # ------------------------------------------------------------- embedding --
@@ -685,16 +799,20 @@ def bench_embed(args, rank, world, dev):
             model.embed(x)
         barrier(world)
         reps = 5 if n < 1_000_000 else 3
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
+        e0.record()  # nrk_embed launches on torch's current stream
         for _ in range(reps):
             y = model.embed(x)
+        e1.record()
         barrier(world)
         el = max_over_ranks(time.perf_counter() - t0, world, dev) / reps
+        ev_ms = e0.elapsed_time(e1) / reps
         rec = {"value": n * world / el, "ms_per_pass": el * 1e3, "rows_per_gpu": n,
                "achieved_tflops": flop_row * n / el / 1e12,
                "frac_fp32_mfma": flop_row * n / el / 1e12 / FP32_MFMA_TFLOPS,
                "bf16_mfma_tflops": mfma_row * n / el / 1e12,
-               "frac_bf16_mfma": mfma_row * n / el / 1e12 / BF16_DENSE_TFLOPS}
+               "frac_bf16_mfma": mfma_row * n / el / 1e12 / BF16_DENSE_TFLOPS, "kernel_ms_hip_events": ev_ms}
         if rank == 0 and name == "reference_364047":
             # parity on a row sample: the reference's eval forward (fc as nn.Sequential, BN unfolded), fp32
             with torch.no_grad():
@@ -704,6 +822,17 @@ def bench_embed(args, rank, world, dev):
         del x, y
         torch.cuda.empty_cache()
     out["value"] = out["corpus_10m"]["value"]
+    c10 = out["corpus_10m"]
+    tf_bf16 = mfma_row * c10["rows_per_gpu"] / (c10["kernel_ms_hip_events"] * 1e-3) / 1e12
+    tf_f32 = flop_row * c10["rows_per_gpu"] / (c10["kernel_ms_hip_events"] * 1e-3) / 1e12
+    out["roofline"] = {"bound": "mfma", "kernel": "embed_mlp_kernel (nrk_embed), 10M rows",
+                       "achieved": tf_bf16, "peak": BF16_DENSE_TFLOPS, "unit": "TFLOP/s",
+                       "frac": tf_bf16 / BF16_DENSE_TFLOPS, "traffic": None,
+                       "fp32_equivalent": {"achieved": tf_f32, "peak": FP32_MFMA_TFLOPS,
+                                           "frac": tf_f32 / FP32_MFMA_TFLOPS},
+                       "algorithmic": f"{mfma_row:.0f} bf16 MFMA flop per row issued (fp32-exact products as six "
+                                      f"3-plane bf16 products; {flop_row:.0f} fp32 flop per row) x "
+                                      f"{c10['rows_per_gpu']} rows, {c10['kernel_ms_hip_events']:.3f} ms (HIP events)"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cores = cpu_cores()
         torch.set_num_threads(cores)
@@ -855,6 +984,9 @@ def bench_din(args, rank, world, dev):
                          "frac": bwd_gbs / HBM_GBS, "traffic": _pmc_traffic(f"din_bwd:{din_key}") if fused else None,
                          "algorithmic": f"{bwd_bytes // B} B/sample x {B} samples"},
     }
+    # the dominant launch of the step: the attention backward (8-wave kernel + slab reduction)
+    out["roofline"] = dict(out["roofline_bwd"], kernel=("din_bwd_deep8g_kernel<128, 64> + din_bwd_reduce_params_kernel"
+                                                        if fused else "attention backward + reduction"))
     if fused and world == 1 and args.din_sweep:
         out["batch_sweep"] = {str(bs): _din_rate(table, hist, tgt, lab, d, A, F, bs, dev) for bs in (16384, 65536)}
     if fused and world == 1 and args.din_d256:
@@ -1032,7 +1164,7 @@ def main():
         r = bench_din(args, rank, world, dev)
         if args.workload == "din":
             rec.update({"metric": r["metric"], "value": r["value"], "unit": r["unit"], "ms_per_step": r["ms_per_step"],
-                        "config": r["config"], "scaling": "weak", "roofline": r["roofline_fwd"]})
+                        "config": r["config"], "scaling": "weak", "roofline": r["roofline"]})
             if "cpu_baseline" in r:
                 rec["cpu_baseline"] = r["cpu_baseline"]
         rec["din"] = r
@@ -1141,8 +1273,6 @@ def isolated_main(args):
                 for k in ("config", "roofline", "cpu_baseline"):
                     if k in r:
                         rec[k] = r[k]
-                if name == "din":
-                    rec["roofline"] = r["roofline_fwd"]
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.barrier()
