@@ -284,3 +284,45 @@ def test_ivf_configs3_full_size_repeated_searches(gpu):
                                  ivf._assign.cpu().numpy(), nprobe, k, ko.METRIC_L2)
     np.testing.assert_array_equal(I0[sample].cpu().numpy(), Io)
     np.testing.assert_array_equal(D0[sample].cpu().numpy(), Do)
+
+
+@pytest.mark.parametrize("metric", [ko.METRIC_IP, ko.METRIC_L2])
+@pytest.mark.parametrize("nq", [1, 3, 257])
+def test_ivf_odd_query_batches(gpu, metric, nq):
+    """Batches that fill no query tile (1, 3) or spill one row into the next
+    (257): the grouping pads every list segment to the tile, the collect's
+    waves skip the padding half-tiles; results equal the oracle's."""
+    xq, xb = _mixture(25_000, nq, 128, seed=300 + nq, centers=32)
+    ivf = _ivf(xb, 24, metric)
+    ivf.nprobe = 6
+    D, I = ivf.search(xq, 5)
+    Do, Io, _, _ = io.ivf_search(xq, xb, ivf.quantizer._xb[:24].cpu().numpy(), ivf._assign.cpu().numpy(), 6, 5,
+                                 metric)
+    np.testing.assert_array_equal(I, Io)
+    np.testing.assert_array_equal(D, Do)
+    ivf.check_guards()
+
+
+def test_ivf_incremental_add_continues_ids(gpu):
+    """faiss IndexIVF.add twice: the second batch's ids continue from ntotal and
+    the inverted lists are rebuilt over both (same result as one add)."""
+    xq, xb = _mixture(30_000, 200, 64, seed=41, centers=24)
+    one = _ivf(xb, 16, ko.METRIC_L2)
+    from newsrecommend_amd import faiss as nf
+
+    q = nf.IndexFlatL2(64)
+    two = nf.IndexIVFFlat(q, 64, 16, ko.METRIC_L2)
+    two.cp.niter = 4
+    two.train(xb)
+    two.add(xb[:12_345])
+    two.add(xb[12_345:])
+    assert two.ntotal == one.ntotal == 30_000
+    for ivf in (one, two):
+        ivf.nprobe = 4
+    D1, I1 = one.search(xq, 8)
+    D2, I2 = two.search(xq, 8)
+    np.testing.assert_array_equal(I1, I2)
+    np.testing.assert_array_equal(D1, D2)
+    Do, Io, _, _ = io.ivf_search(xq, xb, two.quantizer._xb[:16].cpu().numpy(), two._assign.cpu().numpy(), 4, 8,
+                                 ko.METRIC_L2)
+    np.testing.assert_array_equal(I2, Io)
