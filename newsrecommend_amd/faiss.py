@@ -514,8 +514,9 @@ class IndexIVFFlat(_FallbackCounters):
     def search(self, x, k):
         xt, was_numpy = self.flat._as_input(x)
         D, I = self.search_device(xt, k)
-        if was_numpy:
-            return D.cpu().numpy(), I.cpu().numpy()
+        if was_numpy:  # the copy to the host syncs anyway: check the index guards with it
+            D, I = D.cpu().numpy(), I.cpu().numpy()
+            self.check_guards()
         return D, I
 
 
