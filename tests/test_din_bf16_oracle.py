@@ -22,8 +22,10 @@ Oracles:
 Tolerances (written here and in DESIGN.md "Parity"):
   train, emulated (each of 2 steps checked from the kernel's state before
       it): loss 2e-5 abs; each clipped gradient tensor max-abs error
-      <= 2e-3 * its max |g| + 1e-7; parameters after the clip + Adam step
-      5e-5 abs, except entries whose new first moment lies within the
+      <= 2e-3 * its max |g| + 1e-7 (3e-3 for W1 at d = 128 on the padded
+      batches: its key half takes dz as plain bf16 in the 8-wave dW1k MFMA);
+      parameters after
+      the clip + Adam step 5e-5 abs, except entries whose new first moment lies within the
       gradient error of 0 (Adam's sign-normalised step: bound 2 lr);
       BN running stats 1e-5 abs.
   train, reference: loss 2e-3 abs.
@@ -68,11 +70,12 @@ def _bn_inputs(cache, pooled, q):
     return [np.concatenate([q, pooled], 1), np.maximum(cache["pre.relu1"], 0), np.maximum(cache["pre.relu2"], 0)]
 
 
-@pytest.mark.parametrize("d,L,B,steps,A,F", [(128, 50, 512, 2, 128, 32), (256, 64, 64, 2, 128, 32),
-                                             (256, 64, 4096, 1, 128, 32), (128, 50, 512, 1, 64, 128),
-                                             (256, 128, 256, 1, 32, 128), (256, 96, 256, 1, 128, 96),
-                                             (256, 100, 512, 2, 128, 32), (256, 65, 320, 1, 64, 64)])
-def test_fused_train_step_fast_path_vs_oracle_c3_shape(gpu, d, L, B, steps, A, F):
+@pytest.mark.parametrize("d,L,B,steps,A,F,pad", [(128, 50, 512, 2, 128, 32, False), (256, 64, 64, 2, 128, 32, False),
+                                                 (256, 64, 4096, 1, 128, 32, False), (128, 50, 512, 1, 64, 128, False),
+                                                 (256, 128, 256, 1, 32, 128, False), (256, 96, 256, 1, 128, 96, False),
+                                                 (256, 100, 512, 2, 128, 32, False), (256, 65, 320, 1, 64, 64, False),
+                                                 (128, 50, 512, 2, 128, 32, True), (256, 100, 256, 1, 128, 32, True)])
+def test_fused_train_step_fast_path_vs_oracle_c3_shape(gpu, d, L, B, steps, A, F, pad):
     """(128, 50, 512): configs[2]'s shape.  (256, 64, 64) and (256, 64, 4096):
     the reference's own training shape (DIN.py:16 EMBED_DIM from the 256-d
     corpus of embedding_generate.py:14; main(): A 128, F 32, max_history 64,
@@ -83,7 +86,9 @@ def test_fused_train_step_fast_path_vs_oracle_c3_shape(gpu, d, L, B, steps, A, F
     longer than 64 the column-split backward in two half-samples per sample
     (din_cdot_kernel's softmax term first); (256, 100, 512): a ragged second
     half (36 rows) over two steps; (256, 65, 320): a one-row second half and a
-    batch that is not a multiple of the workgroup count."""
+    batch that is not a multiple of the workgroup count.  pad: every 7th sample
+    with no clicked item at all (softmax over L padding slots, pooled = 0), the
+    next with one, the next with all but the first L - 1 slots empty."""
     from newsrecommend_amd.data import synthetic_click_rows
     from newsrecommend_amd.din import DIN, FusedTrainStep
     from oracle import din_oracle as o
@@ -94,6 +99,10 @@ def test_fused_train_step_fast_path_vs_oracle_c3_shape(gpu, d, L, B, steps, A, F
     g = torch.Generator(device=dev).manual_seed(21)
     table = (torch.randn((N, d), generator=g, device=dev) * 0.5).to(torch.bfloat16)
     hist, tgt, lab = synthetic_click_rows(max(4 * B, 2048), N, L, seed=9, device=dev)
+    if pad:
+        hist[0::7] = -1
+        hist[1::7, 1:] = -1
+        hist[2::7, L - 1:] = -1
     torch.manual_seed(3)
     model = DIN(d, A, F, 0.0).to(dev)
     fused = FusedTrainStep(model, table, hist, tgt, lab, B, lr=lr, weight_decay=wd, clip=1.0, graph=False)
@@ -143,7 +152,11 @@ def test_fused_train_step_fast_path_vs_oracle_c3_shape(gpu, d, L, B, steps, A, F
             g_k[n] = prm.grad.detach().cpu().numpy().astype(np.float64)
             err = np.abs(g_k[n] - ref).max()
             print(f"step {s} grad {n}: max abs err {err:.3g} (rel {err / max(np.abs(ref).max(), 1e-30):.3g})")
-            assert err <= 2e-3 * np.abs(ref).max() + 1e-7, (s, n, err, np.abs(ref).max())
+            # dW1's key half on the d = 128 path: dz enters its MFMA as plain bf16
+            # (1.7-1.9e-3 of max |g| on the unpadded batches, up to 2.4e-3 on the
+            # padded ones, whose smaller max |g| the same absolute errors are measured against)
+            rel = 3e-3 if (pad and n == "attn.attn.0.weight" and d < 256) else 2e-3
+            assert err <= rel * np.abs(ref).max() + 1e-7, (s, n, err, np.abs(ref).max())
         sd = model.state_dict()
         for bn, x in zip(("fc.0", "fc.4", "fc.8"), _bn_inputs(cache, pooled, q)):
             n_ = x.shape[0]  # torch BatchNorm1d: momentum 0.1, unbiased running variance
