@@ -813,6 +813,52 @@ __global__ __launch_bounds__(256) void small_scores_kernel(const float* __restri
   }
 }
 
+// Few queries (nq < SM_T: the reference's one-profile-at-a-time loop,
+// Retrieval.py:28-34): one thread per (query, item) instead of 64 x 64 tiles,
+// so nb items spread over nb threads rather than over nb / 64 tile workgroups
+// (small_best_kernel spent 188 us on one query over 300 centroids in one
+// workgroup).  The arithmetic is small_tile's: fp64 over the dims in order,
+// (q - x)^2 or q x fma'd into one accumulator, so the goodness is bit-identical.
+template <bool L2>
+__global__ __launch_bounds__(256) void small_rows_kernel(const float* __restrict__ xq, int64_t q0, int64_t nc,
+                                                         const float* __restrict__ xb, int64_t nb, int d,
+                                                         double* __restrict__ G, int64_t ldg) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= nc * nb) return;
+  const int64_t ql = e / nb, j = e - ql * nb;
+  const float* q = xq + (q0 + ql) * d;
+  const float* x = xb + j * d;
+  double acc = 0.0;
+  int c = 0;
+  if ((d & 3) == 0) {
+    for (; c < d; c += 4) {
+      const float4 qv = *reinterpret_cast<const float4*>(q + c);
+      const float4 xv = *reinterpret_cast<const float4*>(x + c);
+      const double qd[4] = {(double)qv.x, (double)qv.y, (double)qv.z, (double)qv.w};
+      const double xd[4] = {(double)xv.x, (double)xv.y, (double)xv.z, (double)xv.w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (L2) {
+          const double t = qd[u] - xd[u];
+          acc = fma(t, t, acc);
+        } else {
+          acc = fma(qd[u], xd[u], acc);
+        }
+      }
+    }
+  }
+  for (; c < d; ++c) {
+    const double qd = q[c], xd = x[c];
+    if (L2) {
+      const double t = qd - xd;
+      acc = fma(t, t, acc);
+    } else {
+      acc = fma(qd, xd, acc);
+    }
+  }
+  G[ql * ldg + j] = L2 ? -acc : acc;
+}
+
 // k > 1, pass 2: one workgroup per query of the chunk sorts its nb goodness values.
 __global__ __launch_bounds__(256) void small_select_kernel(const double* __restrict__ G, int64_t ldg, int64_t q0,
                                                            int64_t nq, int64_t nb, int k, int l2, int P,
@@ -1554,7 +1600,8 @@ static FlatPlan make_plan(int64_t nq, int64_t nb, int d, int k) {
     p.small_chunk = want < SM_T ? SM_T : want / SM_T * SM_T;
     if (p.small_chunk > (int64_t)align_up((size_t)nq, SM_T)) p.small_chunk = align_up((size_t)nq, SM_T);
     p.small_P = (int)P;
-    p.total = k == 1 ? 256 : align_up((size_t)p.small_chunk * p.small_ld * 8, 256);
+    // (k = 1 with a full query tile: small_best_kernel, no goodness buffer)
+    p.total = k == 1 && nq >= SM_T ? 256 : align_up((size_t)p.small_chunk * p.small_ld * 8, 256);
     return p;
   }
   p.exact_only = nb < EXACT_BELOW || d > 256 || k > 256 || nb >= (1ll << 31) || nq == 0;
@@ -1741,7 +1788,7 @@ using namespace nrk;
 
 static int small_launch(const FlatPlan& p, const float* xq, int64_t nq, const float* xb, int64_t nb, int d, int k,
                         int l2, float* D, int64_t* I, double* S, int64_t id_offset, void* ws, hipStream_t st) {
-  if (k == 1) {
+  if (k == 1 && nq >= SM_T) {
     const unsigned grid = (unsigned)cdiv(nq, SM_T);
     if (l2)
       hipLaunchKernelGGL(small_best_kernel<true>, dim3(grid), dim3(256), 0, st, xq, nq, xb, nb, d, D, I, S, id_offset);
@@ -1755,7 +1802,14 @@ static int small_launch(const FlatPlan& p, const float* xq, int64_t nq, const fl
   const size_t smem = (size_t)p.small_P * 16;
   for (int64_t q0 = 0; q0 < nq; q0 += p.small_chunk) {
     const int64_t nc = nq - q0 < p.small_chunk ? nq - q0 : p.small_chunk;
-    if (nb > 0) {
+    if (nb > 0 && nc < SM_T) {  // few queries: a thread per (query, item)
+      const unsigned grid = (unsigned)cdiv(nc * nb, (int64_t)256);
+      if (l2)
+        hipLaunchKernelGGL(small_rows_kernel<true>, dim3(grid), dim3(256), 0, st, xq, q0, nc, xb, nb, d, G, p.small_ld);
+      else
+        hipLaunchKernelGGL(small_rows_kernel<false>, dim3(grid), dim3(256), 0, st, xq, q0, nc, xb, nb, d, G, p.small_ld);
+      NRK_CHECK_LAUNCH("small_rows_kernel");
+    } else if (nb > 0) {
       const dim3 grid((unsigned)cdiv(nb, SM_T), (unsigned)cdiv(nc, SM_T));
       if (l2)
         hipLaunchKernelGGL(small_scores_kernel<true>, grid, dim3(256), 0, st, xq, q0, nq, xb, nb, d, G, p.small_ld);

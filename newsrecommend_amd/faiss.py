@@ -152,18 +152,9 @@ class IndexFlat(_FallbackCounters):
             self._ws = torch.zeros(max(nbytes, 1), dtype=torch.uint8, device=self.device)
         return self._ws
 
-    def search_device(self, xq: torch.Tensor, k: int, exact_scores: bool = False, id_offset: int = 0,
-                      stage_events=None):
-        """Device-in, device-out search: returns (D f32, I int64[, S f64]) on the GPU."""
-        k = int(k)
-        if k <= 0:
-            raise ValueError("k must be positive")
-        xq = self._as_query(xq)
-        nq = xq.shape[0]
+    def _launch(self, xq: torch.Tensor, nq: int, k: int, D, I, S, id_offset: int = 0, stage_events=None):
+        """nrk_knn_flat over device buffers (xq (nq, d) f32, D / I / S (nq, k)) on the device's stream."""
         L = _lib.load()
-        D = torch.empty((nq, k), dtype=torch.float32, device=self.device)
-        I = torch.empty((nq, k), dtype=torch.int64, device=self.device)
-        S = torch.empty((nq, k), dtype=torch.float64, device=self.device) if exact_scores else None
         if self.fallback_counts is None:
             self.fallback_counts = torch.zeros(2, dtype=torch.int32, device=self.device)
         with torch.cuda.device(self.device):
@@ -177,15 +168,68 @@ class IndexFlat(_FallbackCounters):
                 _lib.ptr(D), _lib.ptr(I), _lib.ptr(S), int(id_offset), _lib.ptr(self.fallback_counts), _lib.ptr(ws),
                 ws.numel(), stage_events.ev if stage_events is not None else None, _lib.stream(self.device)),
                 "knn_flat")
+
+    def search_device(self, xq: torch.Tensor, k: int, exact_scores: bool = False, id_offset: int = 0,
+                      stage_events=None):
+        """Device-in, device-out search: returns (D f32, I int64[, S f64]) on the GPU."""
+        k = int(k)
+        if k <= 0:
+            raise ValueError("k must be positive")
+        xq = self._as_query(xq)
+        nq = xq.shape[0]
+        D = torch.empty((nq, k), dtype=torch.float32, device=self.device)
+        I = torch.empty((nq, k), dtype=torch.int64, device=self.device)
+        S = torch.empty((nq, k), dtype=torch.float64, device=self.device) if exact_scores else None
+        self._launch(xq, nq, k, D, I, S, id_offset, stage_events)
         return (D, I, S) if exact_scores else (D, I)
 
+    def _host_buffers(self, nq: int, k: int):
+        """Persistent staging for numpy searches: pinned host query / result
+        buffers and their device twins, grown to the largest call."""
+        hb = getattr(self, "_hb", None)
+        if hb is None or hb["nq"] < nq or hb["nqk"] < nq * k:
+            cq = max(nq, hb["nq"] if hb else 0)
+            ck = max(nq * k, hb["nqk"] if hb else 0)
+            dev = self.device
+            hb = {"nq": cq, "nqk": ck,
+                  "hq": torch.empty((cq, self.d), dtype=torch.float32).pin_memory(),
+                  "hD": torch.empty(ck, dtype=torch.float32).pin_memory(),
+                  "hI": torch.empty(ck, dtype=torch.int64).pin_memory(),
+                  "dq": torch.empty((cq, self.d), dtype=torch.float32, device=dev),
+                  "dD": torch.empty(ck, dtype=torch.float32, device=dev),
+                  "dI": torch.empty(ck, dtype=torch.int64, device=dev)}
+            self._hb = hb
+        return hb
+
     def search(self, x, k):
-        """faiss Index.search(x, k) -> (D, I)."""
-        xt, was_numpy = self._as_input(x)
-        D, I = self.search_device(xt, k)
-        if was_numpy:
-            return D.cpu().numpy(), I.cpu().numpy()
-        return D, I
+        """faiss Index.search(x, k) -> (D, I).  numpy in, numpy out: the queries
+        go through a pinned staging buffer (one async copy each way, one stream
+        sync), so the reference's one-profile-at-a-time loop (Retrieval.py:28-34)
+        pays a few tens of microseconds per call, not a synchronous copy each way."""
+        if isinstance(x, torch.Tensor):
+            xt, _ = self._as_input(x)
+            return self.search_device(xt, k)
+        k = int(k)
+        if k <= 0:
+            raise ValueError("k must be positive")
+        a = np.ascontiguousarray(x, dtype=np.float32)
+        if a.ndim != 2 or a.shape[1] != self.d:
+            raise AssertionError(f"expected (n, {self.d}) input, got {a.shape}")
+        nq = a.shape[0]
+        if nq == 0:
+            return np.empty((0, k), np.float32), np.empty((0, k), np.int64)
+        hb = self._host_buffers(nq, k)
+        hb["hq"][:nq].numpy()[...] = a
+        with torch.cuda.device(self.device):
+            st = torch.cuda.current_stream(self.device)
+            dq = hb["dq"][:nq]
+            dq.copy_(hb["hq"][:nq], non_blocking=True)
+            D, I = hb["dD"][:nq * k].view(nq, k), hb["dI"][:nq * k].view(nq, k)
+            self._launch(dq, nq, k, D, I, None)
+            hb["hD"][:nq * k].copy_(hb["dD"][:nq * k], non_blocking=True)
+            hb["hI"][:nq * k].copy_(hb["dI"][:nq * k], non_blocking=True)
+            st.synchronize()
+        return hb["hD"][:nq * k].numpy().reshape(nq, k).copy(), hb["hI"][:nq * k].numpy().reshape(nq, k).copy()
 
 
 class IndexFlatIP(IndexFlat):

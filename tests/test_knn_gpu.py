@@ -244,12 +244,15 @@ def test_collect_rounds_beyond_the_slot_budget(gpu, monkeypatch, metric):
 @pytest.mark.parametrize("metric", [ko.METRIC_IP, ko.METRIC_L2])
 @pytest.mark.parametrize("nb,nq,d,k", [(300, 4100, 128, 32), (300, 777, 256, 1), (1, 70, 32, 3), (63, 65, 100, 63),
                                        (4096, 5000, 32, 10), (2048, 300, 300, 200), (500, 129, 64, 700),
-                                       (512, 1000, 256, 64), (257, 33, 36, 17), (64, 16, 4, 64)])
+                                       (512, 1000, 256, 64), (257, 33, 36, 17), (64, 16, 4, 64),
+                                       (300, 1, 256, 1), (3000, 63, 100, 1), (1000, 5, 99, 40)])
 def test_small_corpus_exact_path(gpu, metric, nb, nq, d, k):
     """nb <= 4096 (the coarse quantizer, k-means assignment, IndexIVFFlat.add):
     the fp64 tile-GEMM path (k = 1: fused arg-best; k > 1: goodness chunks +
     per-query select, several chunks at nb = 4096) equals the oracle bit for
-    bit, including k > nb padding, d > 256 and exact duplicates."""
+    bit, including k > nb padding, d > 256 and exact duplicates.  Fewer than 64
+    queries take a thread per (query, item) (small_rows_kernel, also at k = 1
+    and for d not a multiple of 4)."""
     xq, xb = _mixture(nb, nq, d, seed=nb + nq + d + k)
     if nb > 10:
         xb[nb // 2] = xb[3]
@@ -311,3 +314,21 @@ def test_search_device_input_checks(gpu):
     assert torch.equal(I1, I2)
     with pytest.raises(AssertionError):
         ivf.search_device(q, 5, probe=probe[:, :2])
+
+
+def test_numpy_search_one_query_at_a_time(gpu):
+    """The reference's per-user loop (Retrieval.py:28-34: centroid_index.search
+    (profile, 1) for each profile): the numpy path (pinned staging, one sync)
+    returns fresh arrays equal to one batched device search, call after call."""
+    from newsrecommend_amd import faiss as nf
+
+    xq, xb = _mixture(300, 40, 256, seed=5)
+    idx = nf.IndexFlatL2(256)
+    idx.add(xb)
+    Db, Ib = idx.search_device(torch.from_numpy(xq).cuda(), 1)
+    got = [idx.search(xq[i:i + 1], 1) for i in range(len(xq))]
+    np.testing.assert_array_equal(np.concatenate([g[1] for g in got]), Ib.cpu().numpy())
+    np.testing.assert_array_equal(np.concatenate([g[0] for g in got]), Db.cpu().numpy())
+    D2, I2 = idx.search(xq, 3)  # a larger call grows the staging; earlier results stay intact
+    np.testing.assert_array_equal(I2[:, :1], Ib.cpu().numpy())
+    np.testing.assert_array_equal(np.concatenate([g[1] for g in got]), Ib.cpu().numpy())
