@@ -20,6 +20,8 @@ for i in range(2000):
     _, I = idx.search(prof[i:i + 1], 1)
 dt = (time.perf_counter() - t) / 2000
 print(f"single-query search (300 x 256, k = 1): {dt * 1e6:.1f} us per call")
+idx.search(prof, 1)  # grows the pinned staging once
 t = time.perf_counter()
-_, Ib = idx.search(prof, 1)
-print(f"batched 2000 queries: {(time.perf_counter() - t) * 1e3:.2f} ms")
+for _ in range(20):
+    _, Ib = idx.search(prof, 1)
+print(f"batched 2000 queries: {(time.perf_counter() - t) / 20 * 1e3:.3f} ms per call")
