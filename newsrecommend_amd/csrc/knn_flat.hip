@@ -738,10 +738,12 @@ template <bool L2>
 __global__ __launch_bounds__(256) void small_best_kernel(const float* __restrict__ xq, int64_t nq,
                                                          const float* __restrict__ xb, int64_t nb, int d,
                                                          float* __restrict__ D, int64_t* __restrict__ I,
-                                                         double* __restrict__ S, int64_t id_offset) {
+                                                         double* __restrict__ S, int64_t id_offset,
+                                                         int32_t* __restrict__ nfb) {
   __shared__ __attribute__((aligned(16))) float Qs[SM_DC * SM_LD];
   __shared__ __attribute__((aligned(16))) float Xs[SM_DC * SM_LD];
   const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  if (nfb && blockIdx.x == 0 && tid < 2) nfb[tid] = 0;  // n_fallback: the exact path answers every query
   const int64_t q0 = (int64_t)blockIdx.x * SM_T;
   double bg[4];
   int64_t bi[4];
@@ -863,10 +865,12 @@ __global__ __launch_bounds__(256) void small_rows_kernel(const float* __restrict
 __global__ __launch_bounds__(256) void small_select_kernel(const double* __restrict__ G, int64_t ldg, int64_t q0,
                                                            int64_t nq, int64_t nb, int k, int l2, int P,
                                                            float* __restrict__ D, int64_t* __restrict__ I,
-                                                           double* __restrict__ S, int64_t id_offset) {
+                                                           double* __restrict__ S, int64_t id_offset,
+                                                           int32_t* __restrict__ nfb) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* g = reinterpret_cast<double*>(smem);
   int64_t* id = reinterpret_cast<int64_t*>(g + P);
+  if (nfb && blockIdx.x == 0 && threadIdx.x < 2) nfb[threadIdx.x] = 0;
   const int64_t qi = q0 + blockIdx.x;
   if (qi >= nq) return;
   const double* row = G + (int64_t)blockIdx.x * ldg;
@@ -898,7 +902,9 @@ constexpr int SW_K = 64;
 // __shfl_xor, which moves each 32-bit half through a ds_bpermute round trip (18
 // dependent LDS trips per selection round: 46 us for 4096 queries at k = 32).
 __device__ __forceinline__ void am_take(double& v, int& i, double ov, int oi) {
-  const bool t = ov > v || (ov == v && oi < i);
+  // bitwise | and & (no short circuit): the compiler otherwise branches on exec
+  // masks at every step (two s_cbranch per step, ~39 us for 4096 queries at k = 32)
+  const bool t = (ov > v) | ((ov == v) & (oi < i));
   v = t ? ov : v;
   i = t ? oi : i;
 }
@@ -935,8 +941,10 @@ template <int VPL>
 __global__ __launch_bounds__(256) void small_select_wave_kernel(const double* __restrict__ G, int64_t ldg, int64_t q0,
                                                                 int64_t nc, int64_t nq, int64_t nb, int k, int l2,
                                                                 float* __restrict__ D, int64_t* __restrict__ I,
-                                                                double* __restrict__ S, int64_t id_offset) {
+                                                                double* __restrict__ S, int64_t id_offset,
+                                                                int32_t* __restrict__ nfb) {
   const int lane = threadIdx.x & 63;
+  if (nfb && blockIdx.x == 0 && threadIdx.x < 2) nfb[threadIdx.x] = 0;
   const int64_t ql = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t qi = q0 + ql;
   if (ql >= nc || qi >= nq) return;
@@ -955,7 +963,7 @@ __global__ __launch_bounds__(256) void small_select_wave_kernel(const double* __
     int bj = VPL;
 #pragma unroll
     for (int j = 0; j < VPL; ++j)
-      if ((int64_t)j * 64 + lane < nb && (bj == VPL || v[j] > bv)) {
+      if (((int64_t)j * 64 + lane < nb) & ((bj == VPL) | (v[j] > bv))) {
         bv = v[j];
         bj = j;
       }
@@ -1787,14 +1795,16 @@ using namespace nrk;
 
 
 static int small_launch(const FlatPlan& p, const float* xq, int64_t nq, const float* xb, int64_t nb, int d, int k,
-                        int l2, float* D, int64_t* I, double* S, int64_t id_offset, void* ws, hipStream_t st) {
+                        int l2, float* D, int64_t* I, double* S, int64_t id_offset, void* ws, hipStream_t st,
+                        int32_t* nfb) {
   if (k == 1 && nq >= SM_T) {
     const unsigned grid = (unsigned)cdiv(nq, SM_T);
     if (l2)
-      hipLaunchKernelGGL(small_best_kernel<true>, dim3(grid), dim3(256), 0, st, xq, nq, xb, nb, d, D, I, S, id_offset);
+      hipLaunchKernelGGL(small_best_kernel<true>, dim3(grid), dim3(256), 0, st, xq, nq, xb, nb, d, D, I, S, id_offset,
+                         nfb);
     else
       hipLaunchKernelGGL(small_best_kernel<false>, dim3(grid), dim3(256), 0, st, xq, nq, xb, nb, d, D, I, S,
-                         id_offset);
+                         id_offset, nfb);
     NRK_CHECK_LAUNCH("small_best_kernel");
     return NRK_OK;
   }
@@ -1821,17 +1831,17 @@ static int small_launch(const FlatPlan& p, const float* xq, int64_t nq, const fl
       const dim3 g4((unsigned)cdiv(nc, (int64_t)4));
       if (nb <= 256)
         hipLaunchKernelGGL(small_select_wave_kernel<4>, g4, dim3(256), 0, st, G, p.small_ld, q0, nc, nq, nb, k, l2, D,
-                           I, S, id_offset);
+                           I, S, id_offset, nfb);
       else if (nb <= 512)
         hipLaunchKernelGGL(small_select_wave_kernel<8>, g4, dim3(256), 0, st, G, p.small_ld, q0, nc, nq, nb, k, l2, D,
-                           I, S, id_offset);
+                           I, S, id_offset, nfb);
       else
         hipLaunchKernelGGL(small_select_wave_kernel<16>, g4, dim3(256), 0, st, G, p.small_ld, q0, nc, nq, nb, k, l2, D,
-                           I, S, id_offset);
+                           I, S, id_offset, nfb);
       NRK_CHECK_LAUNCH("small_select_wave_kernel");
     } else {
       hipLaunchKernelGGL(small_select_kernel, dim3((unsigned)nc), dim3(256), smem, st, G, p.small_ld, q0, nq, nb, k,
-                         l2, p.small_P, D, I, S, id_offset);
+                         l2, p.small_P, D, I, S, id_offset, nfb);
       NRK_CHECK_LAUNCH("small_select_kernel");
     }
   }
@@ -1943,8 +1953,9 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
   int* fbc = reinterpret_cast<int*>(w + p.off_fbc);
   // the screened path zeroes its counters in query_prepare_kernel and publishes
   // them from exact_topk_kernel; the other paths use memsets
+  // (the small path zeroes n_fallback in its kernels and uses no counters: no memsets)
   const bool fused_counts = nq > 0 && !p.small && !p.exact_only;
-  if (!fused_counts) {
+  if (!fused_counts && !p.small) {
     if (hipMemsetAsync(fbc, 0, 16, st) != hipSuccess) return fail(NRK_ELAUNCH, "knn_flat: memset failed");
     if (n_fallback && hipMemsetAsync(n_fallback, 0, 8, st) != hipSuccess)
       return fail(NRK_ELAUNCH, "knn_flat: memset failed");
@@ -1952,7 +1963,7 @@ extern "C" int nrk_knn_flat(const float* xq, int64_t nq, const float* xb, const 
   if (nq == 0) return NRK_OK;
   NRK_CHECK_ARG(xq && D && I && (xb || nb == 0), "knn_flat: null pointer");
   const int l2 = metric == NRK_METRIC_L2;
-  if (p.small) return small_launch(p, xq, nq, xb, nb, d, k, l2, D, I, S, id_offset, ws, st);
+  if (p.small) return small_launch(p, xq, nq, xb, nb, d, k, l2, D, I, S, id_offset, ws, st, n_fallback);
   if (p.exact_only) {
     // a shape the screen cannot plan (merge union > 2048, d or k > 256) runs the
     // fp64 brute force for every query: say so through the fallback count
@@ -2214,12 +2225,33 @@ static IvfPlan make_ivf_plan(int64_t nq, int nprobe, int nlist, int64_t max_list
   return p;
 }
 
+// The search's start-of-call state in ONE launch instead of five blits (each a
+// ~4.5 us fill kernel on the stream): the counters and guard word (fbc[0..16)),
+// n_fallback, the phase-A probe copy p0 (the nA nearest lists of each query),
+// the phase-A lane maxima (all bits set: NaN, never selected), the candidate
+// counts and phase A's slot -> pair table (all -1).
+__global__ __launch_bounds__(256) void ivf_init_kernel(int* __restrict__ fbc, int32_t* __restrict__ nfb,
+                                                       int64_t* __restrict__ p0, const int64_t* __restrict__ probe,
+                                                       int64_t nq, int64_t nq_p0, int nprobe, int nA,
+                                                       uint32_t* __restrict__ pt, int64_t npt, int* __restrict__ ccnt,
+                                                       int* __restrict__ sp, int64_t nsp) {
+  const int64_t t0 = (int64_t)blockIdx.x * 256 + threadIdx.x, stride = (int64_t)gridDim.x * 256;
+  if (t0 < 16) fbc[t0] = 0;
+  if (nfb && t0 < 2) nfb[t0] = 0;
+  for (int64_t i = t0; i < nq_p0 * nA; i += stride) p0[i] = probe[(i / nA) * nprobe + i % nA];
+  for (int64_t i = t0; i < npt; i += stride) pt[i] = 0xffffffffu;
+  for (int64_t i = t0; i < nq; i += stride) ccnt[i] = 0;
+  for (int64_t i = t0; i < nsp; i += stride) sp[i] = -1;
+}
+
 // group (query, probe) pairs by list and gather the probing queries list-major
+// (fill_sp: set the slot -> pair table to -1 first; the first grouping's was set
+// by ivf_init_kernel)
 static int ivf_group(const int64_t* probe, int64_t nq, int nprobe, int nlist, const int64_t* list_off, int wq, int ch,
                      int dp, int64_t max_rows, const uint16_t* qh, int* cnt, int* fill, int* seg, int* work, int* sp,
-                     uint16_t* qi, int* H, int* err, hipStream_t st) {
+                     uint16_t* qi, int* H, int* err, hipStream_t st, bool fill_sp = true) {
   const int64_t npairs = nq * nprobe;
-  if (hipMemsetAsync(sp, 0xff, (size_t)max_rows * 4, st) != hipSuccess)
+  if (fill_sp && hipMemsetAsync(sp, 0xff, (size_t)max_rows * 4, st) != hipSuccess)
     return fail(NRK_ELAUNCH, "ivf_search: memset failed");
   if (nlist <= GROUP_LDS_LISTS) {
     const size_t lds = (size_t)nlist * 4;
@@ -2278,11 +2310,7 @@ extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe,
   NRK_CHECK_ARG(ws != nullptr, "ivf_search: null workspace");
   char* w = static_cast<char*>(ws);
   int* fbc = reinterpret_cast<int*>(w + p.off_fbc);
-  if (hipMemsetAsync(fbc, 0, 64, st) != hipSuccess) return fail(NRK_ELAUNCH, "ivf_search: memset failed");
-  if (n_fallback && hipMemsetAsync(n_fallback, 0, 8, st) != hipSuccess)
-    return fail(NRK_ELAUNCH, "ivf_search: memset failed");
-  if (nq == 0) return NRK_OK;
-  NRK_CHECK_ARG(xq && probe && D && I && list_off, "ivf_search: null pointer");
+  NRK_CHECK_ARG(nq == 0 || (xq && probe && D && I && list_off), "ivf_search: null pointer");
   NRK_CHECK_ARG(n == 0 || (xb && xbh_ivf && meta_ivf && stats && pos2id && pos2list), "ivf_search: null index data");
   const int l2 = metric == NRK_METRIC_L2;
   auto mark = [&](int i) {
@@ -2322,21 +2350,28 @@ extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe,
   int* gerr = fbc + 4;  // the guard word (zeroed with the counters; nrk_ivf_search_status)
   IvfFb ivf{pos2id, pos2list, list_off, probe, nprobe, nlist, nq, gerr};
   const bool force_fb = test_hook("NRK_FORCE_FALLBACK", 0) != 0;
-
   mark(0);
+  {  // counters, guard word, n_fallback, candidate counts; with rows: phase A's p0 / pt / sp
+    const bool rows = n > 0 && nq > 0;
+    const int64_t npt = rows ? nq * p.nA * p.cmaxA * 2 : 0, nsp = rows ? p.max_rows : 0;
+    int64_t big = npt > nsp ? npt : nsp;
+    if (nq * p.nA > big) big = nq * p.nA;
+    const unsigned gi = (unsigned)(big > 16 ? (cdiv(big, 256) < 2048 ? cdiv(big, 256) : 2048) : 1);
+    hipLaunchKernelGGL(ivf_init_kernel, dim3(gi), dim3(256), 0, st, fbc, n_fallback, p0, probe, nq, rows ? nq : 0,
+                       nprobe, p.nA, reinterpret_cast<uint32_t*>(pt), npt, ccnt, sp, nsp);
+    NRK_CHECK_LAUNCH("ivf_init_kernel");
+  }
+  if (nq == 0) return NRK_OK;
+
   hipLaunchKernelGGL(query_prepare_kernel, dim3((unsigned)cdiv(p.nq_pad, 4)), dim3(256), 0, st, xq, nq, p.nq_pad, d,
                      p.dp, qh, qmeta);
   NRK_CHECK_LAUNCH("query_prepare_kernel");
   if (n > 0) {
     // ---- phase A: lane maxima over the nearest list of every query -> tau
-    if (hipMemcpy2DAsync(p0, (size_t)p.nA * 8, probe, (size_t)nprobe * 8, (size_t)p.nA * 8, (size_t)nq,
-                         hipMemcpyDeviceToDevice, st) != hipSuccess ||
-        hipMemsetAsync(pt, 0xff, (size_t)nq * p.nA * p.cmaxA * 2 * 4, st) != hipSuccess ||  // NaN: never selected
-        hipMemsetAsync(ccnt, 0, (size_t)nq * 4, st) != hipSuccess)
-      return fail(NRK_ELAUNCH, "ivf_search: copy/memset failed");
+    // (p0, pt (NaN: never selected), ccnt and sp were set by ivf_init_kernel)
     int rc =
         ivf_group(p0, nq, p.nA, nlist, list_off, p.wqA, p.chA, p.dp, p.max_rows, qh, cnt, fill, seg, work, sp, qi, hist, gerr,
-                  st);
+                  st, false);
     if (rc != NRK_OK) return rc;
     screen_fn fa = pick_screen(p.dp, p.qtA, p.M, l2 != 0, 4);
     if (!fa) return fail(NRK_EUNSUPPORTED, "ivf_search: no screen kernel for dp=%d", p.dp);
@@ -2359,9 +2394,7 @@ extern "C" int nrk_ivf_search(const float* xq, int64_t nq, const int64_t* probe,
     rc = ivf_group(probe, nq, nprobe, nlist, list_off, p.wq, p.chB, p.dp, p.max_rows, qh, cnt, fill, seg, work, sp, qi,
                    hist, gerr, st);
     if (rc != NRK_OK) return rc;
-  } else if (hipMemsetAsync(ccnt, 0, (size_t)nq * 4, st) != hipSuccess) {  // empty index: all -1
-    return fail(NRK_ELAUNCH, "ivf_search: memset");
-  }
+  }  // (empty index: ccnt zeroed by ivf_init_kernel, so every query reads all -1)
 
   mark(1);
   if (n > 0) {

@@ -176,7 +176,7 @@ __device__ __forceinline__ bool guard_ok(bool ok, int* err, int code) {
 // "goodness" g: larger is better.  IP: g = score; L2: g = -distance.
 // Ties on g break toward the lower id.
 __device__ inline bool better(double ga, int64_t ia, double gb, int64_t ib) {
-  return ga > gb || (ga == gb && ia < ib);
+  return (ga > gb) | ((ga == gb) & (ia < ib));  // no short circuit: no exec-mask branches
 }
 
 // Bitonic sort of n (power of two) (g, id) pairs in LDS, best first.
