@@ -861,6 +861,61 @@ __global__ __launch_bounds__(256) void small_rows_kernel(const float* __restrict
   G[ql * ldg + j] = L2 ? -acc : acc;
 }
 
+// k > 1, pass 1 on 32 x 32 tiles (2 x 2 outputs per thread) where 64 x 64 tiles
+// give the chip too few workgroups (the coarse quantizer: 4096 queries x 300
+// centroids is 320 of them); the same fp64 arithmetic per output.
+constexpr int S2_T = 32, S2_LD = S2_T + 2;
+template <bool L2>
+__global__ __launch_bounds__(256) void small_scores32_kernel(const float* __restrict__ xq, int64_t q0, int64_t nq,
+                                                             const float* __restrict__ xb, int64_t nb, int d,
+                                                             double* __restrict__ G, int64_t ldg) {
+  __shared__ __attribute__((aligned(16))) float Qs[SM_DC * S2_LD];
+  __shared__ __attribute__((aligned(16))) float Xs[SM_DC * S2_LD];
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  const int64_t j0 = (int64_t)blockIdx.x * S2_T;
+  const int64_t qt = q0 + (int64_t)blockIdx.y * S2_T;
+  double acc[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
+  for (int dc = 0; dc < d; dc += SM_DC) {
+    const int w = d - dc < SM_DC ? d - dc : SM_DC;
+    __syncthreads();  // previous step's readers are done
+#pragma unroll
+    for (int u = 0; u < (S2_T * SM_DC) / 256; ++u) {
+      const int e = tid + u * 256;
+      const int r = e / SM_DC, c = e % SM_DC;
+      const int64_t qi = qt + r, xi = j0 + r;
+      Qs[c * S2_LD + r] = (c < w && qi < nq) ? xq[qi * d + dc + c] : 0.f;
+      Xs[c * S2_LD + r] = (c < w && xi < nb) ? xb[xi * d + dc + c] : 0.f;
+    }
+    __syncthreads();
+    for (int j = 0; j < w; ++j) {
+      const float2 qv = *reinterpret_cast<const float2*>(Qs + j * S2_LD + ty * 2);
+      const float2 xv = *reinterpret_cast<const float2*>(Xs + j * S2_LD + tx * 2);
+      const double qd[2] = {(double)qv.x, (double)qv.y};
+      const double xd[2] = {(double)xv.x, (double)xv.y};
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          if (L2) {
+            const double t = qd[r] - xd[c];
+            acc[r][c] = fma(t, t, acc[r][c]);
+          } else {
+            acc[r][c] = fma(qd[r], xd[c], acc[r][c]);
+          }
+        }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int64_t qi = qt + ty * 2 + r;
+    if (qi >= nq) continue;
+    double* row = G + (qi - q0) * ldg + j0 + tx * 2;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+      if (j0 + tx * 2 + c < nb) row[c] = L2 ? -acc[r][c] : acc[r][c];
+  }
+}
+
 // k > 1, pass 2: one workgroup per query of the chunk sorts its nb goodness values.
 __global__ __launch_bounds__(256) void small_select_kernel(const double* __restrict__ G, int64_t ldg, int64_t q0,
                                                            int64_t nq, int64_t nb, int k, int l2, int P,
@@ -1819,6 +1874,13 @@ static int small_launch(const FlatPlan& p, const float* xq, int64_t nq, const fl
       else
         hipLaunchKernelGGL(small_rows_kernel<false>, dim3(grid), dim3(256), 0, st, xq, q0, nc, xb, nb, d, G, p.small_ld);
       NRK_CHECK_LAUNCH("small_rows_kernel");
+    } else if (nb > 0 && cdiv(nb, SM_T) * cdiv(nc, SM_T) < 1024) {  // few tiles: 32 x 32 ones
+      const dim3 grid((unsigned)cdiv(nb, S2_T), (unsigned)cdiv(nc, S2_T));
+      if (l2)
+        hipLaunchKernelGGL(small_scores32_kernel<true>, grid, dim3(256), 0, st, xq, q0, nq, xb, nb, d, G, p.small_ld);
+      else
+        hipLaunchKernelGGL(small_scores32_kernel<false>, grid, dim3(256), 0, st, xq, q0, nq, xb, nb, d, G, p.small_ld);
+      NRK_CHECK_LAUNCH("small_scores32_kernel");
     } else if (nb > 0) {
       const dim3 grid((unsigned)cdiv(nb, SM_T), (unsigned)cdiv(nc, SM_T));
       if (l2)
